@@ -1,0 +1,157 @@
+/*
+ * va355.h -- C ABI of libva355.so, the MI355X (gfx950) implementation of
+ * vision-assist's per-frame hot path:
+ *
+ *     frame -> YOLOv8-seg -> mask -> grid (+penalties) -> protrusions -> A*
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes (device
+ * pointers for bulk data, a hipStream_t passed as void*), allocates nothing,
+ * and returns an int status (VA_OK = 0, < 0 = error).  No C++ exception crosses
+ * this boundary.  All device buffers are caller-owned (PyTorch tensors in the
+ * Python host layer, see INTEGRATION.md for ctypes / cffi bindings).
+ *
+ * Reference interfaces each group replaces (paths under the reference repo):
+ *   va_nav_*   FrameProcessor._extract_grid_information     FrameProcessor.py:50-171
+ *              FrameProcessor._calculate_penalties          FrameProcessor.py:173-182
+ *                + PenaltyCalculator.calculate_penalty      PenaltyCalculator.py:26-142
+ *              FrameProcessor._create_graph                 FrameProcessor.py:184-207
+ *              ProtrusionDetector.__call__                  ProtrusionDetector.py:419-535
+ *              FrameProcessor._find_paths                   FrameProcessor.py:230-271
+ *                + utils.get_closest_grid_to_point          utils.py:6-32
+ *                + PathFinder.find_path                     PathFinder.py:119-186
+ *   va_seg_*   YOLO.predict (Ultralytics, external) as called at FrameProcessor.py:322:
+ *              letterbox/normalise, YOLOv8-seg forward, NMS, process_mask,
+ *              masks.xy -> largest mask -> fillPoly          FrameProcessor.py:67-86
+ */
+#ifndef VA355_H
+#define VA355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status */
+#define VA_OK 0
+#define VA_ERR_ARG (-1)       /* bad argument (shape not a multiple of 20, null ptr, ...) */
+#define VA_ERR_HIP (-2)       /* a HIP runtime call failed */
+#define VA_ERR_RANGE (-3)     /* input outside the compiled limits */
+
+/* per-frame nav status (va_frame_hdr.status) */
+#define VA_FRAME_OK 0
+#define VA_FRAME_EMPTY 1      /* no cell centre inside the mask: FrameProcessor.py:99-101 -> __call__ returns [] */
+#define VA_FRAME_INDEX_ERROR 2 /* the reference raises IndexError */
+#define VA_FRAME_NO_MASK 3    /* no mask at all (no detection): FrameProcessor.py:68-69 */
+
+/* per-query status (va_query_hdr.status) */
+#define VA_QUERY_NONE 0       /* no query in this slot */
+#define VA_QUERY_FOUND 1
+#define VA_QUERY_NO_PATH 2    /* find_path returned ([], inf): "No path found." FrameProcessor.py:252-253 */
+
+#define VA_GRID 20            /* config.py:1 grid_size */
+
+/* ---------------------------------------------------------------- nav layout */
+/* Geometry of one frame size.  "lattice" = the H/20 x W/20 cell lattice on
+ * which every grid coordinate of the reference lies (x, y multiples of 20).
+ * A lattice node index is yi * LC + xi. */
+typedef struct va_nav_dims {
+    int32_t H, W;          /* frame size in pixels (multiples of 20) */
+    int32_t LR, LC;        /* lattice rows / cols */
+    int32_t start_y;       /* first artificial row y: FrameProcessor.py:126-127 */
+    int32_t NART;          /* number of artificial rows (start_y .. H-20) */
+    int32_t PMAX;          /* max list positions in self.grids = LR + NART */
+    int32_t MAXPK;         /* max protrusion peaks (= queries) per frame */
+    int32_t NODES;         /* LR * LC */
+    int32_t pad;
+    /* byte offsets inside one frame record */
+    int64_t frame_bytes;
+    int64_t off_hdr, off_peaks, off_pos_obj, off_pos_y, off_pos_attr;
+    int64_t off_cell_flags, off_cell_pen, off_node_flags, off_node_pen;
+    /* byte offsets inside one query record */
+    int64_t query_bytes;
+    int64_t off_q_hdr, off_q_path;
+    /* workspace = B frame records | B*MAXPK query records | control block */
+    int64_t off_queries_per_frame; /* = frame_bytes (queries start after all frames) */
+} va_nav_dims;
+
+typedef struct va_frame_hdr {
+    int32_t status;        /* VA_FRAME_* */
+    int32_t x0, y0;        /* snapped rect origin (pixels): FrameProcessor.py:79-80 */
+    int32_t C, Rm;         /* columns (len(j_vals)), main rows (len(i_vals)) */
+    int32_t P;             /* len(self.grids) after the artificial-row loop */
+    int32_t npeaks;        /* protrusion peaks = A* queries */
+    int32_t start_p, start_c; /* start Grid = self.grids[start_p][start_c] (utils.py:6-32) */
+    int32_t min_y;         /* y of the top-most non-empty row (pixels) */
+    int32_t rounds;        /* speculative A* rounds this frame took part in */
+    int32_t pad[5];
+} va_frame_hdr;            /* 64 bytes; followed by int32 peak_x/peak_y/end_p/end_c[MAXPK] */
+
+/* cell flag bits (per list position p, column c): the Grid object self.grids[p][c] */
+#define VA_CELL_EMPTY 1u
+#define VA_CELL_ARTIFICIAL 2u
+/* node flag bits (per lattice node): the object self.grid_lookup[(x, y)] */
+#define VA_NODE_EXISTS 1u      /* (x, y) in grid_lookup */
+#define VA_NODE_NONEMPTY 2u    /* grid_lookup[(x, y)].empty == False */
+#define VA_NODE_IN_GRIDS 4u    /* that object is also in self.grids (not an orphan) */
+#define VA_NODE_MULT_SHIFT 3   /* bits 3-4: len(graph[(x, y)]) / 4 (duplicate rows, Q19) */
+
+typedef struct va_query_hdr {
+    int32_t status;        /* VA_QUERY_* */
+    int32_t len;           /* path length (Grid count) */
+    double cost;           /* total_cost (g of the end node) */
+    uint64_t miss[2];      /* angle keys this query added to the seen set */
+    int32_t frame, k;      /* frame index, peak index */
+    int32_t expansions;    /* A* pops */
+    int32_t unique;        /* 1 = kept by the Jaccard/subset filter (FrameProcessor.py:256-269) */
+    int32_t order;         /* index in the returned path list (-1 if dropped) */
+    int32_t pad;
+} va_query_hdr;            /* 56 bytes; followed by uint16 path[NODES] (lattice nodes, start..end) */
+
+/* Fill *out for an H x W frame.  Returns VA_ERR_ARG unless H, W are positive
+ * multiples of 20 and within the compiled limits (W/20, H/20 <= 64). */
+int va_nav_dims_for(int32_t H, int32_t W, va_nav_dims* out);
+
+/* Bytes of device workspace va_nav_run needs for B frames. */
+int64_t va_nav_workspace_bytes(int32_t B, int32_t H, int32_t W);
+
+/* Sample the cell lattice of B filled masks: cells[b][yi][xi] = mask[b][20*yi+10][20*xi+10] != 0
+ * (FrameProcessor.py:88-97 samples exactly these pixels).  masks: uint8 [B][H][pitch]. */
+int va_nav_sample_cells(void* stream, const uint8_t* masks, int64_t pitch, int32_t B, int32_t H, int32_t W,
+                        uint8_t* cells);
+
+/* The whole grid-level hot path for B frames of size H x W.
+ *   cells   device uint8 [B][H/20][W/20]: lattice samples of the filled mask (cv2.fillPoly result)
+ *   rects   device int32 [B][4]: cv2.boundingRect (x, y, w, h) of the mask polygon; w <= 0 = no mask
+ *   seen    device uint64 [2] in/out: PathFinder.angle_cache key set (128 bits, key = prev*8+next;
+ *           the process-global cache of PathFinder.py:32, never cleared).  Queries are ordered
+ *           (frame, peak) exactly as the reference issues them; the result is bit-identical to
+ *           running them one after the other.
+ *   work    device workspace of va_nav_workspace_bytes(B, H, W) bytes: frame + query records.
+ *   rounds  host out (may be NULL): speculative A* rounds needed (1 = no re-run).
+ * Synchronises `stream` once per speculative round (to read the round's verdict). */
+int va_nav_run(void* stream, const uint8_t* cells, const int32_t* rects, int32_t B, int32_t H, int32_t W,
+               uint64_t* seen, void* work, int32_t* rounds);
+
+/* Standalone A* over an explicit lattice (PathFinder.find_path surface, PathFinder.py:119-186)
+ * for Q queries that share one lattice of LR x LC nodes.
+ *   node_flags  device uint8 [LR*LC] (VA_NODE_* bits; multiplicity in bits 3-4)
+ *   node_pen    device double [LR*LC] (Grid.penalty of grid_lookup[(x, y)], None -> 0)
+ *   starts/ends device int32 [Q] lattice node indices
+ *   seen        device uint64 [2] in/out
+ *   qwork       device workspace of va_astar_workspace_bytes(Q, LR*LC) bytes: Q query records of
+ *               va_nav_query_bytes(LR*LC) bytes each, then a 64-byte control block */
+int64_t va_nav_query_bytes(int32_t nodes);
+int64_t va_astar_workspace_bytes(int32_t Q, int32_t nodes);
+int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen, int32_t LR, int32_t LC,
+                 const int32_t* starts, const int32_t* ends, int32_t Q, uint64_t* seen, void* qwork,
+                 int32_t* rounds);
+
+/* Library version / build info string. */
+const char* va_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VA355_H */

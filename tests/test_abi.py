@@ -1,0 +1,63 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/va355.h
+declares, and its host-side layout functions agree with the python decoders.
+(No compute entry point is called here: there is no GPU in the build container.)"""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, "include", "va355.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(va_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_symbols():
+    syms = _declared_symbols()
+    assert "va_nav_run" in syms and "va_astar_run" in syms and len(syms) >= 8
+
+
+def test_library_exports_every_declared_symbol():
+    from vision_assist_amd import _lib
+    lib = _lib.load()
+    for s in _declared_symbols():
+        assert hasattr(lib, s), f"libva355.so does not export {s}"
+    assert {s for s, _, _ in _lib.SIGNATURES} >= set(_declared_symbols())
+
+
+@pytest.mark.parametrize("H,W", [(640, 640), (1280, 1280), (1280, 720)])
+def test_nav_dims(H, W):
+    from vision_assist_amd import _lib
+    d = _lib.nav_dims(H, W)
+    assert (d.LR, d.LC) == (H // 20, W // 20)
+    sy = int(H * 0.875)
+    sy = sy + (20 - sy % 20) % 20
+    assert d.start_y == sy and d.NART == (H - sy) // 20
+    assert d.frame_bytes % 16 == 0 and d.query_bytes % 16 == 0
+    assert _lib.load().va_nav_workspace_bytes(4, H, W) >= 4 * d.frame_bytes
+
+
+def test_nav_dims_rejects_bad_shapes():
+    from vision_assist_amd import _lib
+    d = _lib.VaNavDims()
+    lib = _lib.load()
+    assert lib.va_nav_dims_for(630, 640, ctypes.byref(d)) != 0
+    assert lib.va_nav_dims_for(640, 2000, ctypes.byref(d)) != 0
+    assert lib.va_nav_workspace_bytes(0, 640, 640) < 0
+
+
+def test_angle_table_header_matches_reference():
+    """va_angle_table.h (baked into the library) == the reference-generated table."""
+    from tests.golden_io import load_goldens
+    txt = open(os.path.join(REPO, "vision_assist_amd", "csrc", "va_angle_table.h")).read()
+    pens = re.search(r"VA_ANGLE_PEN\[128\] = \{([^}]*)\}", txt).group(1).split(",")
+    degs = re.search(r"VA_ANGLE_DEG\[128\] = \{([^}]*)\}", txt).group(1).split(",")
+    golden = load_goldens()["angle_table"]
+    assert len(pens) == len(degs) == len(golden) == 128
+    for (a, b, c, dd, gdeg, gpen), deg, pen in zip(golden, degs, pens):
+        assert float.fromhex(deg.strip()).hex() == gdeg
+        want = 0.0 if gpen.startswith("i") else float.fromhex(gpen)
+        assert float.fromhex(pen.strip()) == want

@@ -1,0 +1,92 @@
+"""ctypes binding of libva355.so (the HIP/gfx950 C-ABI, include/va355.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C
+vision_assist_amd/csrc``).  There is NO fallback: if the shared object is
+missing or a GPU is absent, every entry point raises.  torch is imported first
+so that the process has exactly one HIP runtime (torch's bundled
+libamdhip64.so.7 satisfies the library's DT_NEEDED of the same soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before ours)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libva355.so")
+
+VA_OK = 0
+VA_FRAME_OK, VA_FRAME_EMPTY, VA_FRAME_INDEX_ERROR, VA_FRAME_NO_MASK = 0, 1, 2, 3
+VA_QUERY_NONE, VA_QUERY_FOUND, VA_QUERY_NO_PATH = 0, 1, 2
+VA_CELL_EMPTY, VA_CELL_ARTIFICIAL = 1, 2
+VA_NODE_EXISTS, VA_NODE_NONEMPTY, VA_NODE_IN_GRIDS, VA_NODE_MULT_SHIFT = 1, 2, 4, 3
+
+
+class VaNavDims(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("H", "W", "LR", "LC", "start_y", "NART", "PMAX", "MAXPK", "NODES", "pad")] + \
+               [(n, ctypes.c_int64) for n in
+                ("frame_bytes", "off_hdr", "off_peaks", "off_pos_obj", "off_pos_y", "off_pos_attr",
+                 "off_cell_flags", "off_cell_pen", "off_node_flags", "off_node_pen",
+                 "query_bytes", "off_q_hdr", "off_q_path", "off_queries_per_frame")]
+
+
+class VaError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+# (name, restype, argtypes) for every symbol include/va355.h declares
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+SIGNATURES = [
+    ("va_nav_dims_for", I32, [I32, I32, ctypes.POINTER(VaNavDims)]),
+    ("va_nav_workspace_bytes", I64, [I32, I32, I32]),
+    ("va_nav_sample_cells", I32, [P, P, I64, I32, I32, I32, P]),
+    ("va_nav_run", I32, [P, P, P, I32, I32, I32, P, P, ctypes.POINTER(I32)]),
+    ("va_nav_query_bytes", I64, [I32]),
+    ("va_astar_workspace_bytes", I64, [I32, I32]),
+    ("va_astar_run", I32, [P, P, P, I32, I32, P, P, I32, P, P, ctypes.POINTER(I32)]),
+    ("va_version", ctypes.c_char_p, []),
+]
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes handle.  Raises if the .so is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise VaError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "(the HIP extension is required; there is no CPU fallback)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != VA_OK:
+        raise VaError(f"{what} failed with status {rc}")
+
+
+def nav_dims(H: int, W: int) -> VaNavDims:
+    d = VaNavDims()
+    check(load().va_nav_dims_for(H, W, ctypes.byref(d)), f"va_nav_dims_for({H}, {W})")
+    return d
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise VaError("vision_assist_amd needs a ROCm GPU (MI355X); torch.cuda.is_available() is False")
