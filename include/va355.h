@@ -148,6 +148,63 @@ int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen
                  const int32_t* starts, const int32_t* ends, int32_t Q, uint64_t* seen, void* qwork,
                  int32_t* rounds);
 
+
+/* ---------------------------------------------------------------- segmentation (YOLOv8-seg) */
+#define VA_DTYPE_BF16 1
+#define VA_DTYPE_F32 2
+
+/* One Conv2d (+ folded BN bias, optional SiLU, optional residual add) as an implicit GEMM on MFMA.
+ * Replaces the Conv / Bottleneck / C2f / SPPF / Detect / Proto convolutions Ultralytics runs inside
+ * YOLO.predict (FrameProcessor.py:322; modules conv.py:54, block.py:237-239, head.py per the
+ * reference's profile.svg).  Activations are NHWC channel slices: element (n, h, w, c) of a tensor
+ * lives at ptr[((n*H + h)*W + w)*ld + c]. */
+typedef struct va_conv_args {
+    const void* x;          /* input slice (dtype) */
+    int32_t N, H, W, Cin, ldx;
+    int32_t kh, kw, stride, pad;
+    int32_t Ho, Wo;
+    const void* w;          /* packed weights (dtype) [Npad][Kpad], K ordered (ky, kx, ci), zero padded */
+    const float* bias;      /* [Npad] */
+    int32_t Cout, Npad, K, Kpad; /* K = kh*kw*Cin; Kpad % 32 == 0; Npad % 128 == 0 */
+    void* y;                /* output slice (dtype, or float if out_f32) */
+    int32_t ldy;
+    const void* res;        /* residual slice (dtype) added after the activation, or NULL */
+    int32_t ldr;
+    int32_t act;            /* 1 = SiLU */
+    int32_t mode;           /* 0 = conv, 1 = ConvTranspose2d(k=2, s=2) packed as a 1x1 conv with Cout = 4*C */
+    int32_t M;              /* N * Ho * Wo */
+    int32_t dtype;          /* VA_DTYPE_BF16 (MFMA bf16, f32 accumulate) or VA_DTYPE_F32 (exact f32 MFMA) */
+    int32_t out_f32;        /* bf16 inputs with a float output (head logits) */
+    int32_t pad_;
+} va_conv_args;
+
+int va_seg_conv(void* stream, const va_conv_args* a);
+
+/* uint8 BGR frames [B][H][W][3] -> RGB / 255 NHWC with 8 channels (3 used), dtype VA_DTYPE_*. */
+int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H, int32_t W, int32_t dtype, void* out);
+
+/* SPPF (block.py SPPF): slice 0 (c channels) of an NHWC buffer of channel stride ld >= 4c -> slices 1..3
+ * = MaxPool2d(5, 1, 2) applied once, twice, three times. */
+int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld, int32_t dtype);
+
+/* nn.Upsample(scale_factor=2, mode="nearest") from a slice into a concat slice. */
+int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, int32_t ld_d, int32_t N, int32_t H,
+                      int32_t W, int32_t c, int32_t dtype);
+
+/* A whole forward as a list of ops executed back-to-back on one stream by ONE call (no per-layer
+ * host round trip; the list is built once per (batch, frame size) by the host planner). */
+#define VA_OP_CONV 1        /* conv: all fields of .a */
+#define VA_OP_SPPF 2        /* sppf pool: a.y = buffer, a.N/H/W, a.Cin = c, a.ldy = ld, a.dtype */
+#define VA_OP_UPSAMPLE 3    /* upsample2x: a.x/a.ldx -> a.y/a.ldy, a.N/H/W (source size), a.Cin = c, a.dtype */
+#define VA_OP_PREPROCESS 4  /* preprocess: a.x = uint8 frames, a.y = out, a.N/H/W, a.dtype */
+typedef struct va_seg_op {
+    int32_t kind;
+    int32_t pad_;
+    va_conv_args a;
+} va_seg_op;
+
+int va_seg_run(void* stream, const va_seg_op* ops, int32_t n);
+
 /* Library version / build info string. */
 const char* va_version(void);
 

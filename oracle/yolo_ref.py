@@ -1,0 +1,210 @@
+"""Plain-PyTorch fp32 (CPU) reference of the segmentation stage (TEST INFRASTRUCTURE).
+
+Checker for the HIP YOLOv8-seg path and the cpu_baseline leg of bench.py;
+never imported by the product.  The algorithms live in the third-party
+``ultralytics`` package (version evidence 8.3.3:
+model/runs/segment/train16/weights/best_saved_model/metadata.yaml:4), absent
+from the reference tree and from this image, together with torchvision and
+OpenCV; they are restated here from their published definitions and from the
+vendored spec copies in the reference:
+
+  preprocess      LetterBox (identity for a 640x640 frame), BGR->RGB, HWC->CHW, /255
+                  testing/old/segmenting_using_tflite/just_segmentation_using_tflite_model.py:36-115
+  forward         Conv(+BN folded)+SiLU, C2f, SPPF, FPN/PAN, Segment head
+  decode          DFL softmax expectation, dist2bbox (xywh) * stride, class sigmoid
+  NMS             testing/old/segmenting_using_tflite/ops.py:214-363 (+ torchvision.ops.nms:
+                  greedy, IoU > iou_thres suppresses; ties kept in index order here)
+  process_mask    ops.py:707-737 (coef @ proto, crop to box/4, bilinear x4, > 0)
+  mask -> grid    FrameProcessor.py:67-86 via Results.masks.xy (ops.py:837-859 'largest').
+                  PARITY UNPINNED: cv2.findContours / contourArea / fillPoly are not available.
+                  Restated as: instance with the most mask pixels (first wins), its whole
+                  mask as the filled polygon, its pixel bounding box as boundingRect.  Exact
+                  for single hole-free components.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+REG_MAX = 16
+STRIDES = (8, 16, 32)
+MAX_WH = 7680
+
+
+def preprocess(frames_bgr_u8: torch.Tensor) -> torch.Tensor:
+    """uint8 [B, H, W, 3] BGR -> float32 [B, 3, H, W] RGB in [0, 1]."""
+    x = frames_bgr_u8[..., [2, 1, 0]].permute(0, 3, 1, 2).contiguous().float()
+    return x / 255.0
+
+
+def forward(arch, fw: dict, x: torch.Tensor):
+    """Raw head outputs: (box [B,64,A], cls [B,nc,A], coef [B,32,A], proto [B,32,H/4,W/4]), fp32."""
+
+    def conv(p, t, k, s=1, act=True):
+        w, b = fw[p]
+        y = F.conv2d(t, w, b, s, k // 2)
+        return F.silu(y) if act else y
+
+    def c2f(i, t, n, shortcut):
+        y = conv(f"model.{i}.cv1", t, 1)
+        ys = list(y.chunk(2, 1))
+        for j in range(n):
+            u = conv(f"model.{i}.m.{j}.cv1", ys[-1], 3)
+            u = conv(f"model.{i}.m.{j}.cv2", u, 3)
+            ys.append(ys[-1] + u if shortcut else u)
+        return conv(f"model.{i}.cv2", torch.cat(ys, 1), 1)
+
+    plan = {i: (n, sc) for i, _, _, n, sc in arch.c2f_plan()}
+    x = conv("model.0", x, 3, 2)
+    x = conv("model.1", x, 3, 2)
+    x = c2f(2, x, *plan[2])
+    x = conv("model.3", x, 3, 2)
+    p3 = c2f(4, x, *plan[4])
+    x = conv("model.5", p3, 3, 2)
+    p4 = c2f(6, x, *plan[6])
+    x = conv("model.7", p4, 3, 2)
+    x = c2f(8, x, *plan[8])
+    # SPPF
+    y0 = conv("model.9.cv1", x, 1)
+    y1 = F.max_pool2d(y0, 5, 1, 2)
+    y2 = F.max_pool2d(y1, 5, 1, 2)
+    y3 = F.max_pool2d(y2, 5, 1, 2)
+    p5 = conv("model.9.cv2", torch.cat([y0, y1, y2, y3], 1), 1)
+    # head
+    x = torch.cat([F.interpolate(p5, scale_factor=2, mode="nearest"), p4], 1)
+    h12 = c2f(12, x, *plan[12])
+    x = torch.cat([F.interpolate(h12, scale_factor=2, mode="nearest"), p3], 1)
+    o3 = c2f(15, x, *plan[15])
+    x = torch.cat([conv("model.16", o3, 3, 2), h12], 1)
+    o4 = c2f(18, x, *plan[18])
+    x = torch.cat([conv("model.19", o4, 3, 2), p5], 1)
+    o5 = c2f(21, x, *plan[21])
+    outs = {"cv2": [], "cv3": [], "cv4": []}
+    for l, t in enumerate((o3, o4, o5)):
+        for br in outs:
+            u = conv(f"model.22.{br}.{l}.0", t, 3)
+            u = conv(f"model.22.{br}.{l}.1", u, 3)
+            u = conv(f"model.22.{br}.{l}.2", u, 1, act=False)
+            outs[br].append(u.flatten(2))
+    box = torch.cat(outs["cv2"], 2)
+    cls = torch.cat(outs["cv3"], 2)
+    coef = torch.cat(outs["cv4"], 2)
+    # proto
+    u = conv("model.22.proto.cv1", o3, 3)
+    w, b = fw["model.22.proto.upsample"]
+    u = F.conv_transpose2d(u, w, b, stride=2)
+    u = conv("model.22.proto.cv2", u, 3)
+    proto = conv("model.22.proto.cv3", u, 1)
+    return box, cls, coef, proto
+
+
+def anchors(H: int, W: int):
+    pts, st = [], []
+    for s in STRIDES:
+        h, w = H // s, W // s
+        sy, sx = torch.meshgrid(torch.arange(h, dtype=torch.float32) + 0.5,
+                                torch.arange(w, dtype=torch.float32) + 0.5, indexing="ij")
+        pts.append(torch.stack((sx, sy), -1).view(-1, 2))
+        st.append(torch.full((h * w, 1), float(s)))
+    return torch.cat(pts).T, torch.cat(st).T  # [2, A], [1, A]
+
+
+def decode(box: torch.Tensor, cls: torch.Tensor, H: int, W: int):
+    """Detect inference tail: DFL -> dist2bbox(xywh) * stride; class sigmoid.  -> [B, 4+nc, A]."""
+    B, _, A = box.shape
+    prob = box.view(B, 4, REG_MAX, A).softmax(2)
+    dist = (prob * torch.arange(REG_MAX, dtype=torch.float32).view(1, 1, REG_MAX, 1)).sum(2)
+    ap, st = anchors(H, W)
+    lt, rb = dist[:, :2], dist[:, 2:]
+    x1y1 = ap.unsqueeze(0) - lt
+    x2y2 = ap.unsqueeze(0) + rb
+    dbox = torch.cat(((x1y1 + x2y2) / 2, x2y2 - x1y1), 1) * st
+    return torch.cat((dbox, cls.sigmoid()), 1)
+
+
+def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: float = 0.7, max_det: int = 300):
+    """non_max_suppression for one image (ops.py:214-363): pred [4+nc, A], coef [32, A]
+    -> [k, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) in decreasing score order."""
+    nc = pred.shape[0] - 4
+    x = torch.cat((pred, coef), 0).T  # [A, 4+nc+32]
+    xc = x[:, 4:4 + nc].amax(1) > conf
+    x = x[xc]
+    if not x.shape[0]:
+        return torch.zeros((0, 6 + coef.shape[0]))
+    xy, wh = x[:, :2], x[:, 2:4]
+    boxes = torch.cat((xy - wh / 2, xy + wh / 2), 1)
+    score, j = x[:, 4:4 + nc].max(1, keepdim=True)
+    det = torch.cat((boxes, score, j.float(), x[:, 4 + nc:]), 1)[score.view(-1) > conf]
+    keep = greedy_nms(det[:, :4] + det[:, 5:6] * MAX_WH, det[:, 4], iou)[:max_det]
+    return det[keep]
+
+
+def greedy_nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float) -> torch.Tensor:
+    """torchvision.ops.nms semantics (float32 IoU, suppress IoU > thr); stable order for ties."""
+    order = torch.sort(scores, descending=True, stable=True).indices
+    b = boxes[order]
+    area = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    n = b.shape[0]
+    sup = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    for i in range(n):
+        if sup[i]:
+            continue
+        keep.append(int(order[i]))
+        xx1 = torch.maximum(b[i, 0], b[i + 1:, 0])
+        yy1 = torch.maximum(b[i, 1], b[i + 1:, 1])
+        xx2 = torch.minimum(b[i, 2], b[i + 1:, 2])
+        yy2 = torch.minimum(b[i, 3], b[i + 1:, 3])
+        inter = (xx2 - xx1).clamp(min=0) * (yy2 - yy1).clamp(min=0)
+        ovr = inter / (area[i] + area[i + 1:] - inter)
+        sup[i + 1:] |= ovr.double() > thr
+    return torch.tensor(keep, dtype=torch.long)
+
+
+def process_mask(proto: torch.Tensor, coef: torch.Tensor, boxes: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """ops.process_mask(upsample=True) (ops.py:707-737): [n,32] @ [32, h*w] -> crop -> bilinear -> > 0."""
+    c, mh, mw = proto.shape
+    masks = (coef @ proto.float().view(c, -1)).view(-1, mh, mw)
+    db = boxes.clone()
+    db[:, 0] *= mw / W
+    db[:, 2] *= mw / W
+    db[:, 3] *= mh / H
+    db[:, 1] *= mh / H
+    x1, y1, x2, y2 = torch.chunk(db[:, :, None], 4, 1)
+    r = torch.arange(mw, dtype=x1.dtype)[None, None, :]
+    cc = torch.arange(mh, dtype=x1.dtype)[None, :, None]
+    masks = masks * ((r >= x1) * (r < x2) * (cc >= y1) * (cc < y2))
+    masks = F.interpolate(masks[None], (H, W), mode="bilinear", align_corners=False)[0]
+    return masks.gt_(0.0)
+
+
+def select_mask(masks: torch.Tensor):
+    """Restated FrameProcessor.py:67-86 (see module docstring: parity unpinned vs OpenCV).
+    -> (filled uint8 [H, W] or None, rect (x, y, w, h))."""
+    if masks.shape[0] == 0:
+        return None, (0, 0, 0, 0)
+    counts = masks.flatten(1).sum(1)
+    i = int(torch.argmax(counts))  # first maximum
+    if counts[i] == 0:
+        return None, (0, 0, 0, 0)
+    m = masks[i].to(torch.uint8)
+    ys, xs = torch.nonzero(m, as_tuple=True)
+    x0, x1, y0, y1 = int(xs.min()), int(xs.max()), int(ys.min()), int(ys.max())
+    return m, (x0, y0, x1 - x0 + 1, y1 - y0 + 1)
+
+
+def predict(arch, fw, frames_bgr_u8: torch.Tensor, conf=0.5, iou=0.7, max_det=300):
+    """Full segmentation stage for a batch: -> list of (det [k, 38], masks [k, H, W] bool)."""
+    B, H, W, _ = frames_bgr_u8.shape
+    x = preprocess(frames_bgr_u8)
+    box, cls, coef, proto = forward(arch, fw, x)
+    pred = decode(box, cls, H, W)
+    out = []
+    for b in range(B):
+        det = nms_image(pred[b], coef[b], conf, iou, max_det)
+        if det.shape[0]:
+            masks = process_mask(proto[b], det[:, 6:], det[:, :4], H, W)
+        else:
+            masks = torch.zeros((0, H, W))
+        out.append((det, masks))
+    return out

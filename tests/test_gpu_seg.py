@@ -1,0 +1,148 @@
+"""GPU numerics of the segmentation kernels vs a plain PyTorch fp32 reference.
+
+* single ops (va_seg_conv incl. stride 2, residual, channel slices, ConvTranspose;
+  SPPF pool; nearest upsample) against torch.nn.functional on the CPU;
+* the whole YOLOv8-seg forward (oracle/yolo_ref.py, seeded synthetic weights):
+  f32 mode (exact-f32 MFMA) within 1e-3 of the fp32 reference logits
+  (BASELINE.json north_star tolerance); bf16 mode within a relative bound.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import yolo_ref as Y
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(dtype, scale="s", nc=80, seed=0, cls_bias=None):
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch(scale, nc)
+    fw = fold(arch, synthetic_state_dict(arch, seed=seed, cls_bias=cls_bias))
+    return arch, fw, SegNet(arch, fw, dtype=dtype)
+
+
+def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, act=True):
+    from vision_assist_amd import seg as S
+    from vision_assist_amd.seg_arch import Arch
+    g = torch.Generator().manual_seed(cin * 1000 + cout + k)
+    B = 2
+    if deconv:
+        w = torch.randn(cin, cout, 2, 2, generator=g) * 0.2
+    else:
+        w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(B, cin, H, W, generator=g)
+    net = S.SegNet.__new__(S.SegNet)
+    net.arch = Arch("n")
+    net.dtype = dtype
+    net.tdtype = torch.bfloat16 if dtype == "bf16" else torch.float32
+    net.va_dtype = S.VA_DTYPE_BF16 if dtype == "bf16" else S.VA_DTYPE_F32
+    net.vec = 8 if dtype == "bf16" else 4
+    net.device = torch.device("cuda")
+    from vision_assist_amd import _lib
+    net.lib = _lib.load()
+    p = net._pack(w, b, deconv=deconv)
+    ld_in = cin + slice_in + 8
+    xin = torch.zeros(B, H, W, ld_in, dtype=net.tdtype, device="cuda")
+    xin[..., slice_in:slice_in + cin] = x.permute(0, 2, 3, 1).to(net.tdtype).cuda()
+    xr = xin[..., slice_in:slice_in + cin].float().cpu().permute(0, 3, 1, 2)  # what the kernel sees
+    pad = k // 2 if not deconv else 0
+    if deconv:
+        Ho, Wo, oh, ow = H, W, 2 * H, 2 * W
+    else:
+        Ho = (H + 2 * pad - k) // stride + 1
+        Wo = (W + 2 * pad - k) // stride + 1
+        oh, ow = Ho, Wo
+    ld_out = cout + 16
+    y = torch.zeros(B, oh, ow, ld_out, dtype=net.tdtype, device="cuda")
+    res = None
+    if residual:
+        res = torch.randn(B, oh, ow, cout, generator=g).to(net.tdtype).cuda()
+    args = S.ConvArgs(x=xin.data_ptr() + slice_in * xin.element_size(), N=B, H=H, W=W, Cin=p.cin, ldx=ld_in,
+                      kh=p.k, kw=p.k, stride=stride if not deconv else 1, pad=pad, Ho=Ho, Wo=Wo,
+                      w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
+                      y=y.data_ptr() + 8 * y.element_size(), ldy=ld_out,
+                      res=res.data_ptr() if res is not None else None, ldr=cout, act=1 if act else 0,
+                      mode=1 if deconv else 0, M=B * Ho * Wo, dtype=net.va_dtype, out_f32=0)
+    _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), __import__("ctypes").byref(args)), "va_seg_conv")
+    torch.cuda.synchronize()
+    got = y[..., 8:8 + cout].float().cpu().permute(0, 3, 1, 2)
+    wr = w.to(net.tdtype).float() if dtype == "bf16" else w
+    if deconv:
+        ref = F.conv_transpose2d(xr, wr, b, stride=2)
+    else:
+        ref = F.conv2d(xr, wr, b, stride, pad)
+    if act:
+        ref = F.silu(ref)
+    if residual:
+        ref = ref + res.float().cpu().permute(0, 3, 1, 2)
+    return got, ref
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,deconv,slice_in", [
+    (8, 32, 3, 2, 34, 30, False, False, 0),
+    (32, 64, 3, 1, 20, 20, True, False, 16),
+    (64, 96, 1, 1, 24, 17, False, False, 8),
+    (96, 80, 1, 1, 13, 13, False, False, 0),
+    (16, 256, 3, 2, 40, 40, False, False, 0),
+    (64, 32, 2, 1, 10, 12, False, True, 0),
+])
+def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
+    got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in, act=not deconv)
+    if dtype == "f32":
+        assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+    else:
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 2e-2, err
+
+
+def _ref_heads(arch, fw, frames):
+    box, cls, coef, proto = Y.forward(arch, fw, Y.preprocess(frames))
+    return box, cls, coef, proto
+
+
+def _gpu_heads(net, frames):
+    out = net.forward(frames.cuda())
+    torch.cuda.synchronize()
+    lv = [t.float().cpu().flatten(1, 2) for t in out.levels]  # [B, hw, no]
+    cat = torch.cat(lv, 1).permute(0, 2, 1)  # [B, no, A]
+    nc = net.arch.nc
+    return cat[:, :64], cat[:, 64:64 + nc], cat[:, 64 + nc:], out.proto.float().cpu().permute(0, 3, 1, 2)
+
+
+def _frames(B, H=640, W=640, seed=0):
+    return torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(seed), dtype=torch.uint8)
+
+
+def test_forward_f32_within_1e3_of_torch_reference():
+    torch.set_num_threads(8)
+    arch, fw, net = _net("f32", "s")
+    frames = _frames(2)
+    ref = _ref_heads(arch, fw, frames)
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        err = (g - r).abs().max().item()
+        assert err <= 1e-3, f"{name}: max |gpu - torch fp32| = {err}"
+
+
+def test_forward_bf16_close_to_torch_reference():
+    arch, fw, net = _net("bf16", "s")
+    frames = _frames(2, seed=1)
+    ref = _ref_heads(arch, fw, frames)
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        rel = ((g - r).norm() / r.norm()).item()
+        assert rel < 5e-2, f"{name}: relative L2 error {rel}"
+
+
+def test_forward_f32_nano_1280():
+    arch, fw, net = _net("f32", "n", seed=3)
+    frames = _frames(1, 1280, 1280, seed=2)
+    ref = _ref_heads(arch, fw, frames)
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        err = ((g - r).abs() / (1.0 + r.abs())).max().item()
+        assert err <= 1e-3, f"{name}: max rel err {err}"

@@ -1,0 +1,402 @@
+// va_seg.hip -- YOLOv8-seg forward on MI355X (gfx950): the segmentation half of the hot path
+// (YOLO.predict as called at FrameProcessor.py:322; Ultralytics is external).
+//
+// Activations are NHWC, channel-sliced: every tensor is (pointer to its first channel, channel
+// stride of the buffer it lives in), so C2f's chunk/cat, SPPF's cat and the FPN/PAN concats are
+// zero-copy -- producers write straight into their slice of the consumer's input buffer.
+//
+//   seg_preprocess_kernel   uint8 BGR HWC -> RGB/255 NHWC, channels padded to 8 (LetterBox is the
+//                           identity for a frame that already has the network's input size)
+//   conv_kernel<T, WM, WN>  implicit-GEMM Conv2d (+ folded BN bias, SiLU, residual add) on MFMA:
+//                           bf16 -> v_mfma_f32_16x16x32_bf16, f32 (parity mode) -> v_mfma_f32_16x16x4_f32
+//                           (exact f32 fma chain).  D[cout][pixel] = W[cout][k] * im2col[k][pixel]:
+//                           weights are the MFMA A operand so each lane's accumulator holds 4
+//                           consecutive output channels of one pixel (8/16-byte NHWC stores).
+//                           mode 1 = ConvTranspose2d(k2, s2) as a 1x1 GEMM with 4*C outputs whose
+//                           epilogue scatters the 2x2 sub-pixels (Proto.upsample).
+//   sppf_pool_kernel<T>     SPPF's three chained MaxPool2d(5,1,2) as one pass: 5x5, 9x9, 13x13 maxima
+//   upsample2x_kernel<T>    nearest x2 into a concat slice
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/va355.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace {
+
+__device__ inline float to_f(float v) { return v; }
+__device__ inline float to_f(__bf16 v) { return (float)v; }
+template <typename T>
+__device__ inline T from_f(float v);
+template <>
+__device__ inline float from_f<float>(float v) {
+    return v;
+}
+template <>
+__device__ inline __bf16 from_f<__bf16>(float v) {
+    return (__bf16)v;
+}
+
+__device__ inline float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ inline float silu_exact(float x) { return x / (1.0f + expf(-x)); }
+
+// ----------------------------------------------------------------------------------------- preprocess
+template <typename T>
+__global__ void seg_preprocess_kernel(const uint8_t* __restrict__ frames, int64_t npix, T* __restrict__ out) {
+    // frames: [npix][3] BGR; out: [npix][8] (R, G, B, 0, 0, 0, 0, 0) / 255
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t* p = frames + 3 * i;
+        float b = p[0], g = p[1], r = p[2];
+        T* o = out + 8 * i;
+        o[0] = from_f<T>(r / 255.0f);
+        o[1] = from_f<T>(g / 255.0f);
+        o[2] = from_f<T>(b / 255.0f);
+#pragma unroll
+        for (int c = 3; c < 8; ++c) o[c] = from_f<T>(0.0f);
+    }
+}
+
+// ----------------------------------------------------------------------------------------- conv
+constexpr int BK = 32;
+
+template <typename T, int WM, int WN>
+struct ConvCfg {
+    static constexpr int NT = 64 * WM * WN;           // threads
+    static constexpr int BM = 64 * WM;                // pixels per tile
+    static constexpr int BN = 64 * WN;                // output channels per tile
+    static constexpr int VEC = 16 / sizeof(T);        // elements per 16-byte chunk
+    static constexpr int CPR = BK / VEC;              // chunks per tile row
+    static constexpr int LDSW = BK + VEC;             // padded LDS row (elements)
+    static constexpr int A_CH = BN * CPR / NT;        // weight chunks per thread
+    static constexpr int B_CH = BM * CPR / NT;        // pixel chunks per thread
+    static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for the block");
+};
+
+template <typename T, int WM, int WN, typename OutT>
+__global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
+    using Cfg = ConvCfg<T, WM, WN>;
+    constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, VEC = Cfg::VEC, CPR = Cfg::CPR, LDSW = Cfg::LDSW;
+    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH;
+    __shared__ __align__(16) T As[BN * LDSW];
+    __shared__ __align__(16) T Bs[BM * LDSW];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const T* __restrict__ X = (const T*)a.x;
+    const T* __restrict__ Wt = (const T*)a.w;
+
+    // fixed per-thread k-group and rows
+    const int g = tid % CPR;
+    int b_row[B_CH], b_hi[B_CH], b_wi[B_CH];
+    int64_t b_base[B_CH];
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+        int r = tid / CPR + (NT / CPR) * i;
+        int m = m0 + r;
+        b_row[i] = r;
+        if (m < a.M) {
+            int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi[i] = ho * a.stride - a.pad;
+            b_wi[i] = wo * a.stride - a.pad;
+            b_base[i] = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi[i] = -(1 << 28);  // never in bounds
+            b_wi[i] = 0;
+            b_base[i] = 0;
+        }
+    }
+    const int a_row0 = tid / CPR;
+
+    uint4 ra[A_CH], rb[B_CH];
+    auto load_tile = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+            int r = a_row0 + (NT / CPR) * i;
+            ra[i] = *(const uint4*)(Wt + (int64_t)(n0 + r) * a.Kpad + k0 + g * VEC);
+        }
+        int k = k0 + g * VEC;
+        int tap = k / a.Cin, ci = k - tap * a.Cin;
+        int ky = tap / a.kw, kx = tap - ky * a.kw;
+        bool kin = k < a.K;
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) {
+            int hi = b_hi[i] + ky, wi = b_wi[i] + kx;
+            if (kin && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
+                rb[i] = *(const uint4*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci);
+            else
+                rb[i] = make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+            int r = a_row0 + (NT / CPR) * i;
+            *(uint4*)(As + r * LDSW + g * VEC) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) *(uint4*)(Bs + b_row[i] * LDSW + g * VEC) = rb[i];
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int k0 = 0; k0 < a.Kpad; k0 += BK) {
+        const bool more = k0 + BK < a.Kpad;
+        if (more) load_tile(k0 + BK);
+        if constexpr (sizeof(T) == 2) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(As + (wn * 64 + 16 * i + fr) * LDSW + 8 * fq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(Bs + (wm * 64 + 16 * j + fr) * LDSW + 8 * fq);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < BK / 4; ++kk) {
+                float af[4], bfr[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = As[(wn * 64 + 16 * i + fr) * LDSW + 4 * kk + fq];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) bfr[j] = Bs[(wm * 64 + 16 * j + fr) * LDSW + 4 * kk + fq];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+        if (more) {
+            store_tile();
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: bias (+SiLU) (+residual), 4 consecutive channels per lane
+    OutT* Y = (OutT*)a.y;
+    const T* R = (const T*)a.res;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + 16 * j + fr;
+        if (m >= a.M) continue;
+        int64_t obase;
+        int wo = 0, ho = 0, n = 0;
+        if (a.mode == 1) {
+            wo = m % a.Wo;
+            int t = m / a.Wo;
+            ho = t % a.Ho;
+            n = t / a.Ho;
+            obase = 0;
+        } else {
+            obase = (int64_t)m * a.ldy;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = n0 + wn * 64 + 16 * i + 4 * fq;
+            if (co >= a.Cout) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float x = acc[i][j][r] + a.bias[co + r];
+                if (a.act) x = sizeof(T) == 2 ? silu(x) : silu_exact(x);
+                v[r] = x;
+            }
+            if (R) {
+                const T* rp = R + (int64_t)m * a.ldr + co;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += to_f(rp[r]);
+            }
+            OutT* yp;
+            if (a.mode == 1) {
+                const int cd = a.Cout / 4;
+                const int q = co / cd, c = co - q * cd;
+                const int oy = 2 * ho + (q >> 1), ox = 2 * wo + (q & 1);
+                yp = Y + (((int64_t)n * 2 * a.Ho + oy) * 2 * a.Wo + ox) * a.ldy + c;
+            } else {
+                yp = Y + obase + co;
+            }
+            if (co + 3 < a.Cout) {
+                if constexpr (sizeof(OutT) == 2) {
+                    __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                    *(uint2*)yp = *(uint2*)o4;
+                } else {
+                    *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+                }
+            } else {
+                for (int r = 0; r < 4 && co + r < a.Cout; ++r) yp[r] = from_f<OutT>(v[r]);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------- SPPF pool
+// in: slice 0 of buf (c channels), writes slices 1..3: max over 5x5, 9x9, 13x13 windows (== MaxPool2d(5,1,2)
+// applied 1, 2, 3 times: -inf padding makes the chained pools windowed maxima).
+template <typename T>
+__global__ void sppf_pool_kernel(T* buf, int N, int H, int W, int c, int ld) {
+    int64_t total = (int64_t)N * H * W * c;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int ch = (int)(i % c);
+        int64_t p = i / c;
+        int w = (int)(p % W), h = (int)((p / W) % H), n = (int)(p / ((int64_t)W * H));
+        float m5 = -INFINITY, m9 = -INFINITY, m13 = -INFINITY;
+        for (int dy = -6; dy <= 6; ++dy) {
+            int y = h + dy;
+            if (y < 0 || y >= H) continue;
+            for (int dx = -6; dx <= 6; ++dx) {
+                int x = w + dx;
+                if (x < 0 || x >= W) continue;
+                float v = to_f(buf[(((int64_t)n * H + y) * W + x) * ld + ch]);
+                m13 = fmaxf(m13, v);
+                if (abs(dy) <= 4 && abs(dx) <= 4) m9 = fmaxf(m9, v);
+                if (abs(dy) <= 2 && abs(dx) <= 2) m5 = fmaxf(m5, v);
+            }
+        }
+        T* o = buf + p * ld;
+        o[c + ch] = from_f<T>(m5);
+        o[2 * c + ch] = from_f<T>(m9);
+        o[3 * c + ch] = from_f<T>(m13);
+    }
+}
+
+// nearest x2: src [N,H,W] slice (c channels, ld_s) -> dst [N,2H,2W] slice (ld_d), 16-byte chunks
+template <typename T>
+__global__ void upsample2x_kernel(const T* src, int ld_s, T* dst, int ld_d, int N, int H, int W, int c) {
+    constexpr int VEC = 16 / sizeof(T);
+    int cv = c / VEC;
+    int64_t total = (int64_t)N * 2 * H * 2 * W * cv;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int ch = (int)(i % cv) * VEC;
+        int64_t p = i / cv;
+        int x = (int)(p % (2 * W)), y = (int)((p / (2 * W)) % (2 * H)), n = (int)(p / ((int64_t)4 * W * H));
+        const T* s = src + (((int64_t)n * H + y / 2) * W + x / 2) * ld_s + ch;
+        *(uint4*)(dst + p * ld_d + ch) = *(const uint4*)s;
+    }
+}
+
+int grid_for(int64_t n, int threads) {
+    int64_t b = (n + threads - 1) / threads;
+    return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+}
+
+template <typename T, int WM, int WN, typename OutT>
+hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
+    using Cfg = ConvCfg<T, WM, WN>;
+    dim3 grid((a.M + Cfg::BM - 1) / Cfg::BM, (a.Cout + Cfg::BN - 1) / Cfg::BN);
+    hipLaunchKernelGGL((conv_kernel<T, WM, WN, OutT>), grid, dim3(Cfg::NT), 0, st, a);
+    return hipGetLastError();
+}
+
+template <typename T, typename OutT>
+hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
+    // tile choice: small Cout -> tall pixel tiles
+    if (a.Cout <= 64) return launch_conv<T, 4, 1, OutT>(a, st);
+    return launch_conv<T, 2, 2, OutT>(a, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int va_seg_conv(void* stream, const va_conv_args* a) {
+    if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
+    const int vec = a->dtype == VA_DTYPE_BF16 ? 8 : 4;
+    if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
+    if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e;
+    if (a->dtype == VA_DTYPE_BF16)
+        e = a->out_f32 ? dispatch_conv<__bf16, float>(*a, st) : dispatch_conv<__bf16, __bf16>(*a, st);
+    else if (a->dtype == VA_DTYPE_F32)
+        e = dispatch_conv<float, float>(*a, st);
+    else
+        return VA_ERR_ARG;
+    return e == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H, int32_t W, int32_t dtype,
+                      void* out) {
+    if (!frames || !out || B <= 0 || H <= 0 || W <= 0) return VA_ERR_ARG;
+    int64_t npix = (int64_t)B * H * W;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == VA_DTYPE_BF16)
+        hipLaunchKernelGGL(seg_preprocess_kernel<__bf16>, dim3(grid_for(npix, 256)), dim3(256), 0, st, frames, npix,
+                           (__bf16*)out);
+    else if (dtype == VA_DTYPE_F32)
+        hipLaunchKernelGGL(seg_preprocess_kernel<float>, dim3(grid_for(npix, 256)), dim3(256), 0, st, frames, npix,
+                           (float*)out);
+    else
+        return VA_ERR_ARG;
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld,
+                     int32_t dtype) {
+    if (!buf || N <= 0 || c <= 0 || ld < 4 * c) return VA_ERR_ARG;
+    int64_t total = (int64_t)N * H * W * c;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == VA_DTYPE_BF16)
+        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(grid_for(total, 256)), dim3(256), 0, st, (__bf16*)buf, N, H,
+                           W, c, ld);
+    else
+        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(grid_for(total, 256)), dim3(256), 0, st, (float*)buf, N, H, W,
+                           c, ld);
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, int32_t ld_d, int32_t N, int32_t H,
+                      int32_t W, int32_t c, int32_t dtype) {
+    const int vec = dtype == VA_DTYPE_BF16 ? 8 : 4;
+    if (!src || !dst || c % vec || ld_s % vec || ld_d % vec) return VA_ERR_ARG;
+    int64_t total = (int64_t)N * 4 * H * W * (c / vec);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == VA_DTYPE_BF16)
+        hipLaunchKernelGGL(upsample2x_kernel<__bf16>, dim3(grid_for(total, 256)), dim3(256), 0, st,
+                           (const __bf16*)src, ld_s, (__bf16*)dst, ld_d, N, H, W, c);
+    else
+        hipLaunchKernelGGL(upsample2x_kernel<float>, dim3(grid_for(total, 256)), dim3(256), 0, st, (const float*)src,
+                           ld_s, (float*)dst, ld_d, N, H, W, c);
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
+    if (!ops || n < 0) return VA_ERR_ARG;
+    for (int i = 0; i < n; ++i) {
+        const va_conv_args& a = ops[i].a;
+        int rc;
+        switch (ops[i].kind) {
+            case VA_OP_CONV:
+                rc = va_seg_conv(stream, &a);
+                break;
+            case VA_OP_SPPF:
+                rc = va_seg_sppf_pool(stream, a.y, a.N, a.H, a.W, a.Cin, a.ldy, a.dtype);
+                break;
+            case VA_OP_UPSAMPLE:
+                rc = va_seg_upsample2x(stream, a.x, a.ldx, a.y, a.ldy, a.N, a.H, a.W, a.Cin, a.dtype);
+                break;
+            case VA_OP_PREPROCESS:
+                rc = va_seg_preprocess(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.dtype, a.y);
+                break;
+            default:
+                rc = VA_ERR_ARG;
+        }
+        if (rc != VA_OK) return rc - 1000 * (i + 1);  // encode the failing op index
+    }
+    return VA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,300 @@
+"""YOLOv8-seg on MI355X: weight packing, buffer planning and the forward op list.
+
+``SegNet(arch, folded, dtype)`` packs the folded Conv weights once (K ordered
+(ky, kx, ci), zero padded to the MFMA tile), and ``plan(B, H, W)`` lays out
+every activation of a forward as NHWC channel slices of a few buffers so that
+C2f chunk/cat, SPPF cat and the FPN/PAN concats are free, then emits the list
+of ops (``va_seg_op``) that ``va_seg_run`` executes in ONE C call.
+
+Output of a forward (``SegOutputs``): per pyramid level a float32 NHWC buffer
+[B, h, w, 64 + nc + 32] = (DFL box logits, class logits, mask coefficients) --
+the tensors Ultralytics' Segment head concatenates before decoding -- and the
+proto masks float32 [B, H/4, W/4, 32].
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .seg_arch import NM, REG_MAX, Arch
+
+VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
+VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS = 1, 2, 3, 4
+BK = 32
+NPAD = 128
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("N", ctypes.c_int32), ("H", ctypes.c_int32), ("W", ctypes.c_int32), ("Cin", ctypes.c_int32),
+        ("ldx", ctypes.c_int32),
+        ("kh", ctypes.c_int32), ("kw", ctypes.c_int32), ("stride", ctypes.c_int32), ("pad", ctypes.c_int32),
+        ("Ho", ctypes.c_int32), ("Wo", ctypes.c_int32),
+        ("w", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("Cout", ctypes.c_int32), ("Npad", ctypes.c_int32), ("K", ctypes.c_int32), ("Kpad", ctypes.c_int32),
+        ("y", ctypes.c_void_p), ("ldy", ctypes.c_int32),
+        ("res", ctypes.c_void_p), ("ldr", ctypes.c_int32),
+        ("act", ctypes.c_int32), ("mode", ctypes.c_int32), ("M", ctypes.c_int32), ("dtype", ctypes.c_int32),
+        ("out_f32", ctypes.c_int32), ("pad_", ctypes.c_int32),
+    ]
+
+
+class SegOp(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("pad_", ctypes.c_int32), ("a", ConvArgs)]
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b * b
+
+
+@dataclass
+class Packed:
+    w: torch.Tensor
+    b: torch.Tensor
+    cin: int       # padded input channels the packed K assumes
+    cout: int
+    k: int
+    K: int
+    Kpad: int
+    Npad: int
+    deconv: bool = False
+
+
+class Slice:
+    """A channel slice of an NHWC buffer: (buffer, channel offset, channels)."""
+
+    def __init__(self, buf: torch.Tensor, off: int, c: int):
+        self.buf, self.off, self.c = buf, off, c
+
+    @property
+    def ld(self):
+        return self.buf.shape[-1]
+
+    @property
+    def ptr(self):
+        return self.buf.data_ptr() + self.off * self.buf.element_size()
+
+    def sub(self, off, c):
+        return Slice(self.buf, self.off + off, c)
+
+
+@dataclass
+class SegOutputs:
+    levels: list   # 3 x float32 [B, h, w, 64 + nc + 32]
+    proto: torch.Tensor  # float32 [B, H/4, W/4, 32]
+    strides: tuple = (8, 16, 32)
+
+
+class SegNet:
+    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None):
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.arch = arch
+        self.dtype = dtype
+        self.tdtype = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.va_dtype = VA_DTYPE_BF16 if dtype == "bf16" else VA_DTYPE_F32
+        self.vec = 8 if dtype == "bf16" else 4
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.w = {}
+        for prefix, kind, ci, co, k in arch.conv_specs():
+            w, b = folded[prefix]
+            self.w[prefix] = self._pack(w, b, deconv=(kind == "deconv"))
+        # the three head branches' first 3x3 convs share their input: one GEMM per level
+        for l in range(3):
+            parts = [folded[f"model.22.{br}.{l}.0"] for br in ("cv2", "cv3", "cv4")]
+            w = torch.cat([p[0] for p in parts], 0)
+            b = torch.cat([p[1] for p in parts], 0)
+            self.w[f"head.{l}.0"] = self._pack(w, b)
+        self._plans = {}
+
+    # ------------------------------------------------------------------ packing
+    def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
+        if deconv:  # ConvTranspose2d weight [Cin, Cout, 2, 2] -> 1x1 GEMM rows q*Cout + co, q = dy*2 + dx
+            cin, cout = w.shape[0], w.shape[1]
+            wg = w.permute(2, 3, 1, 0).reshape(4 * cout, cin)  # [dy, dx, co, ci]
+            bg = b.repeat(4)
+            p = self._pack(wg.view(4 * cout, cin, 1, 1), bg)
+            p.deconv = True
+            return p
+        cout, cin, kh, kw = w.shape
+        cin_p = max(_ceil(cin, self.vec), 8) if cin < 8 else _ceil(cin, self.vec)
+        wp = torch.zeros(cout, kh, kw, cin_p, dtype=torch.float32)
+        wp[..., :cin] = w.permute(0, 2, 3, 1)
+        K = kh * kw * cin_p
+        Kpad = _ceil(K, BK)
+        Npad = _ceil(cout, NPAD)
+        wm = torch.zeros(Npad, Kpad, dtype=torch.float32)
+        wm[:cout, :K] = wp.reshape(cout, K)
+        bm = torch.zeros(Npad, dtype=torch.float32)
+        bm[:cout] = b
+        return Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
+                      Kpad, Npad)
+
+    # ------------------------------------------------------------------ planning
+    def _buf(self, B, h, w, c, dtype=None):
+        return torch.empty((B, h, w, c), dtype=dtype or self.tdtype, device=self.device)
+
+    def plan(self, B: int, H: int, W: int):
+        key = (B, H, W)
+        if key in self._plans:
+            return self._plans[key]
+        if H % 32 or W % 32:
+            raise _lib.VaError(f"frame {H}x{W}: the network needs multiples of 32 (pad/letterbox first)")
+        a = self.arch
+        ops = []
+        keep = []  # buffers referenced by the op list
+
+        def new(h, w, c, dtype=None):
+            t = self._buf(B, h, w, c, dtype)
+            keep.append(t)
+            return Slice(t, 0, c)
+
+        def conv(prefix, src: Slice, dst: Slice, h, w, stride=1, act=True, res: Slice | None = None,
+                 out_f32=False):
+            p = self.w[prefix]
+            k = p.k
+            pad = k // 2
+            ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+            if src.c != p.cin and not (src.c < p.cin and src.ld >= p.cin):
+                raise _lib.VaError(f"{prefix}: input has {src.c} channels, packed for {p.cin}")
+            args = ConvArgs(
+                x=src.ptr, N=B, H=h, W=w, Cin=p.cin, ldx=src.ld, kh=k, kw=k, stride=stride, pad=pad, Ho=ho, Wo=wo,
+                w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
+                y=dst.ptr, ldy=dst.ld, res=res.ptr if res is not None else None, ldr=res.ld if res is not None else 0,
+                act=1 if act else 0, mode=1 if p.deconv else 0, M=B * ho * wo, dtype=self.va_dtype,
+                out_f32=1 if (out_f32 and self.dtype == "bf16") else 0)
+            if dst.c != (p.cout // 4 if p.deconv else p.cout):
+                raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {p.cout}")
+            ops.append(SegOp(kind=VA_OP_CONV, a=args))
+            return ho, wo
+
+        def c2f(i, src: Slice, dst: Slice, h, w):
+            _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
+            c = co // 2
+            t = new(h, w, (2 + n) * c)
+            conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w)
+            tmp = new(h, w, c)
+            for j in range(n):
+                x_in = t.sub((1 + j) * c, c)
+                conv(f"model.{i}.m.{j}.cv1", x_in, tmp, h, w)
+                conv(f"model.{i}.m.{j}.cv2", tmp, t.sub((2 + j) * c, c), h, w, res=x_in if shortcut else None)
+            conv(f"model.{i}.cv2", t, dst, h, w)
+
+        def upsample(src: Slice, dst: Slice, h, w):
+            ops.append(SegOp(kind=VA_OP_UPSAMPLE, a=ConvArgs(x=src.ptr, ldx=src.ld, y=dst.ptr, ldy=dst.ld, N=B, H=h, W=w,
+                                                              Cin=src.c, dtype=self.va_dtype)))
+
+        frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
+        x0 = new(H, W, 8)
+        ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
+                                                            dtype=self.va_dtype)))
+        h1, w1 = H // 2, W // 2
+        h2, w2 = H // 4, W // 4
+        h3, w3 = H // 8, W // 8
+        h4, w4 = H // 16, W // 16
+        h5, w5 = H // 32, W // 32
+        a0 = new(h1, w1, a.c1)
+        conv("model.0", x0, a0, H, W, stride=2)
+        a1 = new(h2, w2, a.c2)
+        conv("model.1", a0, a1, h1, w1, stride=2)
+        p2 = new(h2, w2, a.c2)
+        c2f(2, a1, p2, h2, w2)
+        a3 = new(h3, w3, a.c3)
+        conv("model.3", p2, a3, h2, w2, stride=2)
+        cat14 = new(h3, w3, a.c4 + a.c3)          # [up(h12) | P3]
+        P3 = cat14.sub(a.c4, a.c3)
+        c2f(4, a3, P3, h3, w3)
+        a5 = new(h4, w4, a.c4)
+        conv("model.5", P3, a5, h3, w3, stride=2)
+        cat11 = new(h4, w4, a.c5 + a.c4)          # [up(P5) | P4]
+        P4 = cat11.sub(a.c5, a.c4)
+        c2f(6, a5, P4, h4, w4)
+        a7 = new(h5, w5, a.c5)
+        conv("model.7", P4, a7, h4, w4, stride=2)
+        b8 = new(h5, w5, a.c5)
+        c2f(8, a7, b8, h5, w5)
+        cs = a.c5 // 2
+        sp = new(h5, w5, 4 * cs)
+        conv("model.9.cv1", b8, sp.sub(0, cs), h5, w5)
+        ops.append(SegOp(kind=VA_OP_SPPF, a=ConvArgs(y=sp.ptr, N=B, H=h5, W=w5, Cin=cs, ldy=sp.ld, dtype=self.va_dtype)))
+        cat20 = new(h5, w5, a.c4 + a.c5)          # [conv19(o4) | P5]
+        P5 = cat20.sub(a.c4, a.c5)
+        conv("model.9.cv2", sp, P5, h5, w5)
+        upsample(P5, cat11.sub(0, a.c5), h5, w5)
+        cat17 = new(h4, w4, a.c3 + a.c4)          # [conv16(o3) | h12]
+        h12 = cat17.sub(a.c3, a.c4)
+        c2f(12, cat11, h12, h4, w4)
+        upsample(h12, cat14.sub(0, a.c4), h4, w4)
+        o3 = new(h3, w3, a.c3)
+        c2f(15, cat14, o3, h3, w3)
+        conv("model.16", o3, cat17.sub(0, a.c3), h3, w3, stride=2)
+        o4 = new(h4, w4, a.c4)
+        c2f(18, cat17, o4, h4, w4)
+        conv("model.19", o4, cat20.sub(0, a.c4), h4, w4, stride=2)
+        o5 = new(h5, w5, a.c5)
+        c2f(21, cat20, o5, h5, w5)
+        # Segment head: per level [box 64 | cls nc | coef 32] float32
+        cb, cc, cm = a.head_c2, a.head_c3, a.head_c4
+        no = 4 * REG_MAX + a.nc + NM
+        levels = []
+        for l, (src, hh, ww) in enumerate(((o3, h3, w3), (o4, h4, w4), (o5, h5, w5))):
+            hb = new(hh, ww, cb + cc + cm)
+            conv(f"head.{l}.0", src, hb, hh, ww)
+            hb2 = new(hh, ww, cb + cc + cm)
+            out = new(hh, ww, no, torch.float32)
+            levels.append(out.buf)
+            for br, off, cw, ooff, oc in (("cv2", 0, cb, 0, 4 * REG_MAX), ("cv3", cb, cc, 4 * REG_MAX, a.nc),
+                                           ("cv4", cb + cc, cm, 4 * REG_MAX + a.nc, NM)):
+                conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
+                conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False, out_f32=True)
+        # Proto
+        pr1 = new(h3, w3, a.npr)
+        conv("model.22.proto.cv1", o3, pr1, h3, w3)
+        pr2 = new(h2, w2, a.npr)
+        conv("model.22.proto.upsample", pr1, pr2, h3, w3, act=False)
+        pr3 = new(h2, w2, a.npr)
+        conv("model.22.proto.cv2", pr2, pr3, h2, w2)
+        proto = new(h2, w2, NM, torch.float32)
+        conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
+        op_arr = (SegOp * len(ops))(*ops)
+        plan = {"ops": op_arr, "n": len(ops), "keep": keep, "frames": frames,
+                "out": SegOutputs(levels=levels, proto=proto.buf)}
+        self._plans[key] = plan
+        return plan
+
+    def forward(self, frames_u8: torch.Tensor, stream=None) -> SegOutputs:
+        """frames_u8: uint8 [B, H, W, 3] BGR on the device."""
+        B, H, W, _ = frames_u8.shape
+        p = self.plan(B, H, W)
+        p["frames"].copy_(frames_u8, non_blocking=True)
+        self.run_plan(p, stream)
+        return p["out"]
+
+    def run_plan(self, p, stream=None) -> None:
+        _lib.check(self.lib.va_seg_run(_lib.stream_ptr(stream), p["ops"], p["n"]), "va_seg_run")
+
+    def gflop_per_frame(self, H: int, W: int) -> float:
+        """Algorithmic FLOPs (2 x MACs of every conv, unpadded) per frame."""
+        total = 0
+        for prefix, kind, ci, co, k in self.arch.conv_specs():
+            total += 2 * ci * co * k * k * _spatial(prefix, H, W)
+        return total / 1e9
+
+
+def _spatial(prefix: str, H: int, W: int) -> int:
+    """Output pixels of the module `prefix` for an H x W input."""
+    parts = prefix.split(".")
+    i = int(parts[1])
+    if i == 22:
+        if parts[2] == "proto":  # cv1 and the deconv GEMM run at stride 8, cv2/cv3 at stride 4
+            return (H // 8) * (W // 8) if parts[3] in ("cv1", "upsample") else (H // 4) * (W // 4)
+        l = int(parts[3])
+        s = (8, 16, 32)[l]
+        return (H // s) * (W // s)
+    stride = {0: 2, 1: 4, 2: 4, 3: 8, 4: 8, 5: 16, 6: 16, 7: 32, 8: 32, 9: 32, 12: 16, 15: 8, 16: 16, 18: 16,
+              19: 32, 21: 32}[i]
+    return (H // stride) * (W // stride)
