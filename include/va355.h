@@ -205,6 +205,46 @@ typedef struct va_seg_op {
 
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n);
 
+/* ---------------------------------------------------------------- segmentation post-processing */
+typedef struct va_cand { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_cand;  /* NMS candidate */
+typedef struct va_det { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_det;    /* kept detection */
+typedef struct va_mask_stat { int32_t count, x0, y0, x1, y1, pad[3]; } va_mask_stat;        /* mask pixels, bbox */
+
+/* Everything YOLO.predict does after the forward, for B frames, plus the mask choice of
+ * FrameProcessor.py:67-97 (restated, parity unpinned: OpenCV is absent):
+ *   decode (DFL, dist2bbox, sigmoid) -> conf filter -> class-offset greedy NMS (IoU > iou) -> max_det
+ *   -> process_mask (coef . proto, crop, bilinear x4, > 0) -> per-instance pixel count / bbox
+ *   -> (if cells != NULL) the instance with the most pixels, sampled at the 20-px cell centres, and
+ *      its pixel bbox as the boundingRect -> the (cells, rects) input of va_nav_run.
+ * plant_mode: 0 = never plant; 1 = use plant_cells/plant_rects for frames with no mask; 2 = always. */
+typedef struct va_post_args {
+    const float* levels[3];     /* float [B][H/s][W/s][64 + nc + 32], s = 8, 16, 32 */
+    const float* proto;         /* float [B][H/4][W/4][32] */
+    int32_t B, H, W, nc;
+    float conf, iou;            /* 0.5 (FrameProcessor.py:322), 0.7 (Ultralytics default) */
+    int32_t max_det;            /* 300 */
+    int32_t plant_mode;
+    va_cand* cand;              /* scratch [B][A] */
+    int32_t* cand_count;        /* scratch [B] */
+    unsigned long long* keys;   /* scratch [B][A] */
+    va_det* dets;               /* out [B][max_det] */
+    int32_t* ndet;              /* out [B] */
+    va_mask_stat* stats;        /* out [B][max_det] */
+    const uint8_t* plant_cells; /* [B][H/20][W/20] or NULL */
+    const int32_t* plant_rects; /* [B][4] or NULL */
+    uint8_t* cells;             /* out [B][H/20][W/20] or NULL (skip the mask choice) */
+    int32_t* rects;             /* out [B][4] */
+    int32_t* chosen;            /* out [B]: chosen detection, -1 none, -2 planted */
+} va_post_args;
+
+/* Number of anchors A for an H x W input (strides 8, 16, 32), or < 0. */
+int va_post_anchors(int32_t H, int32_t W);
+int va_post_run(void* stream, const va_post_args* p);
+
+/* ABI self-check: writes sizeof() of va_nav_dims, va_frame_hdr, va_query_hdr, va_conv_args, va_seg_op,
+ * va_cand, va_det, va_mask_stat, va_post_args (in that order) into out[0..n-1]; returns how many. */
+int va_abi_struct_sizes(int64_t* out, int32_t n);
+
 /* Library version / build info string. */
 const char* va_version(void);
 

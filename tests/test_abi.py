@@ -61,3 +61,19 @@ def test_angle_table_header_matches_reference():
         assert float.fromhex(deg.strip()).hex() == gdeg
         want = 0.0 if gpen.startswith("i") else float.fromhex(gpen)
         assert float.fromhex(pen.strip()) == want
+
+
+def test_struct_layouts_match_python_mirrors():
+    """Every ctypes / numpy mirror of a va355.h struct has the C sizeof."""
+    import numpy as np
+    from vision_assist_amd import _lib
+    from vision_assist_amd.nav import FRAME_HDR, QUERY_HDR
+    from vision_assist_amd.post import PostArgs
+    from vision_assist_amd.seg import ConvArgs, SegOp
+    lib = _lib.load()
+    out = (ctypes.c_int64 * 9)()
+    assert lib.va_abi_struct_sizes(out, 9) == 9
+    want = [ctypes.sizeof(_lib.VaNavDims), FRAME_HDR.itemsize, QUERY_HDR.itemsize, ctypes.sizeof(ConvArgs),
+            ctypes.sizeof(SegOp), 32, 32, 32, ctypes.sizeof(PostArgs)]
+    assert list(out) == want
+    del np

@@ -1,0 +1,99 @@
+"""GPU post-processing (va_post_run) vs the oracle (oracle/yolo_ref.py) on the SAME head outputs.
+
+The GPU forward runs in exact-f32 mode and its own head tensors are handed to
+the oracle's decode / NMS / process_mask / mask choice, so the comparison
+isolates the post-processing kernels:
+  * kept detections: same count, classes and order; boxes within 1e-3 px, scores within 1e-6;
+  * per-instance mask pixel counts within 0.05 % (sign of bilinear values that are zero to
+    float32 rounding may differ between summation orders);
+  * chosen instance, its boundingRect and the 20-px cell samples.
+Regimes: natural (Ultralytics prior cls bias: no detections with these weights),
+mid (cls bias 0) and dense (cls bias +4: 300 detections survive NMS).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import yolo_ref as Y
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(cls_bias, B=2, H=640, W=640, seed=0):
+    from vision_assist_amd.post import PostEngine
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("s")
+    fw = fold(arch, synthetic_state_dict(arch, seed=seed, cls_bias=cls_bias))
+    net = SegNet(arch, fw, dtype="f32")
+    frames = torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(seed + 11),
+                           dtype=torch.uint8)
+    out = net.forward(frames.cuda())
+    post = PostEngine(B, H, W, arch.nc)
+    post.run(out.levels, out.proto)
+    torch.cuda.synchronize()
+    lv = torch.cat([t.cpu().flatten(1, 2) for t in out.levels], 1).permute(0, 2, 1)
+    nc = arch.nc
+    box, cls, coef = lv[:, :64], lv[:, 64:64 + nc], lv[:, 64 + nc:]
+    proto = out.proto.cpu().permute(0, 3, 1, 2)
+    return post, box, cls, coef, proto
+
+
+@pytest.mark.parametrize("regime,cls_bias", [("natural", None), ("mid", 0.0), ("dense", 4.0)])
+def test_post_matches_oracle(regime, cls_bias):
+    H = W = 640
+    post, box, cls, coef, proto = _setup(cls_bias)
+    pred = Y.decode(box, cls, H, W)
+    for b in range(box.shape[0]):
+        det_ref = Y.nms_image(pred[b], coef[b])
+        det_gpu, _anchors = post.det_tensor(b)
+        assert det_gpu.shape[0] == det_ref.shape[0], (regime, b)
+        if regime == "dense":
+            assert det_ref.shape[0] == 300
+        if not det_ref.shape[0]:
+            continue
+        assert torch.equal(det_gpu[:, 5], det_ref[:, 5]), "classes / order differ"
+        assert torch.allclose(det_gpu[:, :4], det_ref[:, :4], atol=1e-3, rtol=0), (det_gpu[:, :4] - det_ref[:, :4]).abs().max()
+        assert torch.allclose(det_gpu[:, 4], det_ref[:, 4], atol=1e-6, rtol=0)
+        masks = Y.process_mask(proto[b], det_ref[:, 6:], det_ref[:, :4], H, W)
+        cnt_ref = masks.flatten(1).sum(1).long()
+        st = post.stats[b, :det_ref.shape[0]].cpu()
+        cnt_gpu = st[:, 0].long()
+        tol = torch.clamp((cnt_ref.float() * 5e-4).long(), min=2)
+        assert ((cnt_gpu - cnt_ref).abs() <= tol).all(), (cnt_gpu - cnt_ref).abs().max()
+        m, rect = Y.select_mask(masks)
+        chosen = int(post.chosen[b])
+        if m is None:
+            assert chosen < 0
+            continue
+        k_ref = int(torch.argmax(cnt_ref))
+        assert chosen == k_ref
+        got_rect = tuple(int(v) for v in post.rects[b].cpu())
+        assert max(abs(g - r) for g, r in zip(got_rect, rect)) <= 1, (got_rect, rect)
+        cells_ref = m[10::20, 10::20].numpy()
+        cells_gpu = post.cells[b].cpu().numpy()
+        assert (cells_ref != cells_gpu).sum() <= 1
+
+
+def test_pipeline_planted_nav_matches_oracle():
+    """Full fused batch (seg + post + nav) with planted corridor masks: the nav outputs are the
+    oracle's on the same masks."""
+    from oracle import nav as onav
+    from oracle.corridors import cells_rect, cells_to_mask, corridor_cells
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("s")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0))
+    B = 8
+    pipe = FramePipeline(arch, fw, B, 640, 640, dtype="bf16")
+    grids = [corridor_cells(300 + i) for i in range(B)]
+    pc = torch.tensor(np.stack(grids).astype(np.uint8)).cuda()
+    pr = torch.tensor(np.array([cells_rect(g) for g in grids], dtype=np.int32)).cuda()
+    frames = torch.randint(0, 256, (B, 640, 640, 3), dtype=torch.uint8).cuda()
+    res = pipe.run(frames, pc, pr, PLANT_ALWAYS)
+    pf = onav.PathFinderOracle()
+    for i, g in enumerate(grids):
+        out = onav.frame_nav(cells_to_mask(g), cells_rect(g), 640, 640, pf)
+        nf = res.frame(i)
+        assert [q["path"] for q in nf.queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]

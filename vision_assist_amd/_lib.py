@@ -50,6 +50,14 @@ SIGNATURES = [
     ("va_nav_query_bytes", I64, [I32]),
     ("va_astar_workspace_bytes", I64, [I32, I32]),
     ("va_astar_run", I32, [P, P, P, I32, I32, P, P, I32, P, P, ctypes.POINTER(I32)]),
+    ("va_seg_conv", I32, [P, P]),
+    ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
+    ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),
+    ("va_seg_upsample2x", I32, [P, P, I32, P, I32, I32, I32, I32, I32, I32]),
+    ("va_seg_run", I32, [P, P, I32]),
+    ("va_post_anchors", I32, [I32, I32]),
+    ("va_post_run", I32, [P, P]),
+    ("va_abi_struct_sizes", I32, [P, I32]),
     ("va_version", ctypes.c_char_p, []),
 ]
 

@@ -1019,6 +1019,16 @@ int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen
     return astar_rounds(st, aa, ctrl, seen, rounds);
 }
 
+int va_abi_struct_sizes(int64_t* out, int32_t n) {
+    const int64_t sz[] = {(int64_t)sizeof(va_nav_dims), (int64_t)sizeof(va_frame_hdr), (int64_t)sizeof(va_query_hdr),
+                          (int64_t)sizeof(va_conv_args), (int64_t)sizeof(va_seg_op),    (int64_t)sizeof(va_cand),
+                          (int64_t)sizeof(va_det),       (int64_t)sizeof(va_mask_stat), (int64_t)sizeof(va_post_args)};
+    int k = (int)(sizeof sz / sizeof sz[0]);
+    if (!out) return k;
+    for (int i = 0; i < n && i < k; ++i) out[i] = sz[i];
+    return k < n ? k : n;
+}
+
 const char* va_version(void) { return "libva355 0.1 gfx950 (" __DATE__ ")"; }
 
 }  // extern "C"
