@@ -1,0 +1,251 @@
+#!/usr/bin/env python
+"""bench.py -- frames/s end-to-end (seg + mask + grid + penalty + protrusion + A*) at 640x640 on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): YOLOv8s-seg, 640x640 frames, bf16 MFMA,
+post-processing, grid/penalty/protrusion/A* on the GPU.  One step = one pass of
+the fused hot path (vision_assist_amd.pipeline.FramePipeline) over one batch of
+--batch synthetic frames per GPU (uint8 BGR, resident in HBM before the timed
+region; random-init weights of the yolov8s-seg architecture -- no checkpoints
+exist offline).  Navigation runs on the network's mask when it yields one and on
+a planted mask otherwise (13 reference fixtures resampled to 640x640 + seeded
+procedural corridors); with the default "natural" regime the
+synthetic network yields none, so A* always runs on realistic masks.
+
+Multi-GPU: one process per GPU (torch.distributed.run), frames sharded, no
+collective on the data path; barrier + max-over-ranks timing only.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak, MI355X_MICROARCH.md chip table
+F32_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64, help="frames per step per GPU")
+    p.add_argument("--scale", default="s")
+    p.add_argument("--res", type=int, default=640)
+    p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--cpu-sample", type=int, default=160, help="frames timed for the CPU baseline (0 = skip)")
+    p.add_argument("--no-prof", action="store_true", help="skip the live per-op HIP-event timing")
+    return p.parse_args()
+
+
+def planted_pool(n: int, res: int, seed: int):
+    """Planted navigation masks: the reference's 13 fixtures (from the committed goldens) resampled to
+    the frame + seeded procedural corridors."""
+    from workloads.corridors import cells_rect, corridor_cells, fixture_640
+    R = C = res // 20
+    grids = []
+    path = os.path.join(REPO, "tests", "golden", "nav_goldens.json.gz")
+    if res == 640 and os.path.exists(path):
+        with gzip.open(path, "rt") as f:
+            fx = json.load(f)["fixtures"]
+        for name in sorted(fx):
+            g = np.array([[ch == "1" for ch in row] for row in fx[name]], dtype=bool)
+            grids.append(fixture_640(g))
+    i = 0
+    while len(grids) < n:
+        grids.append(corridor_cells(seed * 7919 + i, R, C))
+        i += 1
+    grids = grids[:n]
+    rng = np.random.default_rng(seed)
+    rng.shuffle(grids)
+    cells = np.stack(grids).astype(np.uint8)
+    rects = np.array([cells_rect(g) for g in grids], dtype=np.int32)
+    return cells, rects
+
+
+def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res: int):
+    """The oracle (torch fp32 CPU YOLOv8-seg + post-processing, pure-python grid/A* restatement with the
+    reference's algorithmic structure) on a bounded sample of the same workload."""
+    from oracle import nav as onav
+    from oracle import yolo_ref as Y
+    from workloads.corridors import cells_to_mask
+    pf = onav.PathFinderOracle()
+    n = frames_u8.shape[0]
+    t0 = time.perf_counter()
+    for i in range(n):
+        with torch.no_grad():
+            out = Y.predict(arch, fw, torch.from_numpy(frames_u8[i:i + 1]))
+        det, masks = out[0]
+        m, rect = Y.select_mask(masks)
+        if m is None:  # planted, as on the GPU
+            m = cells_to_mask(plant_cells[i].astype(bool))
+            rect = tuple(int(v) for v in plant_rects[i])
+        else:
+            m = m.numpy()
+        onav.frame_nav(m, rect, res, res, pf)
+    dt = time.perf_counter() - t0
+    return n / dt, dt
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from vision_assist_amd import _lib
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_IF_NONE
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+
+    cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0}[args.regime]
+    arch = Arch(args.scale)
+    fw = fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=cls_bias))
+    B, H, W = args.batch, args.res, args.res
+    pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
+
+    # resident inputs: P batches of frames + planted masks, distinct per rank
+    P = 4
+    frames, pcs, prs = [], [], []
+    for j in range(P):
+        rng = np.random.default_rng(1000 * rank + j)
+        frames.append(torch.from_numpy(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)).to(dev))
+        c, r = planted_pool(B, args.res, 1000 * rank + j)
+        pcs.append(torch.from_numpy(c).to(dev))
+        prs.append(torch.from_numpy(r).to(dev))
+    torch.cuda.synchronize()
+
+    def step(s):
+        pipe.frames.copy_(frames[s % P], non_blocking=True)
+        return pipe.run(None, pcs[s % P], prs[s % P], PLANT_IF_NONE)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+
+    lib = _lib.load()
+    prof = not args.no_prof
+    if prof:
+        _lib.check(lib.va_prof_start(pipe.plan["n"] * args.steps + 16), "va_prof_start")
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rounds = 0
+    paths = 0
+    for s in range(args.steps):
+        res = step(s)
+        rounds += res.rounds
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    conv_ms = conv_n = None
+    if prof:
+        import ctypes
+        ms = (ctypes.c_double * 8)()
+        cnt = (ctypes.c_int64 * 8)()
+        lib.va_prof_stop(ms, cnt, 8)
+        conv_ms, conv_n = ms[1], cnt[1]
+        other_seg_ms = ms[2] + ms[3] + ms[4]
+    # results sanity (last batch): count frames with >= 1 path
+    last = res
+    for i in range(B):
+        fr = last.frame(i)
+        paths += sum(1 for q in fr.queries if q["unique"])
+
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+    gflop = pipe.seg.gflop_per_frame(H, W)
+    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    roofline = None
+    if prof and conv_n:
+        launches_per_step = conv_n / args.steps
+        flops_per_launch = gflop * 1e9 * B / launches_per_step
+        avg_launch_s = conv_ms / 1e3 / conv_n
+        achieved = flops_per_launch / avg_launch_s / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 5), "traffic": None,
+                    "kernel": "conv_kernel (all %d launches/step of the YOLOv8-seg forward)" % round(launches_per_step),
+                    "flops_per_launch": flops_per_launch, "avg_launch_us": round(avg_launch_s * 1e6, 3),
+                    "conv_ms_per_step": round(conv_ms / args.steps, 3),
+                    "other_seg_ops_ms_per_step": round(other_seg_ms / args.steps, 3)}
+        traffic_file = os.path.join(REPO, "profiles", "conv_traffic.json")
+        if os.path.exists(traffic_file):
+            with open(traffic_file) as f:
+                tr = json.load(f)
+            key = f"{args.scale}-{args.res}-b{B}-{args.dtype}"
+            if key in tr:
+                roofline["traffic"] = tr[key]["hbm_bytes_per_launch"]
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        ncpu = torch.get_num_threads()
+        nsamp = min(args.cpu_sample, P * B)
+        fr_all = torch.cat(frames).cpu().numpy()[:nsamp]
+        pc_all = torch.cat(pcs).cpu().numpy()[:nsamp]
+        pr_all = torch.cat(prs).cpu().numpy()[:nsamp]
+        fps_cpu, dt = cpu_baseline(arch, fw, fr_all, pc_all, pr_all, args.res)
+        cpu = {"value": round(fps_cpu, 3), "unit": "frames/s", "cores": ncpu, "kind": "port",
+               "sample": f"first {nsamp} frames of the resident pool (same frames/masks as the GPU run), {dt:.1f} s: torch fp32 "
+                         f"CPU yolov8{args.scale}-seg + decode/NMS/process_mask + pure-python grid/penalty/"
+                         f"protrusion/A* restatement (oracle/)"}
+
+    if rank == 0:
+        line = {
+            "metric": "frames/sec end-to-end (seg+penalty+A*) at 640×640, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded uint8 frames; random-init yolov8%s-seg weights; planted nav masks when "
+                    "the network yields none)" % args.scale,
+            "config": {"workload": f"C3: YOLOv8{args.scale}-seg {H}x{W} {args.dtype} + post-processing + grid/"
+                                   "penalty/protrusion/A* on GPU, end-to-end",
+                       "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
+                       "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",
+                       "gflop_per_frame": round(gflop, 2)},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "astar_rounds_per_step": round(rounds / args.steps, 3),
+            "unique_paths_last_batch": paths,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

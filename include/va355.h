@@ -205,6 +205,13 @@ typedef struct va_seg_op {
 
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n);
 
+/* Optional live timing of va_seg_run: while enabled every op is bracketed by a pair of HIP events on
+ * the launch stream (capacity = max ops recorded).  va_prof_stop waits for the last event and returns,
+ * per op kind (VA_OP_*, index = kind), the summed milliseconds and the launch count; returns the number
+ * of ops recorded. */
+int va_prof_start(int32_t capacity);
+int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds);
+
 /* ---------------------------------------------------------------- segmentation post-processing */
 typedef struct va_cand { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_cand;  /* NMS candidate */
 typedef struct va_det { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_det;    /* kept detection */

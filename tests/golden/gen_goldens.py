@@ -32,7 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
-from oracle.corridors import corridor_cells, cells_to_mask, cells_rect, fixture_640  # noqa: E402
+from workloads.corridors import corridor_cells, cells_to_mask, cells_rect, fixture_640  # noqa: E402
 
 FIXTURE_DIR = os.path.join(REF, "utilities", "generate_testing_grids", "examples")
 

@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from oracle import nav as onav
-from oracle.corridors import cells_rect, cells_to_mask, corridor_cells
+from workloads.corridors import cells_rect, cells_to_mask, corridor_cells
 from tests.golden_io import cells_of, load_goldens
 from tests.nav_check import bits_to_keys, compare_golden_frame, key_index, pen_value, _ptype
 

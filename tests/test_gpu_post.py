@@ -79,7 +79,7 @@ def test_pipeline_planted_nav_matches_oracle():
     """Full fused batch (seg + post + nav) with planted corridor masks: the nav outputs are the
     oracle's on the same masks."""
     from oracle import nav as onav
-    from oracle.corridors import cells_rect, cells_to_mask, corridor_cells
+    from workloads.corridors import cells_rect, cells_to_mask, corridor_cells
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_ALWAYS
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import nav
-from oracle.corridors import cells_to_mask
+from workloads.corridors import cells_to_mask
 from tests.golden_io import cells_of, load_goldens, unhex, key_tuple
 
 

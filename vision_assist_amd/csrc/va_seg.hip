@@ -288,6 +288,11 @@ __global__ void upsample2x_kernel(const T* src, int ld_s, T* dst, int ld_d, int 
     }
 }
 
+// ---- optional per-op timing of va_seg_run (HIP events on the caller's stream), see va_prof_*
+hipEvent_t* g_ev = nullptr;
+int* g_ev_kind = nullptr;
+int g_ev_cap = 0, g_ev_used = 0, g_prof_on = 0;
+
 int grid_for(int64_t n, int threads) {
     int64_t b = (n + threads - 1) / threads;
     return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -373,11 +378,52 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+int va_prof_start(int32_t capacity) {
+    if (capacity <= 0) return VA_ERR_ARG;
+    if (capacity > g_ev_cap) {
+        for (int i = 0; i < 2 * g_ev_cap; ++i) (void)hipEventDestroy(g_ev[i]);
+        delete[] g_ev;
+        delete[] g_ev_kind;
+        g_ev = new hipEvent_t[2 * capacity];
+        g_ev_kind = new int[capacity];
+        for (int i = 0; i < 2 * capacity; ++i)
+            if (hipEventCreate(&g_ev[i]) != hipSuccess) return VA_ERR_HIP;
+        g_ev_cap = capacity;
+    }
+    g_ev_used = 0;
+    g_prof_on = 1;
+    return VA_OK;
+}
+
+int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds) {
+    g_prof_on = 0;
+    if (!ms_by_kind || !n_by_kind || nkinds <= 0) return VA_ERR_ARG;
+    for (int k = 0; k < nkinds; ++k) {
+        ms_by_kind[k] = 0.0;
+        n_by_kind[k] = 0;
+    }
+    if (g_ev_used && hipEventSynchronize(g_ev[2 * g_ev_used - 1]) != hipSuccess) return VA_ERR_HIP;
+    for (int i = 0; i < g_ev_used; ++i) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, g_ev[2 * i], g_ev[2 * i + 1]) != hipSuccess) return VA_ERR_HIP;
+        int k = g_ev_kind[i];
+        if (k >= 0 && k < nkinds) {
+            ms_by_kind[k] += ms;
+            n_by_kind[k] += 1;
+        }
+    }
+    int used = g_ev_used;
+    g_ev_used = 0;
+    return used;
+}
+
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
     if (!ops || n < 0) return VA_ERR_ARG;
     for (int i = 0; i < n; ++i) {
         const va_conv_args& a = ops[i].a;
         int rc;
+        const bool prof = g_prof_on && g_ev_used < g_ev_cap;
+        if (prof && hipEventRecord(g_ev[2 * g_ev_used], (hipStream_t)stream) != hipSuccess) return VA_ERR_HIP;
         switch (ops[i].kind) {
             case VA_OP_CONV:
                 rc = va_seg_conv(stream, &a);
@@ -395,6 +441,10 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                 rc = VA_ERR_ARG;
         }
         if (rc != VA_OK) return rc - 1000 * (i + 1);  // encode the failing op index
+        if (prof) {
+            if (hipEventRecord(g_ev[2 * g_ev_used + 1], (hipStream_t)stream) != hipSuccess) return VA_ERR_HIP;
+            g_ev_kind[g_ev_used++] = ops[i].kind;
+        }
     }
     return VA_OK;
 }

@@ -1,4 +1,4 @@
-"""Seeded procedural walkable-surface masks (TEST INFRASTRUCTURE).
+"""Seeded procedural walkable-surface masks (synthetic workload, not product code).
 
 Used by the golden generator (tests/golden/gen_goldens.py), the parity tests
 and bench.py's planted-mask regime (SURVEY.md §8d "procedural corridor masks
