@@ -751,25 +751,66 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     }
 }
 
-// serial validation of one speculative round (see file header)
-__global__ void nav_validate_kernel(const int32_t* starts, const uint8_t* qwork, int64_t query_bytes, int nslots,
-                                    int slot0, uint64_t* seen, int32_t* ctrl) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    unsigned long long acc0 = seen[0], acc1 = seen[1];
-    int rerun = -1;
-    for (int q = slot0; q < nslots; ++q) {
-        if (starts[q] < 0) continue;
-        const va_query_hdr* qh = (const va_query_hdr*)(qwork + (int64_t)q * query_bytes);
-        if ((qh->miss[0] & acc0) | (qh->miss[1] & acc1)) {
-            rerun = q;
-            break;
-        }
-        acc0 |= qh->miss[0];
-        acc1 |= qh->miss[1];
+// validation of one speculative round (see file header): the first slot q >= slot0 whose
+// newly-missed keys intersect base | (misses of the slots before it).  One 1024-thread workgroup:
+// chunked exclusive OR-scan of the 128-bit miss masks in slot order.
+constexpr int VAL_THREADS = 1024;
+
+__global__ __launch_bounds__(VAL_THREADS) void nav_validate_kernel(const int32_t* starts, const uint8_t* qwork,
+                                                                   int64_t query_bytes, int nslots, int slot0,
+                                                                   uint64_t* seen, int32_t* ctrl) {
+    __shared__ unsigned long long s0[VAL_THREADS], s1[VAL_THREADS];
+    __shared__ int first;
+    __shared__ unsigned long long acc0, acc1;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        first = INT32_MAX;
+        acc0 = seen[0];
+        acc1 = seen[1];
     }
-    seen[0] = acc0;
-    seen[1] = acc1;
-    ctrl[0] = rerun;
+    __syncthreads();
+    for (int base = slot0; base < nslots; base += VAL_THREADS) {
+        const int q = base + tid;
+        unsigned long long m0 = 0, m1 = 0;
+        if (q < nslots && starts[q] >= 0) {
+            const va_query_hdr* qh = (const va_query_hdr*)(qwork + (int64_t)q * query_bytes);
+            m0 = qh->miss[0];
+            m1 = qh->miss[1];
+        }
+        s0[tid] = m0;
+        s1[tid] = m1;
+        __syncthreads();
+        for (int off = 1; off < VAL_THREADS; off <<= 1) {  // inclusive OR-scan (Hillis-Steele)
+            unsigned long long a0 = tid >= off ? s0[tid - off] : 0, a1 = tid >= off ? s1[tid - off] : 0;
+            __syncthreads();
+            s0[tid] |= a0;
+            s1[tid] |= a1;
+            __syncthreads();
+        }
+        unsigned long long p0 = acc0 | (tid ? s0[tid - 1] : 0), p1 = acc1 | (tid ? s1[tid - 1] : 0);
+        if (((m0 & p0) | (m1 & p1)) != 0) atomicMin(&first, q);
+        __syncthreads();
+        if (first != INT32_MAX) {
+            // seen = base | misses of the slots before the first conflict
+            const int fq = first - base;
+            if (tid == 0) {
+                seen[0] = acc0 | (fq ? s0[fq - 1] : 0);
+                seen[1] = acc1 | (fq ? s1[fq - 1] : 0);
+                ctrl[0] = first;
+            }
+            return;
+        }
+        if (tid == 0) {
+            acc0 |= s0[VAL_THREADS - 1];
+            acc1 |= s1[VAL_THREADS - 1];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        seen[0] = acc0;
+        seen[1] = acc1;
+        ctrl[0] = -1;
+    }
 }
 
 // Jaccard / subset filter of FrameProcessor._find_paths (:255-269), one wave per frame.
@@ -867,7 +908,7 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
         a.seen = seen;
         hipLaunchKernelGGL(nav_astar_kernel, dim3(a.nslots), dim3(64), lds, st, a);
         if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-        hipLaunchKernelGGL(nav_validate_kernel, dim3(1), dim3(64), 0, st, a.starts, a.qwork, a.query_bytes,
+        hipLaunchKernelGGL(nav_validate_kernel, dim3(1), dim3(VAL_THREADS), 0, st, a.starts, a.qwork, a.query_bytes,
                            a.nslots, slot0, seen, ctrl);
         if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
         int32_t rerun = -1;

@@ -60,11 +60,24 @@ __global__ void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, in
     int local;
     Level L = level_of(lv.p, H, W, a, &local);
     const float* row = L.p + ((int64_t)b * L.h * L.w + local) * no;
-    // class scores: sigmoid, first maximum (cls.max(1) on sigmoid values)
+    // max class logit first (16-byte loads); sigmoid is monotone, so a frame-typical anchor whose best
+    // logit does not clear the threshold exits after reading only its class logits
+    const float* cl = row + 4 * REG_MAX;
+    float mx = -INFINITY;
+    if ((nc & 3) == 0) {
+        for (int c = 0; c < nc; c += 4) {
+            float4 v = *(const float4*)(cl + c);
+            mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+        }
+    } else {
+        for (int c = 0; c < nc; ++c) mx = fmaxf(mx, cl[c]);
+    }
+    if (!(sigmoidf_(mx) > conf)) return;
+    // class scores: sigmoid, first maximum (cls.max(1) on sigmoid values: saturated ties -> lowest class)
     float best = -1.0f;
     int bc = 0;
     for (int c = 0; c < nc; ++c) {
-        float s = sigmoidf_(row[4 * REG_MAX + c]);
+        float s = sigmoidf_(cl[c]);
         if (s > best) {
             best = s;
             bc = c;

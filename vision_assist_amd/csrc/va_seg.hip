@@ -23,6 +23,9 @@
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+// staging registers: a native vector type (HIP's uint4 is a union-based class whose arrays defeat
+// SROA and end up in scratch / LDS)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 namespace {
 
@@ -110,12 +113,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
     }
     const int a_row0 = tid / CPR;
 
-    uint4 ra[A_CH], rb[B_CH];
+    u32x4 ra[A_CH], rb[B_CH];
     auto load_tile = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < A_CH; ++i) {
             int r = a_row0 + (NT / CPR) * i;
-            ra[i] = *(const uint4*)(Wt + (int64_t)(n0 + r) * a.Kpad + k0 + g * VEC);
+            ra[i] = *(const u32x4*)(Wt + (int64_t)(n0 + r) * a.Kpad + k0 + g * VEC);
         }
         int k = k0 + g * VEC;
         int tap = k / a.Cin, ci = k - tap * a.Cin;
@@ -125,19 +128,19 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
         for (int i = 0; i < B_CH; ++i) {
             int hi = b_hi[i] + ky, wi = b_wi[i] + kx;
             if (kin && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W)
-                rb[i] = *(const uint4*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci);
+                rb[i] = *(const u32x4*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci);
             else
-                rb[i] = make_uint4(0, 0, 0, 0);
+                rb[i] = (u32x4){0u, 0u, 0u, 0u};
         }
     };
     auto store_tile = [&]() {
 #pragma unroll
         for (int i = 0; i < A_CH; ++i) {
             int r = a_row0 + (NT / CPR) * i;
-            *(uint4*)(As + r * LDSW + g * VEC) = ra[i];
+            *(u32x4*)(As + r * LDSW + g * VEC) = ra[i];
         }
 #pragma unroll
-        for (int i = 0; i < B_CH; ++i) *(uint4*)(Bs + b_row[i] * LDSW + g * VEC) = rb[i];
+        for (int i = 0; i < B_CH; ++i) *(u32x4*)(Bs + b_row[i] * LDSW + g * VEC) = rb[i];
     };
 
     f32x4 acc[4][4];
@@ -243,33 +246,228 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
     }
 }
 
-// ----------------------------------------------------------------------------------------- SPPF pool
-// in: slice 0 of buf (c channels), writes slices 1..3: max over 5x5, 9x9, 13x13 windows (== MaxPool2d(5,1,2)
-// applied 1, 2, 3 times: -inf padding makes the chained pools windowed maxima).
-template <typename T>
-__global__ void sppf_pool_kernel(T* buf, int N, int H, int W, int c, int ld) {
-    int64_t total = (int64_t)N * H * W * c;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        int ch = (int)(i % c);
-        int64_t p = i / c;
-        int w = (int)(p % W), h = (int)((p / W) % H), n = (int)(p / ((int64_t)W * H));
-        float m5 = -INFINITY, m9 = -INFINITY, m13 = -INFINITY;
-        for (int dy = -6; dy <= 6; ++dy) {
-            int y = h + dy;
-            if (y < 0 || y >= H) continue;
-            for (int dx = -6; dx <= 6; ++dx) {
-                int x = w + dx;
-                if (x < 0 || x >= W) continue;
-                float v = to_f(buf[(((int64_t)n * H + y) * W + x) * ld + ch]);
-                m13 = fmaxf(m13, v);
-                if (abs(dy) <= 4 && abs(dx) <= 4) m9 = fmaxf(m9, v);
-                if (abs(dy) <= 2 && abs(dx) <= 2) m5 = fmaxf(m5, v);
+// ----------------------------------------------------------------------------------------- conv v2 (bf16)
+// The bf16 production kernel: BK = 64, two LDS stages with ONE barrier per K-step (the next stage is
+// written while the current one is read), incremental im2col (tap, ci) bookkeeping instead of
+// per-step division, and an XCD-aware tile order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
+// "Workgroup dispatch"), so consecutive virtual tiles -- the N tiles of one pixel tile, then its
+// spatial neighbours -- are dealt to the same XCD and share its L2 (activations are re-read once per
+// N tile, weights by every pixel tile).
+constexpr int BK2 = 64;
+constexpr int LDSW2 = BK2 + 8;
+// Out-of-image / K-padding taps load from the (always valid) tensor base and are zeroed by a select:
+// every im2col load is issued unconditionally -- a branch around each load makes hipcc wait vmcnt(0)
+// per load and spill the staging registers (cdna_hip_programming.md §5 item 4(c)).  // 144-byte rows: ds_read_b128 row groups spread over the banks
+
+template <int WM, int WN, typename OutT>
+__global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
+    constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 64 * WN, CPR = BK2 / 8;
+    constexpr int A_CH = BN * CPR / NT, B_CH = BM * CPR / NT, RSTEP = NT / CPR;
+    __shared__ __align__(16) __bf16 As[2][BN * LDSW2];
+    __shared__ __align__(16) __bf16 Bs[2][BM * LDSW2];
+
+    // XCD-aware bijective remap of the 1-D grid (cdna_hip_programming.md §5.5 T1)
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+    const __bf16* __restrict__ Wt = (const __bf16*)a.w;
+    const int g = tid % CPR;  // fixed 8-element k group of this thread
+    const int row0 = tid / CPR;
+
+    int b_hi[B_CH], b_wi[B_CH];
+    int64_t b_base[B_CH];
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+        const int m = m0 + row0 + RSTEP * i;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi[i] = ho * a.stride - a.pad;
+            b_wi[i] = wo * a.stride - a.pad;
+            b_base[i] = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi[i] = -(1 << 28);
+            b_wi[i] = 0;
+            b_base[i] = 0;
+        }
+    }
+    // incremental decomposition of k = kt*64 + 8g into (ky, kx, ci)
+    int ci = 8 * g, ky = 0, kx = 0;
+    while (ci >= a.Cin) {
+        ci -= a.Cin;
+        if (++kx == a.kw) {
+            kx = 0;
+            ++ky;
+        }
+    }
+    int kcur = 8 * g;
+
+    // NOTE: no lambdas here -- staging arrays captured by reference become addressable allocas that
+    // hipcc promotes to LDS / scratch (observed: the weight prefetch went through LDS with a
+    // vmcnt wait at the top of every K-step).
+    u32x4 ra[A_CH], rb[B_CH];
+#define CONV2_LOAD(k0)                                                                                             \
+    {                                                                                                              \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) ra[i] =                                                   \
+            *(const u32x4*)(Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + 8 * g);                        \
+        const bool kin = kcur < a.K;                                                                               \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
+            const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
+            const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
+            const int64_t off = ok ? (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci : 0;                       \
+            const u32x4 v = *(const u32x4*)(X + off);                                                              \
+            rb[i] = ok ? v : (u32x4){0u, 0u, 0u, 0u};                                                           \
+        }                                                                                                          \
+        kcur += BK2;                                                                                               \
+        ci += BK2;                                                                                                 \
+        while (ci >= a.Cin) {                                                                                      \
+            ci -= a.Cin;                                                                                           \
+            if (++kx == a.kw) {                                                                                    \
+                kx = 0;                                                                                            \
+                ++ky;                                                                                              \
+            }                                                                                                      \
+        }                                                                                                          \
+    }
+#define CONV2_STORE(s)                                                                                             \
+    {                                                                                                              \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(&As[s][(row0 + RSTEP * i) * LDSW2 + 8 * g]) =  \
+            ra[i];                                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(&Bs[s][(row0 + RSTEP * i) * LDSW2 + 8 * g]) =  \
+            rb[i];                                                                                                 \
+    }
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.Kpad / BK2;
+    CONV2_LOAD(0);
+    CONV2_STORE(0);
+    __syncthreads();
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int s = kt & 1;
+        const bool more = kt + 1 < nk;
+        if (more) CONV2_LOAD((kt + 1) * BK2);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                af[i] = *(const bf16x8*)(&As[s][(wn * 64 + 16 * i + fr) * LDSW2 + 32 * kh + 8 * fq]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                bfr[j] = *(const bf16x8*)(&Bs[s][(wm * 64 + 16 * j + fr) * LDSW2 + 32 * kh + 8 * fq]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) CONV2_STORE(s ^ 1);
+        __syncthreads();
+    }
+#undef CONV2_LOAD
+#undef CONV2_STORE
+
+    OutT* Y = (OutT*)a.y;
+    const __bf16* R = (const __bf16*)a.res;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + 16 * j + fr;
+        if (m >= a.M) continue;
+        int wo = 0, ho = 0, n = 0;
+        if (a.mode == 1) {
+            wo = m % a.Wo;
+            const int t = m / a.Wo;
+            ho = t % a.Ho;
+            n = t / a.Ho;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = n0 + wn * 64 + 16 * i + 4 * fq;
+            if (co >= a.Cout) continue;
+            const float4 bv = *(const float4*)(a.bias + co);
+            float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+            if (a.act) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+            }
+            if (R) {
+                const uint2 rr = *(const uint2*)(R + (int64_t)m * a.ldr + co);
+                const __bf16* rp = (const __bf16*)&rr;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
+            }
+            OutT* yp;
+            if (a.mode == 1) {
+                const int cd = a.Cout / 4, q = co / cd, c = co - q * cd;
+                yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + c;
+            } else {
+                yp = Y + (int64_t)m * a.ldy + co;
+            }
+            if constexpr (sizeof(OutT) == 2) {
+                __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(uint2*)yp = *(uint2*)o4;
+            } else {
+                *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
-        T* o = buf + p * ld;
-        o[c + ch] = from_f<T>(m5);
-        o[2 * c + ch] = from_f<T>(m9);
-        o[3 * c + ch] = from_f<T>(m13);
+    }
+}
+
+// ----------------------------------------------------------------------------------------- SPPF pool
+// in: slice 0 of buf (c channels), writes slices 1..3 = MaxPool2d(5,1,2) applied 1, 2, 3 times (-inf padding).
+// One workgroup per (image, 8-channel group): the plane lives in LDS, each pool is a separable
+// 5-wide row max then 5-tall column max.
+constexpr int SPPF_CG = 8;
+constexpr int SPPF_MAXPIX = 40 * 40;  // 1280-px input -> 40x40 at stride 32
+
+template <typename T>
+__global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int N, int H, int W, int c, int ld) {
+    __shared__ float t0[SPPF_MAXPIX * SPPF_CG];
+    __shared__ float t1[SPPF_MAXPIX * SPPF_CG];
+    const int groups = c / SPPF_CG;
+    const int n = blockIdx.x / groups, cg = blockIdx.x % groups;
+    const int np = H * W, tid = threadIdx.x;
+    T* base = buf + (int64_t)n * np * ld + cg * SPPF_CG;
+    for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
+        int p = i / SPPF_CG, ch = i % SPPF_CG;
+        t0[i] = to_f(base[(int64_t)p * ld + ch]);
+    }
+    __syncthreads();
+    for (int k = 1; k <= 3; ++k) {
+        for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
+            int p = i / SPPF_CG, ch = i % SPPF_CG;
+            int y = p / W, x = p % W;
+            float m = -INFINITY;
+            for (int dx = -2; dx <= 2; ++dx) {
+                int xx = x + dx;
+                if (xx >= 0 && xx < W) m = fmaxf(m, t0[(y * W + xx) * SPPF_CG + ch]);
+            }
+            t1[i] = m;
+        }
+        __syncthreads();
+        for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
+            int p = i / SPPF_CG, ch = i % SPPF_CG;
+            int y = p / W, x = p % W;
+            float m = -INFINITY;
+            for (int dy = -2; dy <= 2; ++dy) {
+                int yy = y + dy;
+                if (yy >= 0 && yy < H) m = fmaxf(m, t1[(yy * W + x) * SPPF_CG + ch]);
+            }
+            t0[i] = m;
+            base[(int64_t)p * ld + k * c + ch] = from_f<T>(m);
+        }
+        __syncthreads();
     }
 }
 
@@ -306,8 +504,23 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+template <int WM, int WN, typename OutT>
+hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    const int ntm = (a.M + BM - 1) / BM, ntn = (a.Cout + BN - 1) / BN;
+    const int ntiles = ntm * ntn;
+    hipLaunchKernelGGL((conv2_kernel<WM, WN, OutT>), dim3(ntiles), dim3(64 * WM * WN), 0, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
+    if constexpr (sizeof(T) == 2) {
+        if (a.Kpad % BK2 == 0 && a.Cout % 4 == 0) {
+            if (a.Cout <= 64) return launch_conv2<4, 1, OutT>(a, st);
+            return launch_conv2<2, 2, OutT>(a, st);
+        }
+    }
     // tile choice: small Cout -> tall pixel tiles
     if (a.Cout <= 64) return launch_conv<T, 4, 1, OutT>(a, st);
     return launch_conv<T, 2, 2, OutT>(a, st);
@@ -351,15 +564,13 @@ int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H,
 
 int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld,
                      int32_t dtype) {
-    if (!buf || N <= 0 || c <= 0 || ld < 4 * c) return VA_ERR_ARG;
-    int64_t total = (int64_t)N * H * W * c;
+    if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % SPPF_CG || H * W > SPPF_MAXPIX) return VA_ERR_ARG;
+    const int blocks = N * (c / SPPF_CG);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == VA_DTYPE_BF16)
-        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(grid_for(total, 256)), dim3(256), 0, st, (__bf16*)buf, N, H,
-                           W, c, ld);
+        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (__bf16*)buf, N, H, W, c, ld);
     else
-        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(grid_for(total, 256)), dim3(256), 0, st, (float*)buf, N, H, W,
-                           c, ld);
+        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(blocks), dim3(256), 0, st, (float*)buf, N, H, W, c, ld);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

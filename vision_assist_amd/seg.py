@@ -23,7 +23,7 @@ from .seg_arch import NM, REG_MAX, Arch
 
 VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS = 1, 2, 3, 4
-BK = 32
+BK = 64  # K padding: the bf16 kernel steps K by 64 (the f32 kernel by 32)
 NPAD = 128
 
 
