@@ -211,6 +211,8 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n);
  * of ops recorded. */
 int va_prof_start(int32_t capacity);
 int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds);
+/* Per op-list index instead of per kind (call before va_prof_stop, which clears the records). */
+int va_prof_stop_ops(double* ms_by_op, int32_t nops);
 
 /* ---------------------------------------------------------------- segmentation post-processing */
 typedef struct va_cand { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_cand;  /* NMS candidate */

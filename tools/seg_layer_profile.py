@@ -1,0 +1,73 @@
+#!/usr/bin/env python
+"""Per-layer timing of the YOLOv8-seg forward (HIP events around every op of va_seg_run).
+
+Prints one line per op: name, GEMM shape, us, TFLOP/s, GB/s (algorithmic bytes: input
+activations + weights + output), and a JSON summary at the end.  Used to pick what to
+optimise in the conv kernel; run on the GPU box:
+    python tools/seg_layer_profile.py --batch 64 --iters 10
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--res", type=int, default=640)
+    ap.add_argument("--scale", default="s")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--json", default="")
+    args = ap.parse_args()
+    from vision_assist_amd import _lib
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch(args.scale)
+    net = SegNet(arch, fold(arch, synthetic_state_dict(arch, seed=0)), dtype=args.dtype)
+    B, H = args.batch, args.res
+    plan = net.plan(B, H, H)
+    plan["frames"].copy_(torch.randint(0, 256, plan["frames"].shape, dtype=torch.uint8))
+    for _ in range(3):
+        net.run_plan(plan)
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    n = plan["n"]
+    _lib.check(lib.va_prof_start(n * args.iters + 8), "va_prof_start")
+    for _ in range(args.iters):
+        net.run_plan(plan)
+    ms = (ctypes.c_double * n)()
+    lib.va_prof_stop_ops(ms, n)
+    kinds = (ctypes.c_double * 8)()
+    cnt = (ctypes.c_int64 * 8)()
+    lib.va_prof_stop(kinds, cnt, 8)
+    rows = []
+    tot = 0.0
+    for i, m in enumerate(plan["meta"]):
+        us = 1000.0 * ms[i] / args.iters
+        tot += us
+        r = {"i": i, "name": m["name"], "kind": m["kind"], "us": round(us, 2)}
+        if m["kind"] == "conv":
+            fl = 2.0 * m["M"] * m["N"] * m["K"]
+            r.update({"M": m["M"], "N": m["N"], "K": m["K"], "k": m["k"], "s": m["stride"],
+                      "tflops": round(fl / (us * 1e-6) / 1e12, 1), "gbps": round(m["bytes"] / (us * 1e-6) / 1e9, 1)})
+        rows.append(r)
+        print(json.dumps(r))
+    conv_us = sum(r["us"] for r in rows if r["kind"] == "conv")
+    fl = sum(2.0 * m["M"] * m["N"] * m["K"] for m in plan["meta"] if m["kind"] == "conv")
+    summ = {"total_us": round(tot, 1), "conv_us": round(conv_us, 1), "conv_tflops": round(fl / (conv_us * 1e-6) / 1e12, 1),
+            "batch": B, "res": H, "scale": args.scale}
+    print(json.dumps(summ))
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump({"rows": rows, "summary": summ}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -247,26 +247,46 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 }
 
 // ----------------------------------------------------------------------------------------- conv v2 (bf16)
-// The bf16 production kernel: BK = 64, two LDS stages with ONE barrier per K-step (the next stage is
-// written while the current one is read), incremental im2col (tap, ci) bookkeeping instead of
-// per-step division, and an XCD-aware tile order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
-// "Workgroup dispatch"), so consecutive virtual tiles -- the N tiles of one pixel tile, then its
-// spatial neighbours -- are dealt to the same XCD and share its L2 (activations are re-read once per
-// N tile, weights by every pixel tile).
+// The bf16 production kernel.
+//   * tile: WM x WN waves, each wave 64 pixels x (16*TNS) output channels (TNS = 4 or 2 16-wide
+//     MFMA column tiles), BK = 64;
+//   * two LDS stages with ONE barrier per K-step (the next stage is written while the current one
+//     is read); all LDS is one __shared__ array (a second __shared__ object can make hipcc wait
+//     vmcnt(0) before every ds_read, cdna_hip_programming.md §5 "three .s-level traps" (a));
+//   * incremental im2col (tap, ci) bookkeeping instead of per-step division; out-of-image and
+//     K-padding taps load from the tensor base and are zeroed by a select (a branch around each
+//     load makes hipcc wait vmcnt(0) per load);
+//   * staging registers are native vectors (HIP's uint4 is a union class whose arrays end up in
+//     scratch or get promoted to LDS);
+//   * epilogue through LDS: accumulators (+bias, SiLU) are parked as f32 in the freed stage
+//     buffers, then every thread writes whole 16-byte runs of consecutive channels of one pixel
+//     (+ residual read the same way), so the NHWC stores are row-contiguous;
+//   * XCD-aware tile order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md "Workgroup
+//     dispatch"), so consecutive virtual tiles -- the N tiles of one pixel tile, then its spatial
+//     neighbours -- are dealt to the same XCD and share its L2.
 constexpr int BK2 = 64;
-constexpr int LDSW2 = BK2 + 8;
-// Out-of-image / K-padding taps load from the (always valid) tensor base and are zeroed by a select:
-// every im2col load is issued unconditionally -- a branch around each load makes hipcc wait vmcnt(0)
-// per load and spill the staging registers (cdna_hip_programming.md §5 item 4(c)).  // 144-byte rows: ds_read_b128 row groups spread over the banks
+constexpr int LDSW2 = BK2 + 8;  // 144-byte rows: ds_read_b128 row groups spread over the banks
 
-template <int WM, int WN, typename OutT>
+template <int WM, int WN, int TNS>
+struct Conv2Cfg {
+    static constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 16 * TNS * WN, CPR = BK2 / 8;
+    static constexpr int A_CH = BN * CPR / NT, B_CH = BM * CPR / NT, RSTEP = NT / CPR;
+    static constexpr int STAGE = (BN + BM) * LDSW2 * 2;  // bytes per stage (A then B)
+    static constexpr int CW = BN + 4;                    // epilogue f32 row (floats)
+    static constexpr int EPI = BM * CW * 4;
+    static constexpr int LDS = (2 * STAGE > EPI ? 2 * STAGE : EPI);
+    static_assert(A_CH >= 1 && B_CH >= 1 && (BN * CPR) % NT == 0, "tile/block mismatch");
+};
+
+template <int WM, int WN, int TNS, typename OutT>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
-    constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 64 * WN, CPR = BK2 / 8;
-    constexpr int A_CH = BN * CPR / NT, B_CH = BM * CPR / NT, RSTEP = NT / CPR;
-    __shared__ __align__(16) __bf16 As[2][BN * LDSW2];
-    __shared__ __align__(16) __bf16 Bs[2][BM * LDSW2];
+    using Cfg = Conv2Cfg<WM, WN, TNS>;
+    constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
+    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, CW = Cfg::CW;
+    __shared__ __align__(16) unsigned char smem[Cfg::LDS];
+    auto As = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE); };
+    auto Bs = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE + BN * LDSW2 * 2); };
 
-    // XCD-aware bijective remap of the 1-D grid (cdna_hip_programming.md §5.5 T1)
     int bid = blockIdx.x;
     {
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
@@ -297,7 +317,6 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             b_base[i] = 0;
         }
     }
-    // incremental decomposition of k = kt*64 + 8g into (ky, kx, ci)
     int ci = 8 * g, ky = 0, kx = 0;
     while (ci >= a.Cin) {
         ci -= a.Cin;
@@ -308,9 +327,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     }
     int kcur = 8 * g;
 
-    // NOTE: no lambdas here -- staging arrays captured by reference become addressable allocas that
-    // hipcc promotes to LDS / scratch (observed: the weight prefetch went through LDS with a
-    // vmcnt wait at the top of every K-step).
+    // no lambdas around the staging arrays: captured by reference they become addressable allocas
     u32x4 ra[A_CH], rb[B_CH];
 #define CONV2_LOAD(k0)                                                                                             \
     {                                                                                                              \
@@ -322,7 +339,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
             const int64_t off = ok ? (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci : 0;                       \
             const u32x4 v = *(const u32x4*)(X + off);                                                              \
-            rb[i] = ok ? v : (u32x4){0u, 0u, 0u, 0u};                                                           \
+            rb[i] = ok ? v : (u32x4){0u, 0u, 0u, 0u};                                                              \
         }                                                                                                          \
         kcur += BK2;                                                                                               \
         ci += BK2;                                                                                                 \
@@ -336,15 +353,17 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     }
 #define CONV2_STORE(s)                                                                                             \
     {                                                                                                              \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(&As[s][(row0 + RSTEP * i) * LDSW2 + 8 * g]) =  \
+        __bf16* as_ = As(s);                                                                                       \
+        __bf16* bs_ = Bs(s);                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(as_ + (row0 + RSTEP * i) * LDSW2 + 8 * g) =     \
             ra[i];                                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(&Bs[s][(row0 + RSTEP * i) * LDSW2 + 8 * g]) =  \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(bs_ + (row0 + RSTEP * i) * LDSW2 + 8 * g) =     \
             rb[i];                                                                                                 \
     }
 
-    f32x4 acc[4][4];
+    f32x4 acc[TNS][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TNS; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -357,17 +376,19 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int s = kt & 1;
         const bool more = kt + 1 < nk;
         if (more) CONV2_LOAD((kt + 1) * BK2);
+        const __bf16* as_ = As(s);
+        const __bf16* bs_ = Bs(s);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
-            bf16x8 af[4], bfr[4];
+            bf16x8 af[TNS], bfr[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                af[i] = *(const bf16x8*)(&As[s][(wn * 64 + 16 * i + fr) * LDSW2 + 32 * kh + 8 * fq]);
+            for (int i = 0; i < TNS; ++i)
+                af[i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * LDSW2 + 32 * kh + 8 * fq);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                bfr[j] = *(const bf16x8*)(&Bs[s][(wm * 64 + 16 * j + fr) * LDSW2 + 32 * kh + 8 * fq]);
+                bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * LDSW2 + 32 * kh + 8 * fq);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < TNS; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
@@ -378,48 +399,68 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_LOAD
 #undef CONV2_STORE
 
+    // ---- epilogue 1: bias (+SiLU) -> f32 tile in LDS (the stage buffers are free after the last barrier)
+    float* Cs = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) {
+        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+        const float4 bv = *(const float4*)(a.bias + n0 + col);  // bias is padded to Npad
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
+                  v3 = acc[i][j][3] + bv.w;
+            if (a.act) {
+                v0 = silu(v0);
+                v1 = silu(v1);
+                v2 = silu(v2);
+                v3 = silu(v3);
+            }
+            *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
+        }
+    }
+    __syncthreads();
+    // ---- epilogue 2: 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous stores
+    constexpr int OV = 16 / sizeof(OutT);
+    constexpr int CPRO = BN / OV;
     OutT* Y = (OutT*)a.y;
     const __bf16* R = (const __bf16*)a.res;
+    for (int c = tid; c < BM * CPRO; c += NT) {
+        const int pl = c / CPRO, cl = (c % CPRO) * OV;
+        const int m = m0 + pl, co = n0 + cl;
+        if (m >= a.M || co >= a.Cout) continue;
+        float v[OV];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wm * 64 + 16 * j + fr;
-        if (m >= a.M) continue;
-        int wo = 0, ho = 0, n = 0;
-        if (a.mode == 1) {
-            wo = m % a.Wo;
-            const int t = m / a.Wo;
-            ho = t % a.Ho;
-            n = t / a.Ho;
+        for (int r = 0; r < OV; r += 4) {
+            const float4 t = *(const float4*)(Cs + pl * CW + cl + r);
+            v[r] = t.x;
+            v[r + 1] = t.y;
+            v[r + 2] = t.z;
+            v[r + 3] = t.w;
         }
+        if (R) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int co = n0 + wn * 64 + 16 * i + 4 * fq;
-            if (co >= a.Cout) continue;
-            const float4 bv = *(const float4*)(a.bias + co);
-            float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
-            if (a.act) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
-            }
-            if (R) {
-                const uint2 rr = *(const uint2*)(R + (int64_t)m * a.ldr + co);
+            for (int r = 0; r < OV; r += 8) {
+                const u32x4 rr = *(const u32x4*)(R + (int64_t)m * a.ldr + co + r);
                 const __bf16* rp = (const __bf16*)&rr;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
+                for (int e = 0; e < 8 && r + e < OV; ++e) v[r + e] += (float)rp[e];
             }
-            OutT* yp;
-            if (a.mode == 1) {
-                const int cd = a.Cout / 4, q = co / cd, c = co - q * cd;
-                yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + c;
-            } else {
-                yp = Y + (int64_t)m * a.ldy + co;
-            }
-            if constexpr (sizeof(OutT) == 2) {
-                __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-                *(uint2*)yp = *(uint2*)o4;
-            } else {
-                *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
-            }
+        }
+        OutT* yp;
+        if (a.mode == 1) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            const int cd = a.Cout / 4, q = co / cd, cc = co - q * cd;
+            yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + cc;
+        } else {
+            yp = Y + (int64_t)m * a.ldy + co;
+        }
+        if constexpr (sizeof(OutT) == 2) {
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+            *(bf16x8*)yp = o;
+        } else {
+            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
         }
     }
 }
@@ -489,6 +530,7 @@ __global__ void upsample2x_kernel(const T* src, int ld_s, T* dst, int ld_d, int 
 // ---- optional per-op timing of va_seg_run (HIP events on the caller's stream), see va_prof_*
 hipEvent_t* g_ev = nullptr;
 int* g_ev_kind = nullptr;
+int* g_ev_op = nullptr;
 int g_ev_cap = 0, g_ev_used = 0, g_prof_on = 0;
 
 int grid_for(int64_t n, int threads) {
@@ -504,21 +546,23 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int WM, int WN, typename OutT>
+template <int WM, int WN, int TNS, typename OutT>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
-    constexpr int BM = 64 * WM, BN = 64 * WN;
-    const int ntm = (a.M + BM - 1) / BM, ntn = (a.Cout + BN - 1) / BN;
+    using Cfg = Conv2Cfg<WM, WN, TNS>;
+    const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = ntm * ntn;
-    hipLaunchKernelGGL((conv2_kernel<WM, WN, OutT>), dim3(ntiles), dim3(64 * WM * WN), 0, st, a, ntn, ntiles);
+    hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
-        if (a.Kpad % BK2 == 0 && a.Cout % 4 == 0) {
-            if (a.Cout <= 64) return launch_conv2<4, 1, OutT>(a, st);
-            return launch_conv2<2, 2, OutT>(a, st);
+        constexpr int OV = 16 / sizeof(OutT);
+        if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
+            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
+            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
+            return launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
     // tile choice: small Cout -> tall pixel tiles
@@ -595,8 +639,10 @@ int va_prof_start(int32_t capacity) {
         for (int i = 0; i < 2 * g_ev_cap; ++i) (void)hipEventDestroy(g_ev[i]);
         delete[] g_ev;
         delete[] g_ev_kind;
+        delete[] g_ev_op;
         g_ev = new hipEvent_t[2 * capacity];
         g_ev_kind = new int[capacity];
+        g_ev_op = new int[capacity];
         for (int i = 0; i < 2 * capacity; ++i)
             if (hipEventCreate(&g_ev[i]) != hipSuccess) return VA_ERR_HIP;
         g_ev_cap = capacity;
@@ -604,6 +650,19 @@ int va_prof_start(int32_t capacity) {
     g_ev_used = 0;
     g_prof_on = 1;
     return VA_OK;
+}
+
+int va_prof_stop_ops(double* ms_by_op, int32_t nops) {
+    // per op index of the list (summed over every va_seg_run call recorded); keeps the records
+    if (!ms_by_op || nops <= 0) return VA_ERR_ARG;
+    for (int k = 0; k < nops; ++k) ms_by_op[k] = 0.0;
+    if (g_ev_used && hipEventSynchronize(g_ev[2 * g_ev_used - 1]) != hipSuccess) return VA_ERR_HIP;
+    for (int i = 0; i < g_ev_used; ++i) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, g_ev[2 * i], g_ev[2 * i + 1]) != hipSuccess) return VA_ERR_HIP;
+        if (g_ev_op[i] >= 0 && g_ev_op[i] < nops) ms_by_op[g_ev_op[i]] += ms;
+    }
+    return g_ev_used;
 }
 
 int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds) {
@@ -654,6 +713,7 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
         if (rc != VA_OK) return rc - 1000 * (i + 1);  // encode the failing op index
         if (prof) {
             if (hipEventRecord(g_ev[2 * g_ev_used + 1], (hipStream_t)stream) != hipSuccess) return VA_ERR_HIP;
+            g_ev_op[g_ev_used] = i;
             g_ev_kind[g_ev_used++] = ops[i].kind;
         }
     }

@@ -146,6 +146,7 @@ class SegNet:
             raise _lib.VaError(f"frame {H}x{W}: the network needs multiples of 32 (pad/letterbox first)")
         a = self.arch
         ops = []
+        meta = []  # per op: name, kind, GEMM M/N/K (algorithmic), bytes moved
         keep = []  # buffers referenced by the op list
 
         def new(h, w, c, dtype=None):
@@ -170,6 +171,11 @@ class SegNet:
             if dst.c != (p.cout // 4 if p.deconv else p.cout):
                 raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {p.cout}")
             ops.append(SegOp(kind=VA_OP_CONV, a=args))
+            es = 2 if self.dtype == "bf16" else 4
+            meta.append({"name": prefix, "kind": "conv", "M": B * ho * wo, "N": p.cout, "K": k * k * src.c,
+                         "k": k, "stride": stride,
+                         "bytes": es * B * h * w * src.c + es * p.cout * k * k * src.c
+                         + B * ho * wo * p.cout * (4 if out_f32 else es)})
             return ho, wo
 
         def c2f(i, src: Slice, dst: Slice, h, w):
@@ -187,11 +193,13 @@ class SegNet:
         def upsample(src: Slice, dst: Slice, h, w):
             ops.append(SegOp(kind=VA_OP_UPSAMPLE, a=ConvArgs(x=src.ptr, ldx=src.ld, y=dst.ptr, ldy=dst.ld, N=B, H=h, W=w,
                                                               Cin=src.c, dtype=self.va_dtype)))
+            meta.append({"name": "upsample", "kind": "upsample"})
 
         frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
         x0 = new(H, W, 8)
         ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
                                                             dtype=self.va_dtype)))
+        meta.append({"name": "preprocess", "kind": "preprocess"})
         h1, w1 = H // 2, W // 2
         h2, w2 = H // 4, W // 4
         h3, w3 = H // 8, W // 8
@@ -221,6 +229,7 @@ class SegNet:
         sp = new(h5, w5, 4 * cs)
         conv("model.9.cv1", b8, sp.sub(0, cs), h5, w5)
         ops.append(SegOp(kind=VA_OP_SPPF, a=ConvArgs(y=sp.ptr, N=B, H=h5, W=w5, Cin=cs, ldy=sp.ld, dtype=self.va_dtype)))
+        meta.append({"name": "sppf_pool", "kind": "sppf"})
         cat20 = new(h5, w5, a.c4 + a.c5)          # [conv19(o4) | P5]
         P5 = cat20.sub(a.c4, a.c5)
         conv("model.9.cv2", sp, P5, h5, w5)
@@ -261,7 +270,8 @@ class SegNet:
         proto = new(h2, w2, NM, torch.float32)
         conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
         op_arr = (SegOp * len(ops))(*ops)
-        plan = {"ops": op_arr, "n": len(ops), "keep": keep, "frames": frames,
+        assert len(meta) == len(ops)
+        plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
                 "out": SegOutputs(levels=levels, proto=proto.buf)}
         self._plans[key] = plan
         return plan
