@@ -96,6 +96,7 @@ typedef struct va_frame_hdr {
 #define VA_NODE_NONEMPTY 2u    /* grid_lookup[(x, y)].empty == False */
 #define VA_NODE_IN_GRIDS 4u    /* that object is also in self.grids (not an orphan) */
 #define VA_NODE_MULT_SHIFT 3   /* bits 3-4: len(graph[(x, y)]) / 4 (duplicate rows, Q19) */
+#define VA_NODE_ARTIFICIAL 32u /* grid_lookup[(x, y)].artificial */
 
 typedef struct va_query_hdr {
     int32_t status;        /* VA_QUERY_* */

@@ -1,0 +1,364 @@
+"""FrameProcessor: the per-frame hot path with the reference's class surface (FrameProcessor.py).
+
+    from vision_assist_amd.yolo import YOLO
+    from vision_assist_amd.FrameProcessor import FrameProcessor
+    model = YOLO("yolov8s-seg.pt").to("cuda")                      # main.py:43
+    processor = FrameProcessor(model=model, verbose=False, debug=False)  # main.py:44 (imshow defaults to False)
+    instructions = processor(frame)                                   # main.py:82
+
+``__call__`` (FrameProcessor.py:301-360) runs segmentation, post-processing,
+grid build, penalties, protrusions, start/end selection and A* as one device
+pipeline (vision_assist_amd.pipeline), copies one frame record back and hands
+the unique paths to PathAnalyser.  Same return values: the answer string, ``[]``
+when no grid was built (:328-332), ``(frame, answer)`` in debug mode (debug
+drawing needs OpenCV and is out of scope: the frame is returned undrawn).  The
+reference's IndexError on masks confined to the last rows is
+raised the same way.
+
+The step-by-step methods harness scripts call (``_extract_grid_information``,
+``_calculate_penalties``, ``_create_graph``, ``_find_paths``;
+utilities/generate_testing_grids/run_on_main.py:181-193) work too; ``grids``,
+``grid_lookup`` and ``np_grids`` are materialised as pydantic objects only when
+read (building ~1 K Grid objects per frame would cost more than the whole GPU
+pipeline, SURVEY.md §7 hard part 4).
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from typing import ClassVar, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import grid_size
+from .models import Coordinate, Grid, Path
+from .PathAnalyser import path_analyser
+from .PathFinder import path_finder
+from .PenaltyCalculator import penalty_calculator
+from .ProtrusionDetector import ProtrusionDetector
+from .utils import get_closest_grid_to_point
+
+G = grid_size
+
+
+def _pen_value(flags: int, pen: float):
+    """Device float64 penalty -> the python value the reference stores: None / int 0 / int 1 / float."""
+    if flags & _lib.VA_CELL_EMPTY:
+        return None
+    if pen == 0.0:
+        return 0
+    if pen == 1.0:
+        return 1
+    return float(pen)
+
+
+class _FrameState:
+    """Lazy pydantic view of one device frame record (vision_assist_amd.nav.NavFrame)."""
+
+    def __init__(self, nf, dims):
+        self.nf = nf
+        self.dims = dims
+        self._objs: dict[tuple[int, int], Grid] = {}
+        self._grids = None
+        self._lookup = None
+        self._np = None
+        self.penalties_assigned = False
+
+    # object id: main row r -> r, artificial row a -> LR + a (va_nav.hip nav_grid_kernel)
+    def _obj_y(self, o: int) -> int:
+        nf, d = self.nf, self.dims
+        return nf.y0 + G * o if o < d.LR else d.start_y + G * (o - d.LR)
+
+    def _obj_attr(self, o: int) -> int:
+        return o if o < self.dims.LR else (self._obj_y(o) - self.nf.y0) // G
+
+    def _pos_of_obj(self) -> dict[int, int]:
+        return {int(o): p for p, o in enumerate(self.nf.pos_obj)}
+
+    def obj(self, o: int, c: int, flags: int | None = None) -> Grid:
+        key = (o, c)
+        g = self._objs.get(key)
+        if g is None:
+            nf = self.nf
+            x, y = nf.x0 + G * c, self._obj_y(o)
+            if flags is None:
+                p = self._pos_of_obj()[o]
+                flags = int(nf.cell_flags[p, c])
+            g = Grid(coords=Coordinate(x=x, y=y), centre=Coordinate(x=x + G // 2, y=y + G // 2), penalty=None,
+                     row=self._obj_attr(o), col=c, empty=bool(flags & _lib.VA_CELL_EMPTY),
+                     artificial=bool(flags & _lib.VA_CELL_ARTIFICIAL))
+            self._objs[key] = g
+            if self.penalties_assigned and not g.empty:
+                p = self._pos_of_obj().get(o)
+                if p is not None:
+                    g.penalty = _pen_value(flags, float(nf.cell_pen[p, c]))
+        return g
+
+    def lookup_obj(self, x: int, y: int) -> Grid | None:
+        nf, d = self.nf, self.dims
+        yi, xi = y // G, x // G
+        if not (0 <= yi < d.LR and 0 <= xi < d.LC):
+            return None
+        fl = int(nf.node_flags[yi, xi])
+        if not fl & _lib.VA_NODE_EXISTS:
+            return None
+        c = xi - nf.x0 // G
+        ay = d.start_y // G
+        o = d.LR + (yi - ay) if 0 <= yi - ay < d.NART else yi - nf.y0 // G
+        cell_flags = (0 if fl & _lib.VA_NODE_NONEMPTY else _lib.VA_CELL_EMPTY) | \
+                     (_lib.VA_CELL_ARTIFICIAL if fl & _lib.VA_NODE_ARTIFICIAL else 0)
+        return self.obj(o, c, cell_flags)
+
+    @property
+    def grids(self) -> list[list[Grid]]:
+        if self._grids is None:
+            nf = self.nf
+            self._grids = [[self.obj(int(o), c, int(nf.cell_flags[p, c])) for c in range(nf.C)]
+                           for p, o in enumerate(nf.pos_obj)]
+        return self._grids
+
+    @property
+    def grid_lookup(self) -> dict:
+        if self._lookup is None:
+            nf, d = self.nf, self.dims
+            out = {}
+            # insertion order of the reference: main rows first, artificial rows override in place / append
+            ys = [nf.y0 + G * r for r in range(nf.Rm)] + [d.start_y + G * a for a in range(d.NART)]
+            for y in ys:
+                for c in range(nf.C):
+                    x = nf.x0 + G * c
+                    if (x, y) not in out:
+                        out[(x, y)] = None
+            for (x, y) in out:
+                out[(x, y)] = self.lookup_obj(x, y)
+            self._lookup = out
+        return self._lookup
+
+    @property
+    def np_grids(self) -> np.ndarray:
+        if self._np is None:
+            self._np = (~self.nf.cell_flags & _lib.VA_CELL_EMPTY).astype(np.uint8) & 1
+        return self._np
+
+    def assign_penalties(self) -> None:
+        """FrameProcessor._calculate_penalties: the device values onto every non-empty Grid."""
+        nf = self.nf
+        self.penalties_assigned = True
+        table = penalty_calculator._table
+        table.clear()
+        for p, o in enumerate(nf.pos_obj):
+            for c in range(nf.C):
+                fl = int(nf.cell_flags[p, c])
+                if fl & _lib.VA_CELL_EMPTY:
+                    continue
+                g = self.obj(int(o), c, fl)
+                g.penalty = _pen_value(fl, float(nf.cell_pen[p, c]))
+                table[id(g)] = g.penalty
+
+    def graph(self):
+        """FrameProcessor._create_graph from the device lattice (neighbours right, left, down, up)."""
+        nf = self.nf
+        graph = _DeviceGraph(list)
+        graph._state = self
+        for p, o in enumerate(nf.pos_obj):
+            y = self._obj_y(int(o))
+            for c in range(nf.C):
+                if nf.cell_flags[p, c] & _lib.VA_CELL_EMPTY:
+                    continue
+                x = nf.x0 + G * c
+                for nx, ny in ((x + G, y), (x - G, y), (x, y + G), (x, y - G)):
+                    if self.lookup_obj(nx, ny) is not None:
+                        graph[(x, y)].append(((nx, ny), np.float64(20.0)))
+        return graph
+
+    def peaks(self) -> list[Coordinate]:
+        return [Coordinate(x=x, y=y) for x, y in self.nf.peaks]
+
+    def device_paths(self) -> list[Path]:
+        """The unique paths of the device run, in FrameProcessor._find_paths order."""
+        nf = self.nf
+        sp, sc = nf.start
+        start = self.obj(int(nf.pos_obj[sp]), sc, int(nf.cell_flags[sp, sc]))
+        kept = sorted((q for q in nf.queries if q["unique"]), key=lambda q: q["order"])
+        out = []
+        for q in kept:
+            cells = [start] + [self.lookup_obj(x, y) for x, y in q["path"][1:]]
+            cost = 0 if len(q["path"]) == 1 else q["cost"]
+            out.append(Path(grids=cells, total_cost=cost, path_type="path"))
+        return out
+
+
+class _DeviceGraph(defaultdict):
+    """The graph dict of _create_graph, tagged with the frame it was built from."""
+    _state = None
+
+
+class FrameProcessor:
+    _instance: ClassVar[Optional["FrameProcessor"]] = None
+    _initialized: bool = False
+
+    def __new__(cls, model=None, verbose: bool = False, debug: bool = False, imshow: bool = False):
+        if cls._instance is None:
+            cls._instance = super().__new__(cls)
+        return cls._instance
+
+    def __init__(self, model=None, verbose: bool = False, debug: bool = False, imshow: bool = False):
+        if not self._initialized:
+            self._initialized = True
+            self.model = model
+            self.verbose = verbose
+            self.debug = debug
+            self.imshow = imshow
+            self.frame = None
+            self._state: _FrameState | None = None
+            self._pending_seen = None  # angle-cache state after the device run, committed by _find_paths
+            self.protrusion_detector = ProtrusionDetector(debug=debug, imshow=imshow)
+
+    # ---------------------------------------------------------------- lazy reference attributes
+    @property
+    def grids(self) -> list[list[Grid]]:
+        return self._state.grids if self._state is not None else []
+
+    @property
+    def grid_lookup(self) -> dict:
+        return self._state.grid_lookup if self._state is not None else {}
+
+    @property
+    def np_grids(self) -> np.ndarray:
+        return self._state.np_grids if self._state is not None else np.empty((0, 0), dtype=np.uint8)
+
+    def _has_grids(self) -> bool:
+        return self._state is not None and self._state.nf.status == _lib.VA_FRAME_OK
+
+    # ---------------------------------------------------------------- device run
+    def _pipe(self, H: int, W: int):
+        if self.model is None or not hasattr(self.model, "pipeline"):
+            raise TypeError("FrameProcessor needs a vision_assist_amd.yolo.YOLO model (the device pipeline)")
+        return self.model.pipeline(H, W, seen=path_finder.seen)
+
+    def _nav(self, H: int, W: int):
+        """Grid-stage engine alone (the step-by-step methods start from a mask, not a frame)."""
+        from .nav import NavEngine
+        cache = self.__dict__.setdefault("_navs", {})
+        if (H, W) not in cache:
+            cache[(H, W)] = NavEngine(H, W, max_batch=1)
+        return cache[(H, W)]
+
+    def _adopt(self, nav, batch, seen_after=None):
+        nf = batch.frame(0)
+        self._state = _FrameState(nf, nav.dims)
+        self._pending_seen = seen_after
+        if nf.status == _lib.VA_FRAME_INDEX_ERROR:
+            self._state = None
+            raise IndexError("list assignment index out of range")  # FrameProcessor.py:163
+
+    def _run_nav(self, nav, cells: torch.Tensor, rect, commit: bool):
+        """Grid stage for one frame.  commit=False runs A* against a scratch copy of the angle cache
+        (the step-by-step harness commits it in _find_paths, where the reference runs A*)."""
+        from .nav import AngleSeen
+        rects = torch.tensor([list(rect)], dtype=torch.int32, device=cells.device)
+        if commit:
+            return nav.run(cells.reshape(1, *cells.shape[-2:]).contiguous(), rects, path_finder.seen), None
+        scratch = AngleSeen(cells.device)
+        scratch.t.copy_(path_finder.seen.t)
+        return nav.run(cells.reshape(1, *cells.shape[-2:]).contiguous(), rects, scratch), scratch
+
+    # ---------------------------------------------------------------- reference methods
+    def _extract_grid_information(self, results) -> None:
+        """FrameProcessor.py:50-171 on the device, from YOLO.predict results (or any object with
+        ``.masks.cells`` / ``.masks.rect``: the filled mask sampled at the cell centres + boundingRect)."""
+        self._state = None
+        self._pending_seen = None
+        if self.frame is None:
+            raise ValueError("set self.frame first (FrameProcessor.__call__ does)")
+        H, W = self.frame.shape[0], self.frame.shape[1]
+        for res in results:
+            if res.masks is None:
+                continue
+            nav = self._nav(H, W)
+            batch, scratch = self._run_nav(nav, res.masks.cells, res.masks.rect, commit=False)
+            self._adopt(nav, batch, scratch)
+            if not self._has_grids():
+                self._state = None
+            return
+
+    def _calculate_penalties(self) -> None:
+        if self._has_grids():
+            self._state.assign_penalties()
+
+    def _create_graph(self) -> defaultdict:
+        return self._state.graph() if self._has_grids() else defaultdict(list)
+
+    def _calculate_path_similarity(self, path1: Path, path2: Path) -> float:
+        a = {(g.coords.x, g.coords.y) for g in path1.grids}
+        b = {(g.coords.x, g.coords.y) for g in path2.grids}
+        if not a or not b:
+            return 0.0
+        inter = len(a & b)
+        if inter == len(a) or inter == len(b):
+            return 1.0
+        union = len(a | b)
+        return inter / union if union > 0 else 0.0
+
+    def _find_paths(self, protrusion_peaks: list[Coordinate], graph) -> list[Path]:
+        """FrameProcessor.py:230-271.  For this frame's own peaks and graph the device A* results
+        (already computed, bit-identical) are used; anything else runs path_finder.find_path."""
+        if not self._has_grids():
+            return []
+        st = self._state
+        if isinstance(graph, _DeviceGraph) and graph._state is st and \
+                [(p.x, p.y) for p in protrusion_peaks] == [tuple(p) for p in st.nf.peaks]:
+            if self._pending_seen is not None:
+                path_finder.seen.t.copy_(self._pending_seen.t)
+                self._pending_seen = None
+            for q in st.nf.queries:
+                if q["status"] != _lib.VA_QUERY_FOUND:
+                    print("No path found.")
+            return st.device_paths()
+        self._pending_seen = None
+        H, W = self.frame.shape[0], self.frame.shape[1]
+        start = get_closest_grid_to_point(Coordinate(x=W // 2, y=H), self.grids)
+        found = []
+        for peak in protrusion_peaks:
+            end = get_closest_grid_to_point(peak, self.grids)
+            cells, cost = path_finder.find_path(graph, start, end, self.grid_lookup)
+            if cells:
+                found.append(Path(grids=cells, total_cost=cost, path_type="path"))
+            else:
+                print("No path found.")
+        found.sort(key=lambda p: len(p.grids), reverse=True)
+        unique: list[Path] = []
+        for p in found:
+            if all(self._calculate_path_similarity(p, u) < 0.90 for u in unique):
+                unique.append(p)
+        return unique
+
+    # ---------------------------------------------------------------- the hot path
+    def __call__(self, frame) -> tuple[np.ndarray, str] | str:
+        """FrameProcessor.py:301-360 as one device pipeline per frame."""
+        self.frame = frame
+        t = torch.as_tensor(frame) if not isinstance(frame, torch.Tensor) else frame
+        H, W = int(t.shape[0]), int(t.shape[1])
+        pipe = self._pipe(H, W)
+        from .post import PLANT_NEVER
+        batch = pipe.run(t.reshape(1, H, W, 3), plant_mode=PLANT_NEVER)
+        self._adopt(pipe.nav, batch)
+        if not self._has_grids():
+            self._state = None
+            return (self.frame, []) if self.debug else []
+        st = self._state
+        st.penalties_assigned = True
+        if not st.nf.peaks:
+            print("No protrusions detected.")
+        for q in st.nf.queries:
+            if q["status"] != _lib.VA_QUERY_FOUND:
+                print("No path found.")
+        paths = st.device_paths()
+        self.protrusion_detector.frames_processed += 1
+        final_answer = path_analyser(H, W, paths)
+        if self.debug:
+            return self.frame, final_answer
+        return final_answer
+
+    process = __call__  # the name BASELINE.json's north_star uses

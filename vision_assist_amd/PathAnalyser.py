@@ -1,0 +1,169 @@
+"""PathAnalyser: paths -> one instruction string (reference: PathAnalyser.py).
+
+Host-side decision layer.  Restated step for step from
+PathAnalyser.py:15-390, with one addition: the wall clock is injectable
+(``clock``, default ``time.time``), because the reference's answer depends on
+``time.time()`` (:335) and a 5 s instruction history (:375-382) -- a frozen
+clock makes it reproducible (tests/test_surface.py checks the answers of 372
+reference frames run with the same frozen clock).
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, ClassVar, Optional
+
+import numpy as np
+
+from .models import FinalAnswer, Instruction, Path
+
+_TYPE_RANK = {"turn": 0, "curve": 0, "bearing": 1}
+_DANGER_RANK = {"immediate": 0, "high": 1, "medium": 2, "low": 3}
+# danger upgrades when a paired previous instruction turned by more than the threshold (:240-273)
+_BEARING_UPGRADE = {"high": (12.5, "immediate"), "medium": (7.5, "high"), "low": (3.75, "medium")}
+_TURN_UPGRADE = {"high": (15, "immediate"), "medium": (10, "high"), "low": (7.5, "medium")}
+_PAIR_WINDOW_MS = 1500
+_HISTORY_MS = 5000
+
+
+class PathAnalyser:
+    _instance: ClassVar[Optional["PathAnalyser"]] = None
+    _initialized: bool = False
+
+    def __new__(cls, *args, **kwargs):
+        if cls._instance is None:
+            cls._instance = super().__new__(cls)
+        return cls._instance
+
+    def __init__(self, clock: Callable[[], float] | None = None):
+        if not self._initialized:
+            self._initialized = True
+            self.paths: list[Path] = []
+            self.previous_instructions: dict[int, list[Instruction]] = {}
+            self.instructions: list[Instruction] = []
+            self.clock = clock or time.time
+        elif clock is not None:
+            self.clock = clock
+
+    # :35-77
+    def _analyse_path(self, path: Path) -> Instruction | None:
+        angle, length = path.angle, path.length
+        if length < self.frame_height * 0.3:
+            return None
+        a = abs(angle)
+        danger = "high" if a > 45 else "medium" if a > 25 else "low"
+        kind = "bearing" if angle < 20 else "curve" if angle < 35 else "turn"
+        if path.start.x == path.end.x:
+            direction = "straight"
+        else:
+            direction = "left" if path.start.x > path.end.x else "right"
+        return Instruction(direction=direction, danger=danger, distance=length, start=path.start, end=path.end,
+                           angle_change=angle, length=length, instruction_type=kind)
+
+    # :79-143
+    def _analyse_corners(self, path: Path) -> list[Instruction]:
+        out = []
+        for corner in path.corners:
+            dist = corner.start.y  # larger y = closer to the user
+            if dist < self.frame_height * 0.5:
+                continue
+            h_mul = np.exp((np.log(2) / self.frame_height) * dist) - 1
+            a_mul = np.exp((np.log(2) / 90) * abs(corner.angle_change)) - 1
+            score = (h_mul * 0.7) + (a_mul * 0.3)
+            if score > 0.75:
+                danger = "immediate"
+            elif score > 0.65:
+                danger = "high"
+            elif score > 0.45:
+                danger = "medium"
+            else:
+                danger = "low"
+            out.append(Instruction(direction=corner.direction, danger=danger, distance=dist, start=corner.start,
+                                   end=corner.end, angle_change=corner.angle_change, length=corner.length,
+                                   instruction_type="turn" if corner.sharpness == "sharp" else "curve"))
+        return out
+
+    def _analyse_instructions(self, instructions: list[Instruction]) -> list[Instruction]:  # :145-156 (identity)
+        return instructions
+
+    def _pairs(self, previous, current, now):
+        """Previous/current instruction pairs that describe the same feature (:185-230)."""
+        pairs = []
+        for ts, prev_list in previous.items():
+            for p in prev_list:
+                for c in current:
+                    if p.instruction_type == "bearing" and c.instruction_type != "bearing":
+                        continue
+                    if p.distance > c.distance or p.direction != c.direction:
+                        continue
+                    dt = now - ts
+                    dy = abs(p.start.y - c.start.y)
+                    weight = p.start.y / self.frame_height
+                    if not (dt < _PAIR_WINDOW_MS and (dy * weight) < self.frame_height * 0.2):
+                        continue
+                    dx = abs(p.start.x - c.start.x)
+                    if not (dt < _PAIR_WINDOW_MS and (dx * weight) < self.frame_width * 0.2):
+                        continue
+                    if _DANGER_RANK[p.danger] - _DANGER_RANK[c.danger] > 0:
+                        continue
+                    pairs.append((p, c))
+        return pairs
+
+    # :158-284
+    def _analyse_previous_instructions(self, previous_instructions, current_instructions, current_timestamp):
+        if not previous_instructions:
+            return current_instructions
+        for p, c in self._pairs(previous_instructions, current_instructions, current_timestamp):
+            turned = abs(p.angle_change - c.angle_change)
+            table = _BEARING_UPGRADE if c.instruction_type == "bearing" else _TURN_UPGRADE
+            rule = table.get(c.danger)
+            if rule is not None and turned > rule[0]:
+                c.danger = rule[1]
+        # drop low-danger / far non-bearings -- with the reference's remove-while-iterating (:276-282)
+        for ins in current_instructions:
+            if ins.instruction_type != "bearing":
+                if ins.danger == "low":
+                    current_instructions.remove(ins)
+                elif ins.distance < self.frame_height * 0.33:
+                    current_instructions.remove(ins)
+        return current_instructions
+
+    # :286-313
+    def determine_final_instruction(self, instructions: list[Instruction]) -> FinalAnswer:
+        if not instructions:
+            return FinalAnswer.CONTINUE_FORWARD
+        urgent = [i for i in instructions if i.danger == "immediate"]
+        if urgent:
+            return FinalAnswer.MOVE_LEFT if urgent[0].direction == "left" else FinalAnswer.MOVE_RIGHT
+        if len(instructions) == 1 and instructions[0].instruction_type == "bearing":
+            return FinalAnswer.CONTINUE_FORWARD
+        first = instructions[0].direction
+        if first == "left":
+            return FinalAnswer.MOVE_LEFT
+        if first == "right":
+            return FinalAnswer.MOVE_RIGHT
+        return FinalAnswer.CONTINUE_FORWARD
+
+    # :316-386
+    def __call__(self, frame_height: int, frame_width: int, paths: list[Path]) -> str:
+        self.paths = paths
+        self.frame_height = frame_height
+        self.frame_width = frame_width
+        self.instructions = []
+        now = int(self.clock() * 1000)
+        for path in self.paths:
+            ins = self._analyse_path(path)
+            if ins:
+                self.instructions.append(ins)
+            if path.corners:
+                self.instructions.extend(self._analyse_corners(path))
+        self.instructions = self._analyse_instructions(self.instructions)
+        self.unfiltered_instructions = sorted(
+            self.instructions, key=lambda i: (_TYPE_RANK[i.instruction_type], _DANGER_RANK[i.danger]))
+        self.filtered_instructions = self._analyse_previous_instructions(self.previous_instructions,
+                                                                          self.instructions, now)
+        self.previous_instructions[now] = self.unfiltered_instructions
+        self.previous_instructions = {ts: v for ts, v in self.previous_instructions.items() if now - ts <= _HISTORY_MS}
+        return self.determine_final_instruction(self.filtered_instructions).value
+
+
+path_analyser = PathAnalyser()

@@ -20,7 +20,7 @@ VA_OK = 0
 VA_FRAME_OK, VA_FRAME_EMPTY, VA_FRAME_INDEX_ERROR, VA_FRAME_NO_MASK = 0, 1, 2, 3
 VA_QUERY_NONE, VA_QUERY_FOUND, VA_QUERY_NO_PATH = 0, 1, 2
 VA_CELL_EMPTY, VA_CELL_ARTIFICIAL = 1, 2
-VA_NODE_EXISTS, VA_NODE_NONEMPTY, VA_NODE_IN_GRIDS, VA_NODE_MULT_SHIFT = 1, 2, 4, 3
+VA_NODE_EXISTS, VA_NODE_NONEMPTY, VA_NODE_IN_GRIDS, VA_NODE_MULT_SHIFT, VA_NODE_ARTIFICIAL = 1, 2, 4, 3, 32
 
 
 class VaNavDims(ctypes.Structure):

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(VA_NAV_THREADS) void nav_grid_kernel(GridArgs a) {
         if (o >= 0) {
             fl |= VA_NODE_EXISTS;
             if (!(obj_flags[o * LC + c] & VA_CELL_EMPTY)) fl |= VA_NODE_NONEMPTY;
+            if (obj_flags[o * LC + c] & VA_CELL_ARTIFICIAL) fl |= VA_NODE_ARTIFICIAL;
             if (obj_pos[o] >= 0) fl |= VA_NODE_IN_GRIDS;
             // graph multiplicity: non-empty objects of self.grids at these coords (Q19)
             int m = 0;

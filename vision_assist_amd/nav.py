@@ -55,6 +55,7 @@ class NavFrame:
     x0: int = 0
     y0: int = 0
     C: int = 0
+    Rm: int = 0
     P: int = 0
     pos_y: np.ndarray | None = None      # [P] pixel y of each list position
     pos_attr: np.ndarray | None = None   # [P] Grid.row attribute
@@ -93,7 +94,7 @@ class NavBatch:
         rec = fr_all[i * d.frame_bytes:(i + 1) * d.frame_bytes]
         hdr = rec[d.off_hdr:d.off_hdr + 64].view(FRAME_HDR)[0]
         out = NavFrame(status=int(hdr["status"]), H=d.H, W=d.W, x0=int(hdr["x0"]), y0=int(hdr["y0"]),
-                       C=int(hdr["C"]), P=int(hdr["P"]))
+                       C=int(hdr["C"]), Rm=int(hdr["Rm"]), P=int(hdr["P"]))
         if out.status != _lib.VA_FRAME_OK:
             return out
         P, C, LC = out.P, out.C, d.LC

@@ -1,0 +1,106 @@
+"""YOLO model object for FrameProcessor (replaces ``ultralytics.YOLO`` at main.py:43).
+
+``YOLO(weights).to("cuda")`` then ``FrameProcessor(model=...)`` exactly as main.py
+does.  The network is YOLOv8-seg (n / s / m) running on the MI355X MFMA kernels
+of libva355.so; ``predict`` returns per-frame ``Results`` whose mask has already
+been reduced on the device to what FrameProcessor consumes (FrameProcessor.py:67-97):
+the chosen instance's cell-lattice samples and bounding rect.
+
+Weights: a ``.safetensors`` file with Ultralytics state-dict names (export one
+with ``safetensors.torch.save_file(model.model.state_dict(), path)`` where
+ultralytics is available) is folded and packed; a bare model name such as
+``yolov8s-seg.pt`` (main.py:14's default, which Ultralytics would download)
+gets seeded synthetic weights of that architecture -- nothing is downloaded.
+"""
+from __future__ import annotations
+
+import os
+import re
+import warnings
+
+import numpy as np
+import torch
+
+from .seg_arch import Arch, fold, synthetic_state_dict
+
+
+class Masks:
+    """Device mask summary of one frame (the input of the grid stage)."""
+
+    def __init__(self, cells: torch.Tensor, rect: tuple[int, int, int, int], chosen: int):
+        self.cells = cells      # uint8 [H/20, W/20] on the device
+        self.rect = rect        # boundingRect (x, y, w, h) of the chosen mask
+        self.chosen = chosen    # index of the chosen detection, -2 = planted
+
+    @property
+    def xy(self):
+        raise NotImplementedError("mask polygons (cv2.findContours) are not produced: the chosen mask is reduced to "
+                                  "cell samples + boundingRect on the GPU (see vision_assist_amd/csrc/va_post.hip)")
+
+
+class Results:
+    def __init__(self, orig_shape, boxes: np.ndarray, masks: Masks | None):
+        self.orig_shape = orig_shape
+        self.boxes = boxes      # float [k, 6]: x1, y1, x2, y2, conf, cls (kept detections, score order)
+        self.masks = masks      # None when no mask (FrameProcessor.py:68-69)
+
+
+class YOLO:
+    def __init__(self, model: str = "yolov8s-seg.pt", task: str | None = None, *, dtype: str = "bf16", nc: int = 80,
+                 seed: int = 0, cls_bias: float | None = None):
+        name = os.path.basename(str(model))
+        if str(model).endswith(".safetensors") and os.path.exists(model):
+            from safetensors.torch import load_file
+            sd = load_file(model)
+            m = re.search(r"yolov8([nsm])", name)
+            scale = m.group(1) if m else "s"
+            nc = int(sd["model.22.cv3.0.2.weight"].shape[0]) if "model.22.cv3.0.2.weight" in sd else nc
+            self.arch = Arch(scale, nc)
+        else:
+            m = re.search(r"yolov8([nsm])-seg", name)
+            if not m:
+                raise ValueError(f"unknown model {model!r}: expected yolov8{{n,s,m}}-seg or a .safetensors state dict")
+            self.arch = Arch(m.group(1), nc)
+            warnings.warn(f"{model}: no local weights, using seeded synthetic yolov8{m.group(1)}-seg weights "
+                          "(nothing is downloaded)")
+            sd = synthetic_state_dict(self.arch, seed=seed, cls_bias=cls_bias)
+        self.folded = fold(self.arch, sd)
+        self.dtype = dtype
+        self.device = None
+        self._pipes = {}
+
+    def to(self, device):
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        return self
+
+    def pipeline(self, H: int, W: int, conf: float = 0.5, iou: float = 0.7, max_det: int = 300, seen=None):
+        """The fused single-frame device pipeline for H x W frames (cached)."""
+        from .pipeline import FramePipeline
+        key = (H, W, conf, iou, max_det)
+        if key not in self._pipes:
+            if self.device is None:
+                self.to("cuda")
+            self._pipes[key] = FramePipeline(self.arch, self.folded, 1, H, W, dtype=self.dtype, conf=conf, iou=iou,
+                                             max_det=max_det, device=self.device, seen=seen)
+        return self._pipes[key]
+
+    def predict(self, source, conf: float = 0.5, verbose: bool = False, iou: float = 0.7, max_det: int = 300):
+        frames = source if isinstance(source, (list, tuple)) else [source]
+        out = []
+        for fr in frames:
+            t = torch.as_tensor(fr) if not isinstance(fr, torch.Tensor) else fr
+            H, W = int(t.shape[0]), int(t.shape[1])
+            pipe = self.pipeline(H, W, conf, iou, max_det)
+            pipe.plan["frames"].copy_(t.reshape(1, H, W, 3))
+            pipe.seg.run_plan(pipe.plan)
+            o = pipe.plan["out"]
+            pipe.post.run(o.levels, o.proto, select=True)
+            det, _ = pipe.post.det_tensor(0)
+            chosen = int(pipe.post.chosen[0])
+            masks = None
+            if chosen >= 0:
+                masks = Masks(pipe.post.cells[0].clone(), tuple(int(v) for v in pipe.post.rects[0].cpu()), chosen)
+            out.append(Results((H, W), det.numpy(), masks))
+        return out
