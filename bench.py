@@ -147,24 +147,18 @@ def main():
     prof = not args.no_prof
     if prof:
         _lib.check(lib.va_prof_start(pipe.plan["n"] * args.steps + 16), "va_prof_start")
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rounds = 0
+    from vision_assist_amd.shard import timed
+
+    def timed_steps():
+        rounds, res = 0, None
+        for s in range(args.steps):
+            res = step(s)
+            rounds += res.rounds
+        return rounds, res
+
+    # barrier + device sync on both sides, max of the elapsed time over ranks
+    (rounds, res), elapsed = timed(timed_steps, world, sync=torch.cuda.synchronize)
     paths = 0
-    for s in range(args.steps):
-        res = step(s)
-        rounds += res.rounds
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
     conv_ms = conv_n = None
     if prof:
         import ctypes
