@@ -165,7 +165,7 @@ def main():
         ms = (ctypes.c_double * 8)()
         cnt = (ctypes.c_int64 * 8)()
         lib.va_prof_stop(ms, cnt, 8)
-        conv_ms, conv_n = ms[1], cnt[1]
+        conv_ms, conv_n = ms[1] + ms[5], cnt[1] + cnt[5]  # VA_OP_CONV + VA_OP_CONV0 (layer 0 fused)
         other_seg_ms = ms[2] + ms[3] + ms[4]
     # results sanity (last batch): count frames with >= 1 path
     last = res

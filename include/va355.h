@@ -184,6 +184,12 @@ int va_seg_conv(void* stream, const va_conv_args* a);
 /* uint8 BGR frames [B][H][W][3] -> RGB / 255 NHWC with 8 channels (3 used), dtype VA_DTYPE_*. */
 int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H, int32_t W, int32_t dtype, void* out);
 
+/* model.0 fused with the preprocessing (bf16): uint8 BGR [N][H][W][3] -> RGB/255 -> Conv2d(3, Cout, 3, s2, p1)
+ * + folded BN bias + SiLU -> bf16 NHWC [N][H/2][W/2] with channel stride ldy.  w: bf16 [Cout][32], k =
+ * (ky*3 + kx)*3 + c with c in R, G, B order, k >= 27 zero; Cout in {16, 32, 48, 64}. */
+int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
+                 const float* bias, int32_t Cout, void* y, int32_t ldy);
+
 /* SPPF (block.py SPPF): slice 0 (c channels) of an NHWC buffer of channel stride ld >= 4c -> slices 1..3
  * = MaxPool2d(5, 1, 2) applied once, twice, three times. */
 int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld, int32_t dtype);
@@ -198,6 +204,8 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_SPPF 2        /* sppf pool: a.y = buffer, a.N/H/W, a.Cin = c, a.ldy = ld, a.dtype */
 #define VA_OP_UPSAMPLE 3    /* upsample2x: a.x/a.ldx -> a.y/a.ldy, a.N/H/W (source size), a.Cin = c, a.dtype */
 #define VA_OP_PREPROCESS 4  /* preprocess: a.x = uint8 frames, a.y = out, a.N/H/W, a.dtype */
+#define VA_OP_CONV0 5       /* preprocess fused into model.0 (bf16): a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
+                               a.Cout, a.y, a.ldy -- see va_seg_conv0 */
 typedef struct va_seg_op {
     int32_t kind;
     int32_t pad_;

@@ -52,6 +52,7 @@ SIGNATURES = [
     ("va_astar_run", I32, [P, P, P, I32, I32, P, P, I32, P, P, ctypes.POINTER(I32)]),
     ("va_seg_conv", I32, [P, P]),
     ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
+    ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_upsample2x", I32, [P, P, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_run", I32, [P, P, I32]),

@@ -465,6 +465,76 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     }
 }
 
+// ----------------------------------------------------------------------------------------- layer 0
+// model.0 fused with preprocessing: uint8 BGR frame -> RGB/255 -> Conv(3x3, s2, p1) + folded BN + SiLU
+// -> bf16 NHWC.  K = 3x3x3 = 27 (padded to one 32-deep MFMA step), so instead of materialising an
+// 8-channel bf16 copy of the frame (16 B/pixel written + read again) each workgroup stages its
+// 17 x 129 x 3-byte input patch in LDS and builds the B fragments straight from it.
+// Tile: 8 output rows x 64 output columns, 4 waves x 2 rows; weights [Cout][32] bf16 (k = (ky*3+kx)*3 + c,
+// c in R, G, B order) stay in registers as the MFMA A operand.
+constexpr int C0_TH = 8, C0_TW = 64;
+constexpr int C0_PR = 2 * C0_TH + 1, C0_PC = 2 * C0_TW + 1;
+
+template <int NCO>
+__global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
+                                                    const __bf16* __restrict__ w, const float* __restrict__ bias,
+                                                    __bf16* __restrict__ y, int ldy) {
+    __shared__ uint8_t patch[C0_PR * C0_PC * 3];
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    const int tx = blockIdx.x, ty = blockIdx.y, n = blockIdx.z;
+    const int ox0 = tx * C0_TW, oy0 = ty * C0_TH;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint8_t* img = frames + (int64_t)n * H * W * 3;
+    const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+    for (int i = tid; i < C0_PR * C0_PC * 3; i += 256) {
+        const int r = i / (C0_PC * 3), rem = i - r * (C0_PC * 3);
+        const int iy = iy0 + r, ix = ix0 + rem / 3;
+        patch[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                       ? img[((int64_t)iy * W + ix) * 3 + rem % 3]
+                       : (uint8_t)0;
+    }
+    const int fr = lane & 15, fq = lane >> 4;
+    // A fragments (weights): row co = 16 i + fr, k = 8 fq .. 8 fq + 7
+    bf16x8 af[NCO];
+#pragma unroll
+    for (int i = 0; i < NCO; ++i) af[i] = *(const bf16x8*)(w + (16 * i + fr) * 32 + 8 * fq);
+    // this lane's 8 k values -> patch byte offsets (relative to the pixel's window corner); -1 = K padding
+    int koff[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * fq + e;
+        if (k < 27) {
+            const int tap = k / 3, c = k % 3;  // c: 0 = R, 1 = G, 2 = B; the frame is BGR
+            koff[e] = ((tap / 3) * C0_PC + (tap % 3)) * 3 + (2 - c);
+        } else {
+            koff[e] = -1;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // 8 subtiles of 16 pixels per wave: rows 2*wid, 2*wid+1
+        const int rl = 2 * wid + (j >> 2), cl = (j & 3) * 16 + fr;
+        const int base = ((2 * rl) * C0_PC + 2 * cl) * 3;
+        bf16x8 bfr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            bfr[e] = koff[e] >= 0 ? (__bf16)((float)patch[base + koff[e]] / 255.0f) : (__bf16)0.0f;
+        const int oy = oy0 + rl, ox = ox0 + cl;
+#pragma unroll
+        for (int i = 0; i < NCO; ++i) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc, 0, 0, 0);
+            if (oy < Ho && ox < Wo) {
+                const int co = 16 * i + 4 * fq;
+                const float4 bv = *(const float4*)(bias + co);
+                __bf16 o4[4] = {(__bf16)silu(acc[0] + bv.x), (__bf16)silu(acc[1] + bv.y),
+                                (__bf16)silu(acc[2] + bv.z), (__bf16)silu(acc[3] + bv.w)};
+                *(uint2*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * ldy + co) = *(uint2*)o4;
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------- SPPF pool
 // in: slice 0 of buf (c channels), writes slices 1..3 = MaxPool2d(5,1,2) applied 1, 2, 3 times (-inf padding).
 // One workgroup per (image, 8-channel group): the plane lives in LDS, each pool is a separable
@@ -687,6 +757,24 @@ int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds) {
     return used;
 }
 
+int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
+                 const float* bias, int32_t Cout, void* y, int32_t ldy) {
+    if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 4)
+        return VA_ERR_ARG;
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    dim3 grid((Wo + C0_TW - 1) / C0_TW, (Ho + C0_TH - 1) / C0_TH, N);
+    hipStream_t st = (hipStream_t)stream;
+    const __bf16* wp = (const __bf16*)w;
+    __bf16* yp = (__bf16*)y;
+    switch (Cout / 16) {
+        case 1: hipLaunchKernelGGL(conv0_kernel<1>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, yp, ldy); break;
+        case 2: hipLaunchKernelGGL(conv0_kernel<2>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, yp, ldy); break;
+        case 3: hipLaunchKernelGGL(conv0_kernel<3>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, yp, ldy); break;
+        default: hipLaunchKernelGGL(conv0_kernel<4>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, yp, ldy);
+    }
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
     if (!ops || n < 0) return VA_ERR_ARG;
     for (int i = 0; i < n; ++i) {
@@ -706,6 +794,9 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                 break;
             case VA_OP_PREPROCESS:
                 rc = va_seg_preprocess(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.dtype, a.y);
+                break;
+            case VA_OP_CONV0:
+                rc = va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             default:
                 rc = VA_ERR_ARG;

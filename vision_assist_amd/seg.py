@@ -22,7 +22,7 @@ from . import _lib
 from .seg_arch import NM, REG_MAX, Arch
 
 VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
-VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS = 1, 2, 3, 4
+VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0 = 1, 2, 3, 4, 5
 BK = 64  # K padding: the bf16 kernel steps K by 64 (the f32 kernel by 32)
 NPAD = 128
 
@@ -109,6 +109,12 @@ class SegNet:
             w = torch.cat([p[0] for p in parts], 0)
             b = torch.cat([p[1] for p in parts], 0)
             self.w[f"head.{l}.0"] = self._pack(w, b)
+        # model.0 for the fused bf16 first layer: [Cout][32], k = (ky*3 + kx)*3 + c (RGB), zero padded
+        w0, b0 = folded["model.0"]
+        w0p = torch.zeros(w0.shape[0], 32, dtype=torch.float32)
+        w0p[:, :27] = w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27)
+        self.w0 = (w0p.to(self.device, self.tdtype).contiguous(), b0.float().to(self.device).contiguous())
+        self.fuse_first = dtype == "bf16" and w0.shape[0] % 16 == 0 and w0.shape[0] <= 64
         self._plans = {}
 
     # ------------------------------------------------------------------ packing
@@ -196,17 +202,24 @@ class SegNet:
             meta.append({"name": "upsample", "kind": "upsample"})
 
         frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
-        x0 = new(H, W, 8)
-        ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
-                                                            dtype=self.va_dtype)))
-        meta.append({"name": "preprocess", "kind": "preprocess"})
         h1, w1 = H // 2, W // 2
         h2, w2 = H // 4, W // 4
         h3, w3 = H // 8, W // 8
         h4, w4 = H // 16, W // 16
         h5, w5 = H // 32, W // 32
         a0 = new(h1, w1, a.c1)
-        conv("model.0", x0, a0, H, W, stride=2)
+        if self.fuse_first:
+            ops.append(SegOp(kind=VA_OP_CONV0, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, w=self.w0[0].data_ptr(),
+                                                           bias=self.w0[1].data_ptr(), Cout=a.c1, y=a0.ptr, ldy=a0.ld,
+                                                           dtype=self.va_dtype)))
+            meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3, "stride": 2,
+                         "bytes": B * H * W * 3 + 2 * B * h1 * w1 * a.c1})
+        else:
+            x0 = new(H, W, 8)
+            ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
+                                                                dtype=self.va_dtype)))
+            meta.append({"name": "preprocess", "kind": "preprocess"})
+            conv("model.0", x0, a0, H, W, stride=2)
         a1 = new(h2, w2, a.c2)
         conv("model.1", a0, a1, h1, w1, stride=2)
         p2 = new(h2, w2, a.c2)
