@@ -558,16 +558,16 @@ struct AstarArgs {
     const uint64_t* seen;       // base seen set of this round
 };
 
+extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
+extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_min_u32(unsigned int);
+
+// lexicographic (fb, sec) minimum over the wave: two DPP-based wave reductions (ockl) instead of a
+// 6-step xor-shuffle butterfly of three ds_bpermute each
 __device__ inline void wave_argmin(unsigned long long& fb, unsigned& sec) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long ofb = __shfl_xor(fb, o, 64);
-        unsigned osec = __shfl_xor(sec, o, 64);
-        if (ofb < fb || (ofb == fb && osec < sec)) {
-            fb = ofb;
-            sec = osec;
-        }
-    }
+    const unsigned long long m = __ockl_wfred_min_u64(fb);
+    const unsigned s2 = __ockl_wfred_min_u32(fb == m ? sec : ~0u);
+    fb = m;
+    sec = s2;
 }
 
 __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {

@@ -18,6 +18,7 @@
 //   upsample2x_kernel<T>    nearest x2 into a concat slice
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/va355.h"
 
@@ -465,6 +466,148 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     }
 }
 
+// ----------------------------------------------------------------------------------------- small-N conv
+// Narrow layers (Cout <= 64: the C2f bottlenecks of P2/P3, the level-0 box/coef head branches) have
+// too little MFMA work per staged activation byte for the LDS-staged kernel: both its LDS traffic
+// and its 1-block-per-CU footprint bound them.  Here the whole (small) weight matrix lives in LDS,
+// loaded once per workgroup, and every wave streams its activations straight from global memory
+// into MFMA B fragments (lane (p, q) loads the 16 bytes of channels [8q, 8q+8) of its pixel's tap:
+// 16 pixels x 64 contiguous bytes per instruction for Cin = 32), double-buffered in registers.
+// A persistent grid walks 64-pixel tiles per wave, so the weights are read from L2 once per
+// workgroup, not once per tile.
+template <int TNS>
+__global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstride, int ntiles) {
+    extern __shared__ __align__(16) __bf16 wsh[];  // [16*TNS][wstride]
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+    // weights -> LDS (rows beyond Cout are zero in the packed matrix: Npad >= 16*TNS)
+    const int chunks = a.Kpad / 8;
+    for (int i = tid; i < 16 * TNS * chunks; i += 256) {
+        const int r = i / chunks, c = i - r * chunks;
+        *(u32x4*)(wsh + r * wstride + 8 * c) = *(const u32x4*)((const __bf16*)a.w + (int64_t)r * a.Kpad + 8 * c);
+    }
+    __syncthreads();
+    const int nkf = a.Kpad / 32;
+    for (int tile = blockIdx.x * 4 + wid; tile < ntiles; tile += gridDim.x * 4) {
+        const int m0 = tile * 64;
+        int hi0[4], wi0[4];
+        int64_t base[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + 16 * j + fr;
+            if (m < a.M) {
+                const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+                hi0[j] = ho * a.stride - a.pad;
+                wi0[j] = wo * a.stride - a.pad;
+                base[j] = (int64_t)n * a.H * a.W;
+            } else {
+                hi0[j] = -(1 << 28);
+                wi0[j] = 0;
+                base[j] = 0;
+            }
+        }
+        f32x4 acc[4][TNS];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        // k of this lane for K-fragment kf: 32 kf + 8 fq -> (ky, kx, ci), advanced incrementally
+        int ci = 8 * fq, ky = 0, kx = 0;
+        while (ci >= a.Cin) {
+            ci -= a.Cin;
+            if (++kx == a.kw) {
+                kx = 0;
+                ++ky;
+            }
+        }
+        int kcur = 8 * fq;
+        u32x4 bcur[4], bnxt[4];
+#define DN_LOAD(dst)                                                                                              \
+    {                                                                                                             \
+        const bool kin = kcur < a.K;                                                                              \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                           \
+            const int hi = hi0[j] + ky, wi = wi0[j] + kx;                                                         \
+            const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                  \
+            const int64_t off = ok ? (base[j] + (int64_t)hi * a.W + wi) * a.ldx + ci : 0;                        \
+            const u32x4 v = *(const u32x4*)(X + off);                                                             \
+            dst[j] = ok ? v : (u32x4){0u, 0u, 0u, 0u};                                                            \
+        }                                                                                                         \
+        kcur += 32;                                                                                               \
+        ci += 32;                                                                                                 \
+        while (ci >= a.Cin) {                                                                                     \
+            ci -= a.Cin;                                                                                          \
+            if (++kx == a.kw) {                                                                                   \
+                kx = 0;                                                                                           \
+                ++ky;                                                                                             \
+            }                                                                                                     \
+        }                                                                                                         \
+    }
+        DN_LOAD(bcur);
+        for (int kf = 0; kf < nkf; ++kf) {
+            if (kf + 1 < nkf) DN_LOAD(bnxt);
+            bf16x8 af[TNS];
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(wsh + (16 * i + fr) * wstride + 32 * kf + 8 * fq);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bf16x8 bfr = __builtin_bit_cast(bf16x8, bcur[j]);
+#pragma unroll
+                for (int i = 0; i < TNS; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[j][i], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bcur[j] = bnxt[j];
+        }
+#undef DN_LOAD
+        __bf16* Y = (__bf16*)a.y;
+        const __bf16* R = (const __bf16*)a.res;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + 16 * j + fr;
+            if (m >= a.M) continue;
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) {
+                const int co = 16 * i + 4 * fq;
+                if (co >= a.Cout) continue;
+                const float4 bv = *(const float4*)(a.bias + co);
+                float v[4] = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y, acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+                if (a.act) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                }
+                if (R) {
+                    const uint2 rr = *(const uint2*)(R + (int64_t)m * a.ldr + co);
+                    const __bf16* rp = (const __bf16*)&rr;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
+                }
+                __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(uint2*)(Y + (int64_t)m * a.ldy + co) = *(uint2*)o4;
+            }
+        }
+    }
+}
+
+template <int TNS>
+hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
+    const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
+    const size_t lds = (size_t)16 * TNS * wstride * 2;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    const int ntiles = (a.M + 63) / 64;
+    int blocks = (ntiles + 3) / 4;
+    const int cap = 256 * (lds <= 40 * 1024 ? 4 : lds <= 80 * 1024 ? 2 : 1);  // resident workgroups
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL((conv_dn_kernel<TNS>), dim3(blocks), dim3(256), lds, st, a, wstride, ntiles);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------------------- layer 0
 // model.0 fused with preprocessing: uint8 BGR frame -> RGB/255 -> Conv(3x3, s2, p1) + folded BN + SiLU
 // -> bf16 NHWC.  K = 3x3x3 = 27 (padded to one 32-deep MFMA step), so instead of materialising an
@@ -625,9 +768,31 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
+bool getenv_dn() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VA_CONV_DN");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
+        if constexpr (sizeof(OutT) == 2) {
+            // narrow layers: weights in LDS, activations straight into MFMA fragments
+            if (a.mode == 0 && a.Cout <= 64 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
+                (size_t)16 * ((a.Cout + 15) / 16) * (a.Kpad + 8) * 2 <= 120 * 1024 && getenv_dn()) {
+                switch ((a.Cout + 15) / 16) {
+                    case 1: return launch_conv_dn<1>(a, st);
+                    case 2: return launch_conv_dn<2>(a, st);
+                    case 3: return launch_conv_dn<3>(a, st);
+                    default: return launch_conv_dn<4>(a, st);
+                }
+            }
+        }
         constexpr int OV = 16 / sizeof(OutT);
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
