@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--cpu-sample", type=int, default=160, help="frames timed for the CPU baseline (0 = skip)")
     p.add_argument("--no-prof", action="store_true", help="skip the live per-op HIP-event timing")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="serial steps (no overlap of batch k's grid stage with batch k+1's network)")
     return p.parse_args()
 
 
@@ -114,7 +116,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from vision_assist_amd import _lib
-    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
     from vision_assist_amd.post import PLANT_IF_NONE
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
 
@@ -122,7 +124,12 @@ def main():
     arch = Arch(args.scale)
     fw = fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=cls_bias))
     B, H, W = args.batch, args.res, args.res
-    pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
+    overlap = not args.no_overlap
+    if overlap:
+        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev)
+        pipe = opipe.a
+    else:
+        pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
 
     # resident inputs: P batches of frames + planted masks, distinct per rank
     P = 4
@@ -139,8 +146,23 @@ def main():
         pipe.frames.copy_(frames[s % P], non_blocking=True)
         return pipe.run(None, pcs[s % P], prs[s % P], PLANT_IF_NONE)
 
-    for s in range(args.warmup):
-        step(s)
+    def run_steps(n):
+        """n steps; overlapped: batch s+1's network is enqueued before batch s's grid stage runs."""
+        rounds, res = 0, None
+        if not overlap:
+            for s in range(n):
+                res = step(s)
+                rounds += res.rounds
+            return rounds, res
+        opipe.submit(frames[0], pcs[0], prs[0], PLANT_IF_NONE)
+        for s in range(n):
+            if s + 1 < n:
+                opipe.submit(frames[(s + 1) % P], pcs[(s + 1) % P], prs[(s + 1) % P], PLANT_IF_NONE)
+            res = opipe.finish(opipe.k - (2 if s + 1 < n else 1))
+            rounds += res.rounds
+        return rounds, res
+
+    run_steps(args.warmup)
     torch.cuda.synchronize()
 
     lib = _lib.load()
@@ -150,11 +172,9 @@ def main():
     from vision_assist_amd.shard import timed
 
     def timed_steps():
-        rounds, res = 0, None
-        for s in range(args.steps):
-            res = step(s)
-            rounds += res.rounds
-        return rounds, res
+        if overlap:
+            opipe.k = 0
+        return run_steps(args.steps)
 
     # barrier + device sync on both sides, max of the elapsed time over ranks
     (rounds, res), elapsed = timed(timed_steps, world, sync=torch.cuda.synchronize)
@@ -230,6 +250,8 @@ def main():
                                    "penalty/protrusion/A* on GPU, end-to-end",
                        "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
                        "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",
+                       "overlap": "grid stage of batch k on a 2nd HIP stream under the network of batch k+1"
+                       if overlap else "none",
                        "gflop_per_frame": round(gflop, 2)},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -20,11 +20,12 @@ from .seg import SegNet
 
 class FramePipeline:
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", conf: float = 0.5,
-                 iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None):
+                 iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None,
+                 seg: SegNet | None = None, tag: int = 0):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.B, self.H, self.W = B, H, W
-        self.seg = SegNet(arch, folded, dtype=dtype, device=self.device)
-        self.plan = self.seg.plan(B, H, W)
+        self.seg = seg if seg is not None else SegNet(arch, folded, dtype=dtype, device=self.device)
+        self.plan = self.seg.plan(B, H, W, tag)
         self.post = PostEngine(B, H, W, arch.nc, conf, iou, max_det, device=self.device)
         self.nav = NavEngine(H, W, max_batch=B, device=self.device)
         self.seen = seen if seen is not None else AngleSeen(self.device)
@@ -48,5 +49,50 @@ class FramePipeline:
     def run_seg_only(self, stream=None) -> None:
         self.seg.run_plan(self.plan, stream)
 
+    # -- split form, for overlapping the grid stage of batch k with the network of batch k+1 ----
+    def seg_post(self, plant_cells=None, plant_rects=None, plant_mode: int = PLANT_NEVER, stream=None):
+        """Network + post-processing of the frames already in ``self.frames`` (enqueued only)."""
+        self.seg.run_plan(self.plan, stream)
+        out = self.plan["out"]
+        self.post.run(out.levels, out.proto, plant_cells, plant_rects, plant_mode, select=True, stream=stream)
 
-__all__ = ["FramePipeline", "PLANT_IF_NONE", "PLANT_NEVER"]
+    def nav_run(self, stream=None) -> NavBatch:
+        """Grid stage of the batch whose seg_post was enqueued (synchronises `stream`)."""
+        return self.nav.run(self.post.cells, self.post.rects, self.seen, stream)
+
+
+class OverlappedPipelines:
+    """Two FramePipelines sharing weights and the angle cache, on two HIP streams: while batch k's
+    grid stage (a few hundred waves: A* is a chain of dependent pops) runs on the nav stream, batch
+    k+1's network fills the rest of the chip on the seg stream.  Batches still leave in order and
+    the angle cache advances in order (the nav stream is serial)."""
+
+    def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", device=None, **kw):
+        self.a = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, tag=0, **kw)
+        self.b = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=self.a.device, seen=self.a.seen,
+                               seg=self.a.seg, tag=1, **kw)
+        self.pipes = (self.a, self.b)
+        self.s_seg = torch.cuda.Stream(device=self.a.device)
+        self.s_nav = torch.cuda.Stream(device=self.a.device)
+        self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+        self.k = 0
+
+    def submit(self, frames: torch.Tensor, plant_cells=None, plant_rects=None, plant_mode: int = PLANT_NEVER):
+        """Enqueue copy + network + post-processing of the next batch on the seg stream."""
+        p = self.pipes[self.k % 2]
+        self.s_seg.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.s_seg):
+            p.frames.copy_(frames, non_blocking=True)
+            p.seg_post(plant_cells, plant_rects, plant_mode, stream=self.s_seg)
+            self.ev[self.k % 2].record(self.s_seg)
+        self.k += 1
+
+    def finish(self, j: int) -> NavBatch:
+        """Run the grid stage of submitted batch j (in submission order) on the nav stream."""
+        p = self.pipes[j % 2]
+        self.s_nav.wait_event(self.ev[j % 2])
+        with torch.cuda.stream(self.s_nav):
+            return p.nav_run(stream=self.s_nav)
+
+
+__all__ = ["FramePipeline", "OverlappedPipelines", "PLANT_IF_NONE", "PLANT_NEVER"]

@@ -144,8 +144,10 @@ class SegNet:
     def _buf(self, B, h, w, c, dtype=None):
         return torch.empty((B, h, w, c), dtype=dtype or self.tdtype, device=self.device)
 
-    def plan(self, B: int, H: int, W: int):
-        key = (B, H, W)
+    def plan(self, B: int, H: int, W: int, tag: int = 0):
+        """Op list + buffers for B frames of H x W (``tag`` gives independent buffer sets, e.g. for
+        double-buffered batches that overlap on two streams)."""
+        key = (B, H, W, tag)
         if key in self._plans:
             return self._plans[key]
         if H % 32 or W % 32:
