@@ -177,6 +177,15 @@ typedef struct va_conv_args {
     int32_t dtype;          /* VA_DTYPE_BF16 (MFMA bf16, f32 accumulate) or VA_DTYPE_F32 (exact f32 MFMA) */
     int32_t out_f32;        /* bf16 inputs with a float output (head logits) */
     int32_t pad_;
+    /* Optional fused 1x1 tail conv (bf16, mode 0, no residual; Cout == 128 with c2 <= 80, or Cout 32 / 64 with
+     * c2 <= 64 and the weights fitting 120 KiB of LDS): when w2 != NULL the main conv's activations (bias + act,
+     * rounded to bf16 as a stored layer would be) never leave the chip and feed y2 = act2(W2 . a + b2);
+     * y / ldy / out_f32 then describe the TAIL output (c2 channels, c2 % 4 == 0).  Replaces a 1x1 layer that
+     * only consumes this one (proto.cv2 -> proto.cv3, head cv2/cv3/cv4 .l.1 -> .l.2). */
+    const void* w2;         /* [>= ceil16(c2)][Cout] bf16, K contiguous */
+    const float* b2;        /* [>= ceil16(c2)] */
+    int32_t c2;
+    int32_t act2;           /* 1 = SiLU */
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

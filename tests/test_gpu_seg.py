@@ -146,3 +146,47 @@ def test_forward_f32_nano_1280():
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         err = ((g - r).abs() / (1.0 + r.abs())).max().item()
         assert err <= 1e-3, f"{name}: max rel err {err}"
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("H,W,c", [(20, 20, 256), (40, 40, 256), (13, 7, 64)])
+def test_sppf_pool_exact(dtype, H, W, c):
+    """va_seg_sppf_pool == three chained MaxPool2d(5, 1, 2) (SPPF, ultralytics nn/modules/block.py), bit-exact."""
+    import ctypes
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    lib = _lib.load()
+    td = torch.bfloat16 if dtype == "bf16" else torch.float32
+    B, ld = 3, 4 * c + 8
+    g = torch.Generator().manual_seed(H * 100 + W + c)
+    x = torch.randn(B, H, W, c, generator=g).to(td)
+    buf = torch.zeros(B, H, W, ld, dtype=td, device="cuda")
+    buf[..., :c] = x.cuda()
+    vd = S.VA_DTYPE_BF16 if dtype == "bf16" else S.VA_DTYPE_F32
+    _lib.check(lib.va_seg_sppf_pool(_lib.stream_ptr(), ctypes.c_void_p(buf.data_ptr()), B, H, W, c, ld, vd), "sppf")
+    torch.cuda.synchronize()
+    y = x.float().permute(0, 3, 1, 2)
+    for k in range(1, 4):
+        y = F.max_pool2d(y, 5, 1, 2)
+        got = buf[..., k * c:(k + 1) * c].float().cpu().permute(0, 3, 1, 2)
+        assert torch.equal(got, y), (k, (got - y).abs().max())
+
+
+def test_fused_tail_matches_unfused(monkeypatch):
+    """proto.cv2+proto.cv3 and the head's cv2/cv3/cv4 .l.1+.l.2 pairs run as one op (1x1 tail in the 3x3's epilogue, va_conv_args.w2);
+    the tail sees the same bf16-rounded activations the unfused layer stores, so both plans agree to
+    fp32 accumulation-order noise."""
+    arch, fw, net = _net("bf16", "s")
+    frames = _frames(2, seed=5)
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "model.22.proto.cv2+model.22.proto.cv3" in names
+    assert sum("+" in n for n in names) == 10  # proto + cv2/cv3/cv4 at 3 levels
+    fused = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_FUSE_TAIL", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="bf16")
+    assert not any("+" in m["name"] for m in net2.plan(2, 640, 640)["meta"])
+    plain = _gpu_heads(net2, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), fused, plain):
+        err = ((g - r).abs().max() / r.abs().max()).item()
+        assert err < 1e-3, f"{name}: fused vs unfused {err}"

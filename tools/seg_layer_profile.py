@@ -54,13 +54,13 @@ def main():
         tot += us
         r = {"i": i, "name": m["name"], "kind": m["kind"], "us": round(us, 2)}
         if m["kind"] == "conv":
-            fl = 2.0 * m["M"] * m["N"] * m["K"]
+            fl = m.get("flops", 2.0 * m["M"] * m["N"] * m["K"])
             r.update({"M": m["M"], "N": m["N"], "K": m["K"], "k": m["k"], "s": m["stride"],
                       "tflops": round(fl / (us * 1e-6) / 1e12, 1), "gbps": round(m["bytes"] / (us * 1e-6) / 1e9, 1)})
         rows.append(r)
         print(json.dumps(r))
     conv_us = sum(r["us"] for r in rows if r["kind"] == "conv")
-    fl = sum(2.0 * m["M"] * m["N"] * m["K"] for m in plan["meta"] if m["kind"] == "conv")
+    fl = sum(m.get("flops", 2.0 * m["M"] * m["N"] * m["K"]) for m in plan["meta"] if m["kind"] == "conv")
     summ = {"total_us": round(tot, 1), "conv_us": round(conv_us, 1), "conv_tflops": round(fl / (conv_us * 1e-6) / 1e12, 1),
             "batch": B, "res": H, "scale": args.scale}
     print(json.dumps(summ))

@@ -279,6 +279,78 @@ struct Conv2Cfg {
     static_assert(A_CH >= 1 && B_CH >= 1 && (BN * CPR) % NT == 0, "tile/block mismatch");
 };
 
+// Fused 1x1 tail (va_conv_args.w2): the 128 x 128 tile of main-conv activations, rounded to bf16
+// exactly as the unfused layer would have stored them, goes to LDS as the B operand of a second
+// GEMM against the tail's weights (c2 <= 80 rows, read from L2); the tail result is the only write.
+constexpr int TAIL_C2F = 5;  // 16-row tail fragments: c2 <= 80
+
+template <int NT, int TNS, typename OutT>
+__device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
+                                           int n0, int wm, int wn, int wid, int fr, int fq) {
+    constexpr int BM = 128, BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
+    __bf16* Ts = (__bf16*)smem;
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) {
+        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+        const float4 bv = *(const float4*)(a.bias + n0 + col);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+            __bf16 o4[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o4[r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+            *(uint2*)(Ts + (wm * 64 + 16 * j + fr) * TW + col) = *(uint2*)o4;
+        }
+    }
+    __syncthreads();
+    const int nc2 = (a.c2 + 15) / 16;
+    const __bf16* W2 = (const __bf16*)a.w2;
+    f32x4 acc2[TAIL_C2F][PS];
+#pragma unroll
+    for (int c = 0; c < TAIL_C2F; ++c)
+#pragma unroll
+        for (int p = 0; p < PS; ++p) acc2[c][p] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kf = 0; kf < BN / 32; ++kf) {
+        bf16x8 bfr[PS];
+#pragma unroll
+        for (int p = 0; p < PS; ++p) bfr[p] = *(const bf16x8*)(Ts + (wid * PS * 16 + 16 * p + fr) * TW + 32 * kf + 8 * fq);
+#pragma unroll
+        for (int c = 0; c < TAIL_C2F; ++c) {
+            if (c < nc2) {
+                const bf16x8 af = *(const bf16x8*)(W2 + (16 * c + fr) * BN + 32 * kf + 8 * fq);
+#pragma unroll
+                for (int p = 0; p < PS; ++p)
+                    acc2[c][p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[p], acc2[c][p], 0, 0, 0);
+            }
+        }
+    }
+    OutT* Y = (OutT*)a.y;
+#pragma unroll
+    for (int p = 0; p < PS; ++p) {
+        const int m = m0 + wid * PS * 16 + 16 * p + fr;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int c = 0; c < TAIL_C2F; ++c) {
+            const int co = 16 * c + 4 * fq;
+            if (c >= nc2 || co >= a.c2) continue;
+            const float4 bv = *(const float4*)(a.b2 + co);
+            float v[4] = {acc2[c][p][0] + bv.x, acc2[c][p][1] + bv.y, acc2[c][p][2] + bv.z, acc2[c][p][3] + bv.w};
+            if (a.act2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+            }
+            OutT* yp = Y + (int64_t)m * a.ldy + co;
+            if constexpr (sizeof(OutT) == 2) {
+                __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(uint2*)yp = *(uint2*)o4;
+            } else {
+                *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+}
+
 template <int WM, int WN, int TNS, typename OutT>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
     using Cfg = Conv2Cfg<WM, WN, TNS>;
@@ -400,6 +472,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_LOAD
 #undef CONV2_STORE
 
+    if constexpr (BN == 128 && BM == 128) {
+        if (a.w2) {
+            conv2_tail<NT, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq);
+            return;
+        }
+    }
     // ---- epilogue 1: bias (+SiLU) -> f32 tile in LDS (the stage buffers are free after the last barrier)
     float* Cs = (float*)smem;
 #pragma unroll
@@ -475,7 +553,15 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 // 16 pixels x 64 contiguous bytes per instruction for Cin = 32), double-buffered in registers.
 // A persistent grid walks 64-pixel tiles per wave, so the weights are read from L2 once per
 // workgroup, not once per tile.
-template <int TNS>
+//
+// Fused 1x1 tail (va_conv_args.w2, TAIL): a wave holds all Cout = 16*TNS activations of its 64 pixels,
+// lane (p, q) channels 16i + 4q + r of pixel p.  The tail GEMM contracts over channels in any order,
+// so its K fragment kf takes each lane's own 8 values {16(2kf) + 4q + r} u {16(2kf+1) + 4q + r} as
+// k = 32kf + 8q + e, and the tail weights are read in that same order (two 8-byte loads per
+// fragment): no LDS, no cross-lane traffic, no store of the intermediate layer.
+constexpr int DN_TAIL_C2F = 4;  // tail c2 <= 64
+
+template <int TNS, bool TAIL, typename OutT>
 __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstride, int ntiles) {
     extern __shared__ __align__(16) __bf16 wsh[];  // [16*TNS][wstride]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -489,6 +575,21 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
     }
     __syncthreads();
     const int nkf = a.Kpad / 32;
+    constexpr int TKF = TAIL ? TNS / 2 : 1;
+    bf16x8 w2f[DN_TAIL_C2F][TKF];
+    if constexpr (TAIL) {
+        static_assert(TNS % 2 == 0, "tail K fragments pair the 16-channel groups");
+        const __bf16* W2 = (const __bf16*)a.w2;
+#pragma unroll
+        for (int c = 0; c < DN_TAIL_C2F; ++c)
+#pragma unroll
+            for (int kf = 0; kf < TKF; ++kf) {
+                const __bf16* r = W2 + (16 * c + fr) * (16 * TNS) + 32 * kf + 4 * fq;
+                const uint2 lo = 16 * c < a.c2 ? *(const uint2*)r : make_uint2(0u, 0u);
+                const uint2 hi = 16 * c < a.c2 ? *(const uint2*)(r + 16) : make_uint2(0u, 0u);
+                w2f[c][kf] = __builtin_bit_cast(bf16x8, (u32x4){lo.x, lo.y, hi.x, hi.y});
+            }
+    }
     for (int tile = blockIdx.x * 4 + wid; tile < ntiles; tile += gridDim.x * 4) {
         const int m0 = tile * 64;
         int hi0[4], wi0[4];
@@ -560,6 +661,59 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
             for (int j = 0; j < 4; ++j) bcur[j] = bnxt[j];
         }
 #undef DN_LOAD
+        if constexpr (TAIL) {
+            float4 bv[TNS];
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) bv[i] = *(const float4*)(a.bias + 16 * i + 4 * fq);
+            f32x4 acc2[4][DN_TAIL_C2F];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int c = 0; c < DN_TAIL_C2F; ++c) acc2[j][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kf = 0; kf < TKF; ++kf)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bf16x8 b;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int i = 2 * kf + h;
+                        const float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
+                                            acc[j][i][3] + bv[i].w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+                    }
+#pragma unroll
+                    for (int c = 0; c < DN_TAIL_C2F; ++c)
+                        acc2[j][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[c][kf], b, acc2[j][c], 0, 0, 0);
+                }
+            OutT* Y2 = (OutT*)a.y;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int m = m0 + 16 * j + fr;
+                if (m >= a.M) continue;
+#pragma unroll
+                for (int c = 0; c < DN_TAIL_C2F; ++c) {
+                    const int co = 16 * c + 4 * fq;
+                    if (co >= a.c2) continue;
+                    const float4 b2 = *(const float4*)(a.b2 + co);
+                    float v[4] = {acc2[j][c][0] + b2.x, acc2[j][c][1] + b2.y, acc2[j][c][2] + b2.z,
+                                  acc2[j][c][3] + b2.w};
+                    if (a.act2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                    }
+                    OutT* yp = Y2 + (int64_t)m * a.ldy + co;
+                    if constexpr (sizeof(OutT) == 2) {
+                        __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                        *(uint2*)yp = *(uint2*)o4;
+                    } else {
+                        *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+                    }
+                }
+            }
+            continue;
+        }
         __bf16* Y = (__bf16*)a.y;
         const __bf16* R = (const __bf16*)a.res;
 #pragma unroll
@@ -589,13 +743,13 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
     }
 }
 
-template <int TNS>
+template <int TNS, bool TAIL = false, typename OutT = __bf16>
 hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
     const size_t lds = (size_t)16 * TNS * wstride * 2;
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS, TAIL, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
         attr = true;
@@ -604,7 +758,7 @@ hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     int blocks = (ntiles + 3) / 4;
     const int cap = 256 * (lds <= 40 * 1024 ? 4 : lds <= 80 * 1024 ? 2 : 1);  // resident workgroups
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((conv_dn_kernel<TNS>), dim3(blocks), dim3(256), lds, st, a, wstride, ntiles);
+    hipLaunchKernelGGL((conv_dn_kernel<TNS, TAIL, OutT>), dim3(blocks), dim3(256), lds, st, a, wstride, ntiles);
     return hipGetLastError();
 }
 
@@ -680,48 +834,62 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
 
 // ----------------------------------------------------------------------------------------- SPPF pool
 // in: slice 0 of buf (c channels), writes slices 1..3 = MaxPool2d(5,1,2) applied 1, 2, 3 times (-inf padding).
-// One workgroup per (image, 8-channel group): the plane lives in LDS, each pool is a separable
-// 5-wide row max then 5-tall column max.
-constexpr int SPPF_CG = 8;
+// With -inf padding and stride 1, k chained 5x5 pools equal one (4k+1)x(4k+1) pool clipped to the
+// image, and a max pool is separable, so the three outputs are column maxima (radius 2k) of row
+// maxima (radius 2k) of the input -- exact, no arithmetic.  One workgroup per (image, 16-byte
+// channel group): every thread owns whole 16-byte pixel vectors; the plane and its three row-max
+// planes live in LDS ([4][H*W] x 16 B: 25.6 KiB at 20x20, 100 KiB at 40x40).
 constexpr int SPPF_MAXPIX = 40 * 40;  // 1280-px input -> 40x40 at stride 32
 
 template <typename T>
-__global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int N, int H, int W, int c, int ld) {
-    __shared__ float t0[SPPF_MAXPIX * SPPF_CG];
-    __shared__ float t1[SPPF_MAXPIX * SPPF_CG];
-    const int groups = c / SPPF_CG;
+__device__ inline u32x4 vmax16(u32x4 a, u32x4 b) {
+    constexpr int E = 16 / sizeof(T);
+    const T* pa = (const T*)&a;
+    const T* pb = (const T*)&b;
+    u32x4 r;
+    T* pr = (T*)&r;
+#pragma unroll
+    for (int e = 0; e < E; ++e) pr[e] = to_f(pa[e]) >= to_f(pb[e]) ? pa[e] : pb[e];
+    return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int H, int W, int c, int ld) {
+    extern __shared__ __align__(16) u32x4 sp[];  // [4][H*W]
+    constexpr int CG = 16 / sizeof(T);
+    const int groups = c / CG;
     const int n = blockIdx.x / groups, cg = blockIdx.x % groups;
-    const int np = H * W, tid = threadIdx.x;
-    T* base = buf + (int64_t)n * np * ld + cg * SPPF_CG;
-    for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
-        int p = i / SPPF_CG, ch = i % SPPF_CG;
-        t0[i] = to_f(base[(int64_t)p * ld + ch]);
+    const int np = H * W;
+    T* base = buf + (int64_t)n * np * ld + cg * CG;
+    for (int p = threadIdx.x; p < np; p += blockDim.x) sp[p] = *(const u32x4*)(base + (int64_t)p * ld);
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+        const int y = p / W, x = p - y * W;
+        const u32x4* row = sp + y * W;
+        u32x4 m = row[x];
+#pragma unroll
+        for (int k = 1; k <= 3; ++k) {
+#pragma unroll
+            for (int d = 2 * k - 1; d <= 2 * k; ++d) {
+                if (x - d >= 0) m = vmax16<T>(m, row[x - d]);
+                if (x + d < W) m = vmax16<T>(m, row[x + d]);
+            }
+            sp[k * np + p] = m;
+        }
     }
     __syncthreads();
-    for (int k = 1; k <= 3; ++k) {
-        for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
-            int p = i / SPPF_CG, ch = i % SPPF_CG;
-            int y = p / W, x = p % W;
-            float m = -INFINITY;
-            for (int dx = -2; dx <= 2; ++dx) {
-                int xx = x + dx;
-                if (xx >= 0 && xx < W) m = fmaxf(m, t0[(y * W + xx) * SPPF_CG + ch]);
+    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+        const int y = p / W, x = p - y * W;
+#pragma unroll
+        for (int k = 1; k <= 3; ++k) {
+            const u32x4* pl = sp + k * np + x;
+            u32x4 m = pl[y * W];
+            for (int d = 1; d <= 2 * k; ++d) {
+                if (y - d >= 0) m = vmax16<T>(m, pl[(y - d) * W]);
+                if (y + d < H) m = vmax16<T>(m, pl[(y + d) * W]);
             }
-            t1[i] = m;
+            *(u32x4*)(base + (int64_t)p * ld + k * c) = m;
         }
-        __syncthreads();
-        for (int i = tid; i < np * SPPF_CG; i += blockDim.x) {
-            int p = i / SPPF_CG, ch = i % SPPF_CG;
-            int y = p / W, x = p % W;
-            float m = -INFINITY;
-            for (int dy = -2; dy <= 2; ++dy) {
-                int yy = y + dy;
-                if (yy >= 0 && yy < H) m = fmaxf(m, t1[(yy * W + x) * SPPF_CG + ch]);
-            }
-            t0[i] = m;
-            base[(int64_t)p * ld + k * c + ch] = from_f<T>(m);
-        }
-        __syncthreads();
     }
 }
 
@@ -780,6 +948,18 @@ bool getenv_dn() {
 
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
+    if (a.w2) {  // fused 1x1 tail: narrow layers (Cout 32 / 64) in registers, Cout 128 through LDS
+        if constexpr (sizeof(T) == 2) {
+            if ((a.Cout == 32 || a.Cout == 64) && a.mode == 0 && !a.res && a.b2 && a.c2 > 0 &&
+                a.c2 <= 16 * DN_TAIL_C2F && a.c2 % 4 == 0 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
+                (size_t)a.Cout * (a.Kpad + 8) * 2 <= 120 * 1024)
+                return a.Cout == 32 ? launch_conv_dn<2, true, OutT>(a, st) : launch_conv_dn<4, true, OutT>(a, st);
+            if (a.Cout == 128 && a.mode == 0 && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F && a.c2 % 4 == 0 &&
+                a.Kpad % BK2 == 0 && a.ldy % 4 == 0)
+                return launch_conv2<2, 2, 4, OutT>(a, st);
+        }
+        return hipErrorInvalidValue;
+    }
     if constexpr (sizeof(T) == 2) {
         if constexpr (sizeof(OutT) == 2) {
             // narrow layers: weights in LDS, activations straight into MFMA fragments
@@ -814,6 +994,11 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     const int vec = a->dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
+    if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode ||
+                  a->res || !a->b2 || a->c2 <= 0 || a->c2 > 16 * (a->Cout == 128 ? TAIL_C2F : DN_TAIL_C2F) ||
+                  a->c2 % 4 || a->Kpad % (a->Cout == 128 ? BK2 : 32) ||
+                  (a->Cout < 128 && (size_t)a->Cout * (a->Kpad + 8) * 2 > 120 * 1024)))
+        return VA_ERR_ARG;
     hipStream_t st = (hipStream_t)stream;
     hipError_t e;
     if (a->dtype == VA_DTYPE_BF16)
@@ -843,13 +1028,19 @@ int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H,
 
 int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld,
                      int32_t dtype) {
-    if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % SPPF_CG || H * W > SPPF_MAXPIX) return VA_ERR_ARG;
-    const int blocks = N * (c / SPPF_CG);
+    const int cg = dtype == VA_DTYPE_BF16 ? 8 : 4;
+    if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % cg || ld % cg || H * W > SPPF_MAXPIX || ((uintptr_t)buf & 15))
+        return VA_ERR_ARG;
+    const int blocks = N * (c / cg);
+    const size_t lds = (size_t)4 * H * W * 16;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == VA_DTYPE_BF16)
-        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(blocks), dim3(256), 0, st, (__bf16*)buf, N, H, W, c, ld);
-    else
-        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(blocks), dim3(256), 0, st, (float*)buf, N, H, W, c, ld);
+    if (dtype == VA_DTYPE_BF16) {
+        (void)hipFuncSetAttribute((const void*)sppf_pool_kernel<__bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(blocks), dim3(256), lds, st, (__bf16*)buf, H, W, c, ld);
+    } else {
+        (void)hipFuncSetAttribute((const void*)sppf_pool_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(blocks), dim3(256), lds, st, (float*)buf, H, W, c, ld);
+    }
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

@@ -14,6 +14,7 @@ proto masks float32 [B, H/4, W/4, 32].
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -40,6 +41,7 @@ class ConvArgs(ctypes.Structure):
         ("res", ctypes.c_void_p), ("ldr", ctypes.c_int32),
         ("act", ctypes.c_int32), ("mode", ctypes.c_int32), ("M", ctypes.c_int32), ("dtype", ctypes.c_int32),
         ("out_f32", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("c2", ctypes.c_int32), ("act2", ctypes.c_int32),
     ]
 
 
@@ -163,8 +165,11 @@ class SegNet:
             return Slice(t, 0, c)
 
         def conv(prefix, src: Slice, dst: Slice, h, w, stride=1, act=True, res: Slice | None = None,
-                 out_f32=False):
+                 out_f32=False, tail: str | None = None, act2=False):
+            """One conv op; with ``tail`` the named 1x1 conv (the only consumer of this one) runs fused in
+            its epilogue and ``dst`` / ``out_f32`` describe the tail's output."""
             p = self.w[prefix]
+            p2 = self.w[tail] if tail else None
             k = p.k
             pad = k // 2
             ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
@@ -176,14 +181,23 @@ class SegNet:
                 y=dst.ptr, ldy=dst.ld, res=res.ptr if res is not None else None, ldr=res.ld if res is not None else 0,
                 act=1 if act else 0, mode=1 if p.deconv else 0, M=B * ho * wo, dtype=self.va_dtype,
                 out_f32=1 if (out_f32 and self.dtype == "bf16") else 0)
-            if dst.c != (p.cout // 4 if p.deconv else p.cout):
-                raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {p.cout}")
+            cout = p.cout
+            if p2 is not None:
+                if p2.cin != p.cout or p2.k != 1:
+                    raise _lib.VaError(f"{prefix}+{tail}: tail must be a 1x1 conv over all {p.cout} channels")
+                w2 = p2.w[:, :p.cout].contiguous()  # [Npad][Cout]: the tail reads rows of exactly Cout
+                keep.append(w2)
+                args.w2, args.b2, args.c2, args.act2 = w2.data_ptr(), p2.b.data_ptr(), p2.cout, 1 if act2 else 0
+                cout = p2.cout
+            if dst.c != (cout // 4 if p.deconv else cout):
+                raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {cout}")
             ops.append(SegOp(kind=VA_OP_CONV, a=args))
             es = 2 if self.dtype == "bf16" else 4
-            meta.append({"name": prefix, "kind": "conv", "M": B * ho * wo, "N": p.cout, "K": k * k * src.c,
-                         "k": k, "stride": stride,
+            flops = 2 * B * ho * wo * p.cout * k * k * src.c + (2 * B * ho * wo * p.cout * cout if p2 else 0)
+            meta.append({"name": prefix + (f"+{tail}" if tail else ""), "kind": "conv", "M": B * ho * wo,
+                         "N": p.cout, "K": k * k * src.c, "k": k, "stride": stride, "flops": flops,
                          "bytes": es * B * h * w * src.c + es * p.cout * k * k * src.c
-                         + B * ho * wo * p.cout * (4 if out_f32 else es)})
+                         + B * ho * wo * cout * (4 if out_f32 else es)})
             return ho, wo
 
         def c2f(i, src: Slice, dst: Slice, h, w):
@@ -273,6 +287,10 @@ class SegNet:
             levels.append(out.buf)
             for br, off, cw, ooff, oc in (("cv2", 0, cb, 0, 4 * REG_MAX), ("cv3", cb, cc, 4 * REG_MAX, a.nc),
                                            ("cv4", cb + cc, cm, 4 * REG_MAX + a.nc, NM)):
+                if self._can_fuse_tail(f"model.22.{br}.{l}.1", f"model.22.{br}.{l}.2"):
+                    conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), out.sub(ooff, oc), hh, ww, out_f32=True,
+                         tail=f"model.22.{br}.{l}.2", act2=False)
+                    continue
                 conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
                 conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False, out_f32=True)
         # Proto
@@ -280,16 +298,33 @@ class SegNet:
         conv("model.22.proto.cv1", o3, pr1, h3, w3)
         pr2 = new(h2, w2, a.npr)
         conv("model.22.proto.upsample", pr1, pr2, h3, w3, act=False)
-        pr3 = new(h2, w2, a.npr)
-        conv("model.22.proto.cv2", pr2, pr3, h2, w2)
         proto = new(h2, w2, NM, torch.float32)
-        conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
+        if self._can_fuse_tail("model.22.proto.cv2", "model.22.proto.cv3"):
+            conv("model.22.proto.cv2", pr2, proto, h2, w2, out_f32=True, tail="model.22.proto.cv3", act2=True)
+        else:
+            pr3 = new(h2, w2, a.npr)
+            conv("model.22.proto.cv2", pr2, pr3, h2, w2)
+            conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
         op_arr = (SegOp * len(ops))(*ops)
         assert len(meta) == len(ops)
         plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
                 "out": SegOutputs(levels=levels, proto=proto.buf)}
         self._plans[key] = plan
         return plan
+
+    def _can_fuse_tail(self, prefix: str, tail: str) -> bool:
+        """Whether the 1x1 conv ``tail`` (sole consumer of ``prefix``) can run in prefix's epilogue: bf16,
+        a 128-channel main conv with <= 80 tail channels or a 32 / 64-channel one with <= 64 (va355.h
+        va_conv_args.w2).
+        VA_FUSE_TAIL=0 turns it off (A/B timing)."""
+        if self.dtype != "bf16" or os.environ.get("VA_FUSE_TAIL", "1") == "0":
+            return False
+        p, p2 = self.w[prefix], self.w[tail]
+        if p.deconv or p2.k != 1 or p2.cin != p.cout or p2.cout % 4:
+            return False
+        if p.cout == 128:
+            return p2.cout <= 80
+        return p.cout in (32, 64) and p2.cout <= 64 and p.cout * (p.Kpad + 8) * 2 <= 120 * 1024
 
     def forward(self, frames_u8: torch.Tensor, stream=None) -> SegOutputs:
         """frames_u8: uint8 [B, H, W, 3] BGR on the device."""
