@@ -265,14 +265,27 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 //   * XCD-aware tile order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md "Workgroup
 //     dispatch"), so consecutive virtual tiles -- the N tiles of one pixel tile, then its spatial
 //     neighbours -- are dealt to the same XCD and share its L2.
+//   * GLDS variant: both operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging
+//     registers, no ds_write pass).  A DMA wave-instruction writes 1 KiB lane-linearly (8 rows x
+//     128 B), so rows are unpadded and the bank spread comes from an XOR swizzle applied on BOTH
+//     sides (cdna_hip_programming.md §5.4 rule 21): 16-byte chunk c of row r is stored in slot
+//     c ^ (r & 7).  Lane l of a DMA instruction therefore fetches chunk (l & 7) ^ (l >> 3) of row
+//     l >> 3 -- a per-lane constant, so the incremental im2col state is unchanged -- and a fragment
+//     read of chunk c, row r uses slot c ^ (r & 7): each ds_read_b128 lane group of 16 lanes then
+//     covers 16 distinct slots of the 256-byte bank row (conflict-free).  Out-of-image / K-tail
+//     chunks are fetched from a zeroed device page.
 constexpr int BK2 = 64;
 constexpr int LDSW2 = BK2 + 8;  // 144-byte rows: ds_read_b128 row groups spread over the banks
+__device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
+typedef __attribute__((address_space(1))) void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
 
-template <int WM, int WN, int TNS>
+template <int WM, int WN, int TNS, bool GLDS = false>
 struct Conv2Cfg {
     static constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 16 * TNS * WN, CPR = BK2 / 8;
     static constexpr int A_CH = BN * CPR / NT, B_CH = BM * CPR / NT, RSTEP = NT / CPR;
-    static constexpr int STAGE = (BN + BM) * LDSW2 * 2;  // bytes per stage (A then B)
+    static constexpr int RS = GLDS ? BK2 : LDSW2;     // LDS row stride (elements)
+    static constexpr int STAGE = (BN + BM) * RS * 2;  // bytes per stage (A then B)
     static constexpr int CW = BN + 4;                    // epilogue f32 row (floats)
     static constexpr int EPI = BM * CW * 4;
     static constexpr int LDS = (2 * STAGE > EPI ? 2 * STAGE : EPI);
@@ -351,14 +364,14 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
     }
 }
 
-template <int WM, int WN, int TNS, typename OutT>
+template <int WM, int WN, int TNS, typename OutT, bool GLDS = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
-    using Cfg = Conv2Cfg<WM, WN, TNS>;
+    using Cfg = Conv2Cfg<WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
-    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, CW = Cfg::CW;
+    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, CW = Cfg::CW, RS = Cfg::RS;
     __shared__ __align__(16) unsigned char smem[Cfg::LDS];
     auto As = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE); };
-    auto Bs = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE + BN * LDSW2 * 2); };
+    auto Bs = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE + BN * RS * 2); };
 
     int bid = blockIdx.x;
     {
@@ -371,8 +384,10 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     const int m0 = tm * BM, n0 = tn * BN;
     const __bf16* __restrict__ X = (const __bf16*)a.x;
     const __bf16* __restrict__ Wt = (const __bf16*)a.w;
-    const int g = tid % CPR;  // fixed 8-element k group of this thread
-    const int row0 = tid / CPR;
+    // fixed 8-element k group of this thread and its first staged row (rows row0 + RSTEP * i); with
+    // LDS-DMA, instruction i of wave w covers rows 8 (i NT/64 + w) .. +7, lane l row l >> 3
+    const int g = GLDS ? ((lane & 7) ^ (lane >> 3)) : tid % CPR;
+    const int row0 = GLDS ? 8 * wid + (lane >> 3) : tid / CPR;
 
     int b_hi[B_CH], b_wi[B_CH];
     int64_t b_base[B_CH];
@@ -434,6 +449,36 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             rb[i];                                                                                                 \
     }
 
+    // LDS-DMA form of LOAD+STORE: one 1 KiB DMA per operand row block, zero page for masked chunks
+#define CONV2_DMA(k0, s)                                                                                           \
+    {                                                                                                              \
+        __bf16* as_ = As(s);                                                                                       \
+        __bf16* bs_ = Bs(s);                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
+            const __bf16* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + 8 * g;                     \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+                                             0);                                                                   \
+        }                                                                                                          \
+        const bool kin = kcur < a.K;                                                                               \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
+            const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
+            const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
+            const void* src = ok ? (const void*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci)            \
+                                 : (const void*)g_zero_page;                                                       \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+                                             0);                                                                   \
+        }                                                                                                          \
+        kcur += BK2;                                                                                               \
+        ci += BK2;                                                                                                 \
+        while (ci >= a.Cin) {                                                                                      \
+            ci -= a.Cin;                                                                                           \
+            if (++kx == a.kw) {                                                                                    \
+                kx = 0;                                                                                            \
+                ++ky;                                                                                              \
+            }                                                                                                      \
+        }                                                                                                          \
+    }
+
     f32x4 acc[TNS][4];
 #pragma unroll
     for (int i = 0; i < TNS; ++i)
@@ -441,36 +486,50 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const int nk = a.Kpad / BK2;
-    CONV2_LOAD(0);
-    CONV2_STORE(0);
+    if constexpr (GLDS) {
+        CONV2_DMA(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        CONV2_LOAD(0);
+        CONV2_STORE(0);
+    }
     __syncthreads();
     const int fr = lane & 15, fq = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         const int s = kt & 1;
         const bool more = kt + 1 < nk;
-        if (more) CONV2_LOAD((kt + 1) * BK2);
+        if constexpr (GLDS) {
+            if (more) CONV2_DMA((kt + 1) * BK2, s ^ 1);
+        } else {
+            if (more) CONV2_LOAD((kt + 1) * BK2);
+        }
         const __bf16* as_ = As(s);
         const __bf16* bs_ = Bs(s);
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
             bf16x8 af[TNS], bfr[4];
+            // chunk 4 kh + fq of the row; GLDS rows are swizzled (slot = chunk ^ (row & 7), row & 7 == fr & 7)
+            const int ch = GLDS ? (((4 * kh + fq) ^ (fr & 7)) * 8) : 32 * kh + 8 * fq;
 #pragma unroll
-            for (int i = 0; i < TNS; ++i)
-                af[i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * LDSW2 + 32 * kh + 8 * fq);
+            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * LDSW2 + 32 * kh + 8 * fq);
+            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
 #pragma unroll
             for (int i = 0; i < TNS; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (more) CONV2_STORE(s ^ 1);
+        if constexpr (GLDS) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (more) CONV2_STORE(s ^ 1);
+        }
         __syncthreads();
     }
 #undef CONV2_LOAD
 #undef CONV2_STORE
+#undef CONV2_DMA
 
     if constexpr (BN == 128 && BM == 128) {
         if (a.w2) {
@@ -927,12 +986,27 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// VA_CONV_GLDS=0 stages through registers instead of LDS-DMA (A/B timing)
+bool getenv_glds() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VA_CONV_GLDS");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 template <int WM, int WN, int TNS, typename OutT>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     using Cfg = Conv2Cfg<WM, WN, TNS>;
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = ntm * ntn;
-    hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
+    // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of 8 and a 16-byte aligned base
+    if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0)
+        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
+                           ntiles);
+    else
+        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
