@@ -172,7 +172,11 @@ typedef struct va_conv_args {
     const void* res;        /* residual slice (dtype) added after the activation, or NULL */
     int32_t ldr;
     int32_t act;            /* 1 = SiLU */
-    int32_t mode;           /* 0 = conv, 1 = ConvTranspose2d(k=2, s=2) packed as a 1x1 conv with Cout = 4*C */
+    int32_t mode;           /* 0 = conv, 1 = ConvTranspose2d(k=2, s=2) packed as a 1x1 conv with Cout = 4*C,
+                               2 = sub-pixel classes (bf16, Cout > 64): ConvTranspose2d(k=2, s=2) followed by a
+                               3x3 / pad 1 conv, folded: for each class c = 2 dy + dx a 2x2 conv (kh = kw = 2,
+                               stride 1) with pads (1 - dy, 1 - dx) and weights w + c * Npad * Kpad, writing
+                               pixel (2 ho + dy, 2 wo + dx) of a [N][2 Ho][2 Wo] map; M = N * Ho * Wo */
     int32_t M;              /* N * Ho * Wo */
     int32_t dtype;          /* VA_DTYPE_BF16 (MFMA bf16, f32 accumulate) or VA_DTYPE_F32 (exact f32 MFMA) */
     int32_t out_f32;        /* bf16 inputs with a float output (head logits) */

@@ -176,6 +176,7 @@ def test_fused_tail_matches_unfused(monkeypatch):
     """proto.cv2+proto.cv3 and the head's cv2/cv3/cv4 .l.1+.l.2 pairs run as one op (1x1 tail in the 3x3's epilogue, va_conv_args.w2);
     the tail sees the same bf16-rounded activations the unfused layer stores, so both plans agree to
     fp32 accumulation-order noise."""
+    monkeypatch.setenv("VA_FOLD_PROTO", "0")  # keep proto.cv2 -> proto.cv3 as the Cout-128 tail case
     arch, fw, net = _net("bf16", "s")
     frames = _frames(2, seed=5)
     names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
@@ -190,3 +191,22 @@ def test_fused_tail_matches_unfused(monkeypatch):
     for name, g, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         err = ((g - r).abs().max() / r.abs().max()).item()
         assert err < 1e-3, f"{name}: fused vs unfused {err}"
+
+
+def test_proto_subpixel_fold(monkeypatch):
+    """bf16 proto via the sub-pixel fold (upsample + cv2 + cv3 as one mode-2 op) vs the unfolded
+    deconv -> 3x3 -> 1x1 chain and vs the fp32 torch reference: the fold drops the bf16 rounding of
+    the 160x160 intermediate, so it must be at least about as close to fp32 as the unfolded path."""
+    arch, fw, net = _net("bf16", "s")
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert any("sub-pixel fold" in n for n in names)
+    frames = _frames(2, seed=6)
+    ref = _ref_heads(arch, fw, frames)[3]
+    folded = _gpu_heads(net, frames)[3]
+    monkeypatch.setenv("VA_FOLD_PROTO", "0")
+    from vision_assist_amd.seg import SegNet
+    plain = _gpu_heads(SegNet(arch, fw, dtype="bf16"), frames)[3]
+    rel = lambda g, r: ((g - r).norm() / r.norm()).item()
+    assert rel(folded, ref) < 2e-2, rel(folded, ref)
+    assert rel(folded, ref) < 1.25 * rel(plain, ref) + 1e-3, (rel(folded, ref), rel(plain, ref))
+    assert rel(folded, plain) < 3e-2

@@ -292,6 +292,14 @@ struct Conv2Cfg {
     static_assert(A_CH >= 1 && B_CH >= 1 && (BN * CPR) % NT == 0, "tile/block mismatch");
 };
 
+// Output pixel row (NHWC) of GEMM row m: mode 0 -> m; mode 2 (sub-pixel class cls = 2 dy + dx of a
+// [N][2Ho][2Wo] map) -> pixel (2 ho + dy, 2 wo + dx).
+__device__ __forceinline__ int64_t conv_out_row(const va_conv_args& a, int m, int cls) {
+    if (a.mode != 2) return m;
+    const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+    return ((int64_t)n * 2 * a.Ho + 2 * ho + (cls >> 1)) * 2 * a.Wo + 2 * wo + (cls & 1);
+}
+
 // Fused 1x1 tail (va_conv_args.w2): the 128 x 128 tile of main-conv activations, rounded to bf16
 // exactly as the unfused layer would have stored them, goes to LDS as the B operand of a second
 // GEMM against the tail's weights (c2 <= 80 rows, read from L2); the tail result is the only write.
@@ -299,7 +307,7 @@ constexpr int TAIL_C2F = 5;  // 16-row tail fragments: c2 <= 80
 
 template <int NT, int TNS, typename OutT>
 __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
-                                           int n0, int wm, int wn, int wid, int fr, int fq) {
+                                           int n0, int wm, int wn, int wid, int fr, int fq, int cls) {
     constexpr int BM = 128, BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
     __bf16* Ts = (__bf16*)smem;
 #pragma unroll
@@ -353,7 +361,7 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
             }
-            OutT* yp = Y + (int64_t)m * a.ldy + co;
+            OutT* yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
             if constexpr (sizeof(OutT) == 2) {
                 __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
                 *(uint2*)yp = *(uint2*)o4;
@@ -378,12 +386,16 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
+    // mode 2: the 4 sub-pixel classes of one tile are consecutive virtual tiles (same input, same XCD)
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
     const int tm = bid / ntn, tn = bid % ntn;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
     const __bf16* __restrict__ X = (const __bf16*)a.x;
-    const __bf16* __restrict__ Wt = (const __bf16*)a.w;
+    const __bf16* __restrict__ Wt = (const __bf16*)a.w + (int64_t)cls * a.Npad * a.Kpad;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     // fixed 8-element k group of this thread and its first staged row (rows row0 + RSTEP * i); with
     // LDS-DMA, instruction i of wave w covers rows 8 (i NT/64 + w) .. +7, lane l row l >> 3
     const int g = GLDS ? ((lane & 7) ^ (lane >> 3)) : tid % CPR;
@@ -396,8 +408,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int m = m0 + row0 + RSTEP * i;
         if (m < a.M) {
             const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi[i] = ho * a.stride - a.pad;
-            b_wi[i] = wo * a.stride - a.pad;
+            b_hi[i] = ho * a.stride - pad_y;
+            b_wi[i] = wo * a.stride - pad_x;
             b_base[i] = (int64_t)n * a.H * a.W;
         } else {
             b_hi[i] = -(1 << 28);
@@ -533,7 +545,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     if constexpr (BN == 128 && BM == 128) {
         if (a.w2) {
-            conv2_tail<NT, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq);
+            conv2_tail<NT, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq, cls);
             return;
         }
     }
@@ -590,7 +602,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             const int cd = a.Cout / 4, q = co / cd, cc = co - q * cd;
             yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + cc;
         } else {
-            yp = Y + (int64_t)m * a.ldy + co;
+            yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
         }
         if constexpr (sizeof(OutT) == 2) {
             bf16x8 o;
@@ -1000,7 +1012,7 @@ template <int WM, int WN, int TNS, typename OutT>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     using Cfg = Conv2Cfg<WM, WN, TNS>;
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
-    const int ntiles = ntm * ntn;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of 8 and a 16-byte aligned base
     if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0)
         hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
@@ -1028,7 +1040,8 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
                 a.c2 <= 16 * DN_TAIL_C2F && a.c2 % 4 == 0 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
                 (size_t)a.Cout * (a.Kpad + 8) * 2 <= 120 * 1024)
                 return a.Cout == 32 ? launch_conv_dn<2, true, OutT>(a, st) : launch_conv_dn<4, true, OutT>(a, st);
-            if (a.Cout == 128 && a.mode == 0 && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F && a.c2 % 4 == 0 &&
+            if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
+                a.c2 % 4 == 0 &&
                 a.Kpad % BK2 == 0 && a.ldy % 4 == 0)
                 return launch_conv2<2, 2, 4, OutT>(a, st);
         }
@@ -1048,6 +1061,11 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             }
         }
         constexpr int OV = 16 / sizeof(OutT);
+        if (a.mode == 2) {  // sub-pixel classes: the 128-wide LDS-staged tile only
+            if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && a.Cout > 64)
+                return launch_conv2<2, 2, 4, OutT>(a, st);
+            return hipErrorInvalidValue;
+        }
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
             if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
@@ -1068,7 +1086,11 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     const int vec = a->dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
-    if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode ||
+    if (a->mode == 2 && (a->dtype != VA_DTYPE_BF16 || a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res ||
+                         a->Cout <= 64 || a->Kpad % BK2))
+        return VA_ERR_ARG;
+    if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode == 1 ||
+                  (a->mode == 2 && a->Cout != 128) ||
                   a->res || !a->b2 || a->c2 <= 0 || a->c2 > 16 * (a->Cout == 128 ? TAIL_C2F : DN_TAIL_C2F) ||
                   a->c2 % 4 || a->Kpad % (a->Cout == 128 ? BK2 : 32) ||
                   (a->Cout < 128 && (size_t)a->Cout * (a->Kpad + 8) * 2 > 120 * 1024)))
