@@ -199,7 +199,8 @@ int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H,
 
 /* model.0 fused with the preprocessing (bf16): uint8 BGR [N][H][W][3] -> RGB/255 -> Conv2d(3, Cout, 3, s2, p1)
  * + folded BN bias + SiLU -> bf16 NHWC [N][H/2][W/2] with channel stride ldy.  w: bf16 [Cout][32], k =
- * (ky*3 + kx)*3 + c with c in R, G, B order, k >= 27 zero; Cout in {16, 32, 48, 64}. */
+ * (ky*3 + kx)*3 + c with c in R, G, B order, k >= 27 zero; Cout in {16, 32, 48, 64}; W % 16 == 0, ldy % 8 == 0,
+ * frames and y 16-byte aligned. */
 int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
                  const float* bias, int32_t Cout, void* y, int32_t ldy);
 

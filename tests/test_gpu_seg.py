@@ -210,3 +210,33 @@ def test_proto_subpixel_fold(monkeypatch):
     assert rel(folded, ref) < 2e-2, rel(folded, ref)
     assert rel(folded, ref) < 1.25 * rel(plain, ref) + 1e-3, (rel(folded, ref), rel(plain, ref))
     assert rel(folded, plain) < 3e-2
+
+
+@pytest.mark.parametrize("cout,H,W", [(32, 64, 64), (48, 34, 48), (64, 40, 80), (16, 16, 16)])
+def test_conv0_fused_preprocess(cout, H, W):
+    """va_seg_conv0 (uint8 BGR -> RGB/255 -> 3x3 s2 conv + bias + SiLU) vs torch fp32 on the same
+    bf16-rounded inputs/weights; covers odd fragment counts (48) and ragged edges (H = 34)."""
+    import ctypes
+    from vision_assist_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cout + H + W)
+    B = 2
+    frames = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8)
+    w = torch.randn(cout, 3, 3, 3, generator=g) * 0.3
+    b = torch.randn(cout, generator=g) * 0.1
+    wp = torch.zeros(cout, 32)
+    wp[:, :27] = w.permute(0, 2, 3, 1).reshape(cout, 27)  # k = (ky*3 + kx)*3 + c, c in RGB
+    wd = wp.to(torch.bfloat16).cuda()
+    bd = b.float().cuda()
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    y = torch.zeros(B, Ho, Wo, cout, dtype=torch.bfloat16, device="cuda")
+    fd = frames.cuda()
+    rc = lib.va_seg_conv0(_lib.stream_ptr(), ctypes.c_void_p(fd.data_ptr()), B, H, W, ctypes.c_void_p(wd.data_ptr()),
+                          ctypes.c_void_p(bd.data_ptr()), cout, ctypes.c_void_p(y.data_ptr()), cout)
+    _lib.check(rc, "va_seg_conv0")
+    torch.cuda.synchronize()
+    x = (frames.flip(-1).float() / 255.0).to(torch.bfloat16).float().permute(0, 3, 1, 2)
+    ref = F.silu(F.conv2d(x, w.to(torch.bfloat16).float(), b, 2, 1))
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    err = ((got - ref).abs() / (ref.abs() + 0.05)).max().item()
+    assert err < 2e-2, err

@@ -841,31 +841,40 @@ hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
 // Tile: 8 output rows x 64 output columns, 4 waves x 2 rows; weights [Cout][32] bf16 (k = (ky*3+kx)*3 + c,
 // c in R, G, B order) stay in registers as the MFMA A operand.
 constexpr int C0_TH = 8, C0_TW = 64;
-constexpr int C0_PR = 2 * C0_TH + 1, C0_PC = 2 * C0_TW + 1;
+constexpr int C0_PR = 2 * C0_TH + 1;
+// patch rows hold frame bytes [6 ox0 - 16, 6 ox0 + 384): 16-byte aligned (W * 3 and 6 * C0_TW are
+// multiples of 16), so every 16-byte chunk is wholly inside or wholly outside the frame row; the
+// first window pixel (ix0 = 2 ox0 - 1) sits at byte 13
+constexpr int C0_PP = 400, C0_OFF = 13;
 
 template <int NCO>
 __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                     const __bf16* __restrict__ w, const float* __restrict__ bias,
                                                     __bf16* __restrict__ y, int ldy) {
-    __shared__ uint8_t patch[C0_PR * C0_PC * 3];
+    __shared__ __align__(16) uint8_t patch[C0_PR * C0_PP];
     const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
     const int tx = blockIdx.x, ty = blockIdx.y, n = blockIdx.z;
     const int ox0 = tx * C0_TW, oy0 = ty * C0_TH;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint8_t* img = frames + (int64_t)n * H * W * 3;
-    const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
-    for (int i = tid; i < C0_PR * C0_PC * 3; i += 256) {
-        const int r = i / (C0_PC * 3), rem = i - r * (C0_PC * 3);
-        const int iy = iy0 + r, ix = ix0 + rem / 3;
-        patch[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-                       ? img[((int64_t)iy * W + ix) * 3 + rem % 3]
-                       : (uint8_t)0;
+    const int iy0 = 2 * oy0 - 1, rb0 = 6 * ox0 - 16;
+    for (int i = tid; i < C0_PR * (C0_PP / 16); i += 256) {
+        const int r = i / (C0_PP / 16), c = i - r * (C0_PP / 16);
+        const int iy = iy0 + r, rb = rb0 + 16 * c;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if ((unsigned)iy < (unsigned)H && rb >= 0 && rb < 3 * W) v = *(const u32x4*)(img + (int64_t)iy * W * 3 + rb);
+        *(u32x4*)(patch + r * C0_PP + 16 * c) = v;
     }
     const int fr = lane & 15, fq = lane >> 4;
-    // A fragments (weights): row co = 16 i + fr, k = 8 fq .. 8 fq + 7
+    // A fragments (weights), rows permuted so that a lane's two 4-channel results of fragments 2p and
+    // 2p + 1 are 8 consecutive channels (one 16-byte store): fragment i, row r -> channel
+    // 32 (i / 2) + 8 (r / 4) + 4 (i % 2) + r % 4; k = 8 fq .. 8 fq + 7
     bf16x8 af[NCO];
 #pragma unroll
-    for (int i = 0; i < NCO; ++i) af[i] = *(const bf16x8*)(w + (16 * i + fr) * 32 + 8 * fq);
+    for (int i = 0; i < NCO; ++i) {
+        const int co = (NCO % 2 == 0 || i < NCO - 1) ? 32 * (i / 2) + 8 * (fr / 4) + 4 * (i % 2) + fr % 4 : 16 * i + fr;
+        af[i] = *(const bf16x8*)(w + co * 32 + 8 * fq);
+    }
     // this lane's 8 k values -> patch byte offsets (relative to the pixel's window corner); -1 = K padding
     int koff[8];
 #pragma unroll
@@ -873,7 +882,7 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
         const int k = 8 * fq + e;
         if (k < 27) {
             const int tap = k / 3, c = k % 3;  // c: 0 = R, 1 = G, 2 = B; the frame is BGR
-            koff[e] = ((tap / 3) * C0_PC + (tap % 3)) * 3 + (2 - c);
+            koff[e] = (tap / 3) * C0_PP + (tap % 3) * 3 + (2 - c);
         } else {
             koff[e] = -1;
         }
@@ -882,23 +891,40 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {  // 8 subtiles of 16 pixels per wave: rows 2*wid, 2*wid+1
         const int rl = 2 * wid + (j >> 2), cl = (j & 3) * 16 + fr;
-        const int base = ((2 * rl) * C0_PC + 2 * cl) * 3;
+        const int base = (2 * rl) * C0_PP + C0_OFF + 6 * cl;
         bf16x8 bfr;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
             bfr[e] = koff[e] >= 0 ? (__bf16)((float)patch[base + koff[e]] / 255.0f) : (__bf16)0.0f;
         const int oy = oy0 + rl, ox = ox0 + cl;
+        f32x4 acc[NCO];
 #pragma unroll
-        for (int i = 0; i < NCO; ++i) {
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc, 0, 0, 0);
-            if (oy < Ho && ox < Wo) {
-                const int co = 16 * i + 4 * fq;
-                const float4 bv = *(const float4*)(bias + co);
-                __bf16 o4[4] = {(__bf16)silu(acc[0] + bv.x), (__bf16)silu(acc[1] + bv.y),
-                                (__bf16)silu(acc[2] + bv.z), (__bf16)silu(acc[3] + bv.w)};
-                *(uint2*)(y + (((int64_t)n * Ho + oy) * Wo + ox) * ldy + co) = *(uint2*)o4;
-            }
+        for (int i = 0; i < NCO; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        if (oy >= Ho || ox >= Wo) continue;
+        __bf16* yp = y + (((int64_t)n * Ho + oy) * Wo + ox) * ldy;
+#pragma unroll
+        for (int p = 0; p < NCO / 2; ++p) {
+            const int co = 32 * p + 8 * fq;
+            const float4 b0 = *(const float4*)(bias + co), b1 = *(const float4*)(bias + co + 4);
+            bf16x8 o;
+            o[0] = (__bf16)silu(acc[2 * p][0] + b0.x);
+            o[1] = (__bf16)silu(acc[2 * p][1] + b0.y);
+            o[2] = (__bf16)silu(acc[2 * p][2] + b0.z);
+            o[3] = (__bf16)silu(acc[2 * p][3] + b0.w);
+            o[4] = (__bf16)silu(acc[2 * p + 1][0] + b1.x);
+            o[5] = (__bf16)silu(acc[2 * p + 1][1] + b1.y);
+            o[6] = (__bf16)silu(acc[2 * p + 1][2] + b1.z);
+            o[7] = (__bf16)silu(acc[2 * p + 1][3] + b1.w);
+            *(bf16x8*)(yp + co) = o;
+        }
+        if constexpr (NCO % 2) {
+            const int co = 16 * (NCO - 1) + 4 * fq;
+            const float4 bv = *(const float4*)(bias + co);
+            const f32x4 t = acc[NCO - 1];
+            __bf16 o4[4] = {(__bf16)silu(t[0] + bv.x), (__bf16)silu(t[1] + bv.y), (__bf16)silu(t[2] + bv.z),
+                            (__bf16)silu(t[3] + bv.w)};
+            *(uint2*)(yp + co) = *(uint2*)o4;
         }
     }
 }
@@ -1211,7 +1237,8 @@ int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds) {
 
 int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
                  const float* bias, int32_t Cout, void* y, int32_t ldy) {
-    if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 4)
+    if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 8 ||
+        (3 * W) % 16 || ((uintptr_t)frames & 15) || ((uintptr_t)y & 15))
         return VA_ERR_ARG;
     const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
     dim3 grid((Wo + C0_TW - 1) / C0_TW, (Ho + C0_TH - 1) / C0_TH, N);
