@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build an alternative libva355 from a modified va_seg.hip for same-box A/B timing:
+#   tools/build_variant.sh /tmp/va_seg_X.hip X   ->  vision_assist_amd/libva355_X.so
+# then on the GPU box: VA355_LIB=$PWD/vision_assist_amd/libva355_X.so python tools/seg_layer_profile.py
+set -e
+SEG=$1; NAME=$2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+CSRC=$ROOT/vision_assist_amd/csrc
+FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I$CSRC -I$ROOT/include"
+make -s -C "$CSRC" va_nav.o va_post.o
+SRC=$CSRC/.variant_$NAME.hip  # next to the real source: relative includes resolve
+cp "$SEG" "$SRC"
+/opt/rocm/bin/hipcc $FLAGS -c "$SRC" -o "$CSRC/.variant_$NAME.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/vision_assist_amd/libva355_$NAME.so" \
+    "$CSRC/va_nav.o" "$CSRC/va_post.o" "$CSRC/.variant_$NAME.o"
+rm -f "$SRC" "$CSRC/.variant_$NAME.o"
+echo "built vision_assist_amd/libva355_$NAME.so"

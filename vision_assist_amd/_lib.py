@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libva355.so")
+# VA355_LIB: load another build of the same C-ABI (same-box A/B timing of kernel variants, tools/)
+LIB_PATH = os.environ.get("VA355_LIB") or os.path.join(HERE, "libva355.so")
 
 VA_OK = 0
 VA_FRAME_OK, VA_FRAME_EMPTY, VA_FRAME_INDEX_ERROR, VA_FRAME_NO_MASK = 0, 1, 2, 3

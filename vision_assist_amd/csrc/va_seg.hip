@@ -43,7 +43,9 @@ __device__ inline __bf16 from_f<__bf16>(float v) {
     return (__bf16)v;
 }
 
-__device__ inline float silu(float x) { return x / (1.0f + __expf(-x)); }
+// bf16-output kernels: hardware exp and reciprocal (~1 ulp f32, far below the bf16 rounding that
+// follows); the exact-f32 parity path uses silu_exact
+__device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ inline float silu_exact(float x) { return x / (1.0f + expf(-x)); }
 
 // ----------------------------------------------------------------------------------------- preprocess

@@ -365,7 +365,7 @@ class SegNet:
             return False
         if p.cout == 128:
             return p2.cout <= 80
-        return p.cout in (32, 64) and p2.cout <= 64 and p.cout * (p.Kpad + 8) * 2 <= 120 * 1024
+        return p.cout in (32, 64) and p.cin >= 32 and p2.cout <= 64 and p.cout * (p.Kpad + 8) * 2 <= 120 * 1024
 
     def forward(self, frames_u8: torch.Tensor, stream=None) -> SegOutputs:
         """frames_u8: uint8 [B, H, W, 3] BGR on the device."""
