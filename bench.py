@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--cpu-sample", type=int, default=160, help="frames timed for the CPU baseline (0 = skip)")
     p.add_argument("--no-prof", action="store_true", help="skip the live per-op HIP-event timing")
+    p.add_argument("--prof-every", type=int, default=4,
+                   help="bracket every op of every N-th timed step's forward with HIP events (each event pair is a "
+                        "GPU-side packet; sampling keeps their cost out of the other steps)")
     p.add_argument("--no-overlap", action="store_true",
                    help="serial steps (no overlap of batch k's grid stage with batch k+1's network)")
     return p.parse_args()
@@ -146,17 +149,30 @@ def main():
         pipe.frames.copy_(frames[s % P], non_blocking=True)
         return pipe.run(None, pcs[s % P], prs[s % P], PLANT_IF_NONE)
 
+    lib = _lib.load()
+    sampling = {"on": False, "every": max(1, args.prof_every), "n": 0}
+
+    def sample(s):
+        """per-op events on the forward of step s (every prof_every-th step of the timed region)"""
+        if sampling["on"]:
+            on = s % sampling["every"] == 0
+            sampling["n"] += on
+            _lib.check(lib.va_prof_enable(1 if on else 0), "va_prof_enable")
+
     def run_steps(n):
         """n steps; overlapped: batch s+1's network is enqueued before batch s's grid stage runs."""
         rounds, res = 0, None
         if not overlap:
             for s in range(n):
+                sample(s)
                 res = step(s)
                 rounds += res.rounds
             return rounds, res
+        sample(0)
         opipe.submit(frames[0], pcs[0], prs[0], PLANT_IF_NONE)
         for s in range(n):
             if s + 1 < n:
+                sample(s + 1)
                 opipe.submit(frames[(s + 1) % P], pcs[(s + 1) % P], prs[(s + 1) % P], PLANT_IF_NONE)
             res = opipe.finish(opipe.k - (2 if s + 1 < n else 1))
             rounds += res.rounds
@@ -165,10 +181,10 @@ def main():
     run_steps(args.warmup)
     torch.cuda.synchronize()
 
-    lib = _lib.load()
     prof = not args.no_prof
     if prof:
         _lib.check(lib.va_prof_start(pipe.plan["n"] * args.steps + 16), "va_prof_start")
+        sampling["on"] = True
     from vision_assist_amd.shard import timed
 
     def timed_steps():
@@ -184,6 +200,7 @@ def main():
         import ctypes
         ms = (ctypes.c_double * 8)()
         cnt = (ctypes.c_int64 * 8)()
+        sampling["on"] = False
         lib.va_prof_stop(ms, cnt, 8)
         conv_ms, conv_n = ms[1] + ms[5], cnt[1] + cnt[5]  # VA_OP_CONV + VA_OP_CONV0 (layer 0 fused)
         other_seg_ms = ms[2] + ms[3] + ms[4]
@@ -201,17 +218,20 @@ def main():
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
     roofline = None
     if prof and conv_n:
-        launches_per_step = conv_n / args.steps
+        launches_per_step = conv_n / sampling["n"]  # per forward (sampled forwards only)
         # executed GEMM FLOPs of the plan (folded / fused ops counted as run, not the nominal network's)
         flops_per_launch = gflop_exec * 1e9 / launches_per_step
         avg_launch_s = conv_ms / 1e3 / conv_n
         achieved = flops_per_launch / avg_launch_s / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 5), "traffic": None,
-                    "kernel": "conv_kernel (all %d launches/step of the YOLOv8-seg forward)" % round(launches_per_step),
+                    "kernel": "conv kernels conv0/conv_dn/conv2/conv3 (all %d GEMM launches of one YOLOv8-seg forward)"
+                              % round(launches_per_step),
                     "flops_per_launch": flops_per_launch, "avg_launch_us": round(avg_launch_s * 1e6, 3),
-                    "conv_ms_per_step": round(conv_ms / args.steps, 3),
-                    "other_seg_ops_ms_per_step": round(other_seg_ms / args.steps, 3)}
+                    "conv_ms_per_step": round(conv_ms / sampling["n"], 3),
+                    "other_seg_ops_ms_per_step": round(other_seg_ms / sampling["n"], 3),
+                    "timing": f"HIP events around every op of {sampling['n']} of the {args.steps} timed forwards "
+                              f"(every {sampling['every']}-th), on the launch stream"}
         traffic_file = os.path.join(REPO, "profiles", "conv_traffic.json")
         if os.path.exists(traffic_file):
             with open(traffic_file) as f:

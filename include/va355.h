@@ -236,6 +236,9 @@ int va_prof_start(int32_t capacity);
 int va_prof_stop(double* ms_by_kind, int64_t* n_by_kind, int32_t nkinds);
 /* Per op-list index instead of per kind (call before va_prof_stop, which clears the records). */
 int va_prof_stop_ops(double* ms_by_op, int32_t nops);
+/* Suspend (on = 0) / resume (on = 1) the recording between va_prof_start and va_prof_stop, keeping the
+ * records: lets a caller sample some forwards of a timed run (each event pair is a GPU-side packet). */
+int va_prof_enable(int32_t on);
 
 /* ---------------------------------------------------------------- segmentation post-processing */
 typedef struct va_cand { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_cand;  /* NMS candidate */

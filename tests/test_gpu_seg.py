@@ -240,3 +240,19 @@ def test_conv0_fused_preprocess(cout, H, W):
     got = y.float().cpu().permute(0, 3, 1, 2)
     err = ((got - ref).abs() / (ref.abs() + 0.05)).max().item()
     assert err < 2e-2, err
+
+
+def test_conv3_matches_conv2(monkeypatch):
+    """The 256 x 128-tile kernel (conv3: three LDS-DMA stages, two K-tiles in flight) forced onto every wide
+    layer of a bf16 forward -- stride 2, residual C2f bottlenecks, Cout 224 (a ragged channel tile), the fused
+    1x1 tails, the proto sub-pixel fold (mode 2), ragged pixel tiles (M = 2 x 400 at P5) -- gives the
+    same outputs as the 128 x 128 conv2 kernel: same fragments, same MFMA order, so bit-identical."""
+    arch, fw, net = _net("bf16", "s", seed=4)
+    frames = _frames(2, seed=7)
+    monkeypatch.delenv("VA_CONV3", raising=False)
+    ref = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_CONV3", "1")
+    monkeypatch.setenv("VA_CONV3_MIN", "1")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.equal(g, r), f"{name}: conv3 vs conv2 max diff {(g - r).abs().max().item()}"

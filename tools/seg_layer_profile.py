@@ -25,7 +25,13 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
+    ap.add_argument("--ab", default="", help="env switch NAME: interleave rounds with NAME=0 and NAME=1 "
+                                            "(one process, cdna_hip_programming.md §5.4 rule 24)")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VAL set before planning")
     args = ap.parse_args()
+    for kv in args.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     from vision_assist_amd import _lib
     from vision_assist_amd.seg import SegNet
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
@@ -39,14 +45,34 @@ def main():
     torch.cuda.synchronize()
     lib = _lib.load()
     n = plan["n"]
-    _lib.check(lib.va_prof_start(n * args.iters + 8), "va_prof_start")
-    for _ in range(args.iters):
-        net.run_plan(plan)
-    ms = (ctypes.c_double * n)()
-    lib.va_prof_stop_ops(ms, n)
-    kinds = (ctypes.c_double * 8)()
-    cnt = (ctypes.c_int64 * 8)()
-    lib.va_prof_stop(kinds, cnt, 8)
+
+    def timed(iters):
+        _lib.check(lib.va_prof_start(n * iters + 8), "va_prof_start")
+        for _ in range(iters):
+            net.run_plan(plan)
+        ms = (ctypes.c_double * n)()
+        lib.va_prof_stop_ops(ms, n)
+        kinds = (ctypes.c_double * 8)()
+        cnt = (ctypes.c_int64 * 8)()
+        lib.va_prof_stop(kinds, cnt, 8)
+        return list(ms)
+
+    if args.ab:
+        tot = {"0": [0.0] * n, "1": [0.0] * n}
+        for rnd in range(args.iters):
+            for v in ("0", "1"):
+                os.environ[args.ab] = v
+                net.run_plan(plan)  # one untimed forward after the switch
+                t = timed(1)
+                tot[v] = [a + b for a, b in zip(tot[v], t)]
+        for i, m in enumerate(plan["meta"]):
+            a0, a1 = 1000 * tot["0"][i] / args.iters, 1000 * tot["1"][i] / args.iters
+            print(json.dumps({"i": i, "name": m["name"], f"{args.ab}=0": round(a0, 2), f"{args.ab}=1": round(a1, 2),
+                              "ratio": round(a1 / a0, 3) if a0 else None}))
+        s0, s1 = 1000 * sum(tot["0"]) / args.iters, 1000 * sum(tot["1"]) / args.iters
+        print(json.dumps({"total_us": {f"{args.ab}=0": round(s0, 1), f"{args.ab}=1": round(s1, 1)}}))
+        return
+    ms = timed(args.iters)
     rows = []
     tot = 0.0
     for i, m in enumerate(plan["meta"]):

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("va_prof_start", I32, [I32]),
     ("va_prof_stop", I32, [P, P, I32]),
     ("va_prof_stop_ops", I32, [P, I32]),
+    ("va_prof_enable", I32, [I32]),
     ("va_post_anchors", I32, [I32, I32]),
     ("va_post_run", I32, [P, P]),
     ("va_abi_struct_sizes", I32, [P, I32]),

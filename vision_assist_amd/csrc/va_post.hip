@@ -51,28 +51,36 @@ struct LevelPtrs {
     const float* p[3];
 };
 
-__global__ void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, int A, float conf, va_cand* cand,
-                                   int32_t* count) {
+// One 16-lane group per anchor: the group reads the anchor's class logits as consecutive 16-byte
+// chunks (one 320-byte run per anchor at nc = 80, coalesced across the group) and reduces the maximum
+// with xor shuffles inside the group.  Sigmoid is monotone, so an anchor whose best logit does not
+// clear the threshold -- nearly every anchor -- is done after that one coalesced read; the rare
+// candidate is decoded by the group's first lane.
+constexpr int DEC_GROUP = 16;
+
+__global__ __launch_bounds__(256) void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, int A,
+                                                          float conf, va_cand* cand, int32_t* count) {
     const int no = 4 * REG_MAX + nc + NMC;
-    int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (gid >= (int64_t)B * A) return;
+    const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / DEC_GROUP;
+    const int gl = threadIdx.x % DEC_GROUP;
+    if (gid >= (int64_t)B * A) return;  // whole groups leave together
     int b = (int)(gid / A), a = (int)(gid % A);
     int local;
     Level L = level_of(lv.p, H, W, a, &local);
     const float* row = L.p + ((int64_t)b * L.h * L.w + local) * no;
-    // max class logit first (16-byte loads); sigmoid is monotone, so a frame-typical anchor whose best
-    // logit does not clear the threshold exits after reading only its class logits
     const float* cl = row + 4 * REG_MAX;
     float mx = -INFINITY;
-    if ((nc & 3) == 0) {
-        for (int c = 0; c < nc; c += 4) {
-            float4 v = *(const float4*)(cl + c);
+    if ((nc & 3) == 0 && (no & 3) == 0) {
+        for (int c = 4 * gl; c < nc; c += 4 * DEC_GROUP) {
+            const float4 v = *(const float4*)(cl + c);
             mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
         }
     } else {
-        for (int c = 0; c < nc; ++c) mx = fmaxf(mx, cl[c]);
+        for (int c = gl; c < nc; c += DEC_GROUP) mx = fmaxf(mx, cl[c]);
     }
-    if (!(sigmoidf_(mx) > conf)) return;
+#pragma unroll
+    for (int o = DEC_GROUP / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, DEC_GROUP));
+    if (gl != 0 || !(sigmoidf_(mx) > conf)) return;
     // class scores: sigmoid, first maximum (cls.max(1) on sigmoid values: saturated ties -> lowest class)
     float best = -1.0f;
     int bc = 0;
@@ -418,8 +426,8 @@ int va_post_run(void* stream, const va_post_args* p) {
     const int B = p->B;
     if (hipMemsetAsync(p->cand_count, 0, sizeof(int32_t) * B, st) != hipSuccess) return VA_ERR_HIP;
     LevelPtrs lv{{p->levels[0], p->levels[1], p->levels[2]}};
-    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1((int64_t)B * A, 256)), dim3(256), 0, st, lv, B, p->H, p->W, p->nc,
-                       A, p->conf, p->cand, p->cand_count);
+    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1((int64_t)B * A * DEC_GROUP, 256)), dim3(256), 0, st, lv, B, p->H,
+                       p->W, p->nc, A, p->conf, p->cand, p->cand_count);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     static bool mask_attr = false;
     if (!mask_attr) {

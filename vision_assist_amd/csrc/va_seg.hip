@@ -307,10 +307,10 @@ __device__ __forceinline__ int64_t conv_out_row(const va_conv_args& a, int m, in
 // GEMM against the tail's weights (c2 <= 80 rows, read from L2); the tail result is the only write.
 constexpr int TAIL_C2F = 5;  // 16-row tail fragments: c2 <= 80
 
-template <int NT, int TNS, typename OutT>
+template <int NT, int BM, int TNS, typename OutT>
 __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
                                            int n0, int wm, int wn, int wid, int fr, int fq, int cls) {
-    constexpr int BM = 128, BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
+    constexpr int BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
     __bf16* Ts = (__bf16*)smem;
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
@@ -374,11 +374,83 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
     }
 }
 
+// Shared epilogue of the LDS-staged kernels: bias (+SiLU) -> f32 tile in LDS (the stage buffers are free
+// after the last barrier), then 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous
+// stores.  Needs BM * (BN + 4) * 4 bytes of LDS.
+template <int NT, int BM, int BN, int TNS, typename OutT>
+__device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
+                                              int n0, int wm, int wn, int tid, int fr, int fq, int cls) {
+    constexpr int CW = BN + 4;
+    float* Cs = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) {
+        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+        const float4 bv = *(const float4*)(a.bias + n0 + col);  // bias is padded to Npad
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
+                  v3 = acc[i][j][3] + bv.w;
+            if (a.act) {
+                v0 = silu(v0);
+                v1 = silu(v1);
+                v2 = silu(v2);
+                v3 = silu(v3);
+            }
+            *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
+        }
+    }
+    __syncthreads();
+    // ---- epilogue 2: 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous stores
+    constexpr int OV = 16 / sizeof(OutT);
+    constexpr int CPRO = BN / OV;
+    OutT* Y = (OutT*)a.y;
+    const __bf16* R = (const __bf16*)a.res;
+    for (int c = tid; c < BM * CPRO; c += NT) {
+        const int pl = c / CPRO, cl = (c % CPRO) * OV;
+        const int m = m0 + pl, co = n0 + cl;
+        if (m >= a.M || co >= a.Cout) continue;
+        float v[OV];
+#pragma unroll
+        for (int r = 0; r < OV; r += 4) {
+            const float4 t = *(const float4*)(Cs + pl * CW + cl + r);
+            v[r] = t.x;
+            v[r + 1] = t.y;
+            v[r + 2] = t.z;
+            v[r + 3] = t.w;
+        }
+        if (R) {
+#pragma unroll
+            for (int r = 0; r < OV; r += 8) {
+                const u32x4 rr = *(const u32x4*)(R + (int64_t)m * a.ldr + co + r);
+                const __bf16* rp = (const __bf16*)&rr;
+#pragma unroll
+                for (int e = 0; e < 8 && r + e < OV; ++e) v[r + e] += (float)rp[e];
+            }
+        }
+        OutT* yp;
+        if (a.mode == 1) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            const int cd = a.Cout / 4, q = co / cd, cc = co - q * cd;
+            yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + cc;
+        } else {
+            yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
+        }
+        if constexpr (sizeof(OutT) == 2) {
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+            *(bf16x8*)yp = o;
+        } else {
+            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
 template <int WM, int WN, int TNS, typename OutT, bool GLDS = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
     using Cfg = Conv2Cfg<WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
-    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, CW = Cfg::CW, RS = Cfg::RS;
+    constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, RS = Cfg::RS;
     __shared__ __align__(16) unsigned char smem[Cfg::LDS];
     auto As = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE); };
     auto Bs = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE + BN * RS * 2); };
@@ -545,76 +617,158 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_STORE
 #undef CONV2_DMA
 
-    if constexpr (BN == 128 && BM == 128) {
+    if constexpr (BN == 128) {
         if (a.w2) {
-            conv2_tail<NT, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq, cls);
+            conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq, cls);
             return;
         }
     }
-    // ---- epilogue 1: bias (+SiLU) -> f32 tile in LDS (the stage buffers are free after the last barrier)
-    float* Cs = (float*)smem;
-#pragma unroll
-    for (int i = 0; i < TNS; ++i) {
-        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
-        const float4 bv = *(const float4*)(a.bias + n0 + col);  // bias is padded to Npad
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
-                  v3 = acc[i][j][3] + bv.w;
-            if (a.act) {
-                v0 = silu(v0);
-                v1 = silu(v1);
-                v2 = silu(v2);
-                v3 = silu(v3);
-            }
-            *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
-        }
+    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, tid, fr, fq, cls);
+}
+
+// ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
+// 256-pixel x 128-channel tiles for the large layers: 8 waves (4 x 2, each 64 pixels x 64 channels as in
+// conv2), BK = 64, THREE LDS stages filled by LDS-DMA with two K-tiles in flight.  Per K-step: a counted
+// vmcnt that retires only this wave's DMAs of tile kt (2 weight + 4 pixel instructions per tile), a raw
+// s_barrier (a __syncthreads() would add vmcnt(0) and drain the prefetch: cdna_hip_programming.md §5
+// "Pipelining across barriers"), the DMA of tile kt + 2 into the stage every wave finished reading at step
+// kt - 1, then the MFMAs of tile kt.  The XOR swizzle, incremental im2col, epilogue and fused 1x1 tail are
+// conv2's (GLDS form); one 512-thread workgroup per CU (144 KiB of LDS).
+constexpr int C3_BM = 256, C3_BN = 128, C3_NT = 512;
+constexpr int C3_STAGE = (C3_BM + C3_BN) * BK2 * 2;  // 48 KiB
+constexpr int C3_LDS = 3 * C3_STAGE;                 // 144 KiB
+static_assert(C3_BM * (C3_BN + 4) * 4 <= C3_LDS, "epilogue tile must fit the stage buffers");
+
+template <typename OutT, int ABL = 0>  // ABL (diagnosis only): 1 = no in-loop DMA, 2 = no MFMA
+__global__ __launch_bounds__(C3_NT) void conv3_kernel(va_conv_args a, int ntn, int ntiles) {
+    constexpr int NT = C3_NT, BM = C3_BM, BN = C3_BN, TNS = 4, WN = 2;
+    constexpr int A_CH = BN * 8 / NT, B_CH = BM * 8 / NT, RSTEP = NT / 8;  // 2, 4, 64
+    static_assert(A_CH + B_CH == 6, "vmcnt(6) below counts one tile of DMAs per wave");
+    extern __shared__ __align__(16) unsigned char smem3[];
+
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
-    __syncthreads();
-    // ---- epilogue 2: 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous stores
-    constexpr int OV = 16 / sizeof(OutT);
-    constexpr int CPRO = BN / OV;
-    OutT* Y = (OutT*)a.y;
-    const __bf16* R = (const __bf16*)a.res;
-    for (int c = tid; c < BM * CPRO; c += NT) {
-        const int pl = c / CPRO, cl = (c % CPRO) * OV;
-        const int m = m0 + pl, co = n0 + cl;
-        if (m >= a.M || co >= a.Cout) continue;
-        float v[OV];
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+    const __bf16* __restrict__ Wt = (const __bf16*)a.w + (int64_t)cls * a.Npad * a.Kpad;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    // DMA instruction i of wave w writes rows RSTEP i + 8 w .. +7 (lane l: row l >> 3, slot l & 7, which
+    // holds chunk (l & 7) ^ (l >> 3) of that row)
+    const int g = (lane & 7) ^ (lane >> 3);
+    const int row0 = 8 * wid + (lane >> 3);
+    int b_hi[B_CH], b_wi[B_CH];
+    int64_t b_base[B_CH];
 #pragma unroll
-        for (int r = 0; r < OV; r += 4) {
-            const float4 t = *(const float4*)(Cs + pl * CW + cl + r);
-            v[r] = t.x;
-            v[r + 1] = t.y;
-            v[r + 2] = t.z;
-            v[r + 3] = t.w;
-        }
-        if (R) {
-#pragma unroll
-            for (int r = 0; r < OV; r += 8) {
-                const u32x4 rr = *(const u32x4*)(R + (int64_t)m * a.ldr + co + r);
-                const __bf16* rp = (const __bf16*)&rr;
-#pragma unroll
-                for (int e = 0; e < 8 && r + e < OV; ++e) v[r + e] += (float)rp[e];
-            }
-        }
-        OutT* yp;
-        if (a.mode == 1) {
+    for (int i = 0; i < B_CH; ++i) {
+        const int m = m0 + row0 + RSTEP * i;
+        if (m < a.M) {
             const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            const int cd = a.Cout / 4, q = co / cd, cc = co - q * cd;
-            yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + cc;
+            b_hi[i] = ho * a.stride - pad_y;
+            b_wi[i] = wo * a.stride - pad_x;
+            b_base[i] = (int64_t)n * a.H * a.W;
         } else {
-            yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
-        }
-        if constexpr (sizeof(OutT) == 2) {
-            bf16x8 o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
-            *(bf16x8*)yp = o;
-        } else {
-            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+            b_hi[i] = -(1 << 28);
+            b_wi[i] = 0;
+            b_base[i] = 0;
         }
     }
+    int ci = 8 * g, ky = 0, kx = 0;
+    while (ci >= a.Cin) {
+        ci -= a.Cin;
+        if (++kx == a.kw) {
+            kx = 0;
+            ++ky;
+        }
+    }
+    int kcur = 8 * g;  // this lane's k of the next tile to stage (weights and pixels alike)
+
+#define CONV3_DMA(s)                                                                                               \
+    {                                                                                                              \
+        __bf16* as_ = (__bf16*)(smem3 + (s) * C3_STAGE);                                                           \
+        __bf16* bs_ = as_ + BN * BK2;                                                                              \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
+            const __bf16* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + kcur;                             \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+                                             0);                                                                   \
+        }                                                                                                          \
+        const bool kin = kcur < a.K;                                                                               \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
+            const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
+            const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
+            const void* src = ok ? (const void*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci)            \
+                                 : (const void*)g_zero_page;                                                       \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+                                             0);                                                                   \
+        }                                                                                                          \
+        kcur += BK2;                                                                                               \
+        ci += BK2;                                                                                                 \
+        while (ci >= a.Cin) {                                                                                      \
+            ci -= a.Cin;                                                                                           \
+            if (++kx == a.kw) {                                                                                    \
+                kx = 0;                                                                                            \
+                ++ky;                                                                                              \
+            }                                                                                                      \
+        }                                                                                                          \
+    }
+
+    f32x4 acc[TNS][4];
+#pragma unroll
+    for (int i = 0; i < TNS; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.Kpad / BK2;
+    CONV3_DMA(0);
+    if (nk > 1) CONV3_DMA(1);
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        // tile kt landed (this wave's part); tile kt + 1 stays in flight across the barrier
+        if (kt + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (ABL != 1 && kt + 2 < nk) {
+            const int sn = (kt + 2) % 3;
+            CONV3_DMA(sn);
+        }
+        const __bf16* as_ = (const __bf16*)(smem3 + (kt % 3) * C3_STAGE);
+        const __bf16* bs_ = as_ + BN * BK2;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            bf16x8 af[TNS], bfr[4];
+            const int ch = ((4 * kh + fq) ^ (fr & 7)) * 8;  // swizzled slot of chunk 4 kh + fq
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(as_ + (wn * 64 + 16 * i + fr) * BK2 + ch);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * BK2 + ch);
+            if constexpr (ABL == 2) {
+#pragma unroll
+                for (int i = 0; i < TNS; ++i) asm volatile("" ::"v"(af[i]), "v"(bfr[i]));
+                continue;
+            }
+#pragma unroll
+            for (int i = 0; i < TNS; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+#undef CONV3_DMA
+    __syncthreads();  // every wave is done with the stages (no DMA in flight): reuse them for the epilogue
+    if (a.w2) {
+        conv2_tail<NT, BM, TNS, OutT>(a, acc, smem3, m0, n0, wm, wn, wid, fr, fq, cls);
+        return;
+    }
+    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem3, m0, n0, wm, wn, tid, fr, fq, cls);
 }
 
 // ----------------------------------------------------------------------------------------- small-N conv
@@ -1050,6 +1204,43 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// VA_CONV3=1 moves the wide layers to conv3 (A/B timing; read per launch so one process can compare).
+// Off by default: measured 4-19 % slower than conv2 on every wide layer of the s-seg forward (the deeper
+// prefetch does not pay while the LDS-DMA path itself delivers only ~43 GB/s per CU, profiles/r01/).
+// VA_CONV3_MIN = fewest 256 x 128 tiles for which conv3 is used (default 256: one per CU)
+bool use_conv3(const va_conv_args& a) {
+    const char* e = getenv("VA_CONV3");
+    if (!e || e[0] != '1') return false;
+    if (a.Cin % 8 || a.ldx % 8 || ((uintptr_t)a.x & 15) || a.Kpad % BK2 || a.Npad % C3_BN) return false;
+    const char* mn = getenv("VA_CONV3_MIN");
+    const int64_t min_tiles = mn ? atoll(mn) : 256;
+    const int64_t tiles = (int64_t)((a.M + C3_BM - 1) / C3_BM) * ((a.Cout + C3_BN - 1) / C3_BN) * (a.mode == 2 ? 4 : 1);
+    return tiles >= min_tiles;
+}
+
+template <typename OutT, int ABL>
+hipError_t launch_conv3_v(const va_conv_args& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv3_kernel<OutT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                C3_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    const int ntm = (a.M + C3_BM - 1) / C3_BM, ntn = (a.Cout + C3_BN - 1) / C3_BN;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3_kernel<OutT, ABL>), dim3(ntiles), dim3(C3_NT), C3_LDS, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t launch_conv3(const va_conv_args& a, hipStream_t st) {
+    const char* e = getenv("VA_CONV3_ABL");  // diagnosis only (wrong results)
+    if (e && e[0] == '1') return launch_conv3_v<OutT, 1>(a, st);
+    if (e && e[0] == '2') return launch_conv3_v<OutT, 2>(a, st);
+    return launch_conv3_v<OutT, 0>(a, st);
+}
+
 // VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
 bool getenv_dn() {
     static int v = -1;
@@ -1071,7 +1262,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
                 a.c2 % 4 == 0 &&
                 a.Kpad % BK2 == 0 && a.ldy % 4 == 0)
-                return launch_conv2<2, 2, 4, OutT>(a, st);
+                return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
         }
         return hipErrorInvalidValue;
     }
@@ -1091,13 +1282,13 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         constexpr int OV = 16 / sizeof(OutT);
         if (a.mode == 2) {  // sub-pixel classes: the 128-wide LDS-staged tile only
             if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && a.Cout > 64)
-                return launch_conv2<2, 2, 4, OutT>(a, st);
+                return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
             return hipErrorInvalidValue;
         }
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
             if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
-            return launch_conv2<2, 2, 4, OutT>(a, st);
+            return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
     // tile choice: small Cout -> tall pixel tiles
@@ -1199,6 +1390,12 @@ int va_prof_start(int32_t capacity) {
     }
     g_ev_used = 0;
     g_prof_on = 1;
+    return VA_OK;
+}
+
+int va_prof_enable(int32_t on) {
+    if (!g_ev_cap) return VA_ERR_ARG;
+    g_prof_on = on ? 1 : 0;
     return VA_OK;
 }
 
