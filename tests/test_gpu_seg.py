@@ -89,6 +89,8 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
     (96, 80, 1, 1, 13, 13, False, False, 0),
     (16, 256, 3, 2, 40, 40, False, False, 0),
     (64, 32, 2, 1, 10, 12, False, True, 0),
+    (64, 32, 3, 1, 23, 41, False, False, 8),   # patch kernel: ragged 16 x 16 tiles, channel slice
+    (64, 64, 3, 1, 37, 16, True, False, 0),    # patch kernel: residual
 ])
 def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
     got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in, act=not deconv)
@@ -256,3 +258,23 @@ def test_conv3_matches_conv2(monkeypatch):
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: conv3 vs conv2 max diff {(g - r).abs().max().item()}"
+
+
+def test_patch_conv_matches_dn(monkeypatch):
+    """The patch-staged narrow 3x3 kernel (input patch in LDS once per 16 x 16 tile) against the im2col
+    narrow-layer kernel on a whole bf16 forward (P2/P3 bottlenecks with residuals, the fused head tails).
+    The 3x3 GEMMs use the same fragments and K order (bit-identical: cls and proto, which only see those);
+    the fused 1x1 tails (box and coef branches) sum their 64 / 32 channels in a different order (the patch
+    kernel's channel-permuted weights make the tail's K order natural), so those agree to f32 rounding."""
+    arch, fw, net = _net("bf16", "s", seed=8)
+    frames = _frames(2, seed=9)
+    monkeypatch.setenv("VA_CONV_PATCH", "0")
+    ref = _gpu_heads(net, frames)
+    monkeypatch.delenv("VA_CONV_PATCH")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        if name in ("cls", "proto"):
+            assert torch.equal(g, r), f"{name}: patch vs dn max diff {(g - r).abs().max().item()}"
+        else:
+            err = ((g - r).abs().max() / r.abs().max()).item()
+            assert err < 1e-5, f"{name}: patch vs dn rel diff {err}"

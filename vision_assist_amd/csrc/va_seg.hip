@@ -970,6 +970,223 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
     }
 }
 
+// ----------------------------------------------------------------------------------------- patch conv
+// Narrow stride-1 3x3 convs (Cout 32 / 64, Cin 32 / 64: the C2f bottlenecks of P2/P3 and the head's box /
+// coefficient branches).  The im2col kernels fetch every input pixel nine times through L2 (once per tap)
+// and are latency-bound on those gathers; here, per 16 x 16 output tile, the 18 x 18-pixel input patch is
+// staged ONCE into LDS by LDS-DMA and all nine taps read their B fragments from it, while the whole weight
+// matrix stays in LDS for the launch.  Persistent workgroups walk the tiles with two patch buffers: the
+// next tile's patch streams in while the current one is computed.  4 waves, wave w = output rows
+// 4w .. 4w+3 (four 16-pixel MFMA fragments) x all Cout; no barrier inside a tile.
+//
+// Patch image: pixel p (row-major in the 18 x 18 patch) holds its Cin channels as CPP = Cin/8 16-byte
+// chunks; 16/CPP pixels share a 256-byte bank row, and chunk c of pixel p sits in slot
+// c ^ ((p / (16/CPP)) % CPP) of its pixel's CPP slots, so the 16 lanes of a B-fragment read (16
+// consecutive pixels, one chunk) hit 16 distinct slots.  A DMA instruction writes 1 KiB lane-linearly;
+// lane l fetches the chunk that its slot holds (the XOR is an involution).
+constexpr int PT = 16;  // output tile edge
+constexpr int PW3 = PT + 2;
+
+template <int CPP>
+__device__ __forceinline__ int patch_off(int p, int c) {
+    return p * (CPP * 16) + 16 * (c ^ ((p / (16 / CPP)) % CPP));
+}
+
+template <int TNS, int CPP, bool TAIL, typename OutT, int NW, int ABL = 0>  // NW waves; ABL: diagnosis only
+__global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int wstride, int tiles_x, int tiles_y,
+                                                             int ntiles, int patch_bytes) {
+    constexpr int NT = 64 * NW, RPW = PT / NW;       // threads, output rows (16-pixel fragments) per wave
+    constexpr int NKS = 9 * CPP / 4;               // 32-deep K steps: 9 taps x Cin / 32
+    constexpr int PPI = 64 / CPP;                   // patch pixels per DMA instruction
+    constexpr int NI = (PW3 * PW3 + PPI - 1) / PPI; // DMA instructions per patch
+    extern __shared__ __align__(16) unsigned char smemp[];
+    __bf16* wsh = (__bf16*)smemp;                              // [16*TNS][wstride]
+    unsigned char* pbuf = smemp + 16 * TNS * wstride * 2;     // 2 x patch_bytes
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+
+    auto stage_patch = [&](int tile, unsigned char* dst) {
+        const int tx = tile % tiles_x, t2 = tile / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+        const int iy0 = PT * ty - 1, ix0 = PT * tx - 1;
+        for (int i = wid; i < NI; i += NW) {
+            const int off = i * 1024 + 16 * lane;
+            const int p = off / (CPP * 16), slot = (off / 16) % CPP;
+            const int c = slot ^ ((p / (16 / CPP)) % CPP);
+            const int iy = iy0 + p / PW3, ix = ix0 + p % PW3;
+            const bool ok = p < PW3 * PW3 && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            const void* src = ok ? (const void*)(X + (((int64_t)n * a.H + iy) * a.W + ix) * a.ldx + 8 * c)
+                                 : (const void*)g_zero_page;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(dst + i * 1024), 16, 0, 0);
+        }
+    };
+
+    int tile = blockIdx.x;
+    if (tile < ntiles) stage_patch(tile, pbuf);
+    // weights -> LDS once, rows permuted so that MFMA fragments 2p and 2p + 1 give each lane 8 consecutive
+    // output channels (one 16-byte store): LDS row 16 i + r holds channel 32 (i/2) + 8 (r/4) + 4 (i%2) + r%4
+    static_assert(TNS % 2 == 0, "fragments pair up");
+    const int chunks = NKS * 4;
+    for (int i = tid; i < 16 * TNS * chunks; i += NT) {
+        const int r = i / chunks, c = i - r * chunks;
+        const int fi = r / 16, rr = r % 16;
+        const int ch = 32 * (fi / 2) + 8 * (rr / 4) + 4 * (fi % 2) + rr % 4;
+        *(u32x4*)(wsh + r * wstride + 8 * c) = *(const u32x4*)((const __bf16*)a.w + (int64_t)ch * a.Kpad + 8 * c);
+    }
+    constexpr int TKF = TAIL ? TNS / 2 : 1;
+    bf16x8 w2f[DN_TAIL_C2F][TKF];
+    if constexpr (TAIL) {
+        // with the row permutation a lane's fragments 2 kf, 2 kf + 1 hold channels 32 kf + 8 fq + (0..7): the
+        // tail's K fragment kf in natural order
+        const __bf16* W2 = (const __bf16*)a.w2;
+#pragma unroll
+        for (int c = 0; c < DN_TAIL_C2F; ++c)
+#pragma unroll
+            for (int kf = 0; kf < TKF; ++kf)
+                w2f[c][kf] = 16 * c < a.c2 ? *(const bf16x8*)(W2 + (16 * c + fr) * (16 * TNS) + 32 * kf + 8 * fq)
+                                           : (bf16x8){};
+    }
+    float4 bv[TNS];
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) bv[i] = *(const float4*)(a.bias + 32 * (i / 2) + 8 * fq + 4 * (i % 2));
+
+    for (int it = 0; tile < ntiles; tile += gridDim.x, ++it) {
+        unsigned char* cur = pbuf + (it & 1) * patch_bytes;
+        // this tile's patch has landed (every wave's DMAs), and every wave is done with the other buffer
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int next = tile + gridDim.x;
+        if (ABL != 2 && next < ntiles) stage_patch(next, pbuf + ((it + 1) & 1) * patch_bytes);
+
+        f32x4 acc[RPW][TNS];
+#pragma unroll
+        for (int j = 0; j < RPW; ++j)
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const int tap = s / (CPP / 4), ky = tap / 3, kx = tap % 3;
+            const int c = (s % (CPP / 4)) * 4 + fq;
+            bf16x8 af[TNS], bfr[RPW];
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(wsh + (16 * i + fr) * wstride + 32 * s + 8 * fq);
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                const int p = (RPW * wid + j + ky) * PW3 + fr + kx;
+                bfr[j] = *(const bf16x8*)(cur + patch_off<CPP>(p, c));
+            }
+            if constexpr (ABL == 1) {
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) asm volatile("" ::"v"(bfr[j]));
+#pragma unroll
+                for (int i = 0; i < TNS; ++i) asm volatile("" ::"v"(af[i]));
+                continue;
+            }
+#pragma unroll
+            for (int j = 0; j < RPW; ++j)
+#pragma unroll
+                for (int i = 0; i < TNS; ++i)
+                    acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[j][i], 0, 0, 0);
+        }
+
+        const int tx = tile % tiles_x, t2 = tile / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+        const int ox = PT * tx + fr;
+        if constexpr (TAIL) {
+            f32x4 acc2[RPW][DN_TAIL_C2F];
+#pragma unroll
+            for (int j = 0; j < RPW; ++j)
+#pragma unroll
+                for (int c = 0; c < DN_TAIL_C2F; ++c) acc2[j][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kf = 0; kf < TKF; ++kf)
+#pragma unroll
+                for (int j = 0; j < RPW; ++j) {
+                    bf16x8 b;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int i = 2 * kf + h;
+                        const float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
+                                            acc[j][i][3] + bv[i].w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+                    }
+#pragma unroll
+                    for (int c = 0; c < DN_TAIL_C2F; ++c)
+                        acc2[j][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[c][kf], b, acc2[j][c], 0, 0, 0);
+                }
+            OutT* Y2 = (OutT*)a.y;
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                const int oy = PT * ty + RPW * wid + j;
+                if (oy >= a.Ho || ox >= a.Wo) continue;
+                const int64_t m = ((int64_t)n * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+                for (int c = 0; c < DN_TAIL_C2F; ++c) {
+                    const int co = 16 * c + 4 * fq;
+                    if (co >= a.c2) continue;
+                    const float4 b2 = *(const float4*)(a.b2 + co);
+                    float v[4] = {acc2[j][c][0] + b2.x, acc2[j][c][1] + b2.y, acc2[j][c][2] + b2.z,
+                                  acc2[j][c][3] + b2.w};
+                    if (a.act2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                    }
+                    OutT* yp = Y2 + m * a.ldy + co;
+                    if constexpr (sizeof(OutT) == 2) {
+                        __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                        *(uint2*)yp = *(uint2*)o4;
+                    } else {
+                        *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+                    }
+                }
+            }
+            continue;
+        }
+        __bf16* Y = (__bf16*)a.y;
+        const __bf16* R = (const __bf16*)a.res;
+        if (ABL == 3) {
+#pragma unroll
+            for (int j = 0; j < RPW; ++j)
+#pragma unroll
+                for (int i = 0; i < TNS; ++i) asm volatile("" ::"v"(acc[j][i]));
+            continue;
+        }
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int oy = PT * ty + RPW * wid + j;
+            if (oy >= a.Ho || ox >= a.Wo) continue;
+            const int64_t m = ((int64_t)n * a.Ho + oy) * a.Wo + ox;
+#pragma unroll
+            for (int q = 0; q < TNS / 2; ++q) {
+                const int co = 32 * q + 8 * fq;  // 8 consecutive channels: fragments 2q (first 4), 2q + 1
+                float v[8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x4 t = acc[j][2 * q + h];
+                    const float4 b4 = bv[2 * q + h];
+                    v[4 * h] = t[0] + b4.x;
+                    v[4 * h + 1] = t[1] + b4.y;
+                    v[4 * h + 2] = t[2] + b4.z;
+                    v[4 * h + 3] = t[3] + b4.w;
+                }
+                if (a.act) {
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] = silu(v[r]);
+                }
+                if (R) {
+                    const bf16x8 rr = *(const bf16x8*)(R + m * a.ldr + co);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[r] += (float)rr[r];
+                }
+                bf16x8 o;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = (__bf16)v[r];
+                *(bf16x8*)(Y + m * a.ldy + co) = o;
+            }
+        }
+    }
+}
+
 template <int TNS, bool TAIL = false, typename OutT = __bf16>
 hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
@@ -1241,6 +1458,67 @@ hipError_t launch_conv3(const va_conv_args& a, hipStream_t st) {
     return launch_conv3_v<OutT, 0>(a, st);
 }
 
+// VA_CONV_PATCH=0 keeps the narrow 3x3 layers on conv_dn (A/B timing; read per launch)
+bool use_patch(const va_conv_args& a) {
+    const char* e = getenv("VA_CONV_PATCH");
+    if (e && e[0] == '0') return false;
+    return a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.mode == 0 && (a.Cin == 32 || a.Cin == 64) &&
+           (a.Cout == 32 || a.Cout == 64) && a.K == 9 * a.Cin && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 &&
+           a.Ho == a.H && a.Wo == a.W && (a.w2 ? a.ldy % 4 == 0 : (a.ldy % 8 == 0 && ((uintptr_t)a.y & 15) == 0)) &&
+           (!a.res || (a.ldr % 8 == 0 && ((uintptr_t)a.res & 15) == 0));
+}
+
+template <int TNS, int CPP, bool TAIL, typename OutT, int NW, int ABL>
+hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
+    const int K = 9 * CPP * 8;
+    const int wstride = K + 8;
+    constexpr int PPI = 64 / CPP, NI = (PW3 * PW3 + PPI - 1) / PPI;
+    const int patch_bytes = NI * 1024;
+    const size_t lds = (size_t)16 * TNS * wstride * 2 + 2 * (size_t)patch_bytes;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, ABL>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int tiles_x = (a.Wo + PT - 1) / PT, tiles_y = (a.Ho + PT - 1) / PT;
+    const int ntiles = a.N * tiles_x * tiles_y;
+    const int per_cu = (int)((160 * 1024) / lds);
+    int blocks = 256 * (per_cu < 1 ? 1 : per_cu);
+    if (blocks > ntiles) blocks = ntiles;
+    hipLaunchKernelGGL((conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, ABL>), dim3(blocks), dim3(64 * NW), lds, st, a,
+                       wstride, tiles_x, tiles_y, ntiles, patch_bytes);
+    return hipGetLastError();
+}
+
+// VA_PATCH_NW = waves per workgroup (4 or 8, default 8); VA_PATCH_ABL (diagnosis only, wrong results):
+// 1 = no MFMA, 2 = no in-loop patch DMA, 3 = no epilogue
+template <int TNS, int CPP, bool TAIL, typename OutT>
+hipError_t launch_conv_patch_v(const va_conv_args& a, hipStream_t st) {
+    const char* w = getenv("VA_PATCH_NW");
+    const char* e = getenv("VA_PATCH_ABL");
+    const int abl = e ? e[0] - '0' : 0;
+    if (w && w[0] == '4') {
+        if (abl == 1) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 4, 1>(a, st);
+        if (abl == 2) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 4, 2>(a, st);
+        if (abl == 3) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 4, 3>(a, st);
+        return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 4, 0>(a, st);
+    }
+    if (abl == 1) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 1>(a, st);
+    if (abl == 2) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 2>(a, st);
+    if (abl == 3) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 3>(a, st);
+    return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 0>(a, st);
+}
+
+template <bool TAIL, typename OutT>
+hipError_t launch_conv_patch(const va_conv_args& a, hipStream_t st) {
+    if (a.Cin == 32)
+        return a.Cout == 32 ? launch_conv_patch_v<2, 4, TAIL, OutT>(a, st) : launch_conv_patch_v<4, 4, TAIL, OutT>(a, st);
+    return a.Cout == 32 ? launch_conv_patch_v<2, 8, TAIL, OutT>(a, st) : launch_conv_patch_v<4, 8, TAIL, OutT>(a, st);
+}
+
 // VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
 bool getenv_dn() {
     static int v = -1;
@@ -1257,8 +1535,10 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         if constexpr (sizeof(T) == 2) {
             if ((a.Cout == 32 || a.Cout == 64) && a.mode == 0 && !a.res && a.b2 && a.c2 > 0 &&
                 a.c2 <= 16 * DN_TAIL_C2F && a.c2 % 4 == 0 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
-                (size_t)a.Cout * (a.Kpad + 8) * 2 <= 120 * 1024)
+                (size_t)a.Cout * (a.Kpad + 8) * 2 <= 120 * 1024) {
+                if (use_patch(a)) return launch_conv_patch<true, OutT>(a, st);
                 return a.Cout == 32 ? launch_conv_dn<2, true, OutT>(a, st) : launch_conv_dn<4, true, OutT>(a, st);
+            }
             if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
                 a.c2 % 4 == 0 &&
                 a.Kpad % BK2 == 0 && a.ldy % 4 == 0)
@@ -1269,6 +1549,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
         if constexpr (sizeof(OutT) == 2) {
             // narrow layers: weights in LDS, activations straight into MFMA fragments
+            if (use_patch(a)) return launch_conv_patch<false, __bf16>(a, st);
             if (a.mode == 0 && a.Cout <= 64 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
                 (size_t)16 * ((a.Cout + 15) / 16) * (a.Kpad + 8) * 2 <= 120 * 1024 && getenv_dn()) {
                 switch ((a.Cout + 15) / 16) {
