@@ -91,6 +91,8 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
     (64, 32, 2, 1, 10, 12, False, True, 0),
     (64, 32, 3, 1, 23, 41, False, False, 8),   # patch kernel: ragged 16 x 16 tiles, channel slice
     (64, 64, 3, 1, 37, 16, True, False, 0),    # patch kernel: residual
+    (128, 256, 3, 1, 19, 23, True, False, 0),  # wide patch kernel: ragged tiles, two channel tiles, residual
+    (64, 136, 3, 1, 16, 40, False, False, 64), # wide patch kernel: ragged channel tile, channel slice
 ])
 def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
     got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in, act=not deconv)
@@ -278,3 +280,21 @@ def test_patch_conv_matches_dn(monkeypatch):
         else:
             err = ((g - r).abs().max() / r.abs().max()).item()
             assert err < 1e-5, f"{name}: patch vs dn rel diff {err}"
+
+
+def test_wide_patch_conv_matches_conv2(monkeypatch):
+    """The wide patch kernel (off by default, VA_CONV_WP=1; 16 x 16 output tile, 18 x 18 patch per 64-channel chunk, weights streamed per
+    tap) against the im2col conv2 kernel on a whole bf16 forward: its K order is chunk-major / tap-minor
+    instead of tap-major, so the two agree to accumulation-order rounding, amplified through ~60 layers of
+    bf16 storage; both must be equally close to the fp32 torch reference."""
+    arch, fw, net = _net("bf16", "s", seed=10)
+    frames = _frames(2, seed=11)
+    f32 = _ref_heads(arch, fw, frames)
+    monkeypatch.delenv("VA_CONV_WP", raising=False)
+    ref = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_CONV_WP", "1")
+    got = _gpu_heads(net, frames)
+    rel = lambda g, r: ((g - r).norm() / r.norm()).item()
+    for name, g, r, t in zip(("box", "cls", "coef", "proto"), got, ref, f32):
+        assert rel(g, r) < 1e-2, f"{name}: wide patch vs conv2 relative L2 {rel(g, r)}"
+        assert rel(g, t) < 1.25 * rel(r, t) + 1e-3, f"{name}: vs fp32 {rel(g, t)} (conv2 {rel(r, t)})"

@@ -309,9 +309,10 @@ __device__ __forceinline__ int64_t conv_out_row(const va_conv_args& a, int m, in
 // GEMM against the tail's weights (c2 <= 80 rows, read from L2); the tail result is the only write.
 constexpr int TAIL_C2F = 5;  // 16-row tail fragments: c2 <= 80
 
-template <int NT, int BM, int TNS, typename OutT>
-__device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
-                                           int n0, int wm, int wn, int wid, int fr, int fq, int cls) {
+// orow(pl): output row (pixel index of the output tensor) of tile row pl, or -1 when masked
+template <int NT, int BM, int TNS, typename OutT, typename RowFn>
+__device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
+                                           int wm, int wn, int wid, int fr, int fq, RowFn orow) {
     constexpr int BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
     __bf16* Ts = (__bf16*)smem;
 #pragma unroll
@@ -353,8 +354,8 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
     OutT* Y = (OutT*)a.y;
 #pragma unroll
     for (int p = 0; p < PS; ++p) {
-        const int m = m0 + wid * PS * 16 + 16 * p + fr;
-        if (m >= a.M) continue;
+        const int64_t orw = orow(wid * PS * 16 + 16 * p + fr);
+        if (orw < 0) continue;
 #pragma unroll
         for (int c = 0; c < TAIL_C2F; ++c) {
             const int co = 16 * c + 4 * fq;
@@ -365,7 +366,7 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
             }
-            OutT* yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
+            OutT* yp = Y + orw * a.ldy + co;
             if constexpr (sizeof(OutT) == 2) {
                 __bf16 o4[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
                 *(uint2*)yp = *(uint2*)o4;
@@ -379,9 +380,10 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 // Shared epilogue of the LDS-staged kernels: bias (+SiLU) -> f32 tile in LDS (the stage buffers are free
 // after the last barrier), then 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous
 // stores.  Needs BM * (BN + 4) * 4 bytes of LDS.
-template <int NT, int BM, int BN, int TNS, typename OutT>
-__device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int m0,
-                                              int n0, int wm, int wn, int tid, int fr, int fq, int cls) {
+// orow(pl): output row of tile row pl (mode 1: the linear GEMM row, scattered below), or -1 when masked
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn>
+__device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
+                                              int wm, int wn, int tid, int fr, int fq, RowFn orow) {
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
 #pragma unroll
@@ -409,8 +411,9 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
     const __bf16* R = (const __bf16*)a.res;
     for (int c = tid; c < BM * CPRO; c += NT) {
         const int pl = c / CPRO, cl = (c % CPRO) * OV;
-        const int m = m0 + pl, co = n0 + cl;
-        if (m >= a.M || co >= a.Cout) continue;
+        const int co = n0 + cl;
+        const int64_t orw = orow(pl);
+        if (orw < 0 || co >= a.Cout) continue;
         float v[OV];
 #pragma unroll
         for (int r = 0; r < OV; r += 4) {
@@ -423,7 +426,7 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
         if (R) {
 #pragma unroll
             for (int r = 0; r < OV; r += 8) {
-                const u32x4 rr = *(const u32x4*)(R + (int64_t)m * a.ldr + co + r);
+                const u32x4 rr = *(const u32x4*)(R + orw * a.ldr + co + r);
                 const __bf16* rp = (const __bf16*)&rr;
 #pragma unroll
                 for (int e = 0; e < 8 && r + e < OV; ++e) v[r + e] += (float)rp[e];
@@ -431,11 +434,12 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
         }
         OutT* yp;
         if (a.mode == 1) {
+            const int m = (int)orw;
             const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
             const int cd = a.Cout / 4, q = co / cd, cc = co - q * cd;
             yp = Y + (((int64_t)n * 2 * a.Ho + 2 * ho + (q >> 1)) * 2 * a.Wo + 2 * wo + (q & 1)) * a.ldy + cc;
         } else {
-            yp = Y + conv_out_row(a, m, cls) * a.ldy + co;
+            yp = Y + orw * a.ldy + co;
         }
         if constexpr (sizeof(OutT) == 2) {
             bf16x8 o;
@@ -448,7 +452,11 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
     }
 }
 
-template <int WM, int WN, int TNS, typename OutT, bool GLDS = false>
+// FK (LDS-DMA form, Cin % 64 == 0): a 64-deep K-step never straddles a tap, so (ky, kx, channel base) are
+// wave-uniform scalars and each staged row keeps a precomputed base pointer: per K-step and row the B
+// address is one 64-bit add of a scalar offset plus a bounds select (the general form re-derives the
+// im2col coordinates of every lane with 64-bit multiplies).
+template <int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
     using Cfg = Conv2Cfg<WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
@@ -502,6 +510,17 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         }
     }
     int kcur = 8 * g;
+    // FK state: per-row base pointers (pixel at tap (0, 0), this lane's 8-channel group) and weight rows
+    const __bf16* rowp[B_CH];
+    const __bf16* wrow[A_CH];
+    int fk_ky = 0, fk_kx = 0, fk_c = 0;  // tap and 64-channel chunk of the next K-step (wave-uniform)
+    const void* zpage = (const void*)g_zero_page;  // hoisted: the asm waits' memory clobbers force a reload
+    if constexpr (FK) {
+#pragma unroll
+        for (int i = 0; i < B_CH; ++i) rowp[i] = X + (b_base[i] + (int64_t)b_hi[i] * a.W + b_wi[i]) * a.ldx + 8 * g;
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) wrow[i] = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + 8 * g;
+    }
 
     // no lambdas around the staging arrays: captured by reference they become addressable allocas
     u32x4 ra[A_CH], rb[B_CH];
@@ -539,7 +558,27 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     // LDS-DMA form of LOAD+STORE: one 1 KiB DMA per operand row block, zero page for masked chunks
 #define CONV2_DMA(k0, s)                                                                                           \
-    {                                                                                                              \
+    if constexpr (FK) {                                                                                            \
+        __bf16* as_ = As(s);                                                                                       \
+        __bf16* bs_ = Bs(s);                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) __builtin_amdgcn_global_load_lds(                         \
+            (gvoid_t*)(wrow[i] + (k0)), (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0, 0);                 \
+        const int soff = (fk_ky * a.W + fk_kx) * a.ldx + fk_c;                                                     \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
+            const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W; \
+            const void* src = ok ? (const void*)(rowp[i] + soff) : zpage;                                          \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+                                             0);                                                                   \
+        }                                                                                                          \
+        fk_c += BK2;                                                                                               \
+        if (fk_c == a.Cin) {                                                                                       \
+            fk_c = 0;                                                                                              \
+            if (++fk_kx == a.kw) {                                                                                 \
+                fk_kx = 0;                                                                                         \
+                ++fk_ky;                                                                                           \
+            }                                                                                                      \
+        }                                                                                                          \
+    } else {                                                                                                       \
         __bf16* as_ = As(s);                                                                                       \
         __bf16* bs_ = Bs(s);                                                                                       \
         _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
@@ -587,7 +626,9 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int s = kt & 1;
         const bool more = kt + 1 < nk;
         if constexpr (GLDS) {
-            if (more) CONV2_DMA((kt + 1) * BK2, s ^ 1);
+            if (more) {
+                CONV2_DMA((kt + 1) * BK2, s ^ 1);
+            }
         } else {
             if (more) CONV2_LOAD((kt + 1) * BK2);
         }
@@ -619,13 +660,17 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_STORE
 #undef CONV2_DMA
 
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? (a.mode == 1 ? (int64_t)m : conv_out_row(a, m, cls)) : -1;
+    };
     if constexpr (BN == 128) {
         if (a.w2) {
-            conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, wid, fr, fq, cls);
+            conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, n0, wm, wn, wid, fr, fq, orow);
             return;
         }
     }
-    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem, m0, n0, wm, wn, tid, fr, fq, cls);
+    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow);
 }
 
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
@@ -766,11 +811,15 @@ __global__ __launch_bounds__(C3_NT) void conv3_kernel(va_conv_args a, int ntn, i
     }
 #undef CONV3_DMA
     __syncthreads();  // every wave is done with the stages (no DMA in flight): reuse them for the epilogue
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? (a.mode == 1 ? (int64_t)m : conv_out_row(a, m, cls)) : -1;
+    };
     if (a.w2) {
-        conv2_tail<NT, BM, TNS, OutT>(a, acc, smem3, m0, n0, wm, wn, wid, fr, fq, cls);
+        conv2_tail<NT, BM, TNS, OutT>(a, acc, smem3, n0, wm, wn, wid, fr, fq, orow);
         return;
     }
-    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem3, m0, n0, wm, wn, tid, fr, fq, cls);
+    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem3, n0, wm, wn, tid, fr, fq, orow);
 }
 
 // ----------------------------------------------------------------------------------------- small-N conv
@@ -1257,6 +1306,148 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
     }
 }
 
+// ----------------------------------------------------------------------------------------- wide patch conv
+// Wide stride-1 3x3 convs (Cin a multiple of 64, Cout > 64 in 128-channel tiles).  The im2col kernels
+// (conv2/conv3) stage every input pixel nine times -- once per tap -- through the LDS-DMA path, whose
+// per-CU rate bounds them (profiles/r01b/conv3_ablation.log: the DMA-only variant alone takes as long as
+// the MFMA-only one).  Here the 18 x 18-pixel patch of a 16 x 16 output tile is staged ONCE per 64-channel
+// chunk and the nine taps read their B fragments from it: a 64-deep K-step moves a 16 KiB weight tile
+// plus 1/9 of a 41 KiB patch instead of 48 KiB.
+//   K order: chunk-major, tap-minor: step s = 9 c + t uses weight tile W[s] (rows n0 .. n0 + 127,
+//   k = t Cin + 64 c .. + 63 of the packed [Npad][Kpad] matrix, XOR-swizzled as in conv2) and patch P[c]
+//   (patch_off<8> image).  LDS: 3 weight stages (16 KiB) + 2 patch buffers (48 KiB) = 144 KiB.
+//   8 waves, 4 (pixel rows) x 2 (64-channel halves); acc / epilogue / fused tail as conv2's.
+//   DMA schedule per wave: prologue P[0] (6 instructions), W[0], W[1] (2 each); iteration s issues W[s + 2]
+//   after its barrier and, at s % 9 == 1, P[c + 1].  The wait before iteration s's barrier retires W[s]
+//   with the exact count of what this wave issued after it.
+constexpr int WP_NT = 512, WP_BN = 128, WP_PB = 48 * 1024, WP_WS = WP_BN * 64 * 2;
+constexpr int WP_LDS = 3 * WP_WS + 2 * WP_PB;  // 144 KiB
+static_assert(256 * (WP_BN + 4) * 4 <= WP_LDS, "epilogue tile must fit");
+
+__device__ __forceinline__ void wait_vm_lgkm0(int n) {  // s_waitcnt vmcnt(n) lgkmcnt(0), n in {0, 2, 6, 8}
+    if (n == 0)
+        __builtin_amdgcn_s_waitcnt(0x0070);
+    else if (n == 2)
+        __builtin_amdgcn_s_waitcnt(0x0072);
+    else if (n == 6)
+        __builtin_amdgcn_s_waitcnt(0x0076);
+    else
+        __builtin_amdgcn_s_waitcnt(0x0078);
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(WP_NT) void conv_wp_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntn) {
+    extern __shared__ __align__(16) unsigned char smw[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int fr = lane & 15, fq = lane >> 4;
+    int bid = blockIdx.x;
+    {  // XCD-aware order: the channel tiles and spatial neighbours of a tile share an XCD's L2
+        const int ntiles = gridDim.x, nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int tn = bid % ntn, sp = bid / ntn;
+    const int tx = sp % tiles_x, t2 = sp / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+    const int n0 = tn * WP_BN;
+    unsigned char* wstage = smw;
+    unsigned char* pbuf = smw + 3 * WP_WS;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+    const __bf16* __restrict__ Wt = (const __bf16*)a.w;
+    const int nck = a.Cin / 64, nsteps = 9 * nck;
+
+    // weight DMA: instruction i (rows 8i .. 8i + 7) for i = wid, wid + 8; lane l: row 8i + (l >> 3), its
+    // slot l & 7 holds chunk (l & 7) ^ (row & 7) = (l & 7) ^ (l >> 3)
+    const int wrow0 = 8 * wid + (lane >> 3), wg = (lane & 7) ^ (lane >> 3);
+    auto stage_w = [&](int s) {
+        const int c = s / 9, t = s - 9 * c;
+        const int kb = t * a.Cin + 64 * c + 8 * wg;
+        unsigned char* dst = wstage + (s % 3) * WP_WS;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const __bf16* src = Wt + (int64_t)(n0 + wrow0 + 64 * h) * a.Kpad + kb;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(dst + (wid + 8 * h) * 1024), 16, 0, 0);
+        }
+    };
+    // patch DMA: 48 instructions (41 cover the 324 pixels, the rest fetch the zero page into padding),
+    // 6 per wave
+    const int iy0 = PT * ty - 1, ix0 = PT * tx - 1;
+    auto stage_p = [&](int c) {
+        unsigned char* dst = pbuf + (c & 1) * WP_PB;
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            const int i = wid + 8 * u;
+            const int off = i * 1024 + 16 * lane;
+            const int p = off >> 7, ch = ((off >> 4) & 7) ^ patch_swz<8>(p);
+            const int iy = iy0 + p / PW3, ix = ix0 + p % PW3;
+            const bool ok = p < PW3 * PW3 && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            const void* src = ok ? (const void*)(X + (((int64_t)n * a.H + iy) * a.W + ix) * a.ldx + 64 * c + 8 * ch)
+                                 : (const void*)g_zero_page;
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(dst + i * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    // B fragments of step s + 1 come from a patch that is already resident (the same chunk's, or P[c + 1],
+    // retired at step 9 c + 4), so they are read at the end of step s, before the next barrier: after a
+    // barrier a wave only waits for its 8 A reads
+    bf16x8 bnx[2][4];
+    auto read_b = [&](int s2) {
+        const int c = s2 / 9, t = s2 - 9 * c, ky = t / 3, kx = t - 3 * ky;
+        const unsigned char* cur = pbuf + (c & 1) * WP_PB;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                bnx[kh][j] = *(const bf16x8*)(cur + patch_off<8>((4 * wm + j + ky) * PW3 + fr + kx, 4 * kh + fq));
+    };
+    stage_p(0);
+    stage_w(0);
+    stage_w(1);  // nsteps >= 9
+    for (int s = 0; s < nsteps; ++s) {
+        // retire W[s]: after it this wave issued W[s + 1] (if any) and a patch at iteration s - 2 or s - 1
+        const bool pa = s >= 2 && (s - 2) % 9 == 1 && (s - 2) / 9 + 1 < nck;
+        const bool pb = s >= 1 && (s - 1) % 9 == 1 && (s - 1) / 9 + 1 < nck;
+        wait_vm_lgkm0((s + 1 < nsteps ? 2 : 0) + (pa || pb ? 6 : 0));
+        __builtin_amdgcn_s_barrier();
+        if (s == 0) read_b(0);
+        if (s + 2 < nsteps) stage_w(s + 2);
+        if (s % 9 == 1 && s / 9 + 1 < nck) stage_p(s / 9 + 1);
+        const unsigned char* ws = wstage + (s % 3) * WP_WS;
+        bf16x8 af[2][4], bfr[2][4];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                af[kh][i] = *(const bf16x8*)(ws + (wn * 64 + 16 * i + fr) * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[kh][j] = bnx[kh][j];
+        }
+        if (s + 1 < nsteps) read_b(s + 1);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // every wave is done with the stages (no DMA in flight): reuse them for the epilogue
+    auto orow = [&](int pl) -> int64_t {
+        const int oy = PT * ty + pl / PT, ox = PT * tx + pl % PT;
+        return (oy < a.Ho && ox < a.Wo) ? ((int64_t)n * a.Ho + oy) * a.Wo + ox : -1;
+    };
+    if (a.w2) {
+        conv2_tail<WP_NT, 256, 4, OutT>(a, acc, smw, n0, wm, wn, wid, fr, fq, orow);
+        return;
+    }
+    conv_epilogue<WP_NT, 256, WP_BN, 4, OutT>(a, acc, smw, n0, wm, wn, tid, fr, fq, orow);
+}
+
 template <int TNS, bool TAIL = false, typename OutT = __bf16>
 hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
@@ -1483,9 +1674,15 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of 8 and a 16-byte aligned base
-    if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0)
-        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
-                           ntiles);
+    const bool fk = a.Cin % 64 == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
+    if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0) {
+        if (fk)
+            hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a,
+                               ntn, ntiles);
+        else
+            hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
+                               ntiles);
+    }
     else
         hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
@@ -1583,6 +1780,36 @@ hipError_t launch_conv_patch(const va_conv_args& a, hipStream_t st) {
     return a.Cout == 32 ? launch_conv_patch_v<2, 8, TAIL, OutT>(a, st) : launch_conv_patch_v<4, 8, TAIL, OutT>(a, st);
 }
 
+// VA_CONV_WP=1 moves the wide stride-1 3x3 layers to the wide patch kernel (A/B timing; read per launch).
+// Off by default: at P3 (exact 16 x 16 tiling) it ties conv2, on the ragged P4 / P5 tilings it loses 1.4-2x
+// (profiles/r01c/wp_vs_conv2_layers.log) -- the B bytes it saves were not what bounds these layers.
+bool use_wp(const va_conv_args& a) {
+    const char* e = getenv("VA_CONV_WP");
+    if (!e || e[0] != '1') return false;
+    constexpr int OV = 8;  // conv_epilogue's 16-byte runs (bf16); float output runs of 4 are covered too
+    return a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.mode == 0 && a.Cin % 64 == 0 &&
+           a.K == 9 * a.Cin && a.Cout > 64 && a.Npad % WP_BN == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 &&
+           a.Ho == a.H && a.Wo == a.W && a.Kpad % 64 == 0 &&
+           (a.w2 ? (a.Cout == 128 && a.c2 <= 16 * TAIL_C2F && a.c2 % 4 == 0 && !a.res)
+                 : (a.Cout % OV == 0 && a.ldy % OV == 0 && (!a.res || a.ldr % 8 == 0)));
+}
+
+template <typename OutT>
+hipError_t launch_conv_wp(const va_conv_args& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv_wp_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                WP_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    const int tiles_x = (a.Wo + PT - 1) / PT, tiles_y = (a.Ho + PT - 1) / PT;
+    const int ntn = (a.Cout + WP_BN - 1) / WP_BN;
+    const int blocks = a.N * tiles_x * tiles_y * ntn;
+    hipLaunchKernelGGL((conv_wp_kernel<OutT>), dim3(blocks), dim3(WP_NT), WP_LDS, st, a, tiles_x, tiles_y, ntn);
+    return hipGetLastError();
+}
+
 // VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
 bool getenv_dn() {
     static int v = -1;
@@ -1605,8 +1832,10 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             }
             if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
                 a.c2 % 4 == 0 &&
-                a.Kpad % BK2 == 0 && a.ldy % 4 == 0)
+                a.Kpad % BK2 == 0 && a.ldy % 4 == 0) {
+                if (a.mode == 0 && use_wp(a)) return launch_conv_wp<OutT>(a, st);
                 return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
+            }
         }
         return hipErrorInvalidValue;
     }
@@ -1633,6 +1862,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
             if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
+            if (use_wp(a)) return launch_conv_wp<OutT>(a, st);
             return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
