@@ -474,7 +474,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     const int cls = a.mode == 2 ? (bid & 3) : 0;
     if (a.mode == 2) bid >>= 2;
     const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
     const __bf16* __restrict__ X = (const __bf16*)a.x;
@@ -634,21 +634,24 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         }
         const __bf16* as_ = As(s);
         const __bf16* bs_ = Bs(s);
+        // all fragments of the K-step first (the second half's reads overlap the first half's MFMAs)
+        bf16x8 af[2][TNS], bfr[2][4];
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
-            bf16x8 af[TNS], bfr[4];
             // chunk 4 kh + fq of the row; GLDS rows are swizzled (slot = chunk ^ (row & 7), row & 7 == fr & 7)
             const int ch = GLDS ? (((4 * kh + fq) ^ (fr & 7)) * 8) : 32 * kh + 8 * fq;
 #pragma unroll
-            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
+            for (int i = 0; i < TNS; ++i) af[kh][i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
+            for (int j = 0; j < 4; ++j) bfr[kh][j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
             for (int i = 0; i < TNS; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[i][j], 0, 0, 0);
         if constexpr (GLDS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
