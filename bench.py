@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--res", type=int, default=640)
     p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    p.add_argument("--cpu-sample", type=int, default=160, help="frames timed for the CPU baseline (0 = skip)")
+    p.add_argument("--cpu-sample", type=int, default=256,
+                   help="frames timed for the CPU baseline (0 = skip; 256 = the whole resident pool, ~10-15 s)")
     p.add_argument("--no-prof", action="store_true", help="skip the live per-op HIP-event timing")
     p.add_argument("--prof-every", type=int, default=4,
                    help="bracket every op of every N-th timed step's forward with HIP events (each event pair is a "
@@ -225,7 +226,7 @@ def main():
         achieved = flops_per_launch / avg_launch_s / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 5), "traffic": None,
-                    "kernel": "conv kernels conv0/conv_dn/conv2/conv3 (all %d GEMM launches of one YOLOv8-seg forward)"
+                    "kernel": "conv kernels conv0/conv_patch/conv_dn/conv2 (all %d GEMM launches of one YOLOv8-seg forward)"
                               % round(launches_per_step),
                     "flops_per_launch": flops_per_launch, "avg_launch_us": round(avg_launch_s * 1e6, 3),
                     "conv_ms_per_step": round(conv_ms / sampling["n"], 3),
