@@ -535,8 +535,11 @@ __global__ __launch_bounds__(VA_NAV_THREADS) void nav_grid_kernel(GridArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// A*: one wave64 per query.  LDS layout per node: g f64 | key f64 | pen f64 | parent u16 | hist u16 | state u8
-// plus the open list (u16 node ids).
+// A*: one wave64 per query.  LDS layout per node: g f64 | key f64 | parent u16 | hist u16 | state u8 plus the
+// open list (u16 node ids): 23 B per node, 23.5 KiB at 640x640.  The node penalties stay in global memory
+// (8 KiB per frame, L1/L2-resident): with them in LDS (31 KiB) a query wave sharing a CU with two
+// conv2 workgroups (2 x 67.5 KiB) would not fit beside them, and the ~100 query waves of a batch,
+// overlapping the next batch's network, would halve conv occupancy on the CUs they land on.
 #define ST_EXISTS 1u
 #define ST_MULT_SHIFT 1  // bits 1-2
 #define ST_HASG 8u
@@ -585,8 +588,8 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     extern __shared__ __align__(16) uint8_t smem[];
     double* g = (double*)smem;
     double* fk = g + N;
-    double* pen = fk + N;
-    uint16_t* par = (uint16_t*)(pen + N);
+    const double* __restrict__ pen = npen;  // global (see above)
+    uint16_t* par = (uint16_t*)(fk + N);
     uint16_t* hd = par + N;
     uint16_t* open = hd + N;
     uint8_t* st = (uint8_t*)(open + N);
@@ -597,7 +600,6 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         if (fl & VA_NODE_EXISTS) v |= ST_EXISTS;
         v |= (uint8_t)(((fl >> VA_NODE_MULT_SHIFT) & 3u) << ST_MULT_SHIFT);
         st[i] = v;
-        pen[i] = npen[i];
     }
     unsigned long long seen0 = a.seen[0], seen1 = a.seen[1];
     unsigned long long miss0 = 0, miss1 = 0;
@@ -893,7 +895,7 @@ hipError_t ensure_tables() {
     return hipSuccess;
 }
 
-size_t astar_lds(int nodes) { return (size_t)nodes * (8 + 8 + 8 + 2 + 2 + 2 + 1) + 16; }
+size_t astar_lds(int nodes) { return (size_t)nodes * (8 + 8 + 2 + 2 + 2 + 1) + 16; }
 
 // speculative rounds over `nslots` query slots
 int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out) {
