@@ -298,3 +298,32 @@ def test_wide_patch_conv_matches_conv2(monkeypatch):
     for name, g, r, t in zip(("box", "cls", "coef", "proto"), got, ref, f32):
         assert rel(g, r) < 1e-2, f"{name}: wide patch vs conv2 relative L2 {rel(g, r)}"
         assert rel(g, t) < 1.25 * rel(r, t) + 1e-3, f"{name}: vs fp32 {rel(g, t)} (conv2 {rel(r, t)})"
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual", [
+    (128, 256, 3, 1, 23, 21, False),  # ragged pixel tile
+    (128, 224, 3, 2, 40, 38, False),  # stride 2, ragged channel tile (head.l.0 width)
+    (256, 384, 1, 1, 17, 30, True),   # 1x1, two channel tiles, residual
+])
+def test_conv4_op(monkeypatch, cin, cout, k, stride, H, W, residual):
+    """conv4 (256 x 256 tiles, four-phase K-tile with counted vmcnt, permuted weight rows, epilogue from the
+    accumulators) forced on single ops vs torch fp32 on the same bf16-rounded inputs."""
+    monkeypatch.setenv("VA_CONV4", "1")
+    monkeypatch.setenv("VA_CONV4_MIN", "1")
+    got, ref = _run_single_conv("bf16", cin, cout, k, stride, H, W, residual, False, 0, act=True)
+    err = (got - ref).abs().max() / ref.abs().max()
+    assert err < 2e-2, err
+
+
+def test_conv4_matches_conv2(monkeypatch):
+    """conv4 forced onto every eligible layer of a bf16 forward (Cout > 128, Cin % 64 == 0) against conv2:
+    same 32-deep MFMA k-sequence per output, so bit-identical."""
+    arch, fw, net = _net("bf16", "s", seed=12)
+    frames = _frames(2, seed=13)
+    monkeypatch.delenv("VA_CONV4", raising=False)
+    ref = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_CONV4", "1")
+    monkeypatch.setenv("VA_CONV4_MIN", "1")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.equal(g, r), f"{name}: conv4 vs conv2 max diff {(g - r).abs().max().item()}"

@@ -825,6 +825,230 @@ __global__ __launch_bounds__(C3_NT) void conv3_kernel(va_conv_args a, int ntn, i
     conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem3, n0, wm, wn, tid, fr, fq, orow);
 }
 
+// ----------------------------------------------------------------------------------------- conv v4 (bf16, Cout >= 256)
+// 256 output channels x 256 pixels per workgroup with the phase structure of cdna_hip_programming.md §5
+// "The 256² 8-phase template": 8 waves (2 channel halves x 4 pixel quarters; each 128 channels x 64
+// pixels, acc[8][4]), BK = 64, two LDS buffers of (A 256 x 64 | B 256 x 64) bf16 = 128 KiB, XOR-swizzled
+// rows (conv2's image), one workgroup per CU.  A K-tile runs as four phases, one C quadrant each
+// (channel frags 0-3 / 4-7 x pixel frags 0-1 / 2-3); every phase
+//   reads its fragments (data published one phase earlier) -> issues one half-tile of the NEXT K-tile by
+//   LDS-DMA (A rows 0-127, B rows 0-127, B rows 128-255, A rows 128-255 in phases 0..3) -> s_waitcnt
+//   vmcnt(4) (retires exactly the half-tile the next phase reads: two half-tiles of 2 DMAs each stay in
+//   flight across the barrier) -> s_barrier -> lgkmcnt(0) -> 16 MFMAs at priority 1 -> s_barrier.
+// B (pixels) is gathered im2col-style with conv2's FK addressing (Cin % 64 == 0: wave-uniform tap and
+// channel chunk, per-row base pointers).  The weight rows are DMA'd in a channel permutation (LDS row
+// 32 p + 16 h + r holds channel 32 p + 8 (r/4) + 4 h + r%4) so that fragments 2p, 2p+1 give each lane 8
+// consecutive channels: the epilogue stores 16 bytes per lane straight from the accumulators.
+constexpr int C4_NT = 512, C4_BUF = 2 * 256 * BK2 * 2;  // bytes per LDS buffer (A then B)
+
+template <typename OutT>
+__global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn, int ntiles) {
+    extern __shared__ __align__(16) unsigned char sm4[];
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int tn = bid % ntn, tm = bid / ntn;  // channel tile fastest: both channel tiles of a pixel tile
+    const int c0 = tn * 256, p0 = tm * 256;    // share the staged pixels through the XCD's L2
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wid >> 2, wc = wid & 3;     // channel half, pixel quarter
+    const int fr = lane & 15, fq = lane >> 4;
+    const __bf16* __restrict__ X = (const __bf16*)a.x;
+    const __bf16* __restrict__ Wt = (const __bf16*)a.w;
+
+    // Half-tiles are the rows every wave reads in the same phase: A half 0 = rows 0-63 and 128-191 (channel
+    // quarter 0 of both channel halves), A half 1 = 64-127, 192-255; B half 0 = the first 32 rows of each
+    // 64-pixel quarter, B half 1 = the second 32.  A DMA instruction writes 8 consecutive rows; wave w
+    // issues two per half-tile (u = 0, 1); lane l takes row base + (l >> 3) and fetches chunk
+    // (l & 7) ^ (l >> 3) (swizzled slot l & 7).  Staged row of (half, u) for this lane:
+    const int g = (lane & 7) ^ (lane >> 3), lr = lane >> 3;
+    auto a_row0 = [&](int half, int u) { return 64 * half + 8 * wid + 128 * u; };
+    auto b_row0 = [&](int half, int u) { return 64 * ((wid >> 2) + 2 * u) + 32 * half + 8 * (wid & 3); };
+    const __bf16* wrow[4];  // [2 half + u]: permuted-channel weight rows
+    const __bf16* rowp[4];  // [2 half + u]: pixel rows
+    int b_hi[4], b_wi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int R = a_row0(i >> 1, i & 1) + lr;  // LDS row 0..255 of the A image
+        const int pp = R >> 5, hh = (R >> 4) & 1, rr = R & 15;
+        const int ch = c0 + 32 * pp + 8 * (rr >> 2) + 4 * hh + (rr & 3);
+        wrow[i] = Wt + (int64_t)ch * a.Kpad + 8 * g;
+        const int m = p0 + b_row0(i >> 1, i & 1) + lr;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi[i] = ho * a.stride - a.pad;
+            b_wi[i] = wo * a.stride - a.pad;
+            rowp[i] = X + (((int64_t)n * a.H + b_hi[i]) * a.W + b_wi[i]) * a.ldx + 8 * g;
+        } else {
+            b_hi[i] = -(1 << 28);
+            b_wi[i] = 0;
+            rowp[i] = X;
+        }
+    }
+    const void* zpage = (const void*)g_zero_page;
+    int fk_ky = 0, fk_kx = 0, fk_c = 0, fk_k = 0;  // tap / channel chunk / k of the tile being staged
+    auto adv_k = [&]() {
+        fk_k += BK2;
+        fk_c += BK2;
+        if (fk_c == a.Cin) {
+            fk_c = 0;
+            if (++fk_kx == a.kw) {
+                fk_kx = 0;
+                ++fk_ky;
+            }
+        }
+    };
+    // half-tile h of the K-tile being staged into buffer b, in the order the phases read them:
+    // 0 = A half 0, 1 = B half 0, 2 = B half 1, 3 = A half 1
+    auto stage = [&](int b, int h) {
+        unsigned char* buf = sm4 + b * C4_BUF;
+        const bool isA = h == 0 || h == 3;
+        const int half = (h == 0 || h == 1) ? 0 : 1;
+        const int soff = (fk_ky * a.W + fk_kx) * a.ldx + fk_c;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = 2 * half + u;
+            const void* src;
+            unsigned char* dst;
+            if (isA) {
+                src = (const void*)(wrow[i] + fk_k);
+                dst = buf + a_row0(half, u) * 128;
+            } else {
+                const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W;
+                src = ok ? (const void*)(rowp[i] + soff) : zpage;
+                dst = buf + 256 * BK2 * 2 + b_row0(half, u) * 128;
+            }
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)dst, 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.Kpad / BK2;
+    // prologue: K-tile 0 in the order A_lo, B_lo, B_hi, A_hi; phase (0, 0) reads A_lo and B_lo
+    stage(0, 0);
+    stage(0, 1);
+    stage(0, 2);
+    stage(0, 3);
+    adv_k();
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+    bf16x8 fa[4][2], fb01[2][2], fb23[2][2];  // [frag][k half]
+    auto read_a = [&](const unsigned char* buf, int quarter) {  // channel frags 4 quarter .. +3 of this wave
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 128 * wr + 64 * quarter + 16 * i + fr;
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+                fa[i][kh] = *(const bf16x8*)(buf + row * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
+        }
+    };
+    auto read_b = [&](const unsigned char* buf, int pair, bf16x8(&fb)[2][2]) {  // pixel frags 2 pair, +1
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = 64 * wc + 32 * pair + 16 * j + fr;
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+                fb[j][kh] = *(const bf16x8*)(buf + 256 * BK2 * 2 + row * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
+        }
+    };
+    auto mma = [&](int quarter, int pair, bf16x8(&fb)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[4 * quarter + i][2 * pair + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][kh], fb[j][kh], acc[4 * quarter + i][2 * pair + j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+// retire the half-tile the next phase reads (two half-tiles = 4 DMAs may stay in flight; none are issued in
+// the last K-tile), publish it with the barrier, then wait for this phase's own fragment reads
+#define C4_SYNC(more)                                                                        \
+    {                                                                                        \
+        if (more)                                                                            \
+            asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory"); \
+        else                                                                                 \
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory"); \
+    }
+    for (int t = 0; t < nk; ++t) {
+        const unsigned char* buf = sm4 + (t & 1) * C4_BUF;
+        const bool more = t + 1 < nk;
+        const int nb = (t + 1) & 1;
+        // phase 0: A_lo x B_lo
+        read_a(buf, 0);
+        read_b(buf, 0, fb01);
+        if (more) stage(nb, 0);
+        C4_SYNC(more);
+        mma(0, 0, fb01);
+        asm volatile("s_barrier" ::: "memory");
+        // phase 1: A_lo x B_hi
+        read_b(buf, 1, fb23);
+        if (more) stage(nb, 1);
+        C4_SYNC(more);
+        mma(0, 1, fb23);
+        asm volatile("s_barrier" ::: "memory");
+        // phase 2: A_hi x B_hi
+        read_a(buf, 1);
+        if (more) stage(nb, 2);
+        C4_SYNC(more);
+        mma(1, 1, fb23);
+        asm volatile("s_barrier" ::: "memory");
+        // phase 3: A_hi x B_lo (no reads)
+        if (more) {
+            stage(nb, 3);
+            adv_k();
+        }
+        C4_SYNC(more);
+        mma(1, 0, fb01);
+        asm volatile("s_barrier" ::: "memory");
+    }
+
+#undef C4_SYNC
+    // epilogue straight from the accumulators: fragments 2p, 2p+1 hold channels c0 + 128 wr + 32 p + 8 fq .. +7
+    OutT* Y = (OutT*)a.y;
+    const __bf16* R = (const __bf16*)a.res;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = p0 + 64 * wc + 16 * j + fr;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int co = c0 + 128 * wr + 32 * p + 8 * fq;
+            if (co >= a.Cout) continue;
+            const float4 b0 = *(const float4*)(a.bias + co), b1 = *(const float4*)(a.bias + co + 4);
+            const f32x4 t0 = acc[2 * p][j], t1 = acc[2 * p + 1][j];
+            float v[8] = {t0[0] + b0.x, t0[1] + b0.y, t0[2] + b0.z, t0[3] + b0.w,
+                          t1[0] + b1.x, t1[1] + b1.y, t1[2] + b1.z, t1[3] + b1.w};
+            if (a.act) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] = silu(v[r]);
+            }
+            if (R) {
+                const bf16x8 rr = *(const bf16x8*)(R + (int64_t)m * a.ldr + co);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[r] += (float)rr[r];
+            }
+            if constexpr (sizeof(OutT) == 2) {
+                bf16x8 o;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) o[r] = (__bf16)v[r];
+                *(bf16x8*)(Y + (int64_t)m * a.ldy + co) = o;
+            } else {
+                *(float4*)(Y + (int64_t)m * a.ldy + co) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)(Y + (int64_t)m * a.ldy + co + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------- small-N conv
 // Narrow layers (Cout <= 64: the C2f bottlenecks of P2/P3, the level-0 box/coef head branches) have
 // too little MFMA work per staged activation byte for the LDS-staged kernel: both its LDS traffic
@@ -1813,6 +2037,34 @@ hipError_t launch_conv_wp(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// VA_CONV4=1 moves the Cout > 128 layers with at least VA_CONV4_MIN (default 256) 256 x 256 tiles to conv4
+// (A/B timing; read per launch)
+bool use_conv4(const va_conv_args& a) {
+    const char* e = getenv("VA_CONV4");
+    if (!e || e[0] != '1') return false;
+    if (a.mode != 0 || a.w2 || a.Cout <= 128 || a.Cin % 64 || a.K != a.kh * a.kw * a.Cin || a.Kpad != a.K ||
+        a.ldx % 8 || ((uintptr_t)a.x & 15) || a.ldy % 8 || ((uintptr_t)a.y & 15) || a.Npad % 256 ||
+        (a.res && (a.ldr % 8 || ((uintptr_t)a.res & 15))))
+        return false;
+    const char* mn = getenv("VA_CONV4_MIN");
+    const int64_t tiles = (int64_t)((a.M + 255) / 256) * ((a.Cout + 255) / 256);
+    return tiles >= (mn ? atoll(mn) : 256);
+}
+
+template <typename OutT>
+hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)conv4_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * C4_BUF) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    const int ntn = (a.Cout + 255) / 256, ntiles = ntn * ((a.M + 255) / 256);
+    hipLaunchKernelGGL((conv4_kernel<OutT>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
 // VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
 bool getenv_dn() {
     static int v = -1;
@@ -1866,6 +2118,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
             if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
             if (use_wp(a)) return launch_conv_wp<OutT>(a, st);
+            if (use_conv4(a)) return launch_conv4<OutT>(a, st);
             return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
