@@ -53,6 +53,8 @@ def parse():
                         "GPU-side packet; sampling keeps their cost out of the other steps)")
     p.add_argument("--no-overlap", action="store_true",
                    help="serial steps (no overlap of batch k's grid stage with batch k+1's network)")
+    p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2],
+                   help="network streams of the overlapped pipeline (2: consecutive forwards run concurrently)")
     return p.parse_args()
 
 
@@ -130,7 +132,7 @@ def main():
     B, H, W = args.batch, args.res, args.res
     overlap = not args.no_overlap
     if overlap:
-        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev)
+        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev, seg_streams=args.seg_streams)
         pipe = opipe.a
     else:
         pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
@@ -205,6 +207,16 @@ def main():
         lib.va_prof_stop(ms, cnt, 8)
         conv_ms, conv_n = ms[1] + ms[5], cnt[1] + cnt[5]  # VA_OP_CONV + VA_OP_CONV0 (layer 0 fused)
         other_seg_ms = ms[2] + ms[3] + ms[4]
+        # the same per-op events on 3 forwards run alone (after the timed region, untimed): the kernel's
+        # duration without a concurrent forward sharing the chip
+        torch.cuda.synchronize()
+        _lib.check(lib.va_prof_start(pipe.plan["n"] * 3 + 16), "va_prof_start")
+        for _ in range(3):
+            pipe.run_seg_only()
+            torch.cuda.synchronize()
+        iso_ms, iso_cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
+        lib.va_prof_stop(iso_ms, iso_cnt, 8)
+        iso_conv_ms, iso_conv_n = iso_ms[1] + iso_ms[5], iso_cnt[1] + iso_cnt[5]
     # results sanity (last batch): count frames with >= 1 path
     last = res
     for i in range(B):
@@ -232,7 +244,14 @@ def main():
                     "conv_ms_per_step": round(conv_ms / sampling["n"], 3),
                     "other_seg_ops_ms_per_step": round(other_seg_ms / sampling["n"], 3),
                     "timing": f"HIP events around every op of {sampling['n']} of the {args.steps} timed forwards "
-                              f"(every {sampling['every']}-th), on the launch stream"}
+                              f"(every {sampling['every']}-th), on the launch stream; with {args.seg_streams} network "
+                              "streams consecutive forwards overlap, so a launch's duration includes sharing the chip",
+                    "isolated_achieved": round(flops_per_launch / (iso_conv_ms / 1e3 / iso_conv_n) / 1e12, 2),
+                    "isolated_avg_launch_us": round(iso_conv_ms / iso_conv_n * 1e3, 3),
+                    "isolated_def": "same events on 3 forwards run alone after the timed region (untimed)",
+                    "step_achieved": round(gflop_exec * args.steps / elapsed / 1e3, 2),  # per GPU
+                    "step_achieved_def": "executed conv TFLOP of all timed forwards / timed wall time (whole-step "
+                                         "MFMA throughput, everything else included)"}
         traffic_file = os.path.join(REPO, "profiles", "conv_traffic.json")
         if os.path.exists(traffic_file):
             with open(traffic_file) as f:
@@ -273,7 +292,8 @@ def main():
                                    "penalty/protrusion/A* on GPU, end-to-end",
                        "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
                        "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",
-                       "overlap": "grid stage of batch k on a 2nd HIP stream under the network of batch k+1"
+                       "overlap": (f"{args.seg_streams} network stream(s): consecutive forwards run concurrently; "
+                                   "grid stage of batch k on its own stream under the following networks")
                        if overlap else "none",
                        "gflop_per_frame": round(gflop, 2),
                        "gflop_per_frame_executed": round(gflop_exec / B, 2)},

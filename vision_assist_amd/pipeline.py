@@ -62,29 +62,33 @@ class FramePipeline:
 
 
 class OverlappedPipelines:
-    """Two FramePipelines sharing weights and the angle cache, on two HIP streams: while batch k's
-    grid stage (a few hundred waves: A* is a chain of dependent pops) runs on the nav stream, batch
-    k+1's network fills the rest of the chip on the seg stream.  Batches still leave in order and
-    the angle cache advances in order (the nav stream is serial)."""
+    """Two FramePipelines sharing weights and the angle cache.  Each has its own network stream, so two
+    consecutive batches' forwards run concurrently and fill each other's kernel tails and launch gaps;
+    the grid stage (a few hundred waves: A* is a chain of dependent pops) runs on a third stream, in
+    submission order, so batches leave in order and the angle cache advances in order."""
 
-    def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", device=None, **kw):
+    def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", device=None,
+                 seg_streams: int = 2, **kw):
         self.a = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, tag=0, **kw)
         self.b = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=self.a.device, seen=self.a.seen,
                                seg=self.a.seg, tag=1, **kw)
         self.pipes = (self.a, self.b)
-        self.s_seg = torch.cuda.Stream(device=self.a.device)
+        s0 = torch.cuda.Stream(device=self.a.device)
+        self.s_segs = (s0, torch.cuda.Stream(device=self.a.device) if seg_streams == 2 else s0)
         self.s_nav = torch.cuda.Stream(device=self.a.device)
         self.ev = [torch.cuda.Event(), torch.cuda.Event()]
         self.k = 0
 
     def submit(self, frames: torch.Tensor, plant_cells=None, plant_rects=None, plant_mode: int = PLANT_NEVER):
-        """Enqueue copy + network + post-processing of the next batch on the seg stream."""
+        """Enqueue copy + network + post-processing of the next batch on its pipeline's network stream."""
         p = self.pipes[self.k % 2]
-        self.s_seg.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.s_seg):
+        s_seg = self.s_segs[self.k % 2]
+        s_seg.wait_stream(torch.cuda.current_stream())
+        s_seg.wait_stream(self.s_nav)  # the pipeline's previous batch has left its grid stage (buffer reuse)
+        with torch.cuda.stream(s_seg):
             p.frames.copy_(frames, non_blocking=True)
-            p.seg_post(plant_cells, plant_rects, plant_mode, stream=self.s_seg)
-            self.ev[self.k % 2].record(self.s_seg)
+            p.seg_post(plant_cells, plant_rects, plant_mode, stream=s_seg)
+            self.ev[self.k % 2].record(s_seg)
         self.k += 1
 
     def finish(self, j: int) -> NavBatch:
