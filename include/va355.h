@@ -180,7 +180,10 @@ typedef struct va_conv_args {
     int32_t M;              /* N * Ho * Wo */
     int32_t dtype;          /* VA_DTYPE_BF16 (MFMA bf16, f32 accumulate) or VA_DTYPE_F32 (exact f32 MFMA) */
     int32_t out_f32;        /* bf16 inputs with a float output (head logits) */
-    int32_t pad_;
+    int32_t bias4;          /* mode 2 with a fused tail only: bias is a border table [4 classes][2][2][Npad],
+                               entry [c][rf][cf] for output pixels whose class-c taps miss the map's first /
+                               last row (rf) or column (cf) -- the folded deconv bias depends on which taps
+                               fall inside the map, so no constant-1 input channel is needed */
     /* Optional fused 1x1 tail conv (bf16, mode 0, no residual; Cout == 128 with c2 <= 80, or Cout 32 / 64 with
      * c2 <= 64 and the weights fitting 120 KiB of LDS): when w2 != NULL the main conv's activations (bias + act,
      * rounded to bf16 as a stored layer would be) never leave the chip and feed y2 = act2(W2 . a + b2);

@@ -310,17 +310,30 @@ __device__ __forceinline__ int64_t conv_out_row(const va_conv_args& a, int m, in
 constexpr int TAIL_C2F = 5;  // 16-row tail fragments: c2 <= 80
 
 // orow(pl): output row (pixel index of the output tensor) of tile row pl, or -1 when masked
+// bias4 (mode 2): the bias row of GEMM row m0 + pl comes from the border table (va355.h va_conv_args.bias4)
 template <int NT, int BM, int TNS, typename OutT, typename RowFn>
 __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
-                                           int wm, int wn, int wid, int fr, int fq, RowFn orow) {
+                                           int wm, int wn, int wid, int fr, int fq, RowFn orow, int m0 = 0,
+                                           int cls = 0) {
     constexpr int BN = 128, TW = BN + 8, PS = BM / (NT / 64) / 16;
     __bf16* Ts = (__bf16*)smem;
+    int brow[4];  // bias row offset per pixel fragment
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        brow[j] = n0;
+        if (a.bias4) {
+            const int m = m0 + wm * 64 + 16 * j + fr;
+            const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
+            const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
+            brow[j] = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
         const int col = wn * 16 * TNS + 16 * i + 4 * fq;
-        const float4 bv = *(const float4*)(a.bias + n0 + col);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            const float4 bv = *(const float4*)(a.bias + brow[j] + col);
             float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
             __bf16 o4[4];
 #pragma unroll
@@ -669,7 +682,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     };
     if constexpr (BN == 128) {
         if (a.w2) {
-            conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, n0, wm, wn, wid, fr, fq, orow);
+            conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, n0, wm, wn, wid, fr, fq, orow, m0, cls);
             return;
         }
     }
@@ -1921,7 +1934,7 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
 // VA_CONV3_MIN = fewest 256 x 128 tiles for which conv3 is used (default 256: one per CU)
 bool use_conv3(const va_conv_args& a) {
     const char* e = getenv("VA_CONV3");
-    if (!e || e[0] != '1') return false;
+    if (!e || e[0] != '1' || a.bias4) return false;
     if (a.Cin % 8 || a.ldx % 8 || ((uintptr_t)a.x & 15) || a.Kpad % BK2 || a.Npad % C3_BN) return false;
     const char* mn = getenv("VA_CONV3_MIN");
     const int64_t min_tiles = mn ? atoll(mn) : 256;
@@ -2139,6 +2152,7 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     if (a->mode == 2 && (a->dtype != VA_DTYPE_BF16 || a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res ||
                          a->Cout <= 64 || a->Kpad % BK2))
         return VA_ERR_ARG;
+    if (a->bias4 && (a->mode != 2 || !a->w2 || a->Cout != 128)) return VA_ERR_ARG;  // conv2's fused-tail path only
     if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode == 1 ||
                   (a->mode == 2 && a->Cout != 128) ||
                   a->res || !a->b2 || a->c2 <= 0 || a->c2 > 16 * (a->Cout == 128 ? TAIL_C2F : DN_TAIL_C2F) ||

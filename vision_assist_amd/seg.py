@@ -40,7 +40,7 @@ class ConvArgs(ctypes.Structure):
         ("y", ctypes.c_void_p), ("ldy", ctypes.c_int32),
         ("res", ctypes.c_void_p), ("ldr", ctypes.c_int32),
         ("act", ctypes.c_int32), ("mode", ctypes.c_int32), ("M", ctypes.c_int32), ("dtype", ctypes.c_int32),
-        ("out_f32", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("out_f32", ctypes.c_int32), ("bias4", ctypes.c_int32),
         ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("c2", ctypes.c_int32), ("act2", ctypes.c_int32),
     ]
 
@@ -122,19 +122,36 @@ class SegNet:
         self._plans = {}
 
     def _fold_proto(self, folded: dict) -> Packed:
-        """Packed weights of the sub-pixel fold of proto's upsample + cv2 (see fold_proto_weights)."""
+        """Packed weights of the sub-pixel fold of proto's upsample + cv2 (see fold_proto_weights), and its
+        border bias table (va355.h va_conv_args.bias4): the deconv bias reaches an output pixel through
+        the taps that fall inside the low-res map, so it is folded into a per-(class, row border, column
+        border) bias instead of riding on a constant-1 input channel -- K stays 4 x 128 (the FK
+        addressing of conv2 applies, 6 % fewer MACs)."""
         wd, bd = folded["model.22.proto.upsample"]
         w2, b2 = folded["model.22.proto.cv2"]
-        wc = fold_proto_weights(wd, bd, w2)
-        o, cin_p = wc.shape[1], wc.shape[4]
-        K = 4 * cin_p
+        wfull = fold_proto_weights(wd, bd, w2)  # [4][O][2][2][Ci + 8], deconv-bias taps at channel Ci
+        ci = wd.shape[0]
+        wc, wb = wfull[..., :ci], wfull[..., ci]  # weights, per-tap bias contributions [4][O][2][2]
+        o = wc.shape[1]
+        K = 4 * ci
         Kpad, Npad = _ceil(K, BK), _ceil(o, NPAD)
         wm = torch.zeros(4, Npad, Kpad, dtype=torch.float64)
         wm[:, :o, :K] = wc.reshape(4, o, K)
-        bm = torch.zeros(Npad, dtype=torch.float32)
-        bm[:o] = b2.float()
-        return Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, o, 2, K,
-                      Kpad, Npad)
+        bt = torch.zeros(4, 2, 2, Npad, dtype=torch.float64)
+        for c in range(4):
+            dy, dx = c >> 1, c & 1
+            fy_out, fx_out = (0 if dy == 0 else 1), (0 if dx == 0 else 1)  # the tap that leaves the map
+            for rf in range(2):
+                for cf in range(2):
+                    acc = b2.double().clone()
+                    for fy in range(2):
+                        for fx in range(2):
+                            if (rf and fy == fy_out) or (cf and fx == fx_out):
+                                continue
+                            acc += wb[c, :, fy, fx]
+                    bt[c, rf, cf, :o] = acc
+        return Packed(wm.to(self.device, self.tdtype).contiguous(),
+                      bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
 
     # ------------------------------------------------------------------ packing
     def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
@@ -313,10 +330,8 @@ class SegNet:
         # Proto
         if self.proto_fold is not None:
             pf = self.proto_fold
-            pr1 = new(h3, w3, pf.cin)  # [cv1 output | 1 | 0 x 7]: the ones channel carries the deconv bias
-            pr1.buf[..., a.npr:].zero_()
-            pr1.buf[..., a.npr] = 1.0
-            conv("model.22.proto.cv1", o3, pr1.sub(0, a.npr), h3, w3)
+            pr1 = new(h3, w3, a.npr)
+            conv("model.22.proto.cv1", o3, pr1, h3, w3)
             proto = new(h2, w2, NM, torch.float32)
             p3 = self.w["model.22.proto.cv3"]
             w3c = p3.w[:, :pf.cout].contiguous()
@@ -324,7 +339,7 @@ class SegNet:
             ops.append(SegOp(kind=VA_OP_CONV, a=ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
-                y=proto.ptr, ldy=proto.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, out_f32=1,
+                y=proto.ptr, ldy=proto.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, out_f32=1, bias4=1,
                 w2=w3c.data_ptr(), b2=p3.b.data_ptr(), c2=p3.cout, act2=1)))
             meta.append({"name": "model.22.proto.upsample+cv2+cv3 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
