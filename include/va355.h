@@ -197,6 +197,19 @@ typedef struct va_conv_args {
 
 int va_seg_conv(void* stream, const va_conv_args* a);
 
+/* One C2f block with n = 1 and a shortcut, 64 -> 64 channels (block.py C2f / Bottleneck, hidden 32):
+ * cv1 (1x1) -> chunk -> m.0.cv1 (3x3) -> m.0.cv2 (3x3) + residual -> cat -> cv2 (1x1), every conv with
+ * folded BN bias + SiLU, as ONE launch whose intermediates never leave the chip (bf16 only).  Uses
+ * a.x / a.ldx (input, 64 channels), a.N / H / W, a.Cin = a.Cout = 64, a.y / a.ldy (output), a.dtype and:
+ *   a.w    bf16 weight blob in MFMA fragment order (28672 values; layout: seg.py SegNet._pack_c2f)
+ *   a.bias float [192] = cv1 [64] | m.0.cv1 [32] | m.0.cv2 [32] | cv2 [64]
+ * ldx, ldy % 8 == 0; x, y, w, bias 16-byte aligned.  Replaces the four va_seg_conv calls of the
+ * block (the reference's model.2 in YOLOv8s-seg). */
+int va_seg_c2f(void* stream, const va_conv_args* a);
+/* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
+ * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
+int va_c2f_trace(void* buf);
+
 /* uint8 BGR frames [B][H][W][3] -> RGB / 255 NHWC with 8 channels (3 used), dtype VA_DTYPE_*. */
 int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H, int32_t W, int32_t dtype, void* out);
 
@@ -223,6 +236,7 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_PREPROCESS 4  /* preprocess: a.x = uint8 frames, a.y = out, a.N/H/W, a.dtype */
 #define VA_OP_CONV0 5       /* preprocess fused into model.0 (bf16): a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
                                a.Cout, a.y, a.ldy -- see va_seg_conv0 */
+#define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
 typedef struct va_seg_op {
     int32_t kind;
     int32_t pad_;

@@ -327,3 +327,89 @@ def test_conv4_matches_conv2(monkeypatch):
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: conv4 vs conv2 max diff {(g - r).abs().max().item()}"
+
+
+def _c2f_reference(x, fw, i):
+    """block.py C2f(n=1, shortcut) in fp32 on the CPU with every intermediate rounded to bf16 the way the
+    unfused layers store it (x: NCHW float of bf16 values)."""
+    bf = lambda t: t.to(torch.bfloat16).float()
+    silu = torch.nn.functional.silu
+    w1, b1 = fw[f"model.{i}.cv1"]
+    wm1, bm1 = fw[f"model.{i}.m.0.cv1"]
+    wm2, bm2 = fw[f"model.{i}.m.0.cv2"]
+    w2, b2 = fw[f"model.{i}.cv2"]
+    t = bf(silu(F.conv2d(x, w1.float(), b1.float())))
+    a, b = t[:, :32], t[:, 32:]
+    m = bf(silu(F.conv2d(b, wm1.float(), bm1.float(), padding=1)))
+    bp = bf(silu(F.conv2d(m, wm2.float(), bm2.float(), padding=1)) + b)
+    return bf(silu(F.conv2d(torch.cat([a, b, bp], 1), w2.float(), b2.float())))
+
+
+@pytest.mark.parametrize("B,H,W,ldx,ldy", [(3, 160, 160, 64, 64), (1, 40, 56, 72, 80), (3, 24, 20, 64, 64),
+                                           (1, 7, 33, 64, 72)])
+def test_c2f_fused_op(B, H, W, ldx, ldy):
+    """va_seg_c2f (model.2 as one kernel: cv1 -> m.0.cv1 -> m.0.cv2 + residual -> cv2) vs the block in
+    fp32 with the unfused layers' bf16 rounding; ragged tiles (H, W not multiples of 16), channel slices
+    and a persistent grid that walks several tiles per workgroup."""
+    import ctypes
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    arch, fw, net = _net("bf16", "s")
+    assert 2 in net.c2f_fused
+    blob, bias = net.c2f_fused[2]
+    g = torch.Generator().manual_seed(B * 1000 + H + W)
+    xin = torch.zeros(B, H, W, ldx, dtype=torch.bfloat16)
+    xin[..., :64] = (torch.randn(B, H, W, 64, generator=g) * 1.5).to(torch.bfloat16)
+    xd = xin.cuda()
+    y = torch.full((B, H, W, ldy), 7.0, dtype=torch.bfloat16, device="cuda")
+    a = S.ConvArgs(x=xd.data_ptr(), N=B, H=H, W=W, Cin=64, ldx=ldx, w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                   y=y.data_ptr(), ldy=ldy, dtype=S.VA_DTYPE_BF16)
+    lib = _lib.load()
+    _lib.check(lib.va_seg_c2f(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_c2f")
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert (got[..., 64:] == 7.0).all(), "wrote outside its channel slice"
+    ref = _c2f_reference(xin[..., :64].float().permute(0, 3, 1, 2), fw, 2).permute(0, 2, 3, 1)
+    got = got[..., :64]
+    # the same block as the four unfused layers (va_seg_conv through the 96-channel concat buffer)
+    t = torch.zeros(B, H, W, 96, dtype=torch.bfloat16, device="cuda")
+    tmp = torch.zeros(B, H, W, 32, dtype=torch.bfloat16, device="cuda")
+    y2 = torch.zeros(B, H, W, 64, dtype=torch.bfloat16, device="cuda")
+    es = 2
+
+    def conv(prefix, x, ldx_, y_, ldy_, res=None):
+        p = net.w[prefix]
+        c = S.ConvArgs(x=x, N=B, H=H, W=W, Cin=p.cin, ldx=ldx_, kh=p.k, kw=p.k, stride=1, pad=p.k // 2, Ho=H, Wo=W,
+                       w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad, y=y_,
+                       ldy=ldy_, res=res, ldr=96 if res else 0, act=1, mode=0, M=B * H * W, dtype=S.VA_DTYPE_BF16)
+        _lib.check(lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(c)), prefix)
+
+    conv("model.2.cv1", xd.data_ptr(), ldx, t.data_ptr(), 96)
+    conv("model.2.m.0.cv1", t.data_ptr() + 32 * es, 96, tmp.data_ptr(), 32)
+    conv("model.2.m.0.cv2", tmp.data_ptr(), 32, t.data_ptr() + 64 * es, 96, res=t.data_ptr() + 32 * es)
+    conv("model.2.cv2", t.data_ptr(), 96, y2.data_ptr(), 64)
+    torch.cuda.synchronize()
+    plain = y2.float().cpu()
+    rel = lambda u, v: ((u - v).norm() / v.norm()).item()
+    # both differ from the reference by bf16 rounding flips (fast SiLU, accumulation order) that the
+    # chain of four layers spreads; the fused block must be no further from it than the unfused layers
+    assert rel(plain, ref) < 1e-2, rel(plain, ref)
+    assert rel(got, ref) < 1.25 * rel(plain, ref) + 5e-4, (rel(got, ref), rel(plain, ref))
+    assert ((got - ref).abs() <= 0.03 * ref.abs() + 2e-2).float().mean().item() > 0.999
+
+
+def test_c2f_fused_in_plan(monkeypatch):
+    """The bf16 's' plan runs model.2 as one fused op, and the heads match the plan without it."""
+    arch, fw, net = _net("bf16", "s")
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "model.2 (fused C2f)" in names and "model.2.cv1" not in names
+    frames = _frames(2, seed=9)
+    fused = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_C2F", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="bf16")
+    assert "model.2.cv1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
+    plain = _gpu_heads(net2, frames)
+    for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
+        err = ((g_ - r).norm() / r.norm()).item()
+        assert err < 1e-2, f"{name}: fused vs unfused C2f {err}"

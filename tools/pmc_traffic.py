@@ -19,7 +19,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"conv(0|2|3|_dn|_patch|_wp)?_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f)_kernel")
 
 
 def family(name: str) -> str:

@@ -2321,6 +2321,9 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
             case VA_OP_CONV0:
                 rc = va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
+            case VA_OP_C2F:
+                rc = va_seg_c2f(stream, &a);
+                break;
             default:
                 rc = VA_ERR_ARG;
         }

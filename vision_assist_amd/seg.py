@@ -23,7 +23,7 @@ from . import _lib
 from .seg_arch import NM, REG_MAX, Arch
 
 VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
-VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0 = 1, 2, 3, 4, 5
+VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F = 1, 2, 3, 4, 5, 6
 BK = 64  # K padding: the bf16 kernel steps K by 64 (the f32 kernel by 32)
 NPAD = 128
 
@@ -119,7 +119,45 @@ class SegNet:
         self.fuse_first = dtype == "bf16" and w0.shape[0] % 16 == 0 and w0.shape[0] <= 64
         self.proto_fold = self._fold_proto(folded) if (dtype == "bf16" and arch.npr == 128
                                                        and os.environ.get("VA_FOLD_PROTO", "1") != "0") else None
+        # C2f blocks the fused kernel covers (va355.h va_seg_c2f): n = 1, shortcut, 64 -> 64 (model.2 of 's')
+        self.c2f_fused = {}
+        if dtype == "bf16" and os.environ.get("VA_C2F", "1") != "0":
+            for i, ci, co, n, shortcut in arch.c2f_plan():
+                if ci == 64 and co == 64 and n == 1 and shortcut:
+                    self.c2f_fused[i] = self._pack_c2f(folded, i)
         self._plans = {}
+
+    def _pack_c2f(self, folded: dict, i: int):
+        """Weight blob + bias vector of va_seg_c2f for C2f block ``model.{i}`` (block.py C2f / Bottleneck).
+
+        The blob is bf16 MFMA A fragments (64 lanes x 8 values; lane l = 16 fq + fr holds row fr, K
+        8 fq .. 8 fq + 7 of a 16 x 32 tile) in the order F1 cv1 [4 row groups][2 K-steps], F2 m.0.cv1
+        [9 taps][2], F3 m.0.cv2 [9][2], F4 cv2 [4][3].  K inside every 32-channel chunk that the kernel
+        hands over in registers or LDS is in P32 order (the channel a C fragment puts at position k),
+        and cv2's rows are permuted so a lane's two row groups are 8 consecutive output channels."""
+        w1, b1 = folded[f"model.{i}.cv1"]
+        wm1, bm1 = folded[f"model.{i}.m.0.cv1"]
+        wm2, bm2 = folded[f"model.{i}.m.0.cv2"]
+        w2, b2 = folded[f"model.{i}.cv2"]
+        p32 = torch.tensor([4 * (k >> 3) + (k & 3) + 16 * ((k >> 2) & 1) for k in range(32)])
+
+        def frag(a):  # [16][32] -> [64][8]
+            return a.reshape(16, 4, 8).permute(1, 0, 2).reshape(64, 8)
+
+        w1m = w1[:, :, 0, 0].float()  # [64 co][64 ci]
+        f1 = [frag(w1m[16 * q:16 * q + 16, 32 * s:32 * s + 32]) for q in range(4) for s in range(2)]
+        f2 = [frag(wm1[16 * q:16 * q + 16, :, t // 3, t % 3].float()[:, p32]) for t in range(9) for q in range(2)]
+        f3 = [frag(wm2[16 * q:16 * q + 16, :, t // 3, t % 3].float()[:, p32]) for t in range(9) for q in range(2)]
+        w2m = w2[:, :, 0, 0].float()  # [64 co][96 ci]
+        f4 = []
+        for q in range(4):
+            rows = torch.tensor([32 * (q >> 1) + 8 * (r >> 2) + 4 * (q & 1) + (r & 3) for r in range(16)])
+            for s in range(3):
+                f4.append(frag(w2m[rows][:, 32 * s + p32]))
+        blob = torch.stack(f1 + f2 + f3 + f4).reshape(-1)
+        assert blob.numel() == 28672
+        bias = torch.cat([b1, bm1, bm2, b2]).float()
+        return (blob.to(self.device, self.tdtype).contiguous(), bias.to(self.device).contiguous())
 
     def _fold_proto(self, folded: dict) -> Packed:
         """Packed weights of the sub-pixel fold of proto's upsample + cv2 (see fold_proto_weights), and its
@@ -236,6 +274,16 @@ class SegNet:
 
         def c2f(i, src: Slice, dst: Slice, h, w):
             _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
+            if i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
+                blob, bias = self.c2f_fused[i]
+                ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld, w=blob.data_ptr(),
+                                                             bias=bias.data_ptr(), Cout=64, y=dst.ptr, ldy=dst.ld,
+                                                             dtype=self.va_dtype)))
+                macs = 64 * 64 + 2 * 32 * 288 + 64 * 96  # per pixel, the four convs
+                meta.append({"name": f"model.{i} (fused C2f)", "kind": "conv", "M": B * h * w, "N": 64,
+                             "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
+                             "bytes": 2 * B * h * w * 128})
+                return
             c = co // 2
             t = new(h, w, (2 + n) * c)
             conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w)
