@@ -205,7 +205,7 @@ def main():
         cnt = (ctypes.c_int64 * 8)()
         sampling["on"] = False
         lib.va_prof_stop(ms, cnt, 8)
-        conv_ms, conv_n = ms[1] + ms[5] + ms[6], cnt[1] + cnt[5] + cnt[6]  # VA_OP_CONV + CONV0 + C2F (fused)
+        conv_ms, conv_n = ms[1] + ms[5] + ms[6] + ms[7], cnt[1] + cnt[5] + cnt[6] + cnt[7]  # CONV + CONV0 + C2F + STEM
         other_seg_ms = ms[2] + ms[3] + ms[4]
         # the same per-op events on 3 forwards run alone (after the timed region, untimed): the kernel's
         # duration without a concurrent forward sharing the chip
@@ -216,7 +216,8 @@ def main():
             torch.cuda.synchronize()
         iso_ms, iso_cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
         lib.va_prof_stop(iso_ms, iso_cnt, 8)
-        iso_conv_ms, iso_conv_n = iso_ms[1] + iso_ms[5] + iso_ms[6], iso_cnt[1] + iso_cnt[5] + iso_cnt[6]
+        iso_conv_ms = iso_ms[1] + iso_ms[5] + iso_ms[6] + iso_ms[7]
+        iso_conv_n = iso_cnt[1] + iso_cnt[5] + iso_cnt[6] + iso_cnt[7]
     # results sanity (last batch): count frames with >= 1 path
     last = res
     for i in range(B):

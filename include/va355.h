@@ -206,6 +206,14 @@ int va_seg_conv(void* stream, const va_conv_args* a);
  * ldx, ldy % 8 == 0; x, y, w, bias 16-byte aligned.  Replaces the four va_seg_conv calls of the
  * block (the reference's model.2 in YOLOv8s-seg). */
 int va_seg_c2f(void* stream, const va_conv_args* a);
+/* The stem (bf16) as ONE launch: uint8 BGR frames [N][H][W][3] -> RGB / 255 -> model.0 Conv(3, 32, 3x3, s2)
+ * + SiLU -> model.1 Conv(32, 64, 3x3, s2) + SiLU -> a.y [N][ceil(H/4)][ceil(W/4)] (channel stride a.ldy), the
+ * 32-channel model.0 map never leaving the chip.  Replaces va_seg_conv0 + the model.1 va_seg_conv.  Uses
+ * a.x (frames), a.N / H / W (frame size, W % 16 == 0), a.Cin = 32, a.Cout = 64, a.y / a.ldy (ldy % 8 == 0),
+ * a.dtype = VA_DTYPE_BF16 and:
+ *   a.w    bf16 weight blob in MFMA fragment order (19456 values; layout: seg.py SegNet._pack_stem)
+ *   a.bias float [96] = model.0 [32] | model.1 [64] */
+int va_seg_stem(void* stream, const va_conv_args* a);
 /* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
  * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
 int va_c2f_trace(void* buf);
@@ -237,6 +245,7 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_CONV0 5       /* preprocess fused into model.0 (bf16): a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
                                a.Cout, a.y, a.ldy -- see va_seg_conv0 */
 #define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
+#define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: see va_seg_stem */
 typedef struct va_seg_op {
     int32_t kind;
     int32_t pad_;

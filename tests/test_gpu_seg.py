@@ -185,12 +185,12 @@ def test_fused_tail_matches_unfused(monkeypatch):
     frames = _frames(2, seed=5)
     names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
     assert "model.22.proto.cv2+model.22.proto.cv3" in names
-    assert sum("+" in n for n in names) == 10  # proto + cv2/cv3/cv4 at 3 levels
+    assert sum("+" in n and "fused" not in n for n in names) == 10  # proto + cv2/cv3/cv4 at 3 levels
     fused = _gpu_heads(net, frames)
     monkeypatch.setenv("VA_FUSE_TAIL", "0")
     from vision_assist_amd.seg import SegNet
     net2 = SegNet(arch, fw, dtype="bf16")
-    assert not any("+" in m["name"] for m in net2.plan(2, 640, 640)["meta"])
+    assert not any("+" in m["name"] and "fused" not in m["name"] for m in net2.plan(2, 640, 640)["meta"])
     plain = _gpu_heads(net2, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         err = ((g - r).abs().max() / r.abs().max()).item()
@@ -413,3 +413,75 @@ def test_c2f_fused_in_plan(monkeypatch):
     for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         err = ((g_ - r).norm() / r.norm()).item()
         assert err < 1e-2, f"{name}: fused vs unfused C2f {err}"
+
+
+def _stem_reference(frames_u8, fw):
+    """preprocess + model.0 + SiLU (rounded to bf16 as the stored layer) + model.1 + SiLU in fp32 on the CPU
+    (frames: [B, H, W, 3] uint8 BGR)."""
+    bf = lambda t: t.to(torch.bfloat16).float()
+    silu = torch.nn.functional.silu
+    x = bf(frames_u8[..., [2, 1, 0]].float().permute(0, 3, 1, 2) / 255.0)
+    w0, b0 = fw["model.0"]
+    w1, b1 = fw["model.1"]
+    a0 = bf(silu(F.conv2d(x, bf(w0.float()), b0.float(), stride=2, padding=1)))
+    return bf(silu(F.conv2d(a0, bf(w1.float()), b1.float(), stride=2, padding=1)))
+
+
+@pytest.mark.parametrize("B,H,W,ldy", [(3, 640, 640, 64), (1, 96, 160, 72), (2, 64, 48, 64), (1, 40, 80, 64)])
+def test_stem_fused_op(B, H, W, ldy):
+    """va_seg_stem (uint8 frame -> model.0 -> model.1 as one kernel) vs the fp32 reference with the unfused
+    layers' bf16 rounding, and no further from it than the unfused va_seg_conv0 + va_seg_conv pair; ragged
+    tiles (output not a multiple of 16) and a persistent grid walking several tiles per workgroup."""
+    import ctypes
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    arch, fw, net = _net("bf16", "s")
+    assert net.stem is not None
+    blob, bias = net.stem
+    g = torch.Generator().manual_seed(B * 7 + H + W)
+    fr = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8)
+    frd = fr.cuda()
+    Ho1, Wo1 = (H + 3) // 4, (W + 3) // 4
+    y = torch.full((B, Ho1, Wo1, ldy), 7.0, dtype=torch.bfloat16, device="cuda")
+    a = S.ConvArgs(x=frd.data_ptr(), N=B, H=H, W=W, Cin=32, w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                   y=y.data_ptr(), ldy=ldy, dtype=S.VA_DTYPE_BF16)
+    lib = _lib.load()
+    _lib.check(lib.va_seg_stem(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_stem")
+    # unfused: va_seg_conv0 -> [B, H/2, W/2, 32] -> va_seg_conv model.1
+    a0 = torch.zeros(B, (H + 1) // 2, (W + 1) // 2, 32, dtype=torch.bfloat16, device="cuda")
+    _lib.check(lib.va_seg_conv0(_lib.stream_ptr(), ctypes.c_void_p(frd.data_ptr()), B, H, W,
+                                ctypes.c_void_p(net.w0[0].data_ptr()), ctypes.c_void_p(net.w0[1].data_ptr()), 32,
+                                ctypes.c_void_p(a0.data_ptr()), 32), "conv0")
+    y2 = torch.zeros(B, Ho1, Wo1, 64, dtype=torch.bfloat16, device="cuda")
+    p = net.w["model.1"]
+    c = S.ConvArgs(x=a0.data_ptr(), N=B, H=a0.shape[1], W=a0.shape[2], Cin=p.cin, ldx=32, kh=3, kw=3, stride=2, pad=1,
+                   Ho=Ho1, Wo=Wo1, w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=64, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
+                   y=y2.data_ptr(), ldy=64, act=1, mode=0, M=B * Ho1 * Wo1, dtype=S.VA_DTYPE_BF16)
+    _lib.check(lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(c)), "model.1")
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert (got[..., 64:] == 7.0).all(), "wrote outside its channel slice"
+    got = got[..., :64]
+    plain = y2.float().cpu()
+    ref = _stem_reference(fr, fw).permute(0, 2, 3, 1)
+    rel = lambda u, v: ((u - v).norm() / v.norm()).item()
+    assert rel(plain, ref) < 1e-2, rel(plain, ref)
+    assert rel(got, ref) < 1.25 * rel(plain, ref) + 5e-4, (rel(got, ref), rel(plain, ref))
+    assert ((got - ref).abs() <= 0.03 * ref.abs() + 2e-2).float().mean().item() > 0.999
+
+
+def test_stem_fused_in_plan(monkeypatch):
+    """The bf16 's' plan runs preprocess + model.0 + model.1 as one op; heads match the plan without it."""
+    arch, fw, net = _net("bf16", "s")
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "model.0+model.1 (fused stem)" in names and "model.1" not in names
+    frames = _frames(2, seed=11)
+    fused = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_STEM", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="bf16")
+    assert "model.1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
+    plain = _gpu_heads(net2, frames)
+    for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
+        err = ((g_ - r).norm() / r.norm()).item()
+        assert err < 1e-2, f"{name}: fused vs unfused stem {err}"

@@ -31,26 +31,22 @@
 #include <type_traits>
 
 #include "../../include/va355.h"
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#include "va_fuse.h"
 
 namespace {
 
-__device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+using fz::mma;
 
 constexpr int CF_T = 16;      // tile width (a row segment = one 16-pixel MFMA column group)
 constexpr int CF_R1W = CF_T + 4, CF_R2W = CF_T + 2;  // stage-1 / stage-2 region widths (halo 2 / 1)
-constexpr int CF_FRAG = 512;  // bf16 per MFMA operand fragment (64 lanes x 8)
+constexpr int CF_FRAG = fz::FRAG;
 constexpr int CF_PS = 96;     // LDS bytes per pixel of S1 / S2 (32 bf16 channels + 32 bytes of padding)
 // weight blob (bf16, fragment order): F1 cv1 [4 groups][2 k-steps], F2 m.0.cv1 [9 taps][2 groups],
 // F3 m.0.cv2 [9][2], F4 cv2 [4 groups][3 k-steps]
 constexpr int CF_F1 = 0, CF_F2 = 8 * CF_FRAG, CF_F3 = CF_F2 + 18 * CF_FRAG, CF_F4 = CF_F3 + 18 * CF_FRAG;
 constexpr int CF_WBLOB = CF_F4 + 12 * CF_FRAG;  // 28672 bf16 = 56 KiB
 static_assert(CF_WBLOB == 28672, "blob size (seg.py SegNet._pack_c2f)");
-constexpr int CF_OOB = 0x80000000;   // buffer offset past num_records: load returns 0, store is dropped
-constexpr int CF_RSRC = 0x00020000;  // buffer descriptor word 3 (gfx9 raw buffer)
+constexpr int CF_OOB = fz::OOB, CF_RSRC = fz::RSRC;
 
 // Tile geometry and LDS map of one configuration: TH output rows x 16 columns per tile, NW waves,
 // WPC workgroups per CU, the 1x1 weights in registers (WREG) or in LDS.
@@ -83,54 +79,12 @@ struct CfCfg {
 // 2-way, which the write's own transfer time hides
 __device__ __forceinline__ int cf_addr(int p, int c) { return p * CF_PS + 16 * c; }
 
-__device__ __forceinline__ bf16x8 cf_zero_if(bf16x8 v, bool out) {  // masks whole dwords (packed pairs)
-    u32x4 u = (u32x4)v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) u[r] = out ? 0u : u[r];
-    return (bf16x8)u;
-}
-
-__device__ __forceinline__ bf16x8 cf_pack(f32x4 lo, f32x4 hi) {
-    bf16x8 o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        o[r] = (__bf16)lo[r];
-        o[4 + r] = (__bf16)hi[r];
-    }
-    return o;
-}
-
-__device__ __forceinline__ f32x4 cf_act(f32x4 x) { return (f32x4){silu(x[0]), silu(x[1]), silu(x[2]), silu(x[3])}; }
-
-__device__ __forceinline__ int cf_lane() {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
-__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
 struct CfGeom {
     int N, H, W, ldx, ldy, tx, tpf, ntiles;
     int getenv_rt;              // debug: trace with the 100 MHz real-time counter instead of the shader clock
     unsigned long long* trace;  // debug (va_c2f_trace): [grid][NW waves][CF_TR_TILES][CF_TR_PTS] clocks, or null
 };
 constexpr int CF_TR_TILES = 32, CF_TR_PTS = 6;
-
-// k-th tile of workgroup b (or -1): with a grid that is a multiple of 8, the workgroups of one XCD
-// (b mod 8) share a contiguous run of tiles (neighbouring tiles' halo reads hit the same L2)
-__device__ __forceinline__ int cf_tile(const CfGeom& g, int k) {
-    const int G = gridDim.x, b = blockIdx.x;
-    if (G % 8) {
-        const int t = b + k * G;
-        return t < g.ntiles ? t : -1;
-    }
-    const int per = G / 8, run = (g.ntiles + 7) / 8, x = b & 7;
-    const int t = x * run + (b >> 3) + k * per;
-    return (t < g.ntiles && t < (x + 1) * run) ? t : -1;
-}
 
 // ring pixel q of the R1H x 20 stage-1 region minus its TH x 16 centre: rows 0-1, rows R1H-2..R1H-1,
 // then columns 0, 1, 18, 19 of rows 2 .. R1H-3
@@ -164,7 +118,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
     const float* b3 = b1 + 96;                              // m.0.cv2 [32]
     const float* b4 = b1 + 128;                             // cv2 [64]
 
-    int t = cf_tile(g, 0);
+    int t = fz::tile(g.ntiles, 0);
     if (t < 0) return;
     // weights and biases -> LDS (once per workgroup); with WREG the 1x1 weights -> registers
     {
@@ -234,7 +188,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
         // (opaque to the compiler): otherwise it
         // hoists every per-lane LDS address of the body out of the loop and spills them to scratch, whose
         // reloads then wait on the in-flight prefetch (vmcnt is in order)
-        const int lane = (NW == 16 || C::WREG) ? cf_lane() : tid & 63, fr = lane & 15, fq = lane >> 4;
+        const int lane = (NW == 16 || C::WREG) ? fz::lane_id() : tid & 63, fr = lane & 15, fq = lane >> 4;
         auto frag = [&](int base, int f) { return *(const bf16x8*)(cf_smem + base + f * 1024 + 16 * lane); };
         auto bvec = [&](const float* b) {  // bias rows of a C fragment: the accumulators start from the bias
             const float4 v = *(const float4*)b;
@@ -269,12 +223,12 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
 #pragma unroll
             for (int i = 0; i < RPW; ++i) {
                 const int y = RPW * wid + i;
-                ra[i] = cf_pack(cf_act(acc1[i][0]), cf_act(acc1[i][1]));
-                rb[i] = cf_pack(cf_act(acc1[i][2]), cf_act(acc1[i][3]));
+                ra[i] = fz::pack(fz::act(acc1[i][0]), fz::act(acc1[i][1]));
+                rb[i] = fz::pack(fz::act(acc1[i][2]), fz::act(acc1[i][3]));
                 if (!interior) {
                     const bool out = y0 + y >= g.H || x0 + fr >= g.W;
-                    ra[i] = cf_zero_if(ra[i], out);
-                    rb[i] = cf_zero_if(rb[i], out);
+                    ra[i] = fz::zero_if(ra[i], out);
+                    rb[i] = fz::zero_if(rb[i], out);
                 }
                 *(bf16x8*)(cf_smem + C::S1 + cf_addr((y + 2) * CF_R1W + fr + 2, fq)) = rb[i];
             }
@@ -283,16 +237,16 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
                 if (wid + NW * i >= C::NRING) break;
                 int ry, rx;
                 cf_ring<R1H>(16 * (wid + NW * i) + fr, ry, rx);
-                bf16x8 v = cf_pack(cf_act(accr[i][0]), cf_act(accr[i][1]));
+                bf16x8 v = fz::pack(fz::act(accr[i][0]), fz::act(accr[i][1]));
                 if (!interior) {
                     const int y = y0 - 2 + ry, x = x0 - 2 + rx;
-                    v = cf_zero_if(v, (unsigned)y >= (unsigned)g.H || (unsigned)x >= (unsigned)g.W);
+                    v = fz::zero_if(v, (unsigned)y >= (unsigned)g.H || (unsigned)x >= (unsigned)g.W);
                 }
                 *(bf16x8*)(cf_smem + C::S1 + cf_addr(ry * CF_R1W + rx, fq)) = v;
             }
         }
         mark(k, 1);
-        const int tn = cf_tile(g, k);
+        const int tn = fz::tile(g.ntiles, k);
         if (tn >= 0) load_tile(tn);  // lands during stages 2-4
         __syncthreads();
         mark(k, 2);
@@ -347,10 +301,10 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
             }
 #pragma unroll
             for (int j = 0; j < NGJ; ++j) {
-                bf16x8 v = cf_pack(cf_act(acc[j][0]), cf_act(acc[j][1]));
+                bf16x8 v = fz::pack(fz::act(acc[j][0]), fz::act(acc[j][1]));
                 if (!interior) {
                     const int y = y0 - 1 + py[j], x = x0 - 1 + px[j];
-                    v = cf_zero_if(v, (unsigned)y >= (unsigned)g.H || (unsigned)x >= (unsigned)g.W);
+                    v = fz::zero_if(v, (unsigned)y >= (unsigned)g.H || (unsigned)x >= (unsigned)g.W);
                 }
                 const int ad = pv[j] ? C::S2 + cf_addr(py[j] * CF_R2W + px[j], fq) : C::SINK + 16 * lane;
                 *(bf16x8*)(cf_smem + ad) = v;
@@ -400,11 +354,11 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
                 f32x4 v[2];
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
-                    v[q] = cf_act(acc[i][q]);
+                    v[q] = fz::act(acc[i][q]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[q][r] += (float)rb[i][4 * q + r];
                 }
-                rbp[i] = cf_pack(v[0], v[1]);
+                rbp[i] = fz::pack(v[0], v[1]);
             }
             f32x4 o4[RPW][4];
 #pragma unroll
@@ -427,7 +381,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                     __builtin_amdgcn_raw_buffer_store_b128(
-                        (u32x4)cf_pack(cf_act(o4[i][2 * h]), cf_act(o4[i][2 * h + 1])), ry, off, 64 * h, 0);
+                        (u32x4)fz::pack(fz::act(o4[i][2 * h]), fz::act(o4[i][2 * h + 1])), ry, off, 64 * h, 0);
             }
         }
         mark(k, 5);

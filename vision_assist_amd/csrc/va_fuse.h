@@ -1,0 +1,67 @@
+// va_fuse.h -- shared device helpers of the fused multi-layer kernels (va_c2f.hip, va_stem.hip):
+// MFMA 16x16x32 bf16 fragments, SiLU epilogues, buffer-descriptor masking, the XCD-aware persistent
+// tile schedule.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+namespace fz {
+
+constexpr int FRAG = 512;             // bf16 per MFMA operand fragment (64 lanes x 8)
+constexpr int OOB = 0x80000000;       // buffer offset past num_records: a load returns 0, a store is dropped
+constexpr int RSRC = 0x00020000;      // buffer descriptor word 3 (gfx9 raw buffer)
+
+// bf16 epilogues: hardware exp and reciprocal (~1 ulp f32, far below the bf16 rounding that follows),
+// the same expression as va_seg.hip's unfused layers
+__device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ f32x4 act(f32x4 x) { return (f32x4){silu(x[0]), silu(x[1]), silu(x[2]), silu(x[3])}; }
+
+__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// two C fragments (rows 4 fq .. 4 fq + 3 of two 16-row groups) -> one lane's 8 bf16 (P32 order: the
+// channel order a consumer's K is permuted to when it takes this as its B fragment)
+__device__ __forceinline__ bf16x8 pack(f32x4 lo, f32x4 hi) {
+    bf16x8 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        o[r] = (__bf16)lo[r];
+        o[4 + r] = (__bf16)hi[r];
+    }
+    return o;
+}
+
+__device__ __forceinline__ bf16x8 zero_if(bf16x8 v, bool out) {  // masks whole dwords (packed pairs)
+    u32x4 u = (u32x4)v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) u[r] = out ? 0u : u[r];
+    return (bf16x8)u;
+}
+
+// lane id through an opaque asm: stops the compiler hoisting every per-lane address of a persistent
+// loop body out of the loop (and spilling them)
+__device__ __forceinline__ int lane_id() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// k-th tile of workgroup blockIdx.x (or -1): with a grid that is a multiple of 8, the workgroups of one
+// XCD (blockIdx mod 8) share a contiguous run of tiles, so neighbouring tiles' halo reads hit its L2
+__device__ __forceinline__ int tile(int ntiles, int k) {
+    const int G = gridDim.x, b = blockIdx.x;
+    if (G % 8) {
+        const int t = b + k * G;
+        return t < ntiles ? t : -1;
+    }
+    const int per = G / 8, run = (ntiles + 7) / 8, x = b & 7;
+    const int t = x * run + (b >> 3) + k * per;
+    return (t < ntiles && t < (x + 1) * run) ? t : -1;
+}
+
+}  // namespace fz

@@ -23,7 +23,7 @@ from . import _lib
 from .seg_arch import NM, REG_MAX, Arch
 
 VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
-VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F = 1, 2, 3, 4, 5, 6
+VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 BK = 64  # K padding: the bf16 kernel steps K by 64 (the f32 kernel by 32)
 NPAD = 128
 
@@ -119,6 +119,12 @@ class SegNet:
         self.fuse_first = dtype == "bf16" and w0.shape[0] % 16 == 0 and w0.shape[0] <= 64
         self.proto_fold = self._fold_proto(folded) if (dtype == "bf16" and arch.npr == 128
                                                        and os.environ.get("VA_FOLD_PROTO", "1") != "0") else None
+        # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
+        self.stem = None
+        if self.fuse_first and w0.shape[0] == 32 and os.environ.get("VA_STEM", "1") != "0":
+            w1, b1 = folded["model.1"]
+            if tuple(w1.shape) == (64, 32, 3, 3):
+                self.stem = self._pack_stem(w0p, b0, w1, b1)
         # C2f blocks the fused kernel covers (va355.h va_seg_c2f): n = 1, shortcut, 64 -> 64 (model.2 of 's')
         self.c2f_fused = {}
         if dtype == "bf16" and os.environ.get("VA_C2F", "1") != "0":
@@ -126,6 +132,27 @@ class SegNet:
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
         self._plans = {}
+
+    def _pack_stem(self, w0p: torch.Tensor, b0: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
+        """Weight blob + bias vector of va_seg_stem: bf16 MFMA A fragments (see _pack_c2f) W0 = model.0
+        [2 row groups] (K = (ky*3 + kx)*3 + RGB channel, 27 of 32, as va_seg_conv0), then W1 = model.1
+        [9 taps][4 row groups] with K in P32 order inside the tap (the channel order model.0's C fragments
+        leave in LDS) and rows permuted so a lane's two row groups are 8 consecutive output channels."""
+        p32 = torch.tensor([4 * (k >> 3) + (k & 3) + 16 * ((k >> 2) & 1) for k in range(32)])
+
+        def frag(a):  # [16][32] -> [64][8]
+            return a.reshape(16, 4, 8).permute(1, 0, 2).reshape(64, 8)
+
+        f0 = [frag(w0p[16 * q:16 * q + 16].float()) for q in range(2)]
+        f1 = []
+        for t in range(9):
+            for q in range(4):
+                rows = torch.tensor([32 * (q >> 1) + 8 * (r >> 2) + 4 * (q & 1) + (r & 3) for r in range(16)])
+                f1.append(frag(w1[rows][:, :, t // 3, t % 3].float()[:, p32]))
+        blob = torch.stack(f0 + f1).reshape(-1)
+        assert blob.numel() == 19456
+        bias = torch.cat([b0.float(), b1.float()])
+        return (blob.to(self.device, self.tdtype).contiguous(), bias.to(self.device).contiguous())
 
     def _pack_c2f(self, folded: dict, i: int):
         """Weight blob + bias vector of va_seg_c2f for C2f block ``model.{i}`` (block.py C2f / Bottleneck).
@@ -305,21 +332,32 @@ class SegNet:
         h3, w3 = H // 8, W // 8
         h4, w4 = H // 16, W // 16
         h5, w5 = H // 32, W // 32
-        a0 = new(h1, w1, a.c1)
-        if self.fuse_first:
-            ops.append(SegOp(kind=VA_OP_CONV0, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, w=self.w0[0].data_ptr(),
-                                                           bias=self.w0[1].data_ptr(), Cout=a.c1, y=a0.ptr, ldy=a0.ld,
-                                                           dtype=self.va_dtype)))
-            meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3, "stride": 2,
-                         "bytes": B * H * W * 3 + 2 * B * h1 * w1 * a.c1})
+        if self.stem is not None and W % 16 == 0:
+            a1 = new(h2, w2, a.c2)
+            blob, bias = self.stem
+            ops.append(SegOp(kind=VA_OP_STEM, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, w=blob.data_ptr(),
+                                                          bias=bias.data_ptr(), Cout=64, y=a1.ptr, ldy=a1.ld,
+                                                          dtype=self.va_dtype)))
+            macs = 27 * 32 * 4 + 288 * 64  # per model.1 output pixel: 4 model.0 pixels + model.1
+            meta.append({"name": "model.0+model.1 (fused stem)", "kind": "conv", "M": B * h2 * w2, "N": 64,
+                         "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
+                         "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
         else:
-            x0 = new(H, W, 8)
-            ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
-                                                                dtype=self.va_dtype)))
-            meta.append({"name": "preprocess", "kind": "preprocess"})
-            conv("model.0", x0, a0, H, W, stride=2)
-        a1 = new(h2, w2, a.c2)
-        conv("model.1", a0, a1, h1, w1, stride=2)
+            a0 = new(h1, w1, a.c1)
+            if self.fuse_first:
+                ops.append(SegOp(kind=VA_OP_CONV0, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W,
+                                                               w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
+                                                               Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)))
+                meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3,
+                             "stride": 2, "bytes": B * H * W * 3 + 2 * B * h1 * w1 * a.c1})
+            else:
+                x0 = new(H, W, 8)
+                ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
+                                                                    dtype=self.va_dtype)))
+                meta.append({"name": "preprocess", "kind": "preprocess"})
+                conv("model.0", x0, a0, H, W, stride=2)
+            a1 = new(h2, w2, a.c2)
+            conv("model.1", a0, a1, h1, w1, stride=2)
         p2 = new(h2, w2, a.c2)
         c2f(2, a1, p2, h2, w2)
         a3 = new(h3, w3, a.c3)
