@@ -211,12 +211,14 @@ int va_seg_c2f(void* stream, const va_conv_args* a);
  * 32-channel model.0 map never leaving the chip.  Replaces va_seg_conv0 + the model.1 va_seg_conv.  Uses
  * a.x (frames), a.N / H / W (frame size, W % 16 == 0), a.Cin = 32, a.Cout = 64, a.y / a.ldy (ldy % 8 == 0),
  * a.dtype = VA_DTYPE_BF16 and:
- *   a.w    bf16 weight blob in MFMA fragment order (19456 values; layout: seg.py SegNet._pack_stem)
+ *   a.w    bf16 weight blob in MFMA fragment order (20480 values; layout: seg.py SegNet._pack_stem)
  *   a.bias float [96] = model.0 [32] | model.1 [64] */
 int va_seg_stem(void* stream, const va_conv_args* a);
 /* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
  * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
 int va_c2f_trace(void* buf);
+/* Debug: the same for va_seg_stem ([grid][8][32][5] uint64 of the 100 MHz real-time counter). */
+int va_stem_trace(void* buf);
 
 /* uint8 BGR frames [B][H][W][3] -> RGB / 255 NHWC with 8 channels (3 used), dtype VA_DTYPE_*. */
 int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H, int32_t W, int32_t dtype, void* out);

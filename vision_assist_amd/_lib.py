@@ -55,6 +55,7 @@ SIGNATURES = [
     ("va_seg_c2f", I32, [P, P]),
     ("va_seg_stem", I32, [P, P]),
     ("va_c2f_trace", I32, [P]),
+    ("va_stem_trace", I32, [P]),
     ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
     ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),

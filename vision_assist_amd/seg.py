@@ -135,7 +135,7 @@ class SegNet:
 
     def _pack_stem(self, w0p: torch.Tensor, b0: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
         """Weight blob + bias vector of va_seg_stem: bf16 MFMA A fragments (see _pack_c2f) W0 = model.0
-        [2 row groups] (K = (ky*3 + kx)*3 + RGB channel, 27 of 32, as va_seg_conv0), then W1 = model.1
+        [2 row groups][2 K-steps] (K = (ky*3 + kx)*4 + channel, channels R, G, B, 0), then W1 = model.1
         [9 taps][4 row groups] with K in P32 order inside the tap (the channel order model.0's C fragments
         leave in LDS) and rows permuted so a lane's two row groups are 8 consecutive output channels."""
         p32 = torch.tensor([4 * (k >> 3) + (k & 3) + 16 * ((k >> 2) & 1) for k in range(32)])
@@ -143,14 +143,18 @@ class SegNet:
         def frag(a):  # [16][32] -> [64][8]
             return a.reshape(16, 4, 8).permute(1, 0, 2).reshape(64, 8)
 
-        f0 = [frag(w0p[16 * q:16 * q + 16].float()) for q in range(2)]
+        # model.0 with k = tap * 4 + c (c = R, G, B, 0), 36 of 64: from w0p's k = tap * 3 + c
+        w0k = torch.zeros(w0p.shape[0], 64)
+        for tap in range(9):
+            w0k[:, 4 * tap:4 * tap + 3] = w0p[:, 3 * tap:3 * tap + 3].float()
+        f0 = [frag(w0k[16 * q:16 * q + 16, 32 * s:32 * s + 32]) for q in range(2) for s in range(2)]
         f1 = []
         for t in range(9):
             for q in range(4):
                 rows = torch.tensor([32 * (q >> 1) + 8 * (r >> 2) + 4 * (q & 1) + (r & 3) for r in range(16)])
                 f1.append(frag(w1[rows][:, :, t // 3, t % 3].float()[:, p32]))
         blob = torch.stack(f0 + f1).reshape(-1)
-        assert blob.numel() == 19456
+        assert blob.numel() == 20480
         bias = torch.cat([b0.float(), b1.float()])
         return (blob.to(self.device, self.tdtype).contiguous(), bias.to(self.device).contiguous())
 
