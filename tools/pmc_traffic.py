@@ -2,7 +2,7 @@
 """Summarise rocprofv3 output of a bench.py run for profiles/.
 
   stats  <kernel_stats.csv> <out.json>
-      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/conv2/conv3/conv_dn/conv_patch
+      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/2/3/4/_dn/_patch/_wp, c2f, stem
       kernels: every launch of the YOLOv8-seg forward's GEMMs) gives the average launch duration that
       bench.py's roofline.avg_launch_us must agree with.
   traffic <fetch_counter_collection.csv> <write_counter_collection.csv> <key> <out.json>
@@ -19,7 +19,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f)_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f|stem)_kernel")
 
 
 def family(name: str) -> str:
