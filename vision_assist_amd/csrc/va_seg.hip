@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_fuse.h"
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -47,6 +48,17 @@ __device__ inline __bf16 from_f<__bf16>(float v) {
 // follows); the exact-f32 parity path uses silu_exact
 __device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ inline float silu_exact(float x) { return x / (1.0f + expf(-x)); }
+// silu() over an array, the plain f32 steps packed in pairs (fz::silu2): bit-identical to silu() per element
+template <int N>
+__device__ __forceinline__ void silu_n(float (&v)[N]) {
+    static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = fz::silu2((f32x2){v[i], v[i + 1]});
+        v[i] = r[0];
+        v[i + 1] = r[1];
+    }
+}
 
 // ----------------------------------------------------------------------------------------- preprocess
 template <typename T>
@@ -336,8 +348,9 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
             const float4 bv = *(const float4*)(a.bias + brow[j] + col);
             float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
             __bf16 o4[4];
+            if (a.act) silu_n(v);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o4[r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+            for (int r = 0; r < 4; ++r) o4[r] = (__bf16)v[r];
             *(uint2*)(Ts + (wm * 64 + 16 * j + fr) * TW + col) = *(uint2*)o4;
         }
     }
@@ -376,8 +389,7 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
             const float4 bv = *(const float4*)(a.b2 + co);
             float v[4] = {acc2[c][p][0] + bv.x, acc2[c][p][1] + bv.y, acc2[c][p][2] + bv.z, acc2[c][p][3] + bv.w};
             if (a.act2) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                silu_n(v);
             }
             OutT* yp = Y + orw * a.ldy + co;
             if constexpr (sizeof(OutT) == 2) {
@@ -408,10 +420,11 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
             float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
                   v3 = acc[i][j][3] + bv.w;
             if (a.act) {
-                v0 = silu(v0);
-                v1 = silu(v1);
-                v2 = silu(v2);
-                v3 = silu(v3);
+                const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                v0 = s01[0];
+                v1 = s01[1];
+                v2 = s23[0];
+                v3 = s23[1];
             }
             *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
         }
@@ -1041,8 +1054,7 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             float v[8] = {t0[0] + b0.x, t0[1] + b0.y, t0[2] + b0.z, t0[3] + b0.w,
                           t1[0] + b1.x, t1[1] + b1.y, t1[2] + b1.z, t1[3] + b1.w};
             if (a.act) {
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v[r] = silu(v[r]);
+                silu_n(v);
             }
             if (R) {
                 const bf16x8 rr = *(const bf16x8*)(R + (int64_t)m * a.ldr + co);
@@ -1211,10 +1223,11 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int i = 2 * kf + h;
-                        const float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
+                        float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
                                             acc[j][i][3] + bv[i].w};
+                        if (a.act) silu_n(v);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)v[r];
                     }
 #pragma unroll
                     for (int c = 0; c < DN_TAIL_C2F; ++c)
@@ -1233,8 +1246,7 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
                     float v[4] = {acc2[j][c][0] + b2.x, acc2[j][c][1] + b2.y, acc2[j][c][2] + b2.z,
                                   acc2[j][c][3] + b2.w};
                     if (a.act2) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                        silu_n(v);
                     }
                     OutT* yp = Y2 + (int64_t)m * a.ldy + co;
                     if constexpr (sizeof(OutT) == 2) {
@@ -1260,8 +1272,7 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
                 const float4 bv = *(const float4*)(a.bias + co);
                 float v[4] = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y, acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
                 if (a.act) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                    silu_n(v);
                 }
                 if (R) {
                     const uint2 rr = *(const uint2*)(R + (int64_t)m * a.ldr + co);
@@ -1451,10 +1462,11 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int i = 2 * kf + h;
-                        const float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
+                        float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
                                             acc[j][i][3] + bv[i].w};
+                        if (a.act) silu_n(v);
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)(a.act ? silu(v[r]) : v[r]);
+                        for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)v[r];
                     }
 #pragma unroll
                     for (int c = 0; c < TNS; ++c)
@@ -1474,8 +1486,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
                     float v[4] = {acc2[j][c][0] + b2.x, acc2[j][c][1] + b2.y, acc2[j][c][2] + b2.z,
                                   acc2[j][c][3] + b2.w};
                     if (a.act2) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+                        silu_n(v);
                     }
                     OutT* yp = ok ? Y2 + m * a.ldy + co : (OutT*)(g_sink + 4 * lane);
                     if constexpr (sizeof(OutT) == 2) {
@@ -1530,8 +1541,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
                     v[4 * h + 3] = t[3] + b4.w;
                 }
                 if (a.act) {
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) v[r] = silu(v[r]);
+                    silu_n(v);
                 }
                 if (R) {
 #pragma unroll
