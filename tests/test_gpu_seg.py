@@ -320,7 +320,7 @@ def test_conv4_matches_conv2(monkeypatch):
     same 32-deep MFMA k-sequence per output, so bit-identical."""
     arch, fw, net = _net("bf16", "s", seed=12)
     frames = _frames(2, seed=13)
-    monkeypatch.delenv("VA_CONV4", raising=False)
+    monkeypatch.setenv("VA_CONV4", "0")
     ref = _gpu_heads(net, frames)
     monkeypatch.setenv("VA_CONV4", "1")
     monkeypatch.setenv("VA_CONV4_MIN", "1")

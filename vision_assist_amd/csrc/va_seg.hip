@@ -2061,11 +2061,11 @@ hipError_t launch_conv_wp(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV4=1 moves the Cout > 128 layers with at least VA_CONV4_MIN (default 256) 256 x 256 tiles to conv4
-// (A/B timing; read per launch)
+// The Cout > 128 layers with at least VA_CONV4_MIN (default 256) 256 x 256 tiles run on conv4 (P3/P4 1x1 and
+// 3x3 layers 2-18 % faster than conv2, profiles/r01g); VA_CONV4=0 keeps them on conv2 (A/B timing; read per launch)
 bool use_conv4(const va_conv_args& a) {
     const char* e = getenv("VA_CONV4");
-    if (!e || e[0] != '1') return false;
+    if (e && e[0] == '0') return false;
     if (a.mode != 0 || a.w2 || a.Cout <= 128 || a.Cin % 64 || a.K != a.kh * a.kw * a.Cin || a.Kpad != a.K ||
         a.ldx % 8 || ((uintptr_t)a.x & 15) || a.ldy % 8 || ((uintptr_t)a.y & 15) || a.Npad % 256 ||
         (a.res && (a.ldr % 8 || ((uintptr_t)a.res & 15))))
