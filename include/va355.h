@@ -193,6 +193,14 @@ typedef struct va_conv_args {
     const float* b2;        /* [>= ceil16(c2)] */
     int32_t c2;
     int32_t act2;           /* 1 = SiLU */
+    /* Optional nearest-x2 upsampled channel prefix (the FPN's Upsample + Concat read in place, Ultralytics
+     * nn.Upsample + Concat of YOLOv8's head): when xu != NULL, input channels [0, cu) of pixel (n, h, w) are
+     * read from xu at (n, h/2, w/2) -- an [N][H/2][W/2] slice with channel stride ldu -- and channels
+     * [cu, Cin) from x as usual (x's first cu channels are never read).  bf16, 1x1 / stride 1 / mode 0 without
+     * a tail, Cin and cu multiples of 64, H and W even. */
+    const void* xu;
+    int32_t ldu;
+    int32_t cu;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

@@ -485,3 +485,61 @@ def test_stem_fused_in_plan(monkeypatch):
     for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         err = ((g_ - r).norm() / r.norm()).item()
         assert err < 1e-2, f"{name}: fused vs unfused stem {err}"
+
+
+@pytest.mark.parametrize("B,H,W,cu,cin,cout", [(2, 40, 40, 512, 768, 256),   # model.12.cv1 shape (conv2)
+                                                (4, 128, 128, 128, 192, 256),  # conv4 (>= 256 tiles)
+                                                (1, 26, 34, 256, 384, 128),    # model.15.cv1 shape, ragged
+                                                (2, 16, 20, 64, 128, 64)])     # conv2 4 x 1 waves
+def test_conv_upsampled_prefix(B, H, W, cu, cin, cout):
+    """va_conv_args.xu: a 1x1 conv whose first cu input channels are the nearest-x2 upsample of a half-
+    resolution slice, read in place (the FPN Upsample + Concat never materialised) vs torch fp32 on the
+    materialised concat.  The concat buffer's first cu channels hold NaN: any read of them shows."""
+    import ctypes
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    g = torch.Generator().manual_seed(H * W + cin)
+    w = torch.randn(cout, cin, 1, 1, generator=g) * (2.0 / cin) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    net = S.SegNet.__new__(S.SegNet)
+    net.dtype, net.tdtype, net.va_dtype, net.vec = "bf16", torch.bfloat16, S.VA_DTYPE_BF16, 8
+    net.device = torch.device("cuda")
+    p = net._pack(w, b)
+    ldu = cu + 64
+    xu = torch.zeros(B, H // 2, W // 2, ldu, dtype=torch.bfloat16)
+    xu[..., 32:32 + cu] = torch.randn(B, H // 2, W // 2, cu, generator=g).to(torch.bfloat16)
+    xc = torch.full((B, H, W, cin), float("nan"), dtype=torch.bfloat16)
+    xc[..., cu:] = torch.randn(B, H, W, cin - cu, generator=g).to(torch.bfloat16)
+    xud, xcd = xu.cuda(), xc.cuda()
+    y = torch.zeros(B, H, W, cout, dtype=torch.bfloat16, device="cuda")
+    a = S.ConvArgs(x=xcd.data_ptr(), N=B, H=H, W=W, Cin=cin, ldx=cin, kh=1, kw=1, stride=1, pad=0, Ho=H, Wo=W,
+                   w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad, y=y.data_ptr(),
+                   ldy=cout, act=1, mode=0, M=B * H * W, dtype=S.VA_DTYPE_BF16,
+                   xu=xud.data_ptr() + 32 * 2, ldu=ldu, cu=cu)
+    lib = _lib.load()
+    _lib.check(lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_conv xu")
+    torch.cuda.synchronize()
+    up = xu[..., 32:32 + cu].float().repeat_interleave(2, 1).repeat_interleave(2, 2)
+    xin = torch.cat([up, xc[..., cu:].float()], -1).permute(0, 3, 1, 2)
+    ref = F.silu(F.conv2d(xin, w.to(torch.bfloat16).float(), b)).permute(0, 2, 3, 1)
+    got = y.float().cpu()
+    assert torch.isfinite(got).all(), "read the NaN prefix of the concat buffer"
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
+
+
+def test_fpn_upsample_read_in_place(monkeypatch):
+    """The bf16 plan has no upsample ops (model.12 / model.15 cv1 read the upsampled halves in place); the
+    heads match the plan that materialises them (same GEMMs, same operand values)."""
+    arch, fw, net = _net("bf16", "s")
+    kinds = [m["kind"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "upsample" not in kinds
+    frames = _frames(2, seed=14)
+    fused = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_FUSE_UP", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="bf16")
+    assert [m["kind"] for m in net2.plan(2, 640, 640)["meta"]].count("upsample") == 2
+    plain = _gpu_heads(net2, frames)
+    for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
+        assert torch.equal(g_, r), f"{name}: in-place upsample vs materialised, max diff {(g_ - r).abs().max().item()}"

@@ -482,7 +482,10 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 // wave-uniform scalars and each staged row keeps a precomputed base pointer: per K-step and row the B
 // address is one 64-bit add of a scalar offset plus a bounds select (the general form re-derives the
 // im2col coordinates of every lane with 64-bit multiplies).
-template <int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false>
+// UP (FK, 1x1 only): input channels [0, a.cu) come from the half-resolution slice a.xu at (h/2, w/2) -- the
+// FPN's Upsample + Concat read in place (va355.h va_conv_args.xu); a K-step is one 64-channel chunk, so
+// the source is a wave-uniform choice per K-step.
+template <int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
     using Cfg = Conv2Cfg<WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
@@ -513,14 +516,18 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     int b_hi[B_CH], b_wi[B_CH];
     int64_t b_base[B_CH];
+    const __bf16* rowu[UP ? B_CH : 1];  // UP: the pixel's row in the half-resolution source (+ lane's chunk)
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
         const int m = m0 + row0 + RSTEP * i;
+        if constexpr (UP) rowu[i] = (const __bf16*)a.xu + 8 * g;
         if (m < a.M) {
             const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
             b_hi[i] = ho * a.stride - pad_y;
             b_wi[i] = wo * a.stride - pad_x;
             b_base[i] = (int64_t)n * a.H * a.W;
+            if constexpr (UP)
+                rowu[i] = (const __bf16*)a.xu + (((int64_t)n * (a.H / 2) + (ho >> 1)) * (a.W / 2) + (wo >> 1)) * a.ldu + 8 * g;
         } else {
             b_hi[i] = -(1 << 28);
             b_wi[i] = 0;
@@ -592,7 +599,9 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int soff = (fk_ky * a.W + fk_kx) * a.ldx + fk_c;                                                     \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
             const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W; \
-            const void* src = ok ? (const void*)(rowp[i] + soff) : zpage;                                          \
+            const __bf16* sp_ = rowp[i] + soff;                                                                    \
+            if constexpr (UP) sp_ = fk_c < a.cu ? rowu[i] + fk_c : sp_;                                           \
+            const void* src = ok ? (const void*)sp_ : zpage;                                                       \
             __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
                                              0);                                                                   \
         }                                                                                                          \
@@ -867,7 +876,7 @@ __global__ __launch_bounds__(C3_NT) void conv3_kernel(va_conv_args a, int ntn, i
 // consecutive channels: the epilogue stores 16 bytes per lane straight from the accumulators.
 constexpr int C4_NT = 512, C4_BUF = 2 * 256 * BK2 * 2;  // bytes per LDS buffer (A then B)
 
-template <typename OutT>
+template <typename OutT, bool UP = false>  // UP: upsampled channel prefix, as conv2_kernel's UP
 __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn, int ntiles) {
     extern __shared__ __align__(16) unsigned char sm4[];
     int bid = blockIdx.x;
@@ -893,6 +902,7 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
     auto b_row0 = [&](int half, int u) { return 64 * ((wid >> 2) + 2 * u) + 32 * half + 8 * (wid & 3); };
     const __bf16* wrow[4];  // [2 half + u]: permuted-channel weight rows
     const __bf16* rowp[4];  // [2 half + u]: pixel rows
+    const __bf16* rowu[UP ? 4 : 1];  // UP: the pixel's row in the half-resolution source
     int b_hi[4], b_wi[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -906,10 +916,13 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             b_hi[i] = ho * a.stride - a.pad;
             b_wi[i] = wo * a.stride - a.pad;
             rowp[i] = X + (((int64_t)n * a.H + b_hi[i]) * a.W + b_wi[i]) * a.ldx + 8 * g;
+            if constexpr (UP)
+                rowu[i] = (const __bf16*)a.xu + (((int64_t)n * (a.H / 2) + (ho >> 1)) * (a.W / 2) + (wo >> 1)) * a.ldu + 8 * g;
         } else {
             b_hi[i] = -(1 << 28);
             b_wi[i] = 0;
             rowp[i] = X;
+            if constexpr (UP) rowu[i] = (const __bf16*)a.xu;
         }
     }
     const void* zpage = (const void*)g_zero_page;
@@ -942,7 +955,9 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
                 dst = buf + a_row0(half, u) * 128;
             } else {
                 const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W;
-                src = ok ? (const void*)(rowp[i] + soff) : zpage;
+                const __bf16* sp = rowp[i] + soff;
+                if constexpr (UP) sp = fk_c < a.cu ? rowu[i] + fk_c : sp;
+                src = ok ? (const void*)sp : zpage;
                 dst = buf + 256 * BK2 * 2 + b_row0(half, u) * 128;
             }
             __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)dst, 16, 0, 0);
@@ -1926,6 +1941,11 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of 8 and a 16-byte aligned base
     const bool fk = a.Cin % 64 == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
+    if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
+        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a,
+                           ntn, ntiles);
+        return hipGetLastError();
+    }
     if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0) {
         if (fk)
             hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a,
@@ -2080,12 +2100,17 @@ hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute((const void*)conv4_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * C4_BUF) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv4_kernel<OutT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * C4_BUF) != hipSuccess)
             return hipErrorInvalidValue;
         attr = true;
     }
     const int ntn = (a.Cout + 255) / 256, ntiles = ntn * ((a.M + 255) / 256);
-    hipLaunchKernelGGL((conv4_kernel<OutT>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
+    if (a.xu)
+        hipLaunchKernelGGL((conv4_kernel<OutT, true>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
+    else
+        hipLaunchKernelGGL((conv4_kernel<OutT>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
@@ -2119,6 +2144,12 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         return hipErrorInvalidValue;
     }
     if constexpr (sizeof(T) == 2) {
+        if (a.xu) {  // upsampled channel prefix (validated by va_seg_conv): the FK LDS-DMA kernels
+            if (use_conv4(a)) return launch_conv4<OutT>(a, st);
+            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
+            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
+            return launch_conv2<2, 2, 4, OutT>(a, st);
+        }
         if constexpr (sizeof(OutT) == 2) {
             // narrow layers: weights in LDS, activations straight into MFMA fragments
             if (use_patch(a)) return launch_conv_patch<false, __bf16>(a, st);
@@ -2157,6 +2188,11 @@ extern "C" {
 
 int va_seg_conv(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
+    if (a->xu && (a->dtype != VA_DTYPE_BF16 || a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0 ||
+                  a->mode != 0 || a->w2 || a->out_f32 || a->Cin % 64 || a->cu <= 0 || a->cu % 64 || a->cu >= a->Cin ||
+                  a->K != a->Cin || a->Kpad != a->K || a->ldu % 8 || ((uintptr_t)a->xu & 15) || a->H % 2 ||
+                  a->W % 2 || a->ldx % 8 || ((uintptr_t)a->x & 15)))
+        return VA_ERR_ARG;
     const int vec = a->dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;

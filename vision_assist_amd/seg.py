@@ -42,6 +42,7 @@ class ConvArgs(ctypes.Structure):
         ("act", ctypes.c_int32), ("mode", ctypes.c_int32), ("M", ctypes.c_int32), ("dtype", ctypes.c_int32),
         ("out_f32", ctypes.c_int32), ("bias4", ctypes.c_int32),
         ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("c2", ctypes.c_int32), ("act2", ctypes.c_int32),
+        ("xu", ctypes.c_void_p), ("ldu", ctypes.c_int32), ("cu", ctypes.c_int32),
     ]
 
 
@@ -268,9 +269,11 @@ class SegNet:
             return Slice(t, 0, c)
 
         def conv(prefix, src: Slice, dst: Slice, h, w, stride=1, act=True, res: Slice | None = None,
-                 out_f32=False, tail: str | None = None, act2=False):
+                 out_f32=False, tail: str | None = None, act2=False, up: Slice | None = None):
             """One conv op; with ``tail`` the named 1x1 conv (the only consumer of this one) runs fused in
-            its epilogue and ``dst`` / ``out_f32`` describe the tail's output."""
+            its epilogue and ``dst`` / ``out_f32`` describe the tail's output.  With ``up`` the first
+            ``up.c`` input channels are the nearest-x2 upsample of that half-resolution slice, read in
+            place (va355.h va_conv_args.xu) instead of from ``src``."""
             p = self.w[prefix]
             p2 = self.w[tail] if tail else None
             k = p.k
@@ -284,6 +287,8 @@ class SegNet:
                 y=dst.ptr, ldy=dst.ld, res=res.ptr if res is not None else None, ldr=res.ld if res is not None else 0,
                 act=1 if act else 0, mode=1 if p.deconv else 0, M=B * ho * wo, dtype=self.va_dtype,
                 out_f32=1 if (out_f32 and self.dtype == "bf16") else 0)
+            if up is not None:
+                args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
             cout = p.cout
             if p2 is not None:
                 if p2.cin != p.cout or p2.k != 1:
@@ -303,7 +308,7 @@ class SegNet:
                          + B * ho * wo * cout * (4 if out_f32 else es)})
             return ho, wo
 
-        def c2f(i, src: Slice, dst: Slice, h, w):
+        def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None):
             _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
             if i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
@@ -317,7 +322,7 @@ class SegNet:
                 return
             c = co // 2
             t = new(h, w, (2 + n) * c)
-            conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w)
+            conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w, up=up)
             tmp = new(h, w, c)
             for j in range(n):
                 x_in = t.sub((1 + j) * c, c)
@@ -386,13 +391,18 @@ class SegNet:
         cat20 = new(h5, w5, a.c4 + a.c5)          # [conv19(o4) | P5]
         P5 = cat20.sub(a.c4, a.c5)
         conv("model.9.cv2", sp, P5, h5, w5)
-        upsample(P5, cat11.sub(0, a.c5), h5, w5)
+        # the FPN's Upsample + Concat: read in place by the consumer's 1x1 cv1 (bf16) or materialised
+        fuse_up = self.dtype == "bf16" and os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % 64 == 0 \
+            and a.c4 % 64 == 0 and (a.c5 + a.c4) % 64 == 0 and (a.c4 + a.c3) % 64 == 0
+        if not fuse_up:
+            upsample(P5, cat11.sub(0, a.c5), h5, w5)
         cat17 = new(h4, w4, a.c3 + a.c4)          # [conv16(o3) | h12]
         h12 = cat17.sub(a.c3, a.c4)
-        c2f(12, cat11, h12, h4, w4)
-        upsample(h12, cat14.sub(0, a.c4), h4, w4)
+        c2f(12, cat11, h12, h4, w4, up=P5 if fuse_up else None)
+        if not fuse_up:
+            upsample(h12, cat14.sub(0, a.c4), h4, w4)
         o3 = new(h3, w3, a.c3)
-        c2f(15, cat14, o3, h3, w3)
+        c2f(15, cat14, o3, h3, w3, up=h12 if fuse_up else None)
         conv("model.16", o3, cat17.sub(0, a.c3), h3, w3, stride=2)
         o4 = new(h4, w4, a.c4)
         c2f(18, cat17, o4, h4, w4)
