@@ -1850,42 +1850,50 @@ __device__ inline u32x4 vmax16(u32x4 a, u32x4 b) {
     return r;
 }
 
-template <typename T>
+// CGW channel groups per workgroup, the group index fastest over the threads: with CGW = 4 (bf16) a
+// pixel's 64 contiguous bytes are read and written by 4 neighbouring lanes (whole 64-byte sectors instead
+// of 16-byte pieces spread over 4 workgroups)
+template <typename T, int CGW>
 __global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int H, int W, int c, int ld) {
-    extern __shared__ __align__(16) u32x4 sp[];  // [4][H*W]
+    extern __shared__ __align__(16) u32x4 sp[];  // [4][H*W][CGW]
     constexpr int CG = 16 / sizeof(T);
-    const int groups = c / CG;
-    const int n = blockIdx.x / groups, cg = blockIdx.x % groups;
-    const int np = H * W;
-    T* base = buf + (int64_t)n * np * ld + cg * CG;
-    for (int p = threadIdx.x; p < np; p += blockDim.x) sp[p] = *(const u32x4*)(base + (int64_t)p * ld);
+    const int groups = c / (CG * CGW);
+    const int n = blockIdx.x / groups, cg0 = (blockIdx.x % groups) * CGW;
+    const int np = H * W, nq = np * CGW;
+    T* base = buf + (int64_t)n * np * ld + cg0 * CG;
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        const int p = i / CGW, q = i - p * CGW;
+        sp[i] = *(const u32x4*)(base + (int64_t)p * ld + q * CG);
+    }
     __syncthreads();
-    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        const int p = i / CGW, q = i - p * CGW;
         const int y = p / W, x = p - y * W;
-        const u32x4* row = sp + y * W;
-        u32x4 m = row[x];
+        const u32x4* row = sp + y * W * CGW + q;
+        u32x4 m = row[x * CGW];
 #pragma unroll
         for (int k = 1; k <= 3; ++k) {
 #pragma unroll
             for (int d = 2 * k - 1; d <= 2 * k; ++d) {
-                if (x - d >= 0) m = vmax16<T>(m, row[x - d]);
-                if (x + d < W) m = vmax16<T>(m, row[x + d]);
+                if (x - d >= 0) m = vmax16<T>(m, row[(x - d) * CGW]);
+                if (x + d < W) m = vmax16<T>(m, row[(x + d) * CGW]);
             }
-            sp[k * np + p] = m;
+            sp[k * nq + i] = m;
         }
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+        const int p = i / CGW, q = i - p * CGW;
         const int y = p / W, x = p - y * W;
 #pragma unroll
         for (int k = 1; k <= 3; ++k) {
-            const u32x4* pl = sp + k * np + x;
-            u32x4 m = pl[y * W];
+            const u32x4* pl = sp + k * nq + x * CGW + q;
+            u32x4 m = pl[y * W * CGW];
             for (int d = 1; d <= 2 * k; ++d) {
-                if (y - d >= 0) m = vmax16<T>(m, pl[(y - d) * W]);
-                if (y + d < H) m = vmax16<T>(m, pl[(y + d) * W]);
+                if (y - d >= 0) m = vmax16<T>(m, pl[(y - d) * W * CGW]);
+                if (y + d < H) m = vmax16<T>(m, pl[(y + d) * W * CGW]);
             }
-            *(u32x4*)(base + (int64_t)p * ld + k * c) = m;
+            *(u32x4*)(base + (int64_t)p * ld + k * c + q * CG) = m;
         }
     }
 }
@@ -2238,15 +2246,22 @@ int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, i
     const int cg = dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % cg || ld % cg || H * W > SPPF_MAXPIX || ((uintptr_t)buf & 15))
         return VA_ERR_ARG;
-    const int blocks = N * (c / cg);
-    const size_t lds = (size_t)4 * H * W * 16;
+    // 2 channel groups per workgroup while the four planes fit 52 KiB of LDS (20 x 20 maps: three
+    // workgroups per CU), else one
+    const int cgw = ((c / cg) % 2 == 0 && (size_t)4 * H * W * 16 * 2 <= 52 * 1024) ? 2 : 1;
+    const int blocks = N * (c / cg / cgw);
+    const size_t lds = (size_t)4 * H * W * 16 * cgw;
     hipStream_t st = (hipStream_t)stream;
+    auto go = [&](auto kern, auto* p) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, p, H, W, c, ld);
+    };
     if (dtype == VA_DTYPE_BF16) {
-        (void)hipFuncSetAttribute((const void*)sppf_pool_kernel<__bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(sppf_pool_kernel<__bf16>, dim3(blocks), dim3(256), lds, st, (__bf16*)buf, H, W, c, ld);
+        if (cgw == 2) go(sppf_pool_kernel<__bf16, 2>, (__bf16*)buf);
+        else go(sppf_pool_kernel<__bf16, 1>, (__bf16*)buf);
     } else {
-        (void)hipFuncSetAttribute((const void*)sppf_pool_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(sppf_pool_kernel<float>, dim3(blocks), dim3(256), lds, st, (float*)buf, H, W, c, ld);
+        if (cgw == 2) go(sppf_pool_kernel<float, 2>, (float*)buf);
+        else go(sppf_pool_kernel<float, 1>, (float*)buf);
     }
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
