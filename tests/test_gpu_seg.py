@@ -93,6 +93,9 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
     (64, 64, 3, 1, 37, 16, True, False, 0),    # patch kernel: residual
     (128, 256, 3, 1, 19, 23, True, False, 0),  # wide patch kernel: ragged tiles, two channel tiles, residual
     (64, 136, 3, 1, 16, 40, False, False, 64), # wide patch kernel: ragged channel tile, channel slice
+    (128, 128, 1, 1, 20, 20, False, False, 0), # streaming 1x1 (va_pw.hip)
+    (192, 128, 1, 1, 13, 11, False, False, 8), # streaming 1x1: ragged last tile, channel slice
+    (448, 128, 1, 1, 9, 30, False, False, 0),  # streaming 1x1 at its largest K
 ])
 def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
     got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in, act=not deconv)
@@ -543,3 +546,17 @@ def test_fpn_upsample_read_in_place(monkeypatch):
     plain = _gpu_heads(net2, frames)
     for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         assert torch.equal(g_, r), f"{name}: in-place upsample vs materialised, max diff {(g_ - r).abs().max().item()}"
+
+
+def test_forward_deterministic():
+    """Five bf16 forwards of the same frames are bit-identical (every kernel of the plan: stem, C2f, the
+    streaming 1x1, conv2 / conv4 / patch / tails, the proto fold): a scheduling hazard or race shows up as
+    run-to-run differences long before it breaks a tolerance."""
+    arch, fw, net = _net("bf16", "s")
+    frames = _frames(4, seed=21)
+    first = _gpu_heads(net, frames)
+    for _ in range(4):
+        again = _gpu_heads(net, frames)
+        for name, g_, r in zip(("box", "cls", "coef", "proto"), again, first):
+            assert torch.isfinite(g_).all(), name
+            assert torch.equal(g_, r), f"{name}: run-to-run max diff {(g_ - r).abs().max().item()}"

@@ -29,6 +29,10 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 // SROA and end up in scratch / LDS)
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
+// va_pw.hip: the streaming pointwise kernel for 1x1 / Cout-128 layers
+bool va_pw_eligible(const va_conv_args& a);
+hipError_t va_pw_launch(const va_conv_args& a, hipStream_t st);
+
 namespace {
 
 __device__ inline float to_f(float v) { return v; }
@@ -48,16 +52,11 @@ __device__ inline __bf16 from_f<__bf16>(float v) {
 // follows); the exact-f32 parity path uses silu_exact
 __device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ inline float silu_exact(float x) { return x / (1.0f + expf(-x)); }
-// silu() over an array, the plain f32 steps packed in pairs (fz::silu2): bit-identical to silu() per element
+// silu() over an array (scalar per element: see va_fuse.h fz::act on the packed form)
 template <int N>
 __device__ __forceinline__ void silu_n(float (&v)[N]) {
-    static_assert(N % 2 == 0, "pairs");
 #pragma unroll
-    for (int i = 0; i < N; i += 2) {
-        const f32x2 r = fz::silu2((f32x2){v[i], v[i + 1]});
-        v[i] = r[0];
-        v[i + 1] = r[1];
-    }
+    for (int i = 0; i < N; ++i) v[i] = silu(v[i]);
 }
 
 // ----------------------------------------------------------------------------------------- preprocess
@@ -420,11 +419,10 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
             float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
                   v3 = acc[i][j][3] + bv.w;
             if (a.act) {
-                const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
-                v0 = s01[0];
-                v1 = s01[1];
-                v2 = s23[0];
-                v3 = s23[1];
+                v0 = silu(v0);
+                v1 = silu(v1);
+                v2 = silu(v2);
+                v3 = silu(v3);
             }
             *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
         }
@@ -2134,6 +2132,9 @@ bool getenv_dn() {
 
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
+    if constexpr (sizeof(T) == 2 && sizeof(OutT) == 2) {
+        if (va_pw_eligible(a)) return va_pw_launch(a, st);  // streaming 1x1, Cout 128 (va_pw.hip)
+    }
     if (a.w2) {  // fused 1x1 tail: narrow layers (Cout 32 / 64) in registers, Cout 128 through LDS
         if constexpr (sizeof(T) == 2) {
             if ((a.Cout == 32 || a.Cout == 64) && a.mode == 0 && !a.res && a.b2 && a.c2 > 0 &&
