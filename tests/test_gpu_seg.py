@@ -96,6 +96,8 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
     (128, 128, 1, 1, 20, 20, False, False, 0), # streaming 1x1 (va_pw.hip)
     (192, 128, 1, 1, 13, 11, False, False, 8), # streaming 1x1: ragged last tile, channel slice
     (448, 128, 1, 1, 9, 30, False, False, 0),  # streaming 1x1 at its largest K
+    (128, 128, 1, 1, 320, 320, False, False, 0),  # streaming 1x1: > 2 tiles per wave (persistent loop)
+    (256, 128, 1, 1, 200, 328, False, False, 8),  # streaming 1x1: several tiles per wave, K = 256, slice
 ])
 def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
     got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in, act=not deconv)
@@ -546,6 +548,28 @@ def test_fpn_upsample_read_in_place(monkeypatch):
     plain = _gpu_heads(net2, frames)
     for name, g_, r in zip(("box", "cls", "coef", "proto"), fused, plain):
         assert torch.equal(g_, r), f"{name}: in-place upsample vs materialised, max diff {(g_ - r).abs().max().item()}"
+
+
+def test_forward_large_batch_pw_matches_conv2(monkeypatch):
+    """At bench batch sizes the persistent kernels loop over many tiles per wave (the 4-frame tests run one
+    tile per wave): a 64-frame forward is finite, repeatable, and the streaming 1x1 layers agree with the same
+    layers on conv2 (VA_PW=0) to bf16 rounding."""
+    arch, fw, net = _net("bf16", "s")
+    frames = _frames(64, seed=3).cuda()
+
+    def run():
+        out = net.forward(frames)
+        torch.cuda.synchronize()
+        return torch.cat([t.float().flatten(1, 2) for t in out.levels], 1), out.proto.float()
+
+    monkeypatch.setenv("VA_PW", "1")
+    a, b = run(), run()
+    monkeypatch.setenv("VA_PW", "0")
+    c = run()
+    for x, y, z in zip(a, b, c):
+        assert torch.isfinite(x).all()
+        assert torch.equal(x, y)
+        assert ((x - z).abs().max() / z.abs().max()).item() < 2e-2
 
 
 def test_forward_deterministic():

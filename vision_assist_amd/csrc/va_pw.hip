@@ -121,8 +121,12 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int n
         for (int j = 0; j < PW_NB; ++j)
 #pragma unroll
             for (int p = 0; p < 4; ++p)
+                // the channel offset goes into the voffset (folded into the instruction offset), never into
+                // soffset: with an SGPR soffset the compiler treats a VALU write of the 16-byte store data in
+                // the next cycle as safe, and on gfx950 it is not (lanes 12-15 of each row group stored the
+                // overwritten first dword at p = 2, 3 -- tools/pw_debug.py)
                 __builtin_amdgcn_raw_buffer_store_b128(
-                    (u32x4)fz::pack(fz::act(acc[j][2 * p]), fz::act(acc[j][2 * p + 1])), ry, oy[j], 64 * p, 0);
+                    (u32x4)fz::pack(fz::act(acc[j][2 * p]), fz::act(acc[j][2 * p + 1])), ry, oy[j] + 64 * p, 0, 0);
         if (tn >= ntiles) break;
         t = tn;
     }
