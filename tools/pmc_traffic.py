@@ -2,9 +2,13 @@
 """Summarise rocprofv3 output of a bench.py run for profiles/.
 
   stats  <kernel_stats.csv> <out.json>
-      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/2/3/4/_dn/_patch/_wp, c2f, stem
+      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/2/3/4/_dn/_patch/_wp, c2f, stem, pw
       kernels: every launch of the YOLOv8-seg forward's GEMMs) gives the average launch duration that
       bench.py's roofline.avg_launch_us must agree with.
+  agree  <kernel_trace.csv> <bench_under_rocprof.json> <out.json> [launches_per_forward]
+      the conv-family launches of the trace in dispatch order, cut into forwards, averaged per forward;
+      the forwards after the warm-up and before the isolated tail are the timed region whose average must
+      agree with the bench line's roofline.avg_launch_us (and the last three with isolated_avg_launch_us).
   traffic <fetch_counter_collection.csv> <write_counter_collection.csv> <key> <out.json>
       HBM bytes per conv launch from two separate --pmc passes (FETCH_SIZE, WRITE_SIZE), corrected as
       MI355X_MICROARCH.md §HBM prescribes for gfx950: both counters are in KiB; FETCH_SIZE reports half
@@ -19,7 +23,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f|stem)_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f|stem|pw)_kernel")
 
 
 def family(name: str) -> str:
@@ -45,6 +49,35 @@ def stats(path: str, out: str) -> dict:
     conv["avg_us"] = round(conv["total_ns"] / max(conv["calls"], 1) / 1e3, 3)
     res = {"source": os.path.basename(path), "conv_family": conv,
            "families": dict(sorted(fam.items(), key=lambda kv: -kv[1]["total_ns"]))}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    return res
+
+
+def agree(trace: str, bench_json: str, out: str, per_fwd: int = 55) -> dict:
+    rows = []
+    with open(trace) as f:
+        for row in csv.DictReader(f):
+            if CONV_RE.search(row["Kernel_Name"]):
+                rows.append((int(row["Dispatch_Id"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    rows.sort()
+    nf = len(rows) // per_fwd
+    fwd = [sum(d for _, d in rows[i * per_fwd:(i + 1) * per_fwd]) / per_fwd / 1e3 for i in range(nf)]
+    with open(bench_json) as f:
+        b = json.loads(f.read().strip().splitlines()[-1])
+    steps, warm = b["steps"], b["warmup"]
+    timed = fwd[warm:warm + steps]
+    iso = fwd[warm + steps:]
+    rl = b["roofline"]
+    res = {"conv_launches_per_forward": per_fwd, "forwards_in_trace": nf,
+           "rocprof_avg_us_per_forward_in_launch_order": [round(x, 1) for x in fwd],
+           f"rocprof_avg_us_timed_forwards({warm}..{warm + steps - 1})": round(sum(timed) / max(len(timed), 1), 1),
+           "rocprof_avg_us_isolated_forwards": round(sum(iso) / max(len(iso), 1), 1),
+           "bench_avg_launch_us(events, sampled timed forwards)": rl["avg_launch_us"],
+           "bench_isolated_avg_launch_us": rl.get("isolated_avg_launch_us"),
+           "note": "forwards 0..warmup-1 warm-up; then the timed region (two network streams overlapping); "
+                   "the tail = the isolated forwards bench.py runs after the timed region; B = "
+                   f"{b['config']['batch_per_gpu']}"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     return res
@@ -82,7 +115,9 @@ def traffic(fetch_csv: str, write_csv: str, key: str, out: str) -> dict:
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "agree":
+        print(json.dumps(agree(*sys.argv[2:5], *(int(a) for a in sys.argv[5:6]))))
+    elif sys.argv[1] == "stats":
         print(json.dumps(stats(sys.argv[2], sys.argv[3])["conv_family"]))
     elif sys.argv[1] == "traffic":
         print(json.dumps(traffic(*sys.argv[2:6])))
