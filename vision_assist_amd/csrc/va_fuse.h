@@ -19,10 +19,20 @@ constexpr int RSRC = 0x00020000;      // buffer descriptor word 3 (gfx9 raw buff
 // bf16 epilogues: hardware exp and reciprocal (~1 ulp f32, far below the bf16 rounding that follows),
 // the same expression as va_seg.hip's unfused layers
 __device__ __forceinline__ float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-// four SiLUs.  (A form with the plain f32 steps packed in pairs -- v_pk_mul_f32 / v_pk_add_f32 around the
-// transcendentals -- measured 8 % faster in the fused kernels but produced sporadic non-finite outputs in
-// va_pw.hip's epilogue (a few elements per launch, never with this scalar form), so it is not used.)
-__device__ __forceinline__ f32x4 act(f32x4 x) { return (f32x4){silu(x[0]), silu(x[1]), silu(x[2]), silu(x[3])}; }
+// four SiLUs with the plain f32 steps packed in pairs (v_pk_mul_f32 / v_pk_add_f32 around the two
+// 8-cycle transcendentals): the same operations in the same order as silu(), so bit-identical.  (Briefly
+// blamed for va_pw.hip's sporadic non-finite outputs; the cause was that kernel's store hazard)
+__device__ __forceinline__ f32x2 silu2(f32x2 x) {
+    const f32x2 t = x * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+    const f32x2 e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+    const f32x2 d = e + (f32x2){1.0f, 1.0f};
+    const f32x2 r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    return x * r;
+}
+__device__ __forceinline__ f32x4 act(f32x4 x) {
+    const f32x2 lo = silu2((f32x2){x[0], x[1]}), hi = silu2((f32x2){x[2], x[3]});
+    return (f32x4){lo[0], lo[1], hi[0], hi[1]};
+}
 
 __device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

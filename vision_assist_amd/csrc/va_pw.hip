@@ -9,8 +9,9 @@
 //     A-fragment order (one conflict-free ds_read_b128 per fragment), with rows permuted so a lane's
 //     fragment pair (2p, 2p + 1) holds 8 consecutive output channels (16-byte epilogue stores);
 //   * every wave streams its own 48-pixel tiles: B fragments go straight from HBM into registers
-//     (lane (p, q): 16 bytes = channels 8q..8q+7 of pixel p), two 32-deep K-steps ahead in a
-//     2-slot register ring that runs across tile boundaries -- no LDS for activations, no barrier;
+//     (lane (p, q): 16 bytes = channels 8q..8q+7 of pixel p), D 32-deep K-steps ahead in a D-slot
+//     register ring (K fully unrolled per instantiation) that runs across tile boundaries -- no LDS for
+//     activations, no barrier;
 //   * accumulators start from the bias; SiLU epilogue from the accumulators; loads and stores are
 //     buffer ops with out-of-range offsets for pixels past M, so none is conditional;
 //   * the FPN's upsampled channel prefix (va_conv_args.xu) is read in place like conv2/conv4 do.
@@ -31,15 +32,19 @@ constexpr int PW_TP = 16 * PW_NB;  // pixels per wave tile
 constexpr int PW_NQ = 8;    // 16-channel output groups (Cout = 128)
 constexpr int PW_KMAX = 448;
 
+// NK = K / 32 K-steps, fully unrolled; the B fragments run through a ring of D slots (D divides NK, so a
+// K-step's slot is a compile-time constant and the next tile's first D steps land in the slots they are
+// read from: the ring is carried across tiles without register copies or a full vmcnt drain)
+template <int NK, int D>
 __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int ntiles) {
+    static_assert(NK % D == 0 && D >= 2, "ring");
     extern __shared__ __attribute__((aligned(16))) unsigned char pw_smem[];
     const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nk = a.K / 32;                       // 32-deep K-steps (even: K % 64 == 0)
-    float* bias_s = (float*)(pw_smem + nk * PW_NQ * 1024);
+    float* bias_s = (float*)(pw_smem + NK * PW_NQ * 1024);
     // weights -> LDS: fragment f = kf * 8 + q, lane l: row perm(q, l & 15), k = 32 kf + 8 (l >> 4)
     {
         const __bf16* W = (const __bf16*)a.w;
-        for (int i = tid; i < nk * PW_NQ * 64; i += PW_NW * 64) {
+        for (int i = tid; i < NK * PW_NQ * 64; i += PW_NW * 64) {
             const int f = i >> 6, l = i & 63, q = f % PW_NQ, kf = f / PW_NQ, r = l & 15;
             const int row = 32 * (q >> 1) + 8 * (r >> 2) + 4 * (q & 1) + (r & 3);
             *(u32x4*)(pw_smem + 16 * i) = *(const u32x4*)(W + (int64_t)row * a.Kpad + 32 * kf + 8 * (l >> 4));
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int n
     const int HW = a.H * a.W, hw2 = (a.H / 2) * (a.W / 2);
     const int cu = a.xu ? a.cu : 0;
 
-    // per tile: the byte offsets of this lane's 4 pixels in x and (upsampled prefix) in xu
+    // per tile: the byte offsets of this lane's pixels in x and (upsampled prefix) in xu
     int ox[PW_NB], ou[PW_NB];
     auto tile_offsets = [&](int tt) {
 #pragma unroll
@@ -77,19 +82,20 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int n
             }
         }
     };
-    u32x4 bs[2][PW_NB];  // the K-step ring: slot kf & 1
+    u32x4 bs[D][PW_NB];  // the K-step ring: step kf in slot kf % D
     auto load = [&](int slot, int kf) {
         const int c = 32 * kf;
 #pragma unroll
         for (int j = 0; j < PW_NB; ++j)
-            bs[slot][j] = c < cu ? __builtin_amdgcn_raw_buffer_load_b128(ru, ou[j], c * 2, 0)
-                                 : __builtin_amdgcn_raw_buffer_load_b128(rx, ox[j], c * 2, 0);
+            bs[slot][j] = c < cu ? __builtin_amdgcn_raw_buffer_load_b128(ru, ou[j] + c * 2, 0, 0)
+                                 : __builtin_amdgcn_raw_buffer_load_b128(rx, ox[j] + c * 2, 0, 0);
     };
     tile_offsets(t);
-    load(0, 0);
-    load(1, 1);
+#pragma unroll
+    for (int s = 0; s < D; ++s) load(s, s);
     while (true) {
         const int tn = t + stride;
+        const bool more = tn < ntiles;
         f32x4 acc[PW_NB][PW_NQ];
 #pragma unroll
         for (int q = 0; q < PW_NQ; ++q) {
@@ -97,25 +103,29 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int n
 #pragma unroll
             for (int j = 0; j < PW_NB; ++j) acc[j][q] = b;
         }
+        // the weight fragments' LDS address through the opaque lane id, once per tile: keeps the compiler
+        // from hoisting all NK * 8 loop-invariant fragment reads out of the tile loop (and spilling them)
+        const unsigned char* wl = pw_smem + 16 * fz::lane_id();
         int oy[PW_NB];
 #pragma unroll
         for (int j = 0; j < PW_NB; ++j) oy[j] = ox[j] == fz::OOB ? fz::OOB : ((t * PW_TP + 16 * j + fr) * a.ldy + 8 * fq) * 2;
-        for (int kp = 0; kp < nk; kp += 2) {
-            const bool last = kp + 2 >= nk;
-            if (last && tn < ntiles) tile_offsets(tn);  // the ring's next two steps are the next tile's
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int kf = kp + h;
+        for (int kf = 0; kf < NK; ++kf) {
+            // the ring's last D steps of this tile refill with the next tile's first D (past the last tile
+            // every offset is out of range: the loads return 0 without touching memory, and stay
+            // unconditional so the compiler's vmcnt accounting never has to drain the ring)
+            if (kf == NK - D) tile_offsets(tn);
 #pragma unroll
-                for (int q = 0; q < PW_NQ; ++q) {
-                    const bf16x8 wa = *(const bf16x8*)(pw_smem + (kf * PW_NQ + q) * 1024 + 16 * lane);
+            for (int q = 0; q < PW_NQ; ++q) {
+                const bf16x8 wa = *(const bf16x8*)(wl + (kf * PW_NQ + q) * 1024);
 #pragma unroll
-                    for (int j = 0; j < PW_NB; ++j) acc[j][q] = mma(wa, (bf16x8)bs[h][j], acc[j][q]);
-                }
-                // refill the slot just consumed: two K-steps ahead (the next tile's first two at the end)
-                if (!last) load(h, kf + 2);
-                else if (tn < ntiles) load(h, h);
+                for (int j = 0; j < PW_NB; ++j) acc[j][q] = mma(wa, (bf16x8)bs[kf % D][j], acc[j][q]);
             }
+            if (kf + D < NK) load(kf % D, kf + D);
+            else load(kf % D, kf + D - NK);
+            // keep each refill right behind the MFMAs that free its slot (the scheduler otherwise sinks all
+            // of a tile's refills below the last MFMA and drains the ring to vmcnt(0) every D steps)
+            __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int j = 0; j < PW_NB; ++j)
@@ -127,7 +137,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(va_conv_args a, int n
                 // overwritten first dword at p = 2, 3 -- tools/pw_debug.py)
                 __builtin_amdgcn_raw_buffer_store_b128(
                     (u32x4)fz::pack(fz::act(acc[j][2 * p]), fz::act(acc[j][2 * p + 1])), ry, oy[j] + 64 * p, 0, 0);
-        if (tn >= ntiles) break;
+        if (!more) break;
         t = tn;
     }
 }
@@ -151,19 +161,38 @@ bool va_pw_eligible(const va_conv_args& a) {
     return true;
 }
 
+template <int NK, int D>
+hipError_t pw_go(const va_conv_args& a, hipStream_t st, int ntiles, int grid) {
+    const int lds = NK * PW_NQ * 1024 + 128 * 4;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)pw_kernel<NK, D>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+            hipSuccess)
+            return hipErrorInvalidValue;
+        attr = true;
+    }
+    hipLaunchKernelGGL((pw_kernel<NK, D>), dim3(grid), dim3(PW_NW * 64), lds, st, a, ntiles);
+    return hipGetLastError();
+}
+
 hipError_t va_pw_launch(const va_conv_args& a, hipStream_t st) {
-    const int lds = a.K / 32 * PW_NQ * 1024 + 128 * 4;
     if (g_cus == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipFuncSetAttribute((const void*)pw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                PW_KMAX / 32 * PW_NQ * 1024 + 128 * 4) != hipSuccess)
+            hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return hipErrorInvalidValue;
     }
     const int ntiles = (a.M + PW_TP - 1) / PW_TP;
     int grid = g_cus;
     if ((int64_t)grid * PW_NW > ntiles) grid = (ntiles + PW_NW - 1) / PW_NW;
-    hipLaunchKernelGGL(pw_kernel, dim3(grid), dim3(PW_NW * 64), lds, st, a, ntiles);
-    return hipGetLastError();
+    switch (a.K / 32) {
+        case 2: return pw_go<2, 2>(a, st, ntiles, grid);
+        case 4: return pw_go<4, 4>(a, st, ntiles, grid);
+        case 6: return pw_go<6, 3>(a, st, ntiles, grid);
+        case 8: return pw_go<8, 4>(a, st, ntiles, grid);
+        case 10: return pw_go<10, 5>(a, st, ntiles, grid);
+        case 12: return pw_go<12, 4>(a, st, ntiles, grid);
+        case 14: return pw_go<14, 2>(a, st, ntiles, grid);
+        default: return hipErrorInvalidValue;
+    }
 }

@@ -52,11 +52,16 @@ __device__ inline __bf16 from_f<__bf16>(float v) {
 // follows); the exact-f32 parity path uses silu_exact
 __device__ inline float silu(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ inline float silu_exact(float x) { return x / (1.0f + expf(-x)); }
-// silu() over an array (scalar per element: see va_fuse.h fz::act on the packed form)
+// silu() over an array, the plain f32 steps packed in pairs (fz::silu2): bit-identical to silu() per element
 template <int N>
 __device__ __forceinline__ void silu_n(float (&v)[N]) {
+    static_assert(N % 2 == 0, "pairs");
 #pragma unroll
-    for (int i = 0; i < N; ++i) v[i] = silu(v[i]);
+    for (int i = 0; i < N; i += 2) {
+        const f32x2 r = fz::silu2((f32x2){v[i], v[i + 1]});
+        v[i] = r[0];
+        v[i + 1] = r[1];
+    }
 }
 
 // ----------------------------------------------------------------------------------------- preprocess
@@ -419,10 +424,11 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
             float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
                   v3 = acc[i][j][3] + bv.w;
             if (a.act) {
-                v0 = silu(v0);
-                v1 = silu(v1);
-                v2 = silu(v2);
-                v3 = silu(v3);
+                const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                v0 = s01[0];
+                v1 = s01[1];
+                v2 = s23[0];
+                v3 = s23[1];
             }
             *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
         }
