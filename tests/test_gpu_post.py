@@ -97,3 +97,27 @@ def test_pipeline_planted_nav_matches_oracle():
         out = onav.frame_nav(cells_to_mask(g), cells_rect(g), 640, 640, pf)
         nf = res.frame(i)
         assert [q["path"] for q in nf.queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]
+
+
+def test_pipeline_medium_1280_planted_nav_matches_oracle():
+    """C5 shape (YOLOv8m-seg, 1280 x 1280, bf16): the fused batch runs and, with planted 64 x 64-cell
+    corridor masks, its grid / penalty / protrusion / A* outputs are the oracle's."""
+    from oracle import nav as onav
+    from workloads.corridors import cells_rect, cells_to_mask, corridor_cells
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("m")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0))
+    B, H, W = 4, 1280, 1280
+    pipe = FramePipeline(arch, fw, B, H, W, dtype="bf16")
+    grids = [corridor_cells(7300 + i, H // 20, W // 20) for i in range(B)]
+    pc = torch.tensor(np.stack(grids).astype(np.uint8)).cuda()
+    pr = torch.tensor(np.array([cells_rect(g) for g in grids], dtype=np.int32)).cuda()
+    frames = torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(13), dtype=torch.uint8).cuda()
+    res = pipe.run(frames, pc, pr, PLANT_ALWAYS)
+    pf = onav.PathFinderOracle()
+    for i, g in enumerate(grids):
+        out = onav.frame_nav(cells_to_mask(g), cells_rect(g), H, W, pf)
+        nf = res.frame(i)
+        assert [q["path"] for q in nf.queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]

@@ -584,3 +584,37 @@ def test_forward_deterministic():
         for name, g_, r in zip(("box", "cls", "coef", "proto"), again, first):
             assert torch.isfinite(g_).all(), name
             assert torch.equal(g_, r), f"{name}: run-to-run max diff {(g_ - r).abs().max().item()}"
+
+
+# ---- BASELINE.json configs[4] shape (C5): YOLOv8m-seg at 1280 x 1280 (bf16 here; fp8 weights are not built)
+_M1280 = {}
+
+
+def _m1280_ref():
+    if not _M1280:
+        from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+        arch = Arch("m")
+        fw = fold(arch, synthetic_state_dict(arch, seed=4))
+        frames = _frames(1, 1280, 1280, seed=6)
+        torch.set_num_threads(8)
+        _M1280.update(arch=arch, fw=fw, frames=frames, ref=_ref_heads(arch, fw, frames))
+    return _M1280
+
+
+def test_forward_f32_medium_1280_within_1e3():
+    from vision_assist_amd.seg import SegNet
+    c = _m1280_ref()
+    got = _gpu_heads(SegNet(c["arch"], c["fw"], dtype="f32"), c["frames"])
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, c["ref"]):
+        assert g.shape == r.shape, name
+        err = ((g - r).abs() / (1.0 + r.abs())).max().item()
+        assert err <= 1e-3, f"{name}: max rel err {err}"
+
+
+def test_forward_bf16_medium_1280_close():
+    from vision_assist_amd.seg import SegNet
+    c = _m1280_ref()
+    got = _gpu_heads(SegNet(c["arch"], c["fw"], dtype="bf16"), c["frames"])
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, c["ref"]):
+        rel = ((g - r).norm() / r.norm()).item()
+        assert rel < 5e-2, f"{name}: relative L2 error {rel}"
