@@ -275,8 +275,12 @@ def main():
                          f"protrusion/A* restatement (oracle/)"}
 
     if rank == 0:
+        # BASELINE.json configs: C3 (s-seg 640) is the headline; C5's shape (m-seg 1280) runs here with bf16
+        # weights (its fp8 weights are not built), other scale/resolution pairs are labelled custom
+        tag = {("s", 640): "C3", ("m", 1280): "C5 shape (bf16 weights, not fp8)",
+               ("n", 640): "C2 shape (batched)"}.get((args.scale, args.res), "custom")
         line = {
-            "metric": "frames/sec end-to-end (seg+penalty+A*) at 640×640, 1/2/4/8 MI355X",
+            "metric": "frames/sec end-to-end (seg+penalty+A*) at 640×640, 1/2/4/8 MI355X",  # BASELINE.json metric
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -289,7 +293,7 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (seeded uint8 frames; random-init yolov8%s-seg weights; planted nav masks when "
                     "the network yields none)" % args.scale,
-            "config": {"workload": f"C3: YOLOv8{args.scale}-seg {H}x{W} {args.dtype} + post-processing + grid/"
+            "config": {"workload": f"{tag}: YOLOv8{args.scale}-seg {H}x{W} {args.dtype} + post-processing + grid/"
                                    "penalty/protrusion/A* on GPU, end-to-end",
                        "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
                        "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",

@@ -2,11 +2,12 @@
 //
 // Restates (Ultralytics is external; vendored spec copy testing/old/segmenting_using_tflite/ops.py):
 //   post_decode_kernel   Detect inference tail (DFL softmax expectation, dist2bbox, class sigmoid) and
-//                        the candidate filter of non_max_suppression (ops.py:281-317): one thread per anchor
+//                        the candidate filter of non_max_suppression (ops.py:281-317): one 16-lane group
+//                        per anchor, one candidate-list atomic per workgroup
 //   post_nms_kernel      class-offset greedy NMS (torchvision.ops.nms: IoU > thr suppresses, float32 IoU),
-//                        max_det cap (ops.py:318-330): one 1024-thread workgroup per frame, repeated
-//                        "highest remaining score (lowest anchor on ties) -> keep -> suppress" == the
-//                        sorted greedy scan
+//                        max_det cap (ops.py:318-330): one 1024-thread workgroup per frame, candidates
+//                        bitonic-sorted in LDS and scanned greedily in 64-candidate chunks (fallback for
+//                        lists that do not fit: repeated "highest remaining -> keep -> suppress")
 //   post_mask_kernel     process_mask(upsample=True) (ops.py:707-737): coef . proto over the cropped
 //                        low-res box region into LDS, bilinear x4 (align_corners=False), > 0; per
 //                        instance pixel count and pixel bounding box.  One workgroup per detection.
@@ -51,96 +52,243 @@ struct LevelPtrs {
     const float* p[3];
 };
 
-// One 16-lane group per anchor: the group reads the anchor's class logits as consecutive 16-byte
-// chunks (one 320-byte run per anchor at nc = 80, coalesced across the group) and reduces the maximum
-// with xor shuffles inside the group.  Sigmoid is monotone, so an anchor whose best logit does not
-// clear the threshold -- nearly every anchor -- is done after that one coalesced read; the rare
-// candidate is decoded by the group's first lane.
+// One workgroup per (frame, run of DEC_APB anchors); one 16-lane group per anchor: the group reads the
+// anchor's class logits as consecutive 16-byte chunks (one 320-byte run per anchor at nc = 80, coalesced
+// across the group) and reduces the maximum with xor shuffles inside the group.  Sigmoid is monotone, so
+// an anchor whose best logit does not clear the threshold -- nearly every anchor of a trained network --
+// is done after that one coalesced read.  A candidate is decoded by the whole group (class argmax across
+// the lanes, one DFL side per lane 0-3, each in the reference's sequential order) and staged in LDS; the
+// workgroup then reserves its run of the frame's candidate list with ONE global atomic.  (One atomic per
+// candidate serialises on the frame counters' cache lines: 13.8 ms per 256-frame batch when every anchor
+// is a candidate, the synthetic n-seg weights' case.)  NMS orders candidates by (score, anchor), so the
+// list order is free.
 constexpr int DEC_GROUP = 16;
+constexpr int DEC_THREADS = 256;
+constexpr int DEC_APB = 256;  // anchors per workgroup
 
-__global__ __launch_bounds__(256) void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, int A,
-                                                          float conf, va_cand* cand, int32_t* count) {
+__global__ __launch_bounds__(DEC_THREADS) void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, int A,
+                                                                  float conf, va_cand* cand, int32_t* count) {
     const int no = 4 * REG_MAX + nc + NMC;
-    const int64_t gid = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / DEC_GROUP;
-    const int gl = threadIdx.x % DEC_GROUP;
-    if (gid >= (int64_t)B * A) return;  // whole groups leave together
-    int b = (int)(gid / A), a = (int)(gid % A);
-    int local;
-    Level L = level_of(lv.p, H, W, a, &local);
-    const float* row = L.p + ((int64_t)b * L.h * L.w + local) * no;
-    const float* cl = row + 4 * REG_MAX;
-    float mx = -INFINITY;
-    if ((nc & 3) == 0 && (no & 3) == 0) {
-        for (int c = 4 * gl; c < nc; c += 4 * DEC_GROUP) {
-            const float4 v = *(const float4*)(cl + c);
-            mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    const int b = blockIdx.y, a_base = blockIdx.x * DEC_APB;
+    const int grp = threadIdx.x / DEC_GROUP, gl = threadIdx.x % DEC_GROUP;
+    __shared__ va_cand s_c[DEC_APB];
+    __shared__ int s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    for (int ai = grp; ai < DEC_APB; ai += DEC_THREADS / DEC_GROUP) {
+        const int a = a_base + ai;
+        if (a >= A) break;  // whole group
+        int local;
+        Level L = level_of(lv.p, H, W, a, &local);
+        const float* row = L.p + ((int64_t)b * L.h * L.w + local) * no;
+        const float* cl = row + 4 * REG_MAX;
+        float mx = -INFINITY;
+        if ((nc & 3) == 0 && (no & 3) == 0) {
+            for (int c = 4 * gl; c < nc; c += 4 * DEC_GROUP) {
+                const float4 v = *(const float4*)(cl + c);
+                mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+            }
+        } else {
+            for (int c = gl; c < nc; c += DEC_GROUP) mx = fmaxf(mx, cl[c]);
         }
-    } else {
-        for (int c = gl; c < nc; c += DEC_GROUP) mx = fmaxf(mx, cl[c]);
-    }
 #pragma unroll
-    for (int o = DEC_GROUP / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, DEC_GROUP));
-    if (gl != 0 || !(sigmoidf_(mx) > conf)) return;
-    // class scores: sigmoid, first maximum (cls.max(1) on sigmoid values: saturated ties -> lowest class)
-    float best = -1.0f;
-    int bc = 0;
-    for (int c = 0; c < nc; ++c) {
-        float s = sigmoidf_(cl[c]);
-        if (s > best) {
-            best = s;
-            bc = c;
+        for (int o = DEC_GROUP / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, DEC_GROUP));
+        if (!(sigmoidf_(mx) > conf)) continue;  // group-uniform
+        // class scores: sigmoid, first maximum (cls.max(1) on sigmoid values: saturated ties -> lowest class)
+        float best = -1.0f;
+        int bc = 0;
+        for (int c = gl; c < nc; c += DEC_GROUP) {
+            const float sc = sigmoidf_(cl[c]);
+            if (sc > best) {
+                best = sc;
+                bc = c;
+            }
+        }
+#pragma unroll
+        for (int o = DEC_GROUP / 2; o > 0; o >>= 1) {
+            const float ob = __shfl_xor(best, o, DEC_GROUP);
+            const int oc = __shfl_xor(bc, o, DEC_GROUP);
+            if (ob > best || (ob == best && oc < bc)) {
+                best = ob;
+                bc = oc;
+            }
+        }
+        if (!(best > conf)) continue;  // group-uniform
+        // DFL: softmax over 16 bins, expectation -- lane `side` of the group, bins in order
+        float dside = 0.f;
+        if (gl < 4) {
+            const float* v = row + gl * REG_MAX;
+            float m = v[0];
+            for (int i = 1; i < REG_MAX; ++i) m = fmaxf(m, v[i]);
+            float e[REG_MAX], sum = 0.f;
+            for (int i = 0; i < REG_MAX; ++i) {
+                e[i] = expf(v[i] - m);
+                sum += e[i];
+            }
+            for (int i = 0; i < REG_MAX; ++i) dside += (e[i] / sum) * (float)i;
+        }
+        const float d0 = __shfl(dside, 0, DEC_GROUP), d1 = __shfl(dside, 1, DEC_GROUP),
+                    d2 = __shfl(dside, 2, DEC_GROUP), d3 = __shfl(dside, 3, DEC_GROUP);
+        if (gl == 0) {
+            int x = local % L.w, y = local / L.w;
+            float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
+            float x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3;
+            float st = (float)L.stride;
+            float cx = (x1 + x2) / 2.0f * st, cy = (y1 + y2) / 2.0f * st;
+            float bw = (x2 - x1) * st, bh = (y2 - y1) * st;
+            va_cand c;
+            c.x1 = cx - bw / 2.0f;  // xywh2xyxy (ops.py: y[...,0] = x - w/2)
+            c.y1 = cy - bh / 2.0f;
+            c.x2 = cx + bw / 2.0f;
+            c.y2 = cy + bh / 2.0f;
+            c.score = best;
+            c.cls = bc;
+            c.anchor = a;
+            c.pad = 0;
+            s_c[atomicAdd(&s_n, 1)] = c;
         }
     }
-    if (!(best > conf)) return;
-    // DFL: softmax over 16 bins, expectation
-    float d[4];
-    for (int side = 0; side < 4; ++side) {
-        const float* v = row + side * REG_MAX;
-        float m = v[0];
-        for (int i = 1; i < REG_MAX; ++i) m = fmaxf(m, v[i]);
-        float e[REG_MAX], s = 0.f;
-        for (int i = 0; i < REG_MAX; ++i) {
-            e[i] = expf(v[i] - m);
-            s += e[i];
-        }
-        float acc = 0.f;
-        for (int i = 0; i < REG_MAX; ++i) acc += (e[i] / s) * (float)i;
-        d[side] = acc;
-    }
-    int x = local % L.w, y = local / L.w;
-    float ax = (float)x + 0.5f, ay = (float)y + 0.5f;
-    float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
-    float st = (float)L.stride;
-    float cx = (x1 + x2) / 2.0f * st, cy = (y1 + y2) / 2.0f * st;
-    float bw = (x2 - x1) * st, bh = (y2 - y1) * st;
-    va_cand c;
-    c.x1 = cx - bw / 2.0f;  // xywh2xyxy (ops.py: y[...,0] = x - w/2)
-    c.y1 = cy - bh / 2.0f;
-    c.x2 = cx + bw / 2.0f;
-    c.y2 = cy + bh / 2.0f;
-    c.score = best;
-    c.cls = bc;
-    c.anchor = a;
-    c.pad = 0;
-    int slot = atomicAdd(&count[b], 1);
-    cand[(int64_t)b * A + slot] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&count[b], s_n) : 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < s_n; i += DEC_THREADS) cand[(int64_t)b * A + s_base + i] = s_c[i];
 }
 
 // ------------------------------------------------------------------------------------------- NMS
 constexpr int NMS_THREADS = 1024;
+constexpr int NMS_CAP = 16384;       // candidates whose keys fit LDS (128 KiB)
+constexpr int NMS_KEPT_MAX = 1024;   // max_det of the sorted path (kept boxes in LDS)
+constexpr int NMS_CH = 64;           // candidates per greedy-scan chunk (one ballot per row)
+constexpr size_t NMS_LDS = (size_t)NMS_CAP * 8 + (size_t)NMS_KEPT_MAX * 20 + NMS_CH * 32;
 
-constexpr int NMS_LDS_KEYS = 12288;  // keys kept in LDS up to this many candidates (96 KiB)
+// torchvision's suppression test for kept box k against c (class-offset boxes, float32 IoU, > thr)
+__device__ inline bool iou_over(float4 k, float karea, float4 c, float area, float thr) {
+    const float w = fmaxf(0.f, fminf(k.z, c.z) - fmaxf(k.x, c.x));
+    const float h = fmaxf(0.f, fminf(k.w, c.w) - fmaxf(k.y, c.y));
+    const float inter = w * h;
+    const float ovr = inter / (karea + area - inter);
+    return (double)ovr > (double)thr;
+}
 
+__device__ inline float4 offset_box(const va_cand& c) {
+    const float off = (float)c.cls * MAX_WH;
+    return make_float4(c.x1 + off, c.y1 + off, c.x2 + off, c.y2 + off);
+}
+
+__device__ inline va_det to_det(const va_cand& k) {
+    va_det d;
+    d.x1 = k.x1;
+    d.y1 = k.y1;
+    d.x2 = k.x2;
+    d.y2 = k.y2;
+    d.score = k.score;
+    d.cls = k.cls;
+    d.anchor = k.anchor;
+    d.pad = 0;
+    return d;
+}
+
+// One 1024-thread workgroup per frame.  Sorted path (n <= NMS_CAP, A <= 65536, max_det <= NMS_KEPT_MAX):
+// keys (score bits | ~anchor | list index) bitonic-sorted descending in LDS -- the order the greedy scan
+// visits candidates in (highest score, lowest anchor on ties) -- then 64-candidate chunks: each candidate
+// tested against every box kept so far (16 threads per candidate), the chunk's own pairwise suppression
+// as one 64-bit ballot per row, and a one-lane scan of the chunk in order.  Same kept set and order as
+// the repeated "highest remaining -> keep -> suppress" loop of the fallback path, which keeps the
+// candidates that do not fit (keys in LDS up to NMS_CAP, else in global scratch).
 __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* cand, const int32_t* count, int A,
                                                                float iou, int max_det, va_det* dets,
                                                                int32_t* ndet, unsigned long long* gkeys) {
+    extern __shared__ __align__(16) unsigned long long nms_smem[];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int n = count[b];
     const va_cand* C = cand + (int64_t)b * A;
-    __shared__ __align__(16) unsigned long long lkeys[NMS_LDS_KEYS];
+    va_det* D = dets + (int64_t)b * max_det;
+    __shared__ int s_kept;
+    if (n <= NMS_CAP && A <= 65536 && max_det <= NMS_KEPT_MAX) {
+        unsigned long long* sk = nms_smem;
+        float4* kb = (float4*)(sk + NMS_CAP);     // kept boxes, class-offset
+        float* ka = (float*)(kb + NMS_KEPT_MAX);   // their areas
+        float4* cb = (float4*)(ka + NMS_KEPT_MAX); // chunk boxes
+        float* ca = (float*)(cb + NMS_CH);
+        unsigned long long* cm = (unsigned long long*)(ca + NMS_CH);  // chunk row masks
+        int* sup = (int*)(cm + NMS_CH);
+        int P = 2;
+        while (P < n) P <<= 1;
+        for (int i = tid; i < P; i += NMS_THREADS) {
+            unsigned long long k = 0;
+            if (i < n)
+                k = ((unsigned long long)__float_as_uint(C[i].score) << 32) |
+                    ((unsigned long long)(0xFFFFu - (unsigned)C[i].anchor) << 16) | (unsigned long long)i;
+            sk[i] = k;
+        }
+        if (tid == 0) s_kept = 0;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = tid; t < P / 2; t += NMS_THREADS) {
+                    const int i = 2 * j * (t / j) + (t % j), l = i + j;
+                    const unsigned long long x = sk[i], y = sk[l];
+                    if ((i & k) == 0 ? x < y : x > y) {
+                        sk[i] = y;
+                        sk[l] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        for (int c0 = 0; c0 < n; c0 += NMS_CH) {
+            const int kept = s_kept;
+            if (kept >= max_det) break;  // uniform
+            const int m = min(NMS_CH, n - c0);
+            if (tid < NMS_CH) {
+                sup[tid] = tid < m ? 0 : 1;
+                if (tid < m) {
+                    const float4 bx = offset_box(C[sk[c0 + tid] & 0xFFFF]);
+                    cb[tid] = bx;
+                    ca[tid] = (bx.z - bx.x) * (bx.w - bx.y);
+                }
+            }
+            __syncthreads();
+            {  // suppressed by a box kept in an earlier chunk
+                const int t = tid % NMS_CH, part = tid / NMS_CH;
+                if (t < m) {
+                    const float4 c = cb[t];
+                    const float a = ca[t];
+                    bool sp = false;
+                    for (int q = part; q < kept && !sp; q += NMS_THREADS / NMS_CH) sp = iou_over(kb[q], ka[q], c, a, iou);
+                    if (sp) sup[t] = 1;
+                }
+            }
+            {  // chunk-internal: row r = the later candidates r suppresses if kept
+                const int w = tid >> 6, lane = tid & 63;
+                for (int r = w; r < NMS_CH; r += NMS_THREADS / 64) {
+                    const bool pr = r < m && lane < m && lane > r && iou_over(cb[r], ca[r], cb[lane], ca[lane], iou);
+                    const unsigned long long bal = __ballot(pr);
+                    if (lane == 0) cm[r] = bal;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int kk = kept;
+                unsigned long long removed = 0;
+                for (int t = 0; t < m && kk < max_det; ++t) {
+                    if (sup[t] || ((removed >> t) & 1ull)) continue;
+                    removed |= cm[t];
+                    kb[kk] = cb[t];
+                    ka[kk] = ca[t];
+                    D[kk] = to_det(C[sk[c0 + t] & 0xFFFF]);
+                    ++kk;
+                }
+                s_kept = kk;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) ndet[b] = s_kept;
+        return;
+    }
     __shared__ unsigned long long red[NMS_THREADS / 64];
+    __shared__ int red_i[NMS_THREADS / 64];
     // (score bits << 32 | ~anchor): max = highest score, lowest anchor on ties; 0 = kept or suppressed
-    unsigned long long* key = n <= NMS_LDS_KEYS ? lkeys : gkeys + (int64_t)b * A;
+    unsigned long long* key = n <= NMS_CAP ? nms_smem : gkeys + (int64_t)b * A;
     for (int i = tid; i < n; i += NMS_THREADS) {
         unsigned sb = __float_as_uint(C[i].score);
         key[i] = ((unsigned long long)sb << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)C[i].anchor);
@@ -156,7 +304,6 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 bi = i;
             }
         }
-        // block argmax: pack index into the low bits is impossible (64-bit key), so reduce pairs
         for (int o = 32; o > 0; o >>= 1) {
             unsigned long long ob = __shfl_xor(best, o, 64);
             int oi = __shfl_xor(bi, o, 64);
@@ -165,7 +312,6 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 bi = oi;
             }
         }
-        __shared__ int red_i[NMS_THREADS / 64];
         if ((tid & 63) == 0) {
             red[tid >> 6] = best;
             red_i[tid >> 6] = bi;
@@ -182,33 +328,15 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
         if (best == 0) break;
         const va_cand k = C[bi];
         if (tid == 0) {
-            va_det d;
-            d.x1 = k.x1;
-            d.y1 = k.y1;
-            d.x2 = k.x2;
-            d.y2 = k.y2;
-            d.score = k.score;
-            d.cls = k.cls;
-            d.anchor = k.anchor;
-            d.pad = 0;
-            dets[(int64_t)b * max_det + kept] = d;
+            D[kept] = to_det(k);
             key[bi] = 0;
         }
-        // suppress IoU > thr among the remaining (class-offset boxes, torchvision float math)
-        const float off = (float)k.cls * MAX_WH;
-        const float kx1 = k.x1 + off, ky1 = k.y1 + off, kx2 = k.x2 + off, ky2 = k.y2 + off;
-        const float karea = (kx2 - kx1) * (ky2 - ky1);
+        const float4 kbx = offset_box(k);
+        const float karea = (kbx.z - kbx.x) * (kbx.w - kbx.y);
         for (int i = tid; i < n; i += NMS_THREADS) {
             if (key[i] == 0 || i == bi) continue;
-            const va_cand c = C[i];
-            const float o2 = (float)c.cls * MAX_WH;
-            const float x1 = c.x1 + o2, y1 = c.y1 + o2, x2 = c.x2 + o2, y2 = c.y2 + o2;
-            const float area = (x2 - x1) * (y2 - y1);
-            const float w = fmaxf(0.f, fminf(kx2, x2) - fmaxf(kx1, x1));
-            const float h = fmaxf(0.f, fminf(ky2, y2) - fmaxf(ky1, y1));
-            const float inter = w * h;
-            const float ovr = inter / (karea + area - inter);
-            if ((double)ovr > (double)iou) key[i] = 0;
+            const float4 c = offset_box(C[i]);
+            if (iou_over(kbx, karea, c, (c.z - c.x) * (c.w - c.y), iou)) key[i] = 0;
         }
         ++kept;
         __syncthreads();
@@ -301,27 +429,49 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     const int Y0 = max(0, (int)((ry0 - 1) / sy) - 2), Y1 = min(a.H - 1, (int)((ry1 + 1) / sy) + 2);
     const int ow = X1 - X0 + 1, oh = Y1 - Y0 + 1;
     int cnt = 0, bx0 = a.W, bx1 = -1, by0 = a.H, by1 = -1;
-    for (int i = tid; i < ow * oh; i += MASK_THREADS) {
-        int X = X0 + i % ow, Y = Y0 + i / ow;
-        int xa, xb, ya, yb;
-        float wx0, wx1, wy0, wy1;
+    auto val = [&](int yy, int xx) -> float {
+        if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
+        if (in_lds) return tile[(yy - ry0) * tw + (xx - rx0)];
+        const float* p = a.proto + (((int64_t)b * a.mh + yy) * a.mw + xx) * NMC;
+        float s = 0.f;
+        for (int c = 0; c < NMC; ++c) s += coef[c] * p[c];
+        return s;
+    };
+    // one item = one full-res column X over MASK_ROWS consecutive rows: the horizontal interpolation of a
+    // low-res row pair is shared by every output row with the same vertical taps (4 of them at the x4
+    // upsample), so each output pixel costs one vertical blend -- the same float expression as
+    // wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb))
+    constexpr int MASK_ROWS = 8;
+    const int ng = (oh + MASK_ROWS - 1) / MASK_ROWS;
+    for (int i = tid; i < ow * ng; i += MASK_THREADS) {
+        const int X = X0 + i % ow, Yb = Y0 + (i / ow) * MASK_ROWS;
+        int xa, xb;
+        float wx0, wx1;
         taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
-        taps(Y, sy, a.mh, &ya, &yb, &wy0, &wy1);
-        auto val = [&](int yy, int xx) -> float {
-            if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
-            if (in_lds) return tile[(yy - ry0) * tw + (xx - rx0)];
-            const float* p = a.proto + (((int64_t)b * a.mh + yy) * a.mw + xx) * NMC;
-            float s = 0.f;
-            for (int c = 0; c < NMC; ++c) s += coef[c] * p[c];
-            return s;
-        };
-        float v = wy0 * (wx0 * val(ya, xa) + wx1 * val(ya, xb)) + wy1 * (wx0 * val(yb, xa) + wx1 * val(yb, xb));
-        if (v > 0.f) {
-            ++cnt;
-            bx0 = min(bx0, X);
-            bx1 = max(bx1, X);
-            by0 = min(by0, Y);
-            by1 = max(by1, Y);
+        int ca = -1, cb = -1;
+        float ha = 0.f, hb = 0.f;
+        for (int r = 0; r < MASK_ROWS; ++r) {
+            const int Y = Yb + r;
+            if (Y > Y1) break;
+            int ya, yb;
+            float wy0, wy1;
+            taps(Y, sy, a.mh, &ya, &yb, &wy0, &wy1);
+            if (ya != ca) {
+                ha = ya == cb ? hb : wx0 * val(ya, xa) + wx1 * val(ya, xb);
+                ca = ya;
+            }
+            if (yb != cb) {
+                hb = yb == ca ? ha : wx0 * val(yb, xa) + wx1 * val(yb, xb);
+                cb = yb;
+            }
+            const float v = wy0 * ha + wy1 * hb;
+            if (v > 0.f) {
+                ++cnt;
+                bx0 = min(bx0, X);
+                bx1 = max(bx1, X);
+                by0 = min(by0, Y);
+                by1 = max(by1, Y);
+            }
         }
     }
     atomicAdd(&s_cnt, cnt);
@@ -426,8 +576,9 @@ int va_post_run(void* stream, const va_post_args* p) {
     const int B = p->B;
     if (hipMemsetAsync(p->cand_count, 0, sizeof(int32_t) * B, st) != hipSuccess) return VA_ERR_HIP;
     LevelPtrs lv{{p->levels[0], p->levels[1], p->levels[2]}};
-    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1((int64_t)B * A * DEC_GROUP, 256)), dim3(256), 0, st, lv, B, p->H,
-                       p->W, p->nc, A, p->conf, p->cand, p->cand_count);
+    if (B > 65535) return VA_ERR_ARG;
+    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, DEC_APB), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
+                       p->nc, A, p->conf, p->cand, p->cand_count);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     static bool mask_attr = false;
     if (!mask_attr) {
@@ -436,7 +587,14 @@ int va_post_run(void* stream, const va_post_args* p) {
             return VA_ERR_HIP;
         mask_attr = true;
     }
-    hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), 0, st, p->cand, p->cand_count, A, p->iou,
+    static bool nms_attr = false;
+    if (!nms_attr) {
+        if (hipFuncSetAttribute((const void*)post_nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS) !=
+            hipSuccess)
+            return VA_ERR_HIP;
+        nms_attr = true;
+    }
+    hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), NMS_LDS, st, p->cand, p->cand_count, A, p->iou,
                        p->max_det, p->dets, p->ndet, p->keys);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     MaskArgs ma;
