@@ -386,7 +386,7 @@ __device__ inline void taps(int o, float scale, int in, int* i0, int* i1, float*
     *i1 = x0 + p;
 }
 
-constexpr int MASK_THREADS = 256;
+constexpr int MASK_THREADS = 1024;  // the window tile takes up to 100 KiB of LDS: one workgroup per CU, so it brings 16 waves
 constexpr int MASK_LDS_MAX = 160 * 160;
 
 __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
@@ -414,13 +414,21 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     }
     const int tw = rx1 - rx0 + 1, th = ry1 - ry0 + 1;
     const bool in_lds = tw * th <= MASK_LDS_MAX;
-    for (int i = tid; in_lds && i < tw * th; i += MASK_THREADS) {
-        int y = ry0 + i / tw, x = rx0 + i % tw;
-        const float* p = a.proto + (((int64_t)b * a.mh + y) * a.mw + x) * NMC;
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < NMC; ++c) s += coef[c] * p[c];
-        tile[i] = s;
+    // the crop window of coef . proto into LDS: 8 lanes per low-res pixel, each one 16-byte run of its 32
+    // channels (a wave reads 8 whole 128-byte pixels, coalesced), partial dots reduced across the 8 lanes
+    // (a different summation order than a sequential dot: rounding-level differences, like torch's matmul)
+    if (in_lds) {
+        const int sub = tid & 7;
+        const float4 cq = make_float4(coef[4 * sub], coef[4 * sub + 1], coef[4 * sub + 2], coef[4 * sub + 3]);
+        for (int i = tid >> 3; i < tw * th; i += MASK_THREADS / 8) {
+            const int y = ry0 + i / tw, x = rx0 + i % tw;
+            const float4 v = *(const float4*)(a.proto + (((int64_t)b * a.mh + y) * a.mw + x) * NMC + 4 * sub);
+            float s = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
+            s += __shfl_xor(s, 1, 8);
+            s += __shfl_xor(s, 2, 8);
+            s += __shfl_xor(s, 4, 8);
+            if (sub == 0) tile[i] = s;
+        }
     }
     __syncthreads();
     const float sx = (float)a.mw / (float)a.W, sy = (float)a.mh / (float)a.H;
