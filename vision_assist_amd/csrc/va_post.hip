@@ -398,7 +398,9 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     va_mask_stat* st = a.stats + (int64_t)b * a.max_det + k;
     __shared__ float coef[NMC];
     __shared__ int s_cnt, s_x0, s_x1, s_y0, s_y1;
-    extern __shared__ __align__(16) float tile[];  // [(ry1-ry0+1)][(rx1-rx0+1)]
+    extern __shared__ __align__(16) int4 mask_smem[];
+    int4* rt = mask_smem;                  // [H]: vertical taps (ya, yb, wy0, wy1) of the window's rows
+    float* tile = (float*)(mask_smem + a.H);  // [(ry1-ry0+1)][(rx1-rx0+1)]
     if (tid < NMC) coef[tid] = coef_of(a, b, d.anchor)[tid];
     if (tid == 0) {
         s_cnt = 0;
@@ -430,12 +432,18 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
             if (sub == 0) tile[i] = s;
         }
     }
-    __syncthreads();
     const float sx = (float)a.mw / (float)a.W, sy = (float)a.mh / (float)a.H;
     // full-res pixels whose taps can touch the window
     const int X0 = max(0, (int)((rx0 - 1) / sx) - 2), X1 = min(a.W - 1, (int)((rx1 + 1) / sx) + 2);
     const int Y0 = max(0, (int)((ry0 - 1) / sy) - 2), Y1 = min(a.H - 1, (int)((ry1 + 1) / sy) + 2);
     const int ow = X1 - X0 + 1, oh = Y1 - Y0 + 1;
+    for (int r = tid; r < oh; r += MASK_THREADS) {
+        int ya, yb;
+        float wy0, wy1;
+        taps(Y0 + r, sy, a.mh, &ya, &yb, &wy0, &wy1);
+        rt[r] = make_int4(ya, yb, __float_as_int(wy0), __float_as_int(wy1));
+    }
+    __syncthreads();
     int cnt = 0, bx0 = a.W, bx1 = -1, by0 = a.H, by1 = -1;
     auto val = [&](int yy, int xx) -> float {
         if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
@@ -448,22 +456,23 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     // one item = one full-res column X over MASK_ROWS consecutive rows: the horizontal interpolation of a
     // low-res row pair is shared by every output row with the same vertical taps (4 of them at the x4
     // upsample), so each output pixel costs one vertical blend -- the same float expression as
-    // wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb))
+    // wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb)) -- and none
+    // when both blended rows have one sign: wy0, wy1 >= 0 with one of them >= 1/2, so two values >= 2^-100
+    // blend to > 0 and two values <= 0 to <= 0, exactly as the full expression would
     constexpr int MASK_ROWS = 8;
+    constexpr float POS = 7.888609052210118e-31f;  // 2^-100
     const int ng = (oh + MASK_ROWS - 1) / MASK_ROWS;
     for (int i = tid; i < ow * ng; i += MASK_THREADS) {
-        const int X = X0 + i % ow, Yb = Y0 + (i / ow) * MASK_ROWS;
+        const int X = X0 + i % ow, r0 = (i / ow) * MASK_ROWS;
         int xa, xb;
         float wx0, wx1;
         taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
-        int ca = -1, cb = -1;
+        int ca = -1, cb = -1, c = 0, first = -1, last = -1;
         float ha = 0.f, hb = 0.f;
-        for (int r = 0; r < MASK_ROWS; ++r) {
-            const int Y = Yb + r;
-            if (Y > Y1) break;
-            int ya, yb;
-            float wy0, wy1;
-            taps(Y, sy, a.mh, &ya, &yb, &wy0, &wy1);
+        const int rn = min(MASK_ROWS, oh - r0);
+        for (int r = 0; r < rn; ++r) {
+            const int4 t = rt[r0 + r];
+            const int ya = t.x, yb = t.y;
             if (ya != ca) {
                 ha = ya == cb ? hb : wx0 * val(ya, xa) + wx1 * val(ya, xb);
                 ca = ya;
@@ -472,14 +481,22 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
                 hb = yb == ca ? ha : wx0 * val(yb, xa) + wx1 * val(yb, xb);
                 cb = yb;
             }
-            const float v = wy0 * ha + wy1 * hb;
-            if (v > 0.f) {
-                ++cnt;
-                bx0 = min(bx0, X);
-                bx1 = max(bx1, X);
-                by0 = min(by0, Y);
-                by1 = max(by1, Y);
+            bool pos;
+            if (ha >= POS && hb >= POS) pos = true;
+            else if (ha <= 0.f && hb <= 0.f) pos = false;
+            else pos = __int_as_float(t.z) * ha + __int_as_float(t.w) * hb > 0.f;
+            if (pos) {
+                ++c;
+                if (first < 0) first = r;
+                last = r;
             }
+        }
+        if (c) {
+            cnt += c;
+            bx0 = min(bx0, X);
+            bx1 = max(bx1, X);
+            by0 = min(by0, Y0 + r0 + first);
+            by1 = max(by1, Y0 + r0 + last);
         }
     }
     atomicAdd(&s_cnt, cnt);
@@ -591,7 +608,7 @@ int va_post_run(void* stream, const va_post_args* p) {
     static bool mask_attr = false;
     if (!mask_attr) {
         if (hipFuncSetAttribute((const void*)post_mask_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                MASK_LDS_MAX * 4) != hipSuccess)
+                                MASK_LDS_MAX * 4 + 3584 * 16) != hipSuccess)
             return VA_ERR_HIP;
         mask_attr = true;
     }
@@ -621,7 +638,9 @@ int va_post_run(void* stream, const va_post_args* p) {
     ma.ndet = p->ndet;
     ma.stats = p->stats;
     const int tile = ma.mh * ma.mw < MASK_LDS_MAX ? ma.mh * ma.mw : MASK_LDS_MAX;
-    hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), (size_t)tile * 4, st, ma);
+    const size_t mask_lds = (size_t)p->H * 16 + (size_t)tile * 4;
+    if (mask_lds > MASK_LDS_MAX * 4 + 3584 * 16) return VA_ERR_ARG;  // frames up to 3584 rows (160 KiB of LDS)
+    hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), mask_lds, st, ma);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     if (p->cells) {
         if (p->H % VA_GRID || p->W % VA_GRID) return VA_ERR_ARG;
