@@ -386,9 +386,14 @@ __device__ inline void taps(int o, float scale, int in, int* i0, int* i1, float*
     *i1 = x0 + p;
 }
 
-constexpr int MASK_THREADS = 1024;  // the window tile takes up to 100 KiB of LDS: one workgroup per CU, so it brings 16 waves
-constexpr int MASK_LDS_MAX = 160 * 160;
+constexpr int MASK_THREADS = 256;
+constexpr int MASK_STRIP = 6144;    // low-res window values in LDS per strip (24 KiB)
+constexpr int MASK_MAX_STRIPS = 128;
 
+// One workgroup per detection.  The low-res crop window of coef . proto is built in LDS one strip of rows
+// at a time (S rows + the next one, S = MASK_STRIP / width - 1), and each strip upsamples the full-res
+// rows whose upper tap falls in it.  Small LDS (strip + row-tap table, ~34 KiB at 640 x 640) keeps four
+// workgroups per CU: the work per detection is short and latency-bound, so concurrency is what counts.
 __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     const int k = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     if (k >= a.ndet[b]) return;
@@ -398,10 +403,19 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     va_mask_stat* st = a.stats + (int64_t)b * a.max_det + k;
     __shared__ float coef[NMC];
     __shared__ int s_cnt, s_x0, s_x1, s_y0, s_y1;
+    __shared__ int s_rs[MASK_MAX_STRIPS], s_re[MASK_MAX_STRIPS];
     extern __shared__ __align__(16) int4 mask_smem[];
-    int4* rt = mask_smem;                  // [H]: vertical taps (ya, yb, wy0, wy1) of the window's rows
-    float* tile = (float*)(mask_smem + a.H);  // [(ry1-ry0+1)][(rx1-rx0+1)]
+    int4* rt = mask_smem;                     // [H]: vertical taps (ya, yb, wy0, wy1) of the window's rows
+    float* tile = (float*)(mask_smem + a.H);  // [S + 1][tw]: one strip of the crop window
+    if (rx1 < rx0 || ry1 < ry0) {
+        if (tid == 0) *st = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
+        return;
+    }
+    const int tw = rx1 - rx0 + 1, th = ry1 - ry0 + 1;
+    const int S = MASK_STRIP / tw - 1;  // >= 1: the launcher checks mw <= MASK_STRIP / 2
+    const int nstrips = (th + S - 1) / S;
     if (tid < NMC) coef[tid] = coef_of(a, b, d.anchor)[tid];
+    for (int i = tid; i < nstrips; i += MASK_THREADS) s_rs[i] = s_re[i] = 0;
     if (tid == 0) {
         s_cnt = 0;
         s_x0 = a.W;
@@ -409,94 +423,104 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
         s_y0 = a.H;
         s_y1 = -1;
     }
-    __syncthreads();
-    if (rx1 < rx0 || ry1 < ry0) {
-        if (tid == 0) *st = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
-        return;
-    }
-    const int tw = rx1 - rx0 + 1, th = ry1 - ry0 + 1;
-    const bool in_lds = tw * th <= MASK_LDS_MAX;
-    // the crop window of coef . proto into LDS: 8 lanes per low-res pixel, each one 16-byte run of its 32
-    // channels (a wave reads 8 whole 128-byte pixels, coalesced), partial dots reduced across the 8 lanes
-    // (a different summation order than a sequential dot: rounding-level differences, like torch's matmul)
-    if (in_lds) {
-        const int sub = tid & 7;
-        const float4 cq = make_float4(coef[4 * sub], coef[4 * sub + 1], coef[4 * sub + 2], coef[4 * sub + 3]);
-        for (int i = tid >> 3; i < tw * th; i += MASK_THREADS / 8) {
-            const int y = ry0 + i / tw, x = rx0 + i % tw;
-            const float4 v = *(const float4*)(a.proto + (((int64_t)b * a.mh + y) * a.mw + x) * NMC + 4 * sub);
-            float s = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
-            s += __shfl_xor(s, 1, 8);
-            s += __shfl_xor(s, 2, 8);
-            s += __shfl_xor(s, 4, 8);
-            if (sub == 0) tile[i] = s;
-        }
-    }
     const float sx = (float)a.mw / (float)a.W, sy = (float)a.mh / (float)a.H;
     // full-res pixels whose taps can touch the window
     const int X0 = max(0, (int)((rx0 - 1) / sx) - 2), X1 = min(a.W - 1, (int)((rx1 + 1) / sx) + 2);
     const int Y0 = max(0, (int)((ry0 - 1) / sy) - 2), Y1 = min(a.H - 1, (int)((ry1 + 1) / sy) + 2);
     const int ow = X1 - X0 + 1, oh = Y1 - Y0 + 1;
+    // strip of a full-res row: the one holding its upper tap ya (rows whose taps both miss the crop rows are
+    // 0 everywhere and belong to none); ya is non-decreasing in Y, so every strip owns one run of rows
+    auto strip_of = [&](int ya, int yb) { return (yb < ry0 || ya > ry1) ? -1 : (ya < ry0 ? 0 : (ya - ry0) / S); };
+    __syncthreads();
     for (int r = tid; r < oh; r += MASK_THREADS) {
         int ya, yb;
         float wy0, wy1;
         taps(Y0 + r, sy, a.mh, &ya, &yb, &wy0, &wy1);
         rt[r] = make_int4(ya, yb, __float_as_int(wy0), __float_as_int(wy1));
+        const int kr = strip_of(ya, yb);
+        if (kr < 0) continue;
+        int pa, pb, na, nb;
+        float w0, w1;
+        int kp = -1, kn = -1;
+        if (r > 0) {
+            taps(Y0 + r - 1, sy, a.mh, &pa, &pb, &w0, &w1);
+            kp = strip_of(pa, pb);
+        }
+        if (r + 1 < oh) {
+            taps(Y0 + r + 1, sy, a.mh, &na, &nb, &w0, &w1);
+            kn = strip_of(na, nb);
+        }
+        if (kp != kr) s_rs[kr] = r;
+        if (kn != kr) s_re[kr] = r + 1;
     }
-    __syncthreads();
+    const int sub = tid & 7;
+    const float4 cq = make_float4(coef[4 * sub], coef[4 * sub + 1], coef[4 * sub + 2], coef[4 * sub + 3]);
     int cnt = 0, bx0 = a.W, bx1 = -1, by0 = a.H, by1 = -1;
-    auto val = [&](int yy, int xx) -> float {
-        if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
-        if (in_lds) return tile[(yy - ry0) * tw + (xx - rx0)];
-        const float* p = a.proto + (((int64_t)b * a.mh + yy) * a.mw + xx) * NMC;
-        float s = 0.f;
-        for (int c = 0; c < NMC; ++c) s += coef[c] * p[c];
-        return s;
-    };
-    // one item = one full-res column X over MASK_ROWS consecutive rows: the horizontal interpolation of a
-    // low-res row pair is shared by every output row with the same vertical taps (4 of them at the x4
-    // upsample), so each output pixel costs one vertical blend -- the same float expression as
-    // wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb)) -- and none
+    // one item = one full-res column X over MASK_ROWS consecutive rows of the strip: the horizontal
+    // interpolation of a low-res row pair is shared by every output row with the same vertical taps (4 of
+    // them at the x4 upsample), so each output pixel costs one vertical blend -- the same float expression
+    // as wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb)) -- and none
     // when both blended rows have one sign: wy0, wy1 >= 0 with one of them >= 1/2, so two values >= 2^-100
     // blend to > 0 and two values <= 0 to <= 0, exactly as the full expression would
     constexpr int MASK_ROWS = 8;
     constexpr float POS = 7.888609052210118e-31f;  // 2^-100
-    const int ng = (oh + MASK_ROWS - 1) / MASK_ROWS;
-    for (int i = tid; i < ow * ng; i += MASK_THREADS) {
-        const int X = X0 + i % ow, r0 = (i / ow) * MASK_ROWS;
-        int xa, xb;
-        float wx0, wx1;
-        taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
-        int ca = -1, cb = -1, c = 0, first = -1, last = -1;
-        float ha = 0.f, hb = 0.f;
-        const int rn = min(MASK_ROWS, oh - r0);
-        for (int r = 0; r < rn; ++r) {
-            const int4 t = rt[r0 + r];
-            const int ya = t.x, yb = t.y;
-            if (ya != ca) {
-                ha = ya == cb ? hb : wx0 * val(ya, xa) + wx1 * val(ya, xb);
-                ca = ya;
-            }
-            if (yb != cb) {
-                hb = yb == ca ? ha : wx0 * val(yb, xa) + wx1 * val(yb, xb);
-                cb = yb;
-            }
-            bool pos;
-            if (ha >= POS && hb >= POS) pos = true;
-            else if (ha <= 0.f && hb <= 0.f) pos = false;
-            else pos = __int_as_float(t.z) * ha + __int_as_float(t.w) * hb > 0.f;
-            if (pos) {
-                ++c;
-                if (first < 0) first = r;
-                last = r;
-            }
+    for (int ks = 0; ks < nstrips; ++ks) {
+        const int s0 = ry0 + ks * S, s1 = min(s0 + S, ry1);  // crop rows held: s0 .. s1
+        __syncthreads();  // previous strip consumed; strip ranges / coef visible
+        // the strip of coef . proto: 8 lanes per low-res pixel, each one 16-byte run of its 32 channels
+        // (a wave reads 8 whole 128-byte pixels, coalesced), partial dots reduced across the 8 lanes
+        for (int i = tid >> 3; i < (s1 - s0 + 1) * tw; i += MASK_THREADS / 8) {
+            const int y = s0 + i / tw, x = rx0 + i % tw;
+            const float4 v = *(const float4*)(a.proto + (((int64_t)b * a.mh + y) * a.mw + x) * NMC + 4 * sub);
+            float sdot = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
+            sdot += __shfl_xor(sdot, 1, 8);
+            sdot += __shfl_xor(sdot, 2, 8);
+            sdot += __shfl_xor(sdot, 4, 8);
+            if (sub == 0) tile[i] = sdot;
         }
-        if (c) {
-            cnt += c;
-            bx0 = min(bx0, X);
-            bx1 = max(bx1, X);
-            by0 = min(by0, Y0 + r0 + first);
-            by1 = max(by1, Y0 + r0 + last);
+        __syncthreads();
+        auto val = [&](int yy, int xx) -> float {
+            if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
+            return tile[(yy - s0) * tw + (xx - rx0)];
+        };
+        const int rs = s_rs[ks], nr = s_re[ks] - rs;
+        const int ng = (nr + MASK_ROWS - 1) / MASK_ROWS;
+        for (int i = tid; i < ow * ng; i += MASK_THREADS) {
+            const int X = X0 + i % ow, r0 = rs + (i / ow) * MASK_ROWS;
+            int xa, xb;
+            float wx0, wx1;
+            taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
+            int ca = -1, cb = -1, c = 0, first = -1, last = -1;
+            float ha = 0.f, hb = 0.f;
+            const int rn = min(MASK_ROWS, rs + nr - r0);
+            for (int r = 0; r < rn; ++r) {
+                const int4 t = rt[r0 + r];
+                const int ya = t.x, yb = t.y;
+                if (ya != ca) {
+                    ha = ya == cb ? hb : wx0 * val(ya, xa) + wx1 * val(ya, xb);
+                    ca = ya;
+                }
+                if (yb != cb) {
+                    hb = yb == ca ? ha : wx0 * val(yb, xa) + wx1 * val(yb, xb);
+                    cb = yb;
+                }
+                bool pos;
+                if (ha >= POS && hb >= POS) pos = true;
+                else if (ha <= 0.f && hb <= 0.f) pos = false;
+                else pos = __int_as_float(t.z) * ha + __int_as_float(t.w) * hb > 0.f;
+                if (pos) {
+                    ++c;
+                    if (first < 0) first = r;
+                    last = r;
+                }
+            }
+            if (c) {
+                cnt += c;
+                bx0 = min(bx0, X);
+                bx1 = max(bx1, X);
+                by0 = min(by0, Y0 + r0 + first);
+                by1 = max(by1, Y0 + r0 + last);
+            }
         }
     }
     atomicAdd(&s_cnt, cnt);
@@ -605,19 +629,16 @@ int va_post_run(void* stream, const va_post_args* p) {
     hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, DEC_APB), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
                        p->nc, A, p->conf, p->cand, p->cand_count);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    static bool mask_attr = false;
-    if (!mask_attr) {
+    const size_t mask_lds = (size_t)p->H * 16 + (size_t)MASK_STRIP * 4;
+    if (p->W / 4 > MASK_STRIP / 2 || mask_lds > 160 * 1024 - 2048 ||
+        (p->H / 4 + MASK_STRIP / (p->W / 4) - 2) / (MASK_STRIP / (p->W / 4) - 1) > MASK_MAX_STRIPS)
+        return VA_ERR_ARG;  // the strips of the widest window must fit the kernel's tables
+    static size_t mask_attr = 0;
+    if (mask_lds > mask_attr) {
         if (hipFuncSetAttribute((const void*)post_mask_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                MASK_LDS_MAX * 4 + 3584 * 16) != hipSuccess)
+                                (int)mask_lds) != hipSuccess)
             return VA_ERR_HIP;
-        mask_attr = true;
-    }
-    static bool nms_attr = false;
-    if (!nms_attr) {
-        if (hipFuncSetAttribute((const void*)post_nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS) !=
-            hipSuccess)
-            return VA_ERR_HIP;
-        nms_attr = true;
+        mask_attr = mask_lds;
     }
     hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), NMS_LDS, st, p->cand, p->cand_count, A, p->iou,
                        p->max_det, p->dets, p->ndet, p->keys);
@@ -637,9 +658,6 @@ int va_post_run(void* stream, const va_post_args* p) {
     ma.dets = p->dets;
     ma.ndet = p->ndet;
     ma.stats = p->stats;
-    const int tile = ma.mh * ma.mw < MASK_LDS_MAX ? ma.mh * ma.mw : MASK_LDS_MAX;
-    const size_t mask_lds = (size_t)p->H * 16 + (size_t)tile * 4;
-    if (mask_lds > MASK_LDS_MAX * 4 + 3584 * 16) return VA_ERR_ARG;  // frames up to 3584 rows (160 KiB of LDS)
     hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), mask_lds, st, ma);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     if (p->cells) {
