@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256, help="frames per step per GPU (sweep: DESIGN.md §5)")
+    p.add_argument("--batch", type=int, default=384, help="frames per step per GPU (sweep: DESIGN.md §5)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
     p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
