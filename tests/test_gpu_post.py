@@ -19,11 +19,11 @@ from oracle import yolo_ref as Y
 pytestmark = pytest.mark.gpu
 
 
-def _setup(cls_bias, B=2, H=640, W=640, seed=0):
+def _setup(cls_bias, B=2, H=640, W=640, seed=0, scale="s"):
     from vision_assist_amd.post import PostEngine
     from vision_assist_amd.seg import SegNet
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
-    arch = Arch("s")
+    arch = Arch(scale)
     fw = fold(arch, synthetic_state_dict(arch, seed=seed, cls_bias=cls_bias))
     net = SegNet(arch, fw, dtype="f32")
     frames = torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(seed + 11),
@@ -73,6 +73,23 @@ def test_post_matches_oracle(regime, cls_bias):
         cells_ref = m[10::20, 10::20].numpy()
         cells_gpu = post.cells[b].cpu().numpy()
         assert (cells_ref != cells_gpu).sum() <= 1
+
+
+def test_nms_long_candidate_list_matches_oracle():
+    """1280 x 1280 dense regime: > 16384 candidates per frame, so the NMS takes its batched path (exact radix
+    select of the 16384 largest keys below the previous batch, sorted and scanned per batch); the kept
+    detections are the oracle's, in order."""
+    H = W = 1280
+    post, box, cls, coef, proto = _setup(4.0, B=1, H=H, W=W, seed=2, scale="n")
+    pred = Y.decode(box, cls, H, W)
+    n_cand = int((pred[0, 4:].amax(0) > 0.5).sum())
+    assert n_cand > 16384, n_cand
+    det_ref = Y.nms_image(pred[0], coef[0])
+    det_gpu, _anchors = post.det_tensor(0)
+    assert det_gpu.shape[0] == det_ref.shape[0]
+    assert torch.equal(det_gpu[:, 5], det_ref[:, 5]), "classes / order differ"
+    assert torch.allclose(det_gpu[:, :4], det_ref[:, :4], atol=1e-3, rtol=0)
+    assert torch.allclose(det_gpu[:, 4], det_ref[:, 4], atol=1e-6, rtol=0)
 
 
 def test_pipeline_planted_nav_matches_oracle():

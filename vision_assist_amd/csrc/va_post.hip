@@ -204,7 +204,7 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
     const va_cand* C = cand + (int64_t)b * A;
     va_det* D = dets + (int64_t)b * max_det;
     __shared__ int s_kept;
-    if (n <= NMS_CAP && A <= 65536 && max_det <= NMS_KEPT_MAX) {
+    if (A <= 65536 && max_det <= NMS_KEPT_MAX) {
         unsigned long long* sk = nms_smem;
         float4* kb = (float4*)(sk + NMS_CAP);     // kept boxes, class-offset
         float* ka = (float*)(kb + NMS_KEPT_MAX);   // their areas
@@ -212,33 +212,99 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
         float* ca = (float*)(cb + NMS_CH);
         unsigned long long* cm = (unsigned long long*)(ca + NMS_CH);  // chunk row masks
         int* sup = (int*)(cm + NMS_CH);
-        int P = 2;
-        while (P < n) P <<= 1;
-        for (int i = tid; i < P; i += NMS_THREADS) {
-            unsigned long long k = 0;
-            if (i < n)
-                k = ((unsigned long long)__float_as_uint(C[i].score) << 32) |
-                    ((unsigned long long)(0xFFFFu - (unsigned)C[i].anchor) << 16) | (unsigned long long)i;
-            sk[i] = k;
+        __shared__ unsigned s_hist[256];
+        __shared__ unsigned long long s_T;
+        __shared__ int s_m, s_k;
+        auto key_of = [&](int i) {
+            return ((unsigned long long)__float_as_uint(C[i].score) << 32) |
+                   ((unsigned long long)(0xFFFFu - (unsigned)C[i].anchor) << 16) | (unsigned long long)i;
+        };
+        // lists longer than NMS_CAP run in batches: the NMS_CAP largest keys below the previous batch's
+        // smallest (an exact radix select over the keys in global scratch, keys are unique), sorted and
+        // scanned like a short list, until max_det boxes are kept or the list is exhausted
+        const bool big = n > NMS_CAP;
+        unsigned long long* gk = gkeys + (int64_t)b * A;
+        if (big) {
+            for (int i = tid; i < n; i += NMS_THREADS) gk[i] = key_of(i);
         }
         if (tid == 0) s_kept = 0;
+        unsigned long long hi = ~0ull;  // exclusive bound of the remaining keys
         __syncthreads();
-        for (int k = 2; k <= P; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int t = tid; t < P / 2; t += NMS_THREADS) {
-                    const int i = 2 * j * (t / j) + (t % j), l = i + j;
-                    const unsigned long long x = sk[i], y = sk[l];
-                    if ((i & k) == 0 ? x < y : x > y) {
-                        sk[i] = y;
-                        sk[l] = x;
+        while (true) {
+            int nb = n;  // this batch's candidates
+            if (big) {
+                if (tid == 0) {
+                    s_m = 0;
+                    s_T = 0;
+                    s_k = NMS_CAP;
+                }
+                for (int i = tid; i < 256; i += NMS_THREADS) s_hist[i] = 0;
+                __syncthreads();
+                for (int i = tid; i < n; i += NMS_THREADS)
+                    if (gk[i] < hi) atomicAdd(&s_m, 1);
+                __syncthreads();
+                const int rem = s_m;
+                __syncthreads();  // everyone has read s_m before it is reused
+                if (rem > NMS_CAP) {  // T = the NMS_CAP-th largest remaining key, 8 bits per pass
+                    unsigned long long prefix = 0, mask = 0;
+                    for (int shift = 56; shift >= 0; shift -= 8) {
+                        for (int i = tid; i < n; i += NMS_THREADS) {
+                            const unsigned long long kk = gk[i];
+                            if (kk < hi && (kk & mask) == prefix) atomicAdd(&s_hist[(kk >> shift) & 255], 1u);
+                        }
+                        __syncthreads();
+                        if (tid == 0) {
+                            int need = s_k, dsel = 0;
+                            for (int dg = 255; dg >= 0; --dg) {
+                                const int h = (int)s_hist[dg];
+                                if (h >= need) {
+                                    dsel = dg;
+                                    break;
+                                }
+                                need -= h;
+                            }
+                            s_k = need;
+                            s_T = prefix | ((unsigned long long)dsel << shift);
+                        }
+                        __syncthreads();
+                        prefix = s_T;
+                        mask |= 0xFFull << shift;
+                        for (int i = tid; i < 256; i += NMS_THREADS) s_hist[i] = 0;
+                        __syncthreads();
                     }
                 }
+                const unsigned long long T = rem > NMS_CAP ? s_T : 0ull;
+                if (tid == 0) s_m = 0;
                 __syncthreads();
+                for (int i = tid; i < n; i += NMS_THREADS) {
+                    const unsigned long long kk = gk[i];
+                    if (kk >= T && kk < hi) sk[atomicAdd(&s_m, 1)] = kk;
+                }
+                __syncthreads();
+                nb = s_m;
+                hi = T;
             }
-        for (int c0 = 0; c0 < n; c0 += NMS_CH) {
+            int P = 2;
+            while (P < nb) P <<= 1;
+            for (int i = tid; i < P; i += NMS_THREADS)
+                if (big ? i >= nb : true) sk[i] = i < nb ? key_of(i) : 0ull;
+            __syncthreads();
+            for (int k = 2; k <= P; k <<= 1)
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int t = tid; t < P / 2; t += NMS_THREADS) {
+                        const int i = 2 * j * (t / j) + (t % j), l = i + j;
+                        const unsigned long long x = sk[i], y = sk[l];
+                        if ((i & k) == 0 ? x < y : x > y) {
+                            sk[i] = y;
+                            sk[l] = x;
+                        }
+                    }
+                    __syncthreads();
+                }
+        for (int c0 = 0; c0 < nb; c0 += NMS_CH) {
             const int kept = s_kept;
             if (kept >= max_det) break;  // uniform
-            const int m = min(NMS_CH, n - c0);
+            const int m = min(NMS_CH, nb - c0);
             if (tid < NMS_CH) {
                 sup[tid] = tid < m ? 0 : 1;
                 if (tid < m) {
@@ -281,6 +347,8 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 s_kept = kk;
             }
             __syncthreads();
+        }
+            if (!big || s_kept >= max_det || hi == 0ull) break;  // uniform
         }
         if (tid == 0) ndet[b] = s_kept;
         return;
