@@ -53,6 +53,9 @@ def parse():
                         "GPU-side packet; sampling keeps their cost out of the other steps)")
     p.add_argument("--no-overlap", action="store_true",
                    help="serial steps (no overlap of batch k's grid stage with batch k+1's network)")
+    p.add_argument("--pipelines", type=int, default=3,
+                   help="batches in flight (buffer sets): 3 lets batch k+2's network be enqueued before the "
+                        "host blocks in batch k's grid stage")
     p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2],
                    help="network streams of the overlapped pipeline (2: consecutive forwards run concurrently)")
     return p.parse_args()
@@ -132,7 +135,8 @@ def main():
     B, H, W = args.batch, args.res, args.res
     overlap = not args.no_overlap
     if overlap:
-        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev, seg_streams=args.seg_streams)
+        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev, seg_streams=args.seg_streams,
+                                    depth=args.pipelines)
         pipe = opipe.a
     else:
         pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
@@ -171,13 +175,15 @@ def main():
                 res = step(s)
                 rounds += res.rounds
             return rounds, res
-        sample(0)
-        opipe.submit(frames[0], pcs[0], prs[0], PLANT_IF_NONE)
+        ahead = opipe.depth - 1  # batches enqueued beyond the one whose grid stage runs next
+        for s in range(min(ahead, n)):
+            sample(s)
+            opipe.submit(frames[s % P], pcs[s % P], prs[s % P], PLANT_IF_NONE)
         for s in range(n):
-            if s + 1 < n:
-                sample(s + 1)
-                opipe.submit(frames[(s + 1) % P], pcs[(s + 1) % P], prs[(s + 1) % P], PLANT_IF_NONE)
-            res = opipe.finish(opipe.k - (2 if s + 1 < n else 1))
+            if s + ahead < n:
+                sample(s + ahead)
+                opipe.submit(frames[(s + ahead) % P], pcs[(s + ahead) % P], prs[(s + ahead) % P], PLANT_IF_NONE)
+            res = opipe.finish(s)
             rounds += res.rounds
         return rounds, res
 
@@ -297,7 +303,8 @@ def main():
                                    "penalty/protrusion/A* on GPU, end-to-end",
                        "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
                        "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",
-                       "overlap": (f"{args.seg_streams} network stream(s): consecutive forwards run concurrently; "
+                       "overlap": (f"{args.seg_streams} network stream(s), {args.pipelines} batches in flight: "
+                                   "consecutive forwards run concurrently; "
                                    "grid stage of batch k on its own stream under the following networks")
                        if overlap else "none",
                        "gflop_per_frame": round(gflop, 2),

@@ -138,3 +138,41 @@ def test_pipeline_medium_1280_planted_nav_matches_oracle():
         out = onav.frame_nav(cells_to_mask(g), cells_rect(g), H, W, pf)
         nf = res.frame(i)
         assert [q["path"] for q in nf.queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_overlapped_pipelines_match_sequential(depth):
+    """bench.py's overlapped form (two network streams, `depth` batches in flight, grid stage in submission
+    order on its own stream) gives the sequential pipeline's nav answers batch by batch, with the angle
+    cache advancing in the same order."""
+    from workloads.corridors import cells_rect, corridor_cells
+    from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("n")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0))
+    B, nb = 4, 5
+    batches = []
+    for k in range(nb):
+        grids = [corridor_cells(900 + 10 * k + i) for i in range(B)]
+        batches.append((torch.randint(0, 256, (B, 640, 640, 3), generator=torch.Generator().manual_seed(k),
+                                      dtype=torch.uint8).cuda(),
+                        torch.tensor(np.stack(grids).astype(np.uint8)).cuda(),
+                        torch.tensor(np.array([cells_rect(g) for g in grids], dtype=np.int32)).cuda()))
+    seq = FramePipeline(arch, fw, B, 640, 640, dtype="bf16")
+    want = []
+    for fr, pc, pr in batches:
+        res = seq.run(fr, pc, pr, PLANT_ALWAYS)
+        want.append([[q["path"] for q in res.frame(i).queries] for i in range(B)])
+    ov = OverlappedPipelines(arch, fw, B, 640, 640, dtype="bf16", depth=depth)
+    got = []
+    ahead = depth - 1
+    for s in range(min(ahead, nb)):
+        ov.submit(*batches[s], PLANT_ALWAYS)
+    for s in range(nb):
+        if s + ahead < nb:
+            ov.submit(*batches[s + ahead], PLANT_ALWAYS)
+        res = ov.finish(s)
+        got.append([[q["path"] for q in res.frame(i).queries] for i in range(B)])
+    assert got == want
+    assert ov.a.seen.keys() == seq.seen.keys()

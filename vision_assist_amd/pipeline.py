@@ -62,41 +62,52 @@ class FramePipeline:
 
 
 class OverlappedPipelines:
-    """Two FramePipelines sharing weights and the angle cache.  Each has its own network stream, so two
-    consecutive batches' forwards run concurrently and fill each other's kernel tails and launch gaps;
-    the grid stage (a few hundred waves: A* is a chain of dependent pops) runs on a third stream, in
-    submission order, so batches leave in order and the angle cache advances in order."""
+    """`depth` FramePipelines sharing weights and the angle cache, fed round-robin.  Consecutive batches'
+    networks alternate between two network streams, so two forwards run concurrently and fill each other's
+    kernel tails and launch gaps; the grid stage (a few hundred waves: A* is a chain of dependent pops) runs
+    on its own stream, in submission order, so batches leave in order and the angle cache advances in
+    order.  A pipeline's buffers are reused only after its previous batch has left the grid stage; with
+    depth 3 the host can enqueue batch k+2's network before it blocks in batch k's grid stage (whose A*
+    rounds read a device flag), so the GPU always holds two networks."""
 
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", device=None,
-                 seg_streams: int = 2, **kw):
-        self.a = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, tag=0, **kw)
-        self.b = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=self.a.device, seen=self.a.seen,
-                               seg=self.a.seg, tag=1, **kw)
-        self.pipes = (self.a, self.b)
-        s0 = torch.cuda.Stream(device=self.a.device)
-        self.s_segs = (s0, torch.cuda.Stream(device=self.a.device) if seg_streams == 2 else s0)
-        self.s_nav = torch.cuda.Stream(device=self.a.device)
-        self.ev = [torch.cuda.Event(), torch.cuda.Event()]
+                 seg_streams: int = 2, depth: int = 2, **kw):
+        if depth < 2:
+            raise ValueError("depth >= 2")
+        first = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, tag=0, **kw)
+        self.pipes = [first] + [FramePipeline(arch, folded, B, H, W, dtype=dtype, device=first.device,
+                                              seen=first.seen, seg=first.seg, tag=i, **kw) for i in range(1, depth)]
+        self.a, self.b = self.pipes[0], self.pipes[1]
+        self.depth = depth
+        s0 = torch.cuda.Stream(device=first.device)
+        self.s_segs = (s0, torch.cuda.Stream(device=first.device) if seg_streams == 2 else s0)
+        self.s_nav = torch.cuda.Stream(device=first.device)
+        self.ev = [torch.cuda.Event() for _ in range(depth)]        # network + post of the pipeline's batch
+        self.nav_done = [torch.cuda.Event() for _ in range(depth)]  # its grid stage
         self.k = 0
 
     def submit(self, frames: torch.Tensor, plant_cells=None, plant_rects=None, plant_mode: int = PLANT_NEVER):
-        """Enqueue copy + network + post-processing of the next batch on its pipeline's network stream."""
-        p = self.pipes[self.k % 2]
+        """Enqueue copy + network + post-processing of the next batch on its network stream."""
+        i = self.k % self.depth
+        p = self.pipes[i]
         s_seg = self.s_segs[self.k % 2]
         s_seg.wait_stream(torch.cuda.current_stream())
-        s_seg.wait_stream(self.s_nav)  # the pipeline's previous batch has left its grid stage (buffer reuse)
+        s_seg.wait_event(self.nav_done[i])  # the pipeline's previous batch has left its grid stage
         with torch.cuda.stream(s_seg):
             p.frames.copy_(frames, non_blocking=True)
             p.seg_post(plant_cells, plant_rects, plant_mode, stream=s_seg)
-            self.ev[self.k % 2].record(s_seg)
+            self.ev[i].record(s_seg)
         self.k += 1
 
     def finish(self, j: int) -> NavBatch:
         """Run the grid stage of submitted batch j (in submission order) on the nav stream."""
-        p = self.pipes[j % 2]
-        self.s_nav.wait_event(self.ev[j % 2])
+        i = j % self.depth
+        p = self.pipes[i]
+        self.s_nav.wait_event(self.ev[i])
         with torch.cuda.stream(self.s_nav):
-            return p.nav_run(stream=self.s_nav)
+            res = p.nav_run(stream=self.s_nav)
+            self.nav_done[i].record(self.s_nav)
+        return res
 
 
 __all__ = ["FramePipeline", "OverlappedPipelines", "PLANT_IF_NONE", "PLANT_NEVER"]
