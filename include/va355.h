@@ -306,7 +306,19 @@ typedef struct va_post_args {
     uint8_t* cells;             /* out [B][H/20][W/20] or NULL (skip the mask choice) */
     int32_t* rects;             /* out [B][4] */
     int32_t* chosen;            /* out [B]: chosen detection, -1 none, -2 planted */
+    /* LetterBox (Ultralytics predict preprocess, replaced by va_letterbox): cells / rects refer to the
+     * H0 x W0 frame, network pixel = frame pixel * gain + (pad_x, pad_y); polygon coordinates are mapped
+     * back as scale_coords does.  H0 = 0: the network input is the frame (identity). */
+    int32_t H0, W0, pad_x, pad_y;
+    float gain;
 } va_post_args;
+
+/* LetterBox(new_shape, auto=True, stride 32) of uint8 BGR frames [B][H][W][3] into [B][Hn][Wn][3]:
+ * bilinear resize to newh x neww (cv2.INTER_LINEAR fixed-point form; a copy when the size is unchanged)
+ * placed at (top, left), the border filled with 114.  Replaces the LetterBox call inside YOLO.predict
+ * (FrameProcessor.py:322; Ultralytics data/augment.py LetterBox). */
+int va_letterbox(void* stream, const uint8_t* src, int32_t B, int32_t H, int32_t W, uint8_t* dst, int32_t Hn,
+                 int32_t Wn, int32_t top, int32_t left, int32_t newh, int32_t neww);
 
 /* Number of anchors A for an H x W input (strides 8, 16, 32), or < 0. */
 int va_post_anchors(int32_t H, int32_t W);

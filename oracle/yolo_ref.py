@@ -23,12 +23,46 @@ vendored spec copies in the reference:
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
 REG_MAX = 16
 STRIDES = (8, 16, 32)
 MAX_WH = 7680
+
+
+def letterbox_np(frame_bgr_u8: np.ndarray, Hn: int, Wn: int, top: int, left: int, newh: int, neww: int) -> np.ndarray:
+    """Ultralytics LetterBox (data/augment.py, restated; Ultralytics and OpenCV are absent, so parity with
+    cv2.resize is unpinned): cv2.INTER_LINEAR on uint8 in its fixed-point form -- per axis
+    src = (d + 0.5) * (in / out) - 0.5 in float32, clamped at the borders, weights round((1 - f) * 2048) and
+    2048 - that, (sum w_y w_x p + 2^21) >> 22 -- placed at (top, left) on a 114 border."""
+    H, W, _ = frame_bgr_u8.shape
+    out = np.full((Hn, Wn, 3), 114, dtype=np.uint8)
+    if (newh, neww) == (H, W):
+        out[top:top + H, left:left + W] = frame_bgr_u8
+        return out
+
+    def coef(n_out, n_in):
+        inv = np.float32(n_in) / np.float32(n_out)
+        f = (np.arange(n_out, dtype=np.float32) + np.float32(0.5)) * inv - np.float32(0.5)
+        s = np.floor(f).astype(np.int64)
+        f = (f - s.astype(np.float32)).astype(np.float32)
+        lo = s < 0
+        s[lo], f[lo] = 0, 0
+        hi = s >= n_in - 1
+        s[hi], f[hi] = n_in - 1, 0
+        w0 = np.rint((np.float32(1.0) - f) * np.float32(2048.0)).astype(np.int64)
+        return s, np.minimum(s + 1, n_in - 1), w0
+
+    x0, x1, wx0 = coef(neww, W)
+    y0, y1, wy0 = coef(newh, H)
+    src = frame_bgr_u8.astype(np.int64)
+    h0 = src[y0][:, x0] * wx0[None, :, None] + src[y0][:, x1] * (2048 - wx0)[None, :, None]
+    h1 = src[y1][:, x0] * wx0[None, :, None] + src[y1][:, x1] * (2048 - wx0)[None, :, None]
+    v = (h0 * wy0[:, None, None] + h1 * (2048 - wy0)[:, None, None] + (1 << 21)) >> 22
+    out[top:top + newh, left:left + neww] = np.clip(v, 0, 255).astype(np.uint8)
+    return out
 
 
 def preprocess(frames_bgr_u8: torch.Tensor) -> torch.Tensor:

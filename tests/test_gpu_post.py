@@ -176,3 +176,93 @@ def test_overlapped_pipelines_match_sequential(depth):
         got.append([[q["path"] for q in res.frame(i).queries] for i in range(B)])
     assert got == want
     assert ov.a.seen.keys() == seq.seen.keys()
+
+
+@pytest.mark.parametrize("H0,W0", [(720, 1280), (480, 848)])
+def test_letterbox_kernel_matches_restatement(H0, W0):
+    import ctypes  # noqa: F401
+    from vision_assist_amd import _lib
+    from vision_assist_amd.post import letterbox_geometry
+    lib = _lib.load()
+    Hn, Wn, top, left, newh, neww, _g, _px, _py = letterbox_geometry(H0, W0)
+    B = 2
+    fr = torch.randint(0, 256, (B, H0, W0, 3), generator=torch.Generator().manual_seed(H0), dtype=torch.uint8)
+    out = torch.empty((B, Hn, Wn, 3), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.va_letterbox(_lib.stream_ptr(), fr.cuda().data_ptr(), B, H0, W0, out.data_ptr(), Hn, Wn, top, left,
+                                newh, neww), "va_letterbox")
+    torch.cuda.synchronize()
+    for b in range(B):
+        want = Y.letterbox_np(fr[b].numpy(), Hn, Wn, top, left, newh, neww)
+        assert np.array_equal(out[b].cpu().numpy(), want)
+
+
+def test_letterboxed_mask_choice_in_frame_coordinates():
+    """720 x 1280 frame -> 384 x 640 network input: the chosen mask's cells and boundingRect come back in frame
+    coordinates (cell centre (X, Y) -> network pixel (X * gain + pad_x, Y * gain + pad_y); rect corners
+    (v - pad) / gain, clipped, truncated -- scale_coords), against the oracle on the same head outputs."""
+    from vision_assist_amd import _lib
+    from vision_assist_amd.post import PostEngine, letterbox_geometry
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    H0, W0 = 720, 1280
+    Hn, Wn, top, left, newh, neww, gain, px, py = letterbox_geometry(H0, W0)
+    arch = Arch("s")
+    fw = fold(arch, synthetic_state_dict(arch, seed=3, cls_bias=0.0))
+    net = SegNet(arch, fw, dtype="f32")
+    fr = torch.randint(0, 256, (1, H0, W0, 3), generator=torch.Generator().manual_seed(8), dtype=torch.uint8)
+    x = torch.empty((1, Hn, Wn, 3), dtype=torch.uint8, device="cuda")
+    lib = _lib.load()
+    _lib.check(lib.va_letterbox(_lib.stream_ptr(), fr.cuda().data_ptr(), 1, H0, W0, x.data_ptr(), Hn, Wn, top, left,
+                                newh, neww), "va_letterbox")
+    out = net.forward(x)
+    post = PostEngine(1, Hn, Wn, arch.nc, frame=(H0, W0, gain, px, py))
+    post.run(out.levels, out.proto)
+    torch.cuda.synchronize()
+    lv = torch.cat([t.cpu().flatten(1, 2) for t in out.levels], 1).permute(0, 2, 1)
+    box, cls, coef = lv[:, :64], lv[:, 64:64 + arch.nc], lv[:, 64 + arch.nc:]
+    proto = out.proto.cpu().permute(0, 3, 1, 2)
+    pred = Y.decode(box, cls, Hn, Wn)
+    det = Y.nms_image(pred[0], coef[0])
+    assert det.shape[0] > 0, "regime produced no detection"
+    masks = Y.process_mask(proto[0], det[:, 6:], det[:, :4], Hn, Wn)
+    m, (rx, ry, rw, rh) = Y.select_mask(masks)
+    assert m is not None
+    LR, LC = H0 // 20, W0 // 20
+    yy = np.floor((np.arange(LR) * 20 + 10) * gain + py).astype(int)
+    xx = np.floor((np.arange(LC) * 20 + 10) * gain + px).astype(int)
+    cells_ref = m.numpy()[yy][:, xx]
+    cells_gpu = post.cells[0].cpu().numpy()
+    assert cells_gpu.shape == (LR, LC)
+    assert (cells_ref != cells_gpu).sum() <= 1
+
+    def fx(v, pad, lim):
+        return int(min(max((v - pad) / gain, 0.0), lim))
+    x0, x1 = fx(rx, px, W0), fx(rx + rw - 1, px, W0)
+    y0, y1 = fx(ry, py, H0), fx(ry + rh - 1, py, H0)
+    got = [int(v) for v in post.rects[0].cpu()]
+    want = [x0, y0, x1 - x0 + 1, y1 - y0 + 1]
+    assert max(abs(g - w) for g, w in zip(got, want)) <= 2, (got, want)
+
+
+def test_pipeline_720x1280_frames_letterboxed_nav_matches_oracle():
+    """Camera-size frames (720 x 1280, not multiples of 32) run through the letterboxed fused batch; with planted
+    36 x 64-cell corridors the grid / A* outputs are the oracle's at frame resolution."""
+    from oracle import nav as onav
+    from workloads.corridors import cells_rect, cells_to_mask, corridor_cells
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("s")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0))
+    B, H, W = 3, 720, 1280
+    pipe = FramePipeline(arch, fw, B, H, W, dtype="bf16")
+    assert (pipe.Hn, pipe.Wn) == (384, 640)
+    grids = [corridor_cells(8100 + i, H // 20, W // 20) for i in range(B)]
+    pc = torch.tensor(np.stack(grids).astype(np.uint8)).cuda()
+    pr = torch.tensor(np.array([cells_rect(g) for g in grids], dtype=np.int32)).cuda()
+    frames = torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(4), dtype=torch.uint8).cuda()
+    res = pipe.run(frames, pc, pr, PLANT_ALWAYS)
+    pf = onav.PathFinderOracle()
+    for i, g in enumerate(grids):
+        out = onav.frame_nav(cells_to_mask(g), cells_rect(g), H, W, pf)
+        assert [q["path"] for q in res.frame(i).queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]

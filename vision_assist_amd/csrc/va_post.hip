@@ -420,6 +420,8 @@ struct MaskArgs {
     const va_det* dets;
     const int32_t* ndet;
     va_mask_stat* stats;  // [B][max_det]
+    int H0, W0, pad_x, pad_y;  // letterbox (va_post_args): H0 = 0 identity
+    float gain;
 };
 
 __device__ inline const float* coef_of(const MaskArgs& a, int b, int anchor) {
@@ -623,7 +625,10 @@ __device__ float mask_value_at(const MaskArgs& a, int b, const va_det& d, const 
 __global__ void post_select_kernel(MaskArgs a, const uint8_t* plant_cells, const int32_t* plant_rects,
                                    int plant_mode, uint8_t* cells, int32_t* rects, int32_t* chosen) {
     const int b = blockIdx.x, tid = threadIdx.x;
-    const int LR = a.H / VA_GRID, LC = a.W / VA_GRID;
+    const bool lb = a.H0 > 0;  // letterboxed: cells / rects in frame coordinates
+    const int H0 = lb ? a.H0 : a.H, W0 = lb ? a.W0 : a.W;
+    const float gain = lb ? a.gain : 1.0f, px = lb ? (float)a.pad_x : 0.0f, py = lb ? (float)a.pad_y : 0.0f;
+    const int LR = H0 / VA_GRID, LC = W0 / VA_GRID;
     __shared__ int s_k;
     __shared__ float coef[NMC];
     if (tid == 0) {
@@ -659,14 +664,76 @@ __global__ void post_select_kernel(MaskArgs a, const uint8_t* plant_cells, const
     __syncthreads();
     for (int i = tid; i < LR * LC; i += blockDim.x) {
         int r = i / LC, c = i % LC;
-        out[i] = mask_value_at(a, b, d, coef, VA_GRID * c + VA_GRID / 2, VA_GRID * r + VA_GRID / 2) > 0.f;
+        // the cell centre in network pixels (identity without letterbox)
+        const int X = min(a.W - 1, max(0, (int)floorf((float)(VA_GRID * c + VA_GRID / 2) * gain + px)));
+        const int Y = min(a.H - 1, max(0, (int)floorf((float)(VA_GRID * r + VA_GRID / 2) * gain + py)));
+        out[i] = mask_value_at(a, b, d, coef, X, Y) > 0.f;
     }
     if (tid == 0) {
         const va_mask_stat s = a.stats[(int64_t)b * a.max_det + k];
-        rects[4 * b + 0] = s.x0;
-        rects[4 * b + 1] = s.y0;
-        rects[4 * b + 2] = s.x1 - s.x0 + 1;
-        rects[4 * b + 3] = s.y1 - s.y0 + 1;
+        // scale_coords: (network - pad) / gain, clipped to the frame, then np.int32 truncation
+        auto fx = [&](int v) { return (int)fminf(fmaxf(((float)v - px) / gain, 0.0f), (float)W0); };
+        auto fy = [&](int v) { return (int)fminf(fmaxf(((float)v - py) / gain, 0.0f), (float)H0); };
+        const int x0 = lb ? fx(s.x0) : s.x0, x1 = lb ? fx(s.x1) : s.x1;
+        const int y0 = lb ? fy(s.y0) : s.y0, y1 = lb ? fy(s.y1) : s.y1;
+        rects[4 * b + 0] = x0;
+        rects[4 * b + 1] = y0;
+        rects[4 * b + 2] = x1 - x0 + 1;
+        rects[4 * b + 3] = y1 - y0 + 1;
+    }
+}
+
+// LetterBox: one thread per destination pixel (3 bytes).  Resize = cv2.INTER_LINEAR on uint8 in its
+// fixed-point form: per axis src = (d + 0.5) / scale - 0.5, clamped at the borders, weights rounded to
+// 11 bits (w0 = round((1 - f) * 2048), w1 = 2048 - w0); the two passes combine as
+// (sum of w_y * w_x * pixel + 2^21) >> 22.  (OpenCV is absent here: parity with cv2.resize is unpinned.)
+__device__ inline void lin_coef(int d, float inv, int n, int* i0, int* i1, int* w0) {
+    float f = ((float)d + 0.5f) * inv - 0.5f;
+    int s = (int)floorf(f);
+    f -= (float)s;
+    if (s < 0) {
+        s = 0;
+        f = 0.f;
+    }
+    if (s >= n - 1) {
+        s = n - 1;
+        f = 0.f;
+    }
+    *i0 = s;
+    *i1 = min(s + 1, n - 1);
+    *w0 = (int)lrintf((1.0f - f) * 2048.0f);
+}
+
+__global__ void letterbox_kernel(const uint8_t* __restrict__ src, int H, int W, uint8_t* __restrict__ dst, int Hn,
+                                 int Wn, int top, int left, int newh, int neww, int64_t total) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int x = (int)(i % Wn), y = (int)((i / Wn) % Hn), b = (int)(i / ((int64_t)Wn * Hn));
+    uint8_t* o = dst + i * 3;
+    const int ry = y - top, rx = x - left;
+    if (ry < 0 || ry >= newh || rx < 0 || rx >= neww) {
+        o[0] = o[1] = o[2] = 114;
+        return;
+    }
+    const uint8_t* f = src + (int64_t)b * H * W * 3;
+    if (newh == H && neww == W) {
+        const uint8_t* p = f + ((int64_t)ry * W + rx) * 3;
+        o[0] = p[0];
+        o[1] = p[1];
+        o[2] = p[2];
+        return;
+    }
+    int x0, x1, wx0, y0, y1, wy0;
+    lin_coef(rx, (float)W / (float)neww, W, &x0, &x1, &wx0);
+    lin_coef(ry, (float)H / (float)newh, H, &y0, &y1, &wy0);
+    const int wx1 = 2048 - wx0, wy1 = 2048 - wy0;
+    const uint8_t* r0 = f + (int64_t)y0 * W * 3;
+    const uint8_t* r1 = f + (int64_t)y1 * W * 3;
+    for (int c = 0; c < 3; ++c) {
+        const int h0 = r0[x0 * 3 + c] * wx0 + r0[x1 * 3 + c] * wx1;
+        const int h1 = r1[x0 * 3 + c] * wx0 + r1[x1 * 3 + c] * wx1;
+        const int v = (h0 * wy0 + h1 * wy1 + (1 << 21)) >> 22;
+        o[c] = (uint8_t)min(max(v, 0), 255);
     }
 }
 
@@ -675,6 +742,17 @@ int grid1(int64_t n, int t) { return (int)((n + t - 1) / t); }
 }  // namespace
 
 extern "C" {
+
+int va_letterbox(void* stream, const uint8_t* src, int32_t B, int32_t H, int32_t W, uint8_t* dst, int32_t Hn,
+                 int32_t Wn, int32_t top, int32_t left, int32_t newh, int32_t neww) {
+    if (!src || !dst || B <= 0 || H <= 0 || W <= 0 || Hn <= 0 || Wn <= 0 || newh <= 0 || neww <= 0 || top < 0 ||
+        left < 0 || top + newh > Hn || left + neww > Wn)
+        return VA_ERR_ARG;
+    const int64_t total = (int64_t)B * Hn * Wn;
+    hipLaunchKernelGGL(letterbox_kernel, dim3(grid1(total, 256)), dim3(256), 0, (hipStream_t)stream, src, H, W, dst,
+                       Hn, Wn, top, left, newh, neww, total);
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
 
 int va_post_anchors(int32_t H, int32_t W) {
     if (H % 32 || W % 32 || H <= 0 || W <= 0) return VA_ERR_ARG;
@@ -726,10 +804,16 @@ int va_post_run(void* stream, const va_post_args* p) {
     ma.dets = p->dets;
     ma.ndet = p->ndet;
     ma.stats = p->stats;
+    ma.H0 = p->H0;
+    ma.W0 = p->W0;
+    ma.pad_x = p->pad_x;
+    ma.pad_y = p->pad_y;
+    ma.gain = p->gain;
     hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), mask_lds, st, ma);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     if (p->cells) {
-        if (p->H % VA_GRID || p->W % VA_GRID) return VA_ERR_ARG;
+        if (p->H0 > 0 ? (p->H0 % VA_GRID || p->W0 % VA_GRID || !(p->gain > 0.0f)) : (p->H % VA_GRID || p->W % VA_GRID))
+            return VA_ERR_ARG;
         hipLaunchKernelGGL(post_select_kernel, dim3(B), dim3(256), 0, st, ma, p->plant_cells, p->plant_rects,
                            p->plant_mode, p->cells, p->rects, p->chosen);
         if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;

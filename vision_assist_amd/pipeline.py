@@ -13,32 +13,57 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
 from .nav import AngleSeen, NavBatch, NavEngine
-from .post import PLANT_IF_NONE, PLANT_NEVER, PostEngine
+from .post import PLANT_IF_NONE, PLANT_NEVER, PostEngine, letterbox_geometry
 from .seg import SegNet
 
 
 class FramePipeline:
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", conf: float = 0.5,
                  iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None,
-                 seg: SegNet | None = None, tag: int = 0):
+                 seg: SegNet | None = None, tag: int = 0, imgsz: int = 640):
+        """H x W: the frame size.  Frames whose sides are multiples of 32 feed the network as they are (640x640:
+        LetterBox is the identity; 1280x1280 runs the network at 1280, BASELINE.json configs[4]); others are
+        letterboxed to `imgsz` on the device (va_letterbox) as YOLO.predict does, and the mask choice maps
+        back to frame coordinates, so cells / rects / the nav stage stay at H x W."""
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.B, self.H, self.W = B, H, W
+        self.lb = None
+        Hn, Wn, frame = H, W, None
+        if H % 32 or W % 32:
+            Hn, Wn, top, left, newh, neww, gain, pad_x, pad_y = letterbox_geometry(H, W, imgsz)
+            self.lb = (Hn, Wn, top, left, newh, neww)
+            frame = (H, W, gain, pad_x, pad_y)
+        self.Hn, self.Wn = Hn, Wn
         self.seg = seg if seg is not None else SegNet(arch, folded, dtype=dtype, device=self.device)
-        self.plan = self.seg.plan(B, H, W, tag)
-        self.post = PostEngine(B, H, W, arch.nc, conf, iou, max_det, device=self.device)
+        self.plan = self.seg.plan(B, Hn, Wn, tag)
+        self.post = PostEngine(B, Hn, Wn, arch.nc, conf, iou, max_det, device=self.device, frame=frame)
         self.nav = NavEngine(H, W, max_batch=B, device=self.device)
         self.seen = seen if seen is not None else AngleSeen(self.device)
+        self.lib = _lib.load()
 
     @property
     def frames(self) -> torch.Tensor:
-        """The device frame buffer (uint8 [B, H, W, 3]) the forward reads."""
+        """The device buffer (uint8 [B, Hn, Wn, 3]) the forward reads (the letterboxed frames, if any)."""
         return self.plan["frames"]
+
+    def load(self, frames: torch.Tensor, stream=None) -> None:
+        """Frames (uint8 BGR [B, H, W, 3] on the device) into the network's input buffer, letterboxed if needed."""
+        if self.lb is None:
+            self.plan["frames"].copy_(frames, non_blocking=True)
+            return
+        if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
+            raise _lib.VaError(f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
+        frames = frames.to(self.device, non_blocking=True).contiguous()
+        Hn, Wn, top, left, newh, neww = self.lb
+        _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream), frames.data_ptr(), self.B, self.H, self.W,
+                                         self.plan["frames"].data_ptr(), Hn, Wn, top, left, newh, neww), "va_letterbox")
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:
         if frames is not None:
-            self.plan["frames"].copy_(frames, non_blocking=True)
+            self.load(frames, stream)
         self.seg.run_plan(self.plan, stream)
         out = self.plan["out"]
         if plant_mode != PLANT_NEVER and plant_cells is None:
@@ -94,7 +119,7 @@ class OverlappedPipelines:
         s_seg.wait_stream(torch.cuda.current_stream())
         s_seg.wait_event(self.nav_done[i])  # the pipeline's previous batch has left its grid stage
         with torch.cuda.stream(s_seg):
-            p.frames.copy_(frames, non_blocking=True)
+            p.load(frames, stream=s_seg)
             p.seg_post(plant_cells, plant_rects, plant_mode, stream=s_seg)
             self.ev[i].record(s_seg)
         self.k += 1

@@ -25,7 +25,25 @@ class PostArgs(ctypes.Structure):
         ("dets", VOIDP), ("ndet", VOIDP), ("stats", VOIDP),
         ("plant_cells", VOIDP), ("plant_rects", VOIDP),
         ("cells", VOIDP), ("rects", VOIDP), ("chosen", VOIDP),
+        ("H0", ctypes.c_int32), ("W0", ctypes.c_int32), ("pad_x", ctypes.c_int32), ("pad_y", ctypes.c_int32),
+        ("gain", ctypes.c_float),
     ]
+
+
+def letterbox_geometry(H: int, W: int, imgsz: int = 640, stride: int = 32):
+    """Ultralytics LetterBox(new_shape=imgsz, auto=True, scaleup=True, center=True) as YOLO.predict applies
+    it (data/augment.py; restated, Ultralytics is absent) and the matching scale_coords gain / pad:
+    -> (Hn, Wn, top, left, newh, neww, gain, pad_x, pad_y)."""
+    r = min(imgsz / H, imgsz / W)
+    neww, newh = int(round(W * r)), int(round(H * r))
+    dw, dh = (imgsz - neww) % stride, (imgsz - newh) % stride
+    dw, dh = dw / 2, dh / 2
+    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
+    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
+    Hn, Wn = newh + top + bottom, neww + left + right
+    gain = min(Hn / H, Wn / W)  # scale_coords / scale_boxes (ops.py)
+    pad_x, pad_y = int(round((Wn - W * gain) / 2 - 0.1)), int(round((Hn - H * gain) / 2 - 0.1))
+    return Hn, Wn, top, left, newh, neww, gain, pad_x, pad_y
 
 
 PLANT_NEVER, PLANT_IF_NONE, PLANT_ALWAYS = 0, 1, 2
@@ -35,7 +53,9 @@ class PostEngine:
     """Scratch + outputs for B frames of H x W; one ``run`` per batch."""
 
     def __init__(self, B: int, H: int, W: int, nc: int, conf: float = 0.5, iou: float = 0.7, max_det: int = 300,
-                 device=None):
+                 device=None, frame=None):
+        """H x W: the network input.  frame = (H0, W0, gain, pad_x, pad_y) when it is a letterbox of H0 x W0
+        frames: the mask choice then reports cells / rects in frame coordinates."""
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         A = int(self.lib.va_post_anchors(H, W))
@@ -50,7 +70,9 @@ class PostEngine:
         self.dets = torch.empty((B, max_det, 8), dtype=torch.int32, device=dev)  # va_det (5 f32 + 3 i32)
         self.ndet = torch.empty(B, dtype=torch.int32, device=dev)
         self.stats = torch.empty((B, max_det, 8), dtype=torch.int32, device=dev)
-        self.cells = torch.empty((B, H // 20, W // 20), dtype=torch.uint8, device=dev)
+        self.frame = frame
+        H0, W0 = (frame[0], frame[1]) if frame else (H, W)
+        self.cells = torch.empty((B, H0 // 20, W0 // 20), dtype=torch.uint8, device=dev)
         self.rects = torch.empty((B, 4), dtype=torch.int32, device=dev)
         self.chosen = torch.empty(B, dtype=torch.int32, device=dev)
 
@@ -68,6 +90,8 @@ class PostEngine:
             a.plant_cells, a.plant_rects = plant_cells.data_ptr(), plant_rects.data_ptr()
         if select:
             a.cells, a.rects, a.chosen = self.cells.data_ptr(), self.rects.data_ptr(), self.chosen.data_ptr()
+        if self.frame:
+            a.H0, a.W0, a.gain, a.pad_x, a.pad_y = self.frame
         _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream), ctypes.byref(a)), "va_post_run")
 
     def det_tensor(self, b: int) -> torch.Tensor:
