@@ -108,6 +108,29 @@ def test_pathfinder_angle_cache_view():
     assert path_finder.angle_cache == {}
 
 
+def test_call_camera_size_frames_letterboxed():
+    """__call__ on 720 x 1280 frames (the reference fixtures' native size, not multiples of 32): letterboxed to
+    384 x 640 on the device, grids built on the frame's own 36 x 64 lattice."""
+    from vision_assist_amd.FrameProcessor import FrameProcessor
+    from vision_assist_amd.yolo import YOLO
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = YOLO("yolov8s-seg.pt", cls_bias=4.0).to("cuda")
+    fp = FrameProcessor(model=model, verbose=False, debug=False)
+    fp.model = model
+    rng = np.random.default_rng(1)
+    seen_grid = 0
+    for i in range(3):
+        frame = rng.integers(0, 256, (720, 1280, 3), dtype=np.uint8)
+        ans = fp(frame)
+        assert ans == [] or ans in ("move_left", "move_right", "continue_forward")
+        if fp.grids:
+            seen_grid += 1
+            assert all(0 <= g.coords.x < 1280 and 0 <= g.coords.y < 720 for row in fp.grids for g in row)
+    assert seen_grid >= 1
+
+
 def test_call_dense_regime_returns_answer():
     """__call__ on real frames with a network that yields masks (cls bias +4)."""
     from vision_assist_amd.FrameProcessor import FrameProcessor
