@@ -245,7 +245,7 @@ def main():
         achieved = flops_per_launch / avg_launch_s / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 5), "traffic": None,
-                    "kernel": "conv kernels stem/c2f/conv_patch/conv_dn/conv2 (all %d GEMM launches of one YOLOv8-seg forward)"
+                    "kernel": "conv kernels stem/c2f/conv_patch/conv_dn/conv2/conv4/pw (all %d GEMM launches of one YOLOv8-seg forward)"
                               % round(launches_per_step),
                     "flops_per_launch": flops_per_launch, "avg_launch_us": round(avg_launch_s * 1e6, 3),
                     "conv_ms_per_step": round(conv_ms / sampling["n"], 3),
