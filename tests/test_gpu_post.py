@@ -266,3 +266,56 @@ def test_pipeline_720x1280_frames_letterboxed_nav_matches_oracle():
     for i, g in enumerate(grids):
         out = onav.frame_nav(cells_to_mask(g), cells_rect(g), H, W, pf)
         assert [q["path"] for q in res.frame(i).queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]
+
+
+def test_mask_counts_1280_multi_strip():
+    """1280 x 1280 (proto 320 x 320): crop windows up to 320 low-res pixels wide run in several LDS strips of
+    the mask kernel; per-instance pixel counts of the first detections match the oracle's process_mask."""
+    H = W = 1280
+    post, box, cls, coef, proto = _setup(0.0, B=1, H=H, W=W, seed=5, scale="n")
+    pred = Y.decode(box, cls, H, W)
+    det_ref = Y.nms_image(pred[0], coef[0])
+    det_gpu, _anchors = post.det_tensor(0)
+    assert det_gpu.shape[0] == det_ref.shape[0] and det_ref.shape[0] > 0
+    k = min(12, det_ref.shape[0])
+    masks = Y.process_mask(proto[0], det_ref[:k, 6:], det_ref[:k, :4], H, W)
+    cnt_ref = masks.flatten(1).sum(1).long()
+    cnt_gpu = post.stats[0, :k, 0].cpu().long()
+    tol = torch.clamp((cnt_ref.float() * 5e-4).long(), min=2)
+    assert ((cnt_gpu - cnt_ref).abs() <= tol).all(), (cnt_gpu - cnt_ref).abs().max()
+
+
+def test_mask_big_box_many_strips():
+    """A synthetic head with one detection whose box spans ~960 px of a 1280 x 1280 frame: its 240 x 240 low-res
+    crop window needs ten LDS strips of the mask kernel; pixel count and bbox match the oracle's process_mask."""
+    from vision_assist_amd.post import PostEngine
+    H = W = 1280
+    nc, no = 80, 64 + 80 + 32
+    g = torch.Generator().manual_seed(17)
+    levels = []
+    for s in (8, 16, 32):
+        t = torch.zeros(1, H // s, W // s, no)
+        t[..., 64:64 + nc] = -10.0
+        levels.append(t)
+    t = levels[2]
+    t[0, 20, 20, 64 + 3] = 5.0              # one candidate (class 3) at the stride-32 anchor (20, 20)
+    for side in range(4):
+        t[0, 20, 20, side * 16 + 15] = 10.0  # DFL expectation ~15 bins = ~480 px per side
+    t[0, 20, 20, 64 + nc:] = torch.randn(32, generator=g)
+    proto = torch.randn(1, H // 4, W // 4, 32, generator=g)
+    post = PostEngine(1, H, W, nc)
+    post.run([x.cuda().contiguous() for x in levels], proto.cuda().contiguous())
+    torch.cuda.synchronize()
+    lv = torch.cat([x.flatten(1, 2) for x in levels], 1).permute(0, 2, 1)
+    box, cls, coef = lv[:, :64], lv[:, 64:64 + nc], lv[:, 64 + nc:]
+    pred = Y.decode(box, cls, H, W)
+    det_ref = Y.nms_image(pred[0], coef[0])
+    assert det_ref.shape[0] == 1 and int(post.ndet[0]) == 1
+    assert (det_ref[0, 2] - det_ref[0, 0]) > 900
+    m = Y.process_mask(proto[0].permute(2, 0, 1), det_ref[:, 6:], det_ref[:, :4], H, W)[0]
+    st = post.stats[0, 0].cpu()
+    cnt_ref = int(m.sum())
+    assert abs(int(st[0]) - cnt_ref) <= max(2, int(cnt_ref * 5e-4)), (int(st[0]), cnt_ref)
+    ys, xs = torch.nonzero(m, as_tuple=True)
+    want = [int(xs.min()), int(ys.min()), int(xs.max()), int(ys.max())]
+    assert max(abs(int(a) - b) for a, b in zip(st[1:5], want)) <= 1, (st[1:5].tolist(), want)
