@@ -94,6 +94,7 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
     from workloads.corridors import cells_to_mask
     pf = onav.PathFinderOracle()
     n = frames_u8.shape[0]
+    t_grid = 0.0
     t0 = time.perf_counter()
     for i in range(n):
         with torch.no_grad():
@@ -105,9 +106,11 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
             rect = tuple(int(v) for v in plant_rects[i])
         else:
             m = m.numpy()
+        tg = time.perf_counter()
         onav.frame_nav(m, rect, res, res, pf)
+        t_grid += time.perf_counter() - tg
     dt = time.perf_counter() - t0
-    return n / dt, dt
+    return n / dt, dt, 1e3 * t_grid / n
 
 
 def main():
@@ -274,8 +277,9 @@ def main():
         fr_all = torch.cat(frames).cpu().numpy()[:nsamp]
         pc_all = torch.cat(pcs).cpu().numpy()[:nsamp]
         pr_all = torch.cat(prs).cpu().numpy()[:nsamp]
-        fps_cpu, dt = cpu_baseline(arch, fw, fr_all, pc_all, pr_all, args.res)
+        fps_cpu, dt, grid_ms = cpu_baseline(arch, fw, fr_all, pc_all, pr_all, args.res)
         cpu = {"value": round(fps_cpu, 3), "unit": "frames/s", "cores": ncpu, "kind": "port",
+               "grid_stage_ms_per_frame": round(grid_ms, 2),  # pure-python grid/penalty/protrusion/A* (1 core)
                "sample": f"first {nsamp} frames of the resident pool (same frames/masks as the GPU run), {dt:.1f} s: torch fp32 "
                          f"CPU yolov8{args.scale}-seg + decode/NMS/process_mask + pure-python grid/penalty/"
                          f"protrusion/A* restatement (oracle/)"}
