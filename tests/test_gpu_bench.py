@@ -1,0 +1,31 @@
+"""bench.py keeps the driver's contract: one JSON line with the BASELINE.json metric, a positive value, the
+roofline and cpu_baseline objects.  Small run (batch 8, 2 steps) in a child process."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_contract_line():
+    out = subprocess.run([sys.executable, "bench.py", "--batch", "8", "--steps", "2", "--warmup", "1",
+                          "--cpu-sample", "2"], cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        assert d["metric"] == json.load(f)["metric"]
+    assert d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["unit"] == "frames/s" and d["higher_is_better"] is True and d["scaling"] == "weak"
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    c = d["cpu_baseline"]
+    assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1
+    assert d["config"]["workload"].startswith("C3")
