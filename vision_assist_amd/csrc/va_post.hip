@@ -462,8 +462,14 @@ constexpr int MASK_MAX_STRIPS = 128;
 
 // One workgroup per detection.  The low-res crop window of coef . proto is built in LDS one strip of rows
 // at a time (S rows + the next one, S = MASK_STRIP / width - 1), and each strip upsamples the full-res
-// rows whose upper tap falls in it.  Small LDS (strip + row-tap table, ~34 KiB at 640 x 640) keeps four
-// workgroups per CU: the work per detection is short and latency-bound, so concurrency is what counts.
+// rows whose upper tap falls in it.  Work unit = one BLOCK of full-res pixels sharing their four low-res
+// taps (the run of columns with one horizontal tap pair x the run of rows with one vertical pair: 4 x 4
+// inside the map at the x4 upsample).  With one weight of each pair >= 1/2 and both >= 0, four tap values
+// >= 2^-98 blend to > 0 at every pixel of the block and four values <= 0 to <= 0, so a one-sign block is
+// counted whole; only mixed blocks evaluate wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 *
+// v(yb, xa) + wx1 * v(yb, xb)) per pixel, the per-pixel form's exact expression.  Small LDS (strip + run
+// tables, ~27 KiB at 640 x 640) keeps several workgroups per CU: the work per detection is short and
+// latency-bound, so concurrency is what counts.
 __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     const int k = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     if (k >= a.ndet[b]) return;
@@ -473,10 +479,13 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     va_mask_stat* st = a.stats + (int64_t)b * a.max_det + k;
     __shared__ float coef[NMC];
     __shared__ int s_cnt, s_x0, s_x1, s_y0, s_y1;
-    __shared__ int s_rs[MASK_MAX_STRIPS], s_re[MASK_MAX_STRIPS];
-    extern __shared__ __align__(16) int4 mask_smem[];
-    int4* rt = mask_smem;                     // [H]: vertical taps (ya, yb, wy0, wy1) of the window's rows
-    float* tile = (float*)(mask_smem + a.H);  // [S + 1][tw]: one strip of the crop window
+    extern __shared__ __align__(16) int mask_smem_i[];
+    const int MC = a.mw + 4, MR = a.mh + 4;  // run-table capacities (low-res columns / rows)
+    int* cs = mask_smem_i;                   // [MC]: first full-res column whose left tap is xa0 + i
+    int* ce = cs + MC;                       //       one past its last
+    int* rs = ce + MC;                       // [MR]: the same for full-res rows (offsets from Y0)
+    int* re = rs + MR;
+    float* tile = (float*)(re + MR);         // [S + 1][tw]: one strip of the crop window
     if (rx1 < rx0 || ry1 < ry0) {
         if (tid == 0) *st = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
         return;
@@ -485,7 +494,6 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     const int S = MASK_STRIP / tw - 1;  // >= 1: the launcher checks mw <= MASK_STRIP / 2
     const int nstrips = (th + S - 1) / S;
     if (tid < NMC) coef[tid] = coef_of(a, b, d.anchor)[tid];
-    for (int i = tid; i < nstrips; i += MASK_THREADS) s_rs[i] = s_re[i] = 0;
     if (tid == 0) {
         s_cnt = 0;
         s_x0 = a.W;
@@ -498,45 +506,42 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     const int X0 = max(0, (int)((rx0 - 1) / sx) - 2), X1 = min(a.W - 1, (int)((rx1 + 1) / sx) + 2);
     const int Y0 = max(0, (int)((ry0 - 1) / sy) - 2), Y1 = min(a.H - 1, (int)((ry1 + 1) / sy) + 2);
     const int ow = X1 - X0 + 1, oh = Y1 - Y0 + 1;
-    // strip of a full-res row: the one holding its upper tap ya (rows whose taps both miss the crop rows are
-    // 0 everywhere and belong to none); ya is non-decreasing in Y, so every strip owns one run of rows
-    auto strip_of = [&](int ya, int yb) { return (yb < ry0 || ya > ry1) ? -1 : (ya < ry0 ? 0 : (ya - ry0) / S); };
+    int xa0, ya0, xal, yal, u_;
+    float w0_, w1_;
+    taps(X0, sx, a.mw, &xa0, &u_, &w0_, &w1_);
+    taps(Y0, sy, a.mh, &ya0, &u_, &w0_, &w1_);
+    taps(X1, sx, a.mw, &xal, &u_, &w0_, &w1_);
+    taps(Y1, sy, a.mh, &yal, &u_, &w0_, &w1_);
+    const int ncol = xal - xa0 + 1, nrow = yal - ya0 + 1;  // left / upper taps are non-decreasing in X / Y
+    // run tables: the full-res columns (rows) whose left (upper) tap is xa0 + i (ya0 + j)
+    for (int i = tid; i < ncol; i += MASK_THREADS) cs[i] = ce[i] = 0;
+    for (int j = tid; j < nrow; j += MASK_THREADS) rs[j] = re[j] = 0;
     __syncthreads();
-    for (int r = tid; r < oh; r += MASK_THREADS) {
-        int ya, yb;
-        float wy0, wy1;
-        taps(Y0 + r, sy, a.mh, &ya, &yb, &wy0, &wy1);
-        rt[r] = make_int4(ya, yb, __float_as_int(wy0), __float_as_int(wy1));
-        const int kr = strip_of(ya, yb);
-        if (kr < 0) continue;
-        int pa, pb, na, nb;
-        float w0, w1;
-        int kp = -1, kn = -1;
-        if (r > 0) {
-            taps(Y0 + r - 1, sy, a.mh, &pa, &pb, &w0, &w1);
-            kp = strip_of(pa, pb);
-        }
-        if (r + 1 < oh) {
-            taps(Y0 + r + 1, sy, a.mh, &na, &nb, &w0, &w1);
-            kn = strip_of(na, nb);
-        }
-        if (kp != kr) s_rs[kr] = r;
-        if (kn != kr) s_re[kr] = r + 1;
+    for (int x = tid; x < ow; x += MASK_THREADS) {
+        int t0, tp = -1, tn = -1, u;
+        float f0, f1;
+        taps(X0 + x, sx, a.mw, &t0, &u, &f0, &f1);
+        if (x > 0) taps(X0 + x - 1, sx, a.mw, &tp, &u, &f0, &f1);
+        if (x + 1 < ow) taps(X0 + x + 1, sx, a.mw, &tn, &u, &f0, &f1);
+        if (tp != t0) cs[t0 - xa0] = X0 + x;
+        if (tn != t0) ce[t0 - xa0] = X0 + x + 1;
+    }
+    for (int y = tid; y < oh; y += MASK_THREADS) {
+        int t0, tp = -1, tn = -1, u;
+        float f0, f1;
+        taps(Y0 + y, sy, a.mh, &t0, &u, &f0, &f1);
+        if (y > 0) taps(Y0 + y - 1, sy, a.mh, &tp, &u, &f0, &f1);
+        if (y + 1 < oh) taps(Y0 + y + 1, sy, a.mh, &tn, &u, &f0, &f1);
+        if (tp != t0) rs[t0 - ya0] = y;
+        if (tn != t0) re[t0 - ya0] = y + 1;
     }
     const int sub = tid & 7;
     const float4 cq = make_float4(coef[4 * sub], coef[4 * sub + 1], coef[4 * sub + 2], coef[4 * sub + 3]);
     int cnt = 0, bx0 = a.W, bx1 = -1, by0 = a.H, by1 = -1;
-    // one item = one full-res column X over MASK_ROWS consecutive rows of the strip: the horizontal
-    // interpolation of a low-res row pair is shared by every output row with the same vertical taps (4 of
-    // them at the x4 upsample), so each output pixel costs one vertical blend -- the same float expression
-    // as wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 * v(yb, xa) + wx1 * v(yb, xb)) -- and none
-    // when both blended rows have one sign: wy0, wy1 >= 0 with one of them >= 1/2, so two values >= 2^-100
-    // blend to > 0 and two values <= 0 to <= 0, exactly as the full expression would
-    constexpr int MASK_ROWS = 8;
-    constexpr float POS = 7.888609052210118e-31f;  // 2^-100
+    constexpr float POS4 = 3.155443620884047e-30f;  // 2^-98: blended twice it stays >= 2^-100 > 0
     for (int ks = 0; ks < nstrips; ++ks) {
         const int s0 = ry0 + ks * S, s1 = min(s0 + S, ry1);  // crop rows held: s0 .. s1
-        __syncthreads();  // previous strip consumed; strip ranges / coef visible
+        __syncthreads();  // previous strip consumed; run tables / coef visible
         // the strip of coef . proto: 8 lanes per low-res pixel, each one 16-byte run of its 32 channels
         // (a wave reads 8 whole 128-byte pixels, coalesced), partial dots reduced across the 8 lanes
         for (int i = tid >> 3; i < (s1 - s0 + 1) * tw; i += MASK_THREADS / 8) {
@@ -553,43 +558,51 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
             if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
             return tile[(yy - s0) * tw + (xx - rx0)];
         };
-        const int rs = s_rs[ks], nr = s_re[ks] - rs;
-        const int ng = (nr + MASK_ROWS - 1) / MASK_ROWS;
-        for (int i = tid; i < ow * ng; i += MASK_THREADS) {
-            const int X = X0 + i % ow, r0 = rs + (i / ow) * MASK_ROWS;
-            int xa, xb;
-            float wx0, wx1;
-            taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
-            int ca = -1, cb = -1, c = 0, first = -1, last = -1;
-            float ha = 0.f, hb = 0.f;
-            const int rn = min(MASK_ROWS, rs + nr - r0);
-            for (int r = 0; r < rn; ++r) {
-                const int4 t = rt[r0 + r];
-                const int ya = t.x, yb = t.y;
-                if (ya != ca) {
-                    ha = ya == cb ? hb : wx0 * val(ya, xa) + wx1 * val(ya, xb);
-                    ca = ya;
-                }
-                if (yb != cb) {
-                    hb = yb == ca ? ha : wx0 * val(yb, xa) + wx1 * val(yb, xb);
-                    cb = yb;
-                }
-                bool pos;
-                if (ha >= POS && hb >= POS) pos = true;
-                else if (ha <= 0.f && hb <= 0.f) pos = false;
-                else pos = __int_as_float(t.z) * ha + __int_as_float(t.w) * hb > 0.f;
-                if (pos) {
-                    ++c;
-                    if (first < 0) first = r;
-                    last = r;
+        // upper taps this strip owns: s0 .. s0 + S - 1 (strip 0 also the rows above the crop); blocks whose
+        // taps all miss the crop are 0 everywhere (never counted)
+        const int jlo = ks == 0 ? 0 : s0 - ya0, jhi = min(nrow, s0 + S - ya0);
+        const int nj = max(0, jhi - jlo);
+        for (int it = tid; it < ncol * nj; it += MASK_THREADS) {
+            const int i = it % ncol, j = jlo + it / ncol;
+            const int xa = xa0 + i, ya = ya0 + j;
+            const int c0 = cs[i], c1 = ce[i], r0 = rs[j], r1 = re[j];
+            if (c1 <= c0 || r1 <= r0) continue;
+            const int xb = min(xa + 1, a.mw - 1), yb = min(ya + 1, a.mh - 1);
+            if (ya > ry1 || yb < ry0) continue;
+            const float A = val(ya, xa), B = val(ya, xb), C = val(yb, xa), D = val(yb, xb);
+            int c = 0, fx = a.W, lx = -1, fy = a.H, ly = -1;
+            if (A >= POS4 && B >= POS4 && C >= POS4 && D >= POS4) {
+                c = (c1 - c0) * (r1 - r0);
+                fx = c0;
+                lx = c1 - 1;
+                fy = Y0 + r0;
+                ly = Y0 + r1 - 1;
+            } else if (!(A <= 0.f && B <= 0.f && C <= 0.f && D <= 0.f)) {
+                for (int X = c0; X < c1; ++X) {
+                    int ta, tb;
+                    float wx0, wx1;
+                    taps(X, sx, a.mw, &ta, &tb, &wx0, &wx1);
+                    const float ha = wx0 * A + wx1 * B, hb = wx0 * C + wx1 * D;
+                    for (int r = r0; r < r1; ++r) {
+                        int tc, td;
+                        float wy0, wy1;
+                        taps(Y0 + r, sy, a.mh, &tc, &td, &wy0, &wy1);
+                        if (wy0 * ha + wy1 * hb > 0.f) {
+                            ++c;
+                            fx = min(fx, X);
+                            lx = max(lx, X);
+                            fy = min(fy, Y0 + r);
+                            ly = max(ly, Y0 + r);
+                        }
+                    }
                 }
             }
             if (c) {
                 cnt += c;
-                bx0 = min(bx0, X);
-                bx1 = max(bx1, X);
-                by0 = min(by0, Y0 + r0 + first);
-                by1 = max(by1, Y0 + r0 + last);
+                bx0 = min(bx0, fx);
+                bx1 = max(bx1, lx);
+                by0 = min(by0, fy);
+                by1 = max(by1, ly);
             }
         }
     }
@@ -775,7 +788,7 @@ int va_post_run(void* stream, const va_post_args* p) {
     hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, DEC_APB), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
                        p->nc, A, p->conf, p->cand, p->cand_count);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    const size_t mask_lds = (size_t)p->H * 16 + (size_t)MASK_STRIP * 4;
+    const size_t mask_lds = (size_t)2 * (p->W / 4 + 4 + p->H / 4 + 4) * 4 + (size_t)MASK_STRIP * 4;
     if (p->W / 4 > MASK_STRIP / 2 || mask_lds > 160 * 1024 - 2048 ||
         (p->H / 4 + MASK_STRIP / (p->W / 4) - 2) / (MASK_STRIP / (p->W / 4) - 1) > MASK_MAX_STRIPS)
         return VA_ERR_ARG;  // the strips of the widest window must fit the kernel's tables
