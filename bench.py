@@ -1,24 +1,31 @@
 #!/usr/bin/env python
 """bench.py -- frames/s end-to-end (seg + mask + grid + penalty + protrusion + A*) at 640x640 on MI355X.
 
-Workload (BASELINE.json configs[2], "C3"): YOLOv8s-seg, 640x640 frames, bf16 MFMA,
-post-processing, grid/penalty/protrusion/A* on the GPU.  One step = one pass of
-the fused hot path (vision_assist_amd.pipeline.FramePipeline) over one batch of
---batch synthetic frames per GPU (uint8 BGR, resident in HBM before the timed
-region; random-init weights of the yolov8s-seg architecture -- no checkpoints
-exist offline).  Navigation runs on the network's mask when it yields one and on
-a planted mask otherwise (13 reference fixtures resampled to 640x640 + seeded
-procedural corridors); with the default "natural" regime the
-synthetic network yields none, so A* always runs on realistic masks.
+Workload (BASELINE.json configs[2], "C3"): YOLOv8s-seg, 640x640 frames, post-processing,
+grid/penalty/protrusion/A* on the GPU.  The headline runs the network in exact f32 on the
+f32 MFMA (`v_mfma_f32_16x16x4_f32`, an exact f32 fma chain) -- the reference's precision
+(model/runs/segment/train16/args.yaml:43 `half: false`, north_star "logits within 1e-3
+fp32").  The bf16 MFMA pipeline is measured in the same run and reported under "bf16".
 
-Multi-GPU: one process per GPU (torch.distributed.run), frames sharded, no
-collective on the data path; barrier + max-over-ranks timing only.
+One step = one pass of the fused hot path (vision_assist_amd.pipeline) over one batch of
+--batch synthetic frames per GPU (uint8 BGR, resident in HBM before the timed region;
+random-init weights of the yolov8s-seg architecture -- no checkpoints exist offline).
+Navigation runs on the network's mask when it yields one and on a planted mask otherwise
+(13 reference fixtures resampled to 640x640 + seeded procedural corridors);
+with the default "natural" regime the synthetic network yields no detections, so
+post-processing has nothing to keep and A* always runs on the planted masks -- the "dense"
+extra (300 detections per frame) is the post-processing-heavy counterpart.
+
+Multi-GPU: one process per GPU (torch.distributed.run), frames sharded, no collective on the
+data path; a gloo (CPU) process group only for the barrier + max-over-ranks timing.
 
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
+import gc
 import gzip
 import json
 import os
@@ -31,8 +38,10 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak, MI355X_MICROARCH.md chip table
-F32_PEAK_TFLOPS = 157.3
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md chip table
+DEFAULT_BATCH = {"f32": 256, "bf16": 384}     # per-GPU batch (sweeps: DESIGN.md §5)
+PROF_KINDS = 8
+CONV_KINDS = (1, 5, 6, 7)  # va355.h VA_OP_CONV, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM
 
 
 def parse():
@@ -40,17 +49,17 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=384, help="frames per step per GPU (sweep: DESIGN.md §5)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="network arithmetic of the headline")
+    p.add_argument("--batch", type=int, default=0, help="frames per step per GPU (0 = the dtype's default)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
     p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--extras", default="bf16,dense",
+                   help="comma list of extra measurements in the same run: bf16 (the bf16 MFMA pipeline), "
+                        "dense (300 detections per frame); 'none' to skip")
     p.add_argument("--cpu-sample", type=int, default=256,
-                   help="frames timed for the CPU baseline (0 = skip; 256 = the whole resident pool, ~10-15 s)")
-    p.add_argument("--no-prof", action="store_true", help="skip the live per-op HIP-event timing")
-    p.add_argument("--prof-every", type=int, default=4,
-                   help="bracket every op of every N-th timed step's forward with HIP events (each event pair is a "
-                        "GPU-side packet; sampling keeps their cost out of the other steps)")
+                   help="frames timed for the CPU baseline (0 = skip; 256 = ~10-20 s)")
+    p.add_argument("--no-prof", action="store_true", help="skip the HIP-event timing of the isolated forwards")
     p.add_argument("--no-overlap", action="store_true",
                    help="serial steps (no overlap of batch k's grid stage with batch k+1's network)")
     p.add_argument("--pipelines", type=int, default=3,
@@ -88,15 +97,20 @@ def planted_pool(n: int, res: int, seed: int):
 
 def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res: int):
     """The oracle (torch fp32 CPU YOLOv8-seg + post-processing, pure-python grid/A* restatement with the
-    reference's algorithmic structure) on a bounded sample of the same workload."""
+    reference's algorithmic structure, pydantic Path sections/corners and the analyser) on a bounded
+    sample of the same workload.  -> (frames/s, seconds, per-stage ms per frame)."""
     from oracle import nav as onav
     from oracle import yolo_ref as Y
+    from vision_assist_amd.models import Grid, Path
+    from vision_assist_amd.PathAnalyser import PathAnalyser
     from workloads.corridors import cells_to_mask
     pf = onav.PathFinderOracle()
+    analyser = PathAnalyser()
     n = frames_u8.shape[0]
-    t_grid = 0.0
+    stages = {}
     t0 = time.perf_counter()
     for i in range(n):
+        tn = time.perf_counter()
         with torch.no_grad():
             out = Y.predict(arch, fw, torch.from_numpy(frames_u8[i:i + 1]))
         det, masks = out[0]
@@ -106,11 +120,146 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
             rect = tuple(int(v) for v in plant_rects[i])
         else:
             m = m.numpy()
-        tg = time.perf_counter()
-        onav.frame_nav(m, rect, res, res, pf)
-        t_grid += time.perf_counter() - tg
+        stages["network+post"] = stages.get("network+post", 0.0) + time.perf_counter() - tn
+        nav = onav.frame_nav(m, rect, res, res, pf, timings=stages)
+        # FrameProcessor.py:246 Path(...) (sections + corners) for every found path and :349 path_analyser on
+        # the unique ones: the pure-python host classes the product's FrameProcessor surface also runs per
+        # frame (the oracle's cells are re-typed as models.Grid outside the timed span)
+        hits = [q for q in nav["queries"] if q[2]]
+        found = [([Grid(**c.model_dump()) for c in q[2]], q[3]) for q in hits]
+        tp = time.perf_counter()
+        paths = [Path(grids=cells, total_cost=float(cost), path_type="path") for cells, cost in found]
+        if nav["state"].grids:
+            by_list = {id(q[2]): p for q, p in zip(hits, paths)}
+            analyser(res, res, [by_list[id(cells)] for cells, _ in nav["paths"]])
+        stages["path+analyser"] = stages.get("path+analyser", 0.0) + time.perf_counter() - tp
     dt = time.perf_counter() - t0
-    return n / dt, dt, 1e3 * t_grid / n
+    per = {k: round(1e3 * v / n, 3) for k, v in stages.items()}
+    return n / dt, dt, per
+
+
+class Run:
+    """One measured configuration: pipelines, resident inputs and the timed steps."""
+
+    def __init__(self, args, dev, rank, dtype, B, regime):
+        from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
+        from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+        self.args, self.dtype, self.B, self.regime = args, dtype, B, regime
+        cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0}[regime]
+        self.arch = Arch(args.scale)
+        self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, cls_bias=cls_bias))
+        H = W = args.res
+        self.overlap = not args.no_overlap
+        if self.overlap:
+            self.opipe = OverlappedPipelines(self.arch, self.fw, B, H, W, dtype=dtype, device=dev,
+                                             seg_streams=args.seg_streams, depth=args.pipelines)
+            self.pipe = self.opipe.a
+        else:
+            self.pipe = FramePipeline(self.arch, self.fw, B, H, W, dtype=dtype, device=dev)
+        # resident inputs: P batches of frames + planted masks, distinct per rank
+        self.P = 4
+        self.frames, self.pcs, self.prs = [], [], []
+        for j in range(self.P):
+            rng = np.random.default_rng(1000 * rank + j)
+            self.frames.append(torch.from_numpy(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)).to(dev))
+            c, r = planted_pool(B, args.res, 1000 * rank + j)
+            self.pcs.append(torch.from_numpy(c).to(dev))
+            self.prs.append(torch.from_numpy(r).to(dev))
+        torch.cuda.synchronize()
+
+    def steps(self, n):
+        """n steps; overlapped: batch s+1's network is enqueued before batch s's grid stage runs."""
+        from vision_assist_amd.post import PLANT_IF_NONE
+        P, rounds, res = self.P, 0, None
+        if not self.overlap:
+            for s in range(n):
+                res = self.pipe.run(self.frames[s % P], self.pcs[s % P], self.prs[s % P], PLANT_IF_NONE)
+                rounds += res.rounds
+            return rounds, res
+        op = self.opipe
+        ahead = op.depth - 1
+        for s in range(min(ahead, n)):
+            op.submit(self.frames[s % P], self.pcs[s % P], self.prs[s % P], PLANT_IF_NONE)
+        for s in range(n):
+            if s + ahead < n:
+                k = s + ahead
+                op.submit(self.frames[k % P], self.pcs[k % P], self.prs[k % P], PLANT_IF_NONE)
+            res = op.finish(s)
+            rounds += res.rounds
+        return rounds, res
+
+    def measure(self, steps, warmup, world, prof=True) -> dict:
+        from vision_assist_amd import _lib
+        from vision_assist_amd.shard import timed
+        args, B, H = self.args, self.B, self.args.res
+        self.steps(warmup)
+        torch.cuda.synchronize()
+        if self.overlap:
+            self.opipe.k = 0
+        (rounds, res), elapsed = timed(lambda: self.steps(steps), world, sync=torch.cuda.synchronize)
+        res.host()  # (synchronised snapshot of the last batch's records)
+        paths = sum(1 for i in range(B) for q in res.frame(i).queries if q["unique"])
+        seg = self.pipe.seg
+        gflop_alg = seg.gflop_per_frame(H, H)
+        gflop_exec = seg.plan_gflop(self.pipe.plan)  # per B-frame forward
+        out = {"value": world * B * steps / elapsed, "elapsed": elapsed, "ms_per_step": 1e3 * elapsed / steps,
+               "rounds": rounds / steps, "paths": paths, "gflop_alg": gflop_alg, "gflop_exec": gflop_exec}
+        if prof:
+            out["roofline"] = self.roofline(_lib.load(), gflop_alg, gflop_exec, elapsed, steps)
+        return out
+
+    def roofline(self, lib, gflop_alg, gflop_exec, elapsed, steps) -> dict:
+        """The conv family's average launch duration, measured with HIP events around every op of 3 forwards
+        run ALONE (after the timed region, untimed, on the launch stream): during the timed region two
+        forwards share the chip, so an overlapped launch's event span is not that kernel's duration."""
+        from vision_assist_amd import _lib
+        pipe, B = self.pipe, self.B
+        torch.cuda.synchronize()
+        nfwd = 3
+        _lib.check(lib.va_prof_start(pipe.plan["n"] * nfwd + 16), "va_prof_start")
+        for _ in range(nfwd):
+            pipe.run_seg_only()
+            torch.cuda.synchronize()
+        ms, cnt = (ctypes.c_double * PROF_KINDS)(), (ctypes.c_int64 * PROF_KINDS)()
+        lib.va_prof_stop(ms, cnt, PROF_KINDS)
+        conv_ms, conv_n = sum(ms[k] for k in CONV_KINDS), sum(cnt[k] for k in CONV_KINDS)
+        other_ms = sum(ms[k] for k in range(PROF_KINDS) if k not in CONV_KINDS)
+        launches = conv_n / nfwd
+        fl_exec = gflop_exec * 1e9 / launches
+        fl_alg = gflop_alg * B * 1e9 / launches
+        avg_s = conv_ms / 1e3 / conv_n
+        peak = PEAK_TFLOPS[self.dtype]
+        achieved = fl_exec / avg_s / 1e12
+        rl = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+              "frac": round(achieved / peak, 5), "traffic": None,
+              "kernel": f"the {launches:.0f} conv-family launches of one YOLOv8{self.args.scale}-seg forward "
+                        f"({self.dtype} MFMA GEMM kernels: conv/conv2/conv4/conv_dn/conv_patch/pw/c2f/stem)",
+              "flops_per_launch": round(fl_exec), "flops_per_launch_def": "executed GEMM FLOPs of the plan / launch",
+              "avg_launch_us": round(avg_s * 1e6, 3),
+              "achieved_algorithmic": round(fl_alg / avg_s / 1e12, 2),
+              "flops_per_launch_algorithmic": round(fl_alg),
+              "timing": f"HIP events around every op of {nfwd} forwards run alone after the timed region, on the "
+                        "launch stream (rocprofv3 kernel trace: profiles/)",
+              "forward_ms_isolated": round((conv_ms + other_ms) / nfwd, 3),
+              "conv_ms_per_forward_isolated": round(conv_ms / nfwd, 3),
+              "step_achieved": round(gflop_exec * steps / elapsed / 1e3, 2),
+              "step_achieved_def": "executed conv TFLOP of all timed forwards / timed wall time (per GPU)"}
+        traffic_file = os.path.join(REPO, "profiles", "conv_traffic.json")
+        if os.path.exists(traffic_file):
+            with open(traffic_file) as f:
+                tr = json.load(f)
+            key = f"{self.args.scale}-{self.args.res}-b{B}-{self.dtype}"
+            if key in tr:
+                rl["traffic"] = tr[key]["hbm_bytes_per_launch"]
+                rl["traffic_source"] = f"profiles/conv_traffic.json[{key}] (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
+        return rl
+
+    def release(self):
+        for name in ("opipe", "pipe", "frames", "pcs", "prs"):
+            if hasattr(self, name):
+                delattr(self, name)
+        gc.collect()
+        torch.cuda.empty_cache()
 
 
 def main():
@@ -121,205 +270,96 @@ def main():
     dist = world > 1
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        tdist.init_process_group("gloo")  # barrier + max only: no RCCL communicator on the data path
+    # rank r on GPU r of the node (a 1-GPU rehearsal box shares cuda:0 between ranks)
+    torch.cuda.set_device(local % torch.cuda.device_count() if dist else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
-
-    from vision_assist_amd import _lib
-    from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
-    from vision_assist_amd.post import PLANT_IF_NONE
-    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
-
-    cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0}[args.regime]
-    arch = Arch(args.scale)
-    fw = fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=cls_bias))
-    B, H, W = args.batch, args.res, args.res
-    overlap = not args.no_overlap
-    if overlap:
-        opipe = OverlappedPipelines(arch, fw, B, H, W, dtype=args.dtype, device=dev, seg_streams=args.seg_streams,
-                                    depth=args.pipelines)
-        pipe = opipe.a
-    else:
-        pipe = FramePipeline(arch, fw, B, H, W, dtype=args.dtype, device=dev)
-
-    # resident inputs: P batches of frames + planted masks, distinct per rank
-    P = 4
-    frames, pcs, prs = [], [], []
-    for j in range(P):
-        rng = np.random.default_rng(1000 * rank + j)
-        frames.append(torch.from_numpy(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)).to(dev))
-        c, r = planted_pool(B, args.res, 1000 * rank + j)
-        pcs.append(torch.from_numpy(c).to(dev))
-        prs.append(torch.from_numpy(r).to(dev))
-    torch.cuda.synchronize()
-
-    def step(s):
-        pipe.frames.copy_(frames[s % P], non_blocking=True)
-        return pipe.run(None, pcs[s % P], prs[s % P], PLANT_IF_NONE)
-
-    lib = _lib.load()
-    sampling = {"on": False, "every": max(1, args.prof_every), "n": 0}
-
-    def sample(s):
-        """per-op events on the forward of step s (every prof_every-th step of the timed region)"""
-        if sampling["on"]:
-            on = s % sampling["every"] == 0
-            sampling["n"] += on
-            _lib.check(lib.va_prof_enable(1 if on else 0), "va_prof_enable")
-
-    def run_steps(n):
-        """n steps; overlapped: batch s+1's network is enqueued before batch s's grid stage runs."""
-        rounds, res = 0, None
-        if not overlap:
-            for s in range(n):
-                sample(s)
-                res = step(s)
-                rounds += res.rounds
-            return rounds, res
-        ahead = opipe.depth - 1  # batches enqueued beyond the one whose grid stage runs next
-        for s in range(min(ahead, n)):
-            sample(s)
-            opipe.submit(frames[s % P], pcs[s % P], prs[s % P], PLANT_IF_NONE)
-        for s in range(n):
-            if s + ahead < n:
-                sample(s + ahead)
-                opipe.submit(frames[(s + ahead) % P], pcs[(s + ahead) % P], prs[(s + ahead) % P], PLANT_IF_NONE)
-            res = opipe.finish(s)
-            rounds += res.rounds
-        return rounds, res
-
-    run_steps(args.warmup)
-    torch.cuda.synchronize()
-
+    B = args.batch or DEFAULT_BATCH[args.dtype]
     prof = not args.no_prof
-    if prof:
-        _lib.check(lib.va_prof_start(pipe.plan["n"] * args.steps + 16), "va_prof_start")
-        sampling["on"] = True
-    from vision_assist_amd.shard import timed
 
-    def timed_steps():
-        if overlap:
-            opipe.k = 0
-        return run_steps(args.steps)
-
-    # barrier + device sync on both sides, max of the elapsed time over ranks
-    (rounds, res), elapsed = timed(timed_steps, world, sync=torch.cuda.synchronize)
-    paths = 0
-    conv_ms = conv_n = None
-    if prof:
-        import ctypes
-        ms = (ctypes.c_double * 8)()
-        cnt = (ctypes.c_int64 * 8)()
-        sampling["on"] = False
-        lib.va_prof_stop(ms, cnt, 8)
-        conv_ms, conv_n = ms[1] + ms[5] + ms[6] + ms[7], cnt[1] + cnt[5] + cnt[6] + cnt[7]  # CONV + CONV0 + C2F + STEM
-        other_seg_ms = ms[2] + ms[3] + ms[4]
-        # the same per-op events on 3 forwards run alone (after the timed region, untimed): the kernel's
-        # duration without a concurrent forward sharing the chip
-        torch.cuda.synchronize()
-        _lib.check(lib.va_prof_start(pipe.plan["n"] * 3 + 16), "va_prof_start")
-        for _ in range(3):
-            pipe.run_seg_only()
-            torch.cuda.synchronize()
-        iso_ms, iso_cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
-        lib.va_prof_stop(iso_ms, iso_cnt, 8)
-        iso_conv_ms = iso_ms[1] + iso_ms[5] + iso_ms[6] + iso_ms[7]
-        iso_conv_n = iso_cnt[1] + iso_cnt[5] + iso_cnt[6] + iso_cnt[7]
-    # results sanity (last batch): count frames with >= 1 path
-    last = res
-    for i in range(B):
-        fr = last.frame(i)
-        paths += sum(1 for q in fr.queries if q["unique"])
-
-    frames_total = world * B * args.steps
-    value = frames_total / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
-    gflop = pipe.seg.gflop_per_frame(H, W)
-    gflop_exec = pipe.seg.plan_gflop(next(iter(pipe.seg._plans.values())))  # per B-frame forward
-    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
-    roofline = None
-    if prof and conv_n:
-        launches_per_step = conv_n / sampling["n"]  # per forward (sampled forwards only)
-        # executed GEMM FLOPs of the plan (folded / fused ops counted as run, not the nominal network's)
-        flops_per_launch = gflop_exec * 1e9 / launches_per_step
-        avg_launch_s = conv_ms / 1e3 / conv_n
-        achieved = flops_per_launch / avg_launch_s / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 5), "traffic": None,
-                    "kernel": "conv kernels stem/c2f/conv_patch/conv_dn/conv2/conv4/pw (all %d GEMM launches of one YOLOv8-seg forward)"
-                              % round(launches_per_step),
-                    "flops_per_launch": flops_per_launch, "avg_launch_us": round(avg_launch_s * 1e6, 3),
-                    "conv_ms_per_step": round(conv_ms / sampling["n"], 3),
-                    "other_seg_ops_ms_per_step": round(other_seg_ms / sampling["n"], 3),
-                    "timing": f"HIP events around every op of {sampling['n']} of the {args.steps} timed forwards "
-                              f"(every {sampling['every']}-th), on the launch stream; with {args.seg_streams} network "
-                              "streams consecutive forwards overlap, so a launch's duration includes sharing the chip",
-                    "isolated_achieved": round(flops_per_launch / (iso_conv_ms / 1e3 / iso_conv_n) / 1e12, 2),
-                    "isolated_avg_launch_us": round(iso_conv_ms / iso_conv_n * 1e3, 3),
-                    "isolated_def": "same events on 3 forwards run alone after the timed region (untimed)",
-                    "step_achieved": round(gflop_exec * args.steps / elapsed / 1e3, 2),  # per GPU
-                    "step_achieved_def": "executed conv TFLOP of all timed forwards / timed wall time (whole-step "
-                                         "MFMA throughput, everything else included)"}
-        traffic_file = os.path.join(REPO, "profiles", "conv_traffic.json")
-        if os.path.exists(traffic_file):
-            with open(traffic_file) as f:
-                tr = json.load(f)
-            key = f"{args.scale}-{args.res}-b{B}-{args.dtype}"
-            if key in tr:
-                roofline["traffic"] = tr[key]["hbm_bytes_per_launch"]
-
+    run = Run(args, dev, rank, args.dtype, B, args.regime)
+    main_res = run.measure(args.steps, args.warmup, world, prof)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
+        nsamp = min(args.cpu_sample, run.P * B)
+        fr_all = torch.cat(run.frames).cpu().numpy()[:nsamp]
+        pc_all = torch.cat(run.pcs).cpu().numpy()[:nsamp]
+        pr_all = torch.cat(run.prs).cpu().numpy()[:nsamp]
+        arch, fw = run.arch, run.fw
+    run.release()
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
         ncpu = torch.get_num_threads()
-        nsamp = min(args.cpu_sample, P * B)
-        fr_all = torch.cat(frames).cpu().numpy()[:nsamp]
-        pc_all = torch.cat(pcs).cpu().numpy()[:nsamp]
-        pr_all = torch.cat(prs).cpu().numpy()[:nsamp]
-        fps_cpu, dt, grid_ms = cpu_baseline(arch, fw, fr_all, pc_all, pr_all, args.res)
+        fps_cpu, dt, per_stage = cpu_baseline(arch, fw, fr_all, pc_all, pr_all, args.res)
+        grid_ms = sum(v for k, v in per_stage.items() if k != "network+post")
         cpu = {"value": round(fps_cpu, 3), "unit": "frames/s", "cores": ncpu, "kind": "port",
-               "grid_stage_ms_per_frame": round(grid_ms, 2),  # pure-python grid/penalty/protrusion/A* (1 core)
-               "sample": f"first {nsamp} frames of the resident pool (same frames/masks as the GPU run), {dt:.1f} s: torch fp32 "
-                         f"CPU yolov8{args.scale}-seg + decode/NMS/process_mask + pure-python grid/penalty/"
-                         f"protrusion/A* restatement (oracle/)"}
+               "grid_stage_ms_per_frame": round(grid_ms, 2),  # pure-python grid ... analyser (1 core)
+               "stage_ms_per_frame": per_stage,
+               "sample": f"first {nsamp} frames of the resident pool (same frames/masks as the GPU run), {dt:.1f} s: "
+                         f"torch fp32 CPU yolov8{args.scale}-seg + decode/NMS/process_mask ({ncpu} threads) + "
+                         "pure-python grid/penalty/graph/protrusion/A*/Path sections+corners/analyser restatement "
+                         "(oracle/, 1 core)"}
+
+    extras = {}
+    for ex in [e for e in args.extras.split(",") if e and e != "none"]:
+        if ex == "bf16" and args.dtype != "bf16":
+            dt_, B_, reg_ = "bf16", args.batch or DEFAULT_BATCH["bf16"], args.regime
+        elif ex == "dense" and args.regime != "dense":
+            dt_, B_, reg_ = args.dtype, B, "dense"
+        else:
+            continue
+        r = Run(args, dev, rank, dt_, B_, reg_)
+        m = r.measure(args.steps, min(args.warmup, 3), world, prof)
+        r.release()
+        e = {"value": round(m["value"], 2), "ms_per_step": round(m["ms_per_step"], 3), "dtype": dt_,
+             "batch_per_gpu": B_, "regime": reg_}
+        if prof:
+            rl = m["roofline"]
+            e["roofline"] = {k: rl[k] for k in ("achieved", "peak", "frac", "avg_launch_us", "traffic")}
+        if ex == "bf16":
+            e["parity"] = ("bf16 network: tests/test_gpu_chain.py compares its detections / chosen masks / cells / "
+                           "A* paths with the fp32 oracle chain")
+        extras[ex] = e
 
     if rank == 0:
-        # BASELINE.json configs: C3 (s-seg 640) is the headline; C5's shape (m-seg 1280) runs here with bf16
-        # weights (its fp8 weights are not built), other scale/resolution pairs are labelled custom
-        tag = {("s", 640): "C3", ("m", 1280): "C5 shape (bf16 weights, not fp8)",
+        tag = {("s", 640): "C3", ("m", 1280): "C5 shape (bf16 / f32 weights)",
                ("n", 640): "C2 shape (batched)"}.get((args.scale, args.res), "custom")
+        H = W = args.res
         line = {
             "metric": "frames/sec end-to-end (seg+penalty+A*) at 640×640, 1/2/4/8 MI355X",  # BASELINE.json metric
-            "value": round(value, 2),
+            "value": round(main_res["value"], 2),
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step": round(main_res["ms_per_step"], 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (seeded uint8 frames; random-init yolov8%s-seg weights; planted nav masks when "
                     "the network yields none)" % args.scale,
-            "config": {"workload": f"{tag}: YOLOv8{args.scale}-seg {H}x{W} {args.dtype} + post-processing + grid/"
-                                   "penalty/protrusion/A* on GPU, end-to-end",
+            "config": {"workload": f"{tag}: YOLOv8{args.scale}-seg {H}x{W} {args.dtype} MFMA + post-processing + "
+                                   "grid/penalty/protrusion/A* on GPU, end-to-end"
+                                   + (" (natural regime: the synthetic weights yield no detections, so NMS / masks "
+                                      "keep nothing and A* runs on planted masks; see extras.dense)"
+                                      if args.regime == "natural" else ""),
                        "global_batch": world * B, "batch_per_gpu": B, "seq_len": None, "regime": args.regime,
                        "parallelism": f"frames sharded across {world} GPU(s), one process per GPU, no collective",
                        "overlap": (f"{args.seg_streams} network stream(s), {args.pipelines} batches in flight: "
                                    "consecutive forwards run concurrently; "
                                    "grid stage of batch k on its own stream under the following networks")
-                       if overlap else "none",
-                       "gflop_per_frame": round(gflop, 2),
-                       "gflop_per_frame_executed": round(gflop_exec / B, 2)},
-            "roofline": roofline,
+                       if run.overlap else "none",
+                       "gflop_per_frame": round(main_res["gflop_alg"], 2),
+                       "gflop_per_frame_executed": round(main_res["gflop_exec"] / B, 2)},
+            "roofline": main_res.get("roofline"),
             "cpu_baseline": cpu,
-            "astar_rounds_per_step": round(rounds / args.steps, 3),
-            "unique_paths_last_batch": paths,
+            "extras": extras,
+            "astar_rounds_per_step": round(main_res["rounds"], 3),
+            "unique_paths_last_batch": main_res["paths"],
         }
         print(json.dumps(line), flush=True)
     if dist:
+        tdist.barrier()
         tdist.destroy_process_group()
 
 

@@ -311,7 +311,12 @@ typedef struct va_post_args {
      * back as scale_coords does.  H0 = 0: the network input is the frame (identity). */
     int32_t H0, W0, pad_x, pad_y;
     float gain;
+    /* non_max_suppression's max_nms (ops.py:332-333): a candidate list longer than this is cut to its
+     * max_nms highest scores before NMS.  <= 0: VA_MAX_NMS (Ultralytics' 30000). */
+    int32_t max_nms;
 } va_post_args;
+
+#define VA_MAX_NMS 30000
 
 /* LetterBox(new_shape, auto=True, stride 32) of uint8 BGR frames [B][H][W][3] into [B][Hn][Wn][3]:
  * bilinear resize to newh x neww (cv2.INTER_LINEAR fixed-point form; a copy when the size is unchanged)

@@ -362,13 +362,30 @@ def find_paths(st: GridState, peaks, graph, pf: PathFinderOracle):
     return queries, unique
 
 
-def frame_nav(mask_img: np.ndarray, rect, H: int, W: int, pf: PathFinderOracle) -> dict:
-    """Grid-level part of FrameProcessor.__call__ (FrameProcessor.py:325-347)."""
+def frame_nav(mask_img: np.ndarray, rect, H: int, W: int, pf: PathFinderOracle, timings: dict | None = None) -> dict:
+    """Grid-level part of FrameProcessor.__call__ (FrameProcessor.py:325-347).  ``timings``: if given,
+    per-stage seconds are added to it (grid / penalty / graph / protrusion / astar+paths, the split of
+    SURVEY.md §6 S1)."""
+    import time
+    clk = time.perf_counter
+    t = [clk()]
+
+    def lap(name):
+        if timings is not None:
+            now = clk()
+            timings[name] = timings.get(name, 0.0) + now - t[0]
+            t[0] = now
+
     st = build_grids(mask_img, rect, H, W)
+    lap("grid")
     if not st.grids:
         return {"state": st, "peaks": [], "queries": [], "paths": []}
     compute_penalties(st)
+    lap("penalty")
     graph = create_graph(st)
+    lap("graph")
     peaks = protrusion_peaks(st)
+    lap("protrusion")
     queries, unique = find_paths(st, peaks, graph, pf)
+    lap("astar+paths")
     return {"state": st, "peaks": peaks, "queries": queries, "paths": unique}

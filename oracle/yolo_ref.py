@@ -156,9 +156,12 @@ def decode(box: torch.Tensor, cls: torch.Tensor, H: int, W: int):
     return torch.cat((dbox, cls.sigmoid()), 1)
 
 
-def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: float = 0.7, max_det: int = 300):
+def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: float = 0.7, max_det: int = 300,
+              max_nms: int = 30000):
     """non_max_suppression for one image (ops.py:214-363): pred [4+nc, A], coef [32, A]
-    -> [k, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) in decreasing score order."""
+    -> [k, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) in decreasing score order.
+    max_nms (ops.py:332-333): longer candidate lists keep their max_nms highest scores first (torch's
+    argsort is not stable; ties are kept lowest anchor first here, the order the device kernel uses)."""
     nc = pred.shape[0] - 4
     x = torch.cat((pred, coef), 0).T  # [A, 4+nc+32]
     xc = x[:, 4:4 + nc].amax(1) > conf
@@ -169,6 +172,8 @@ def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: fl
     boxes = torch.cat((xy - wh / 2, xy + wh / 2), 1)
     score, j = x[:, 4:4 + nc].max(1, keepdim=True)
     det = torch.cat((boxes, score, j.float(), x[:, 4 + nc:]), 1)[score.view(-1) > conf]
+    if det.shape[0] > max_nms:
+        det = det[torch.sort(det[:, 4], descending=True, stable=True).indices[:max_nms]]
     keep = greedy_nms(det[:, :4] + det[:, 5:6] * MAX_WH, det[:, 4], iou)[:max_det]
     return det[keep]
 
@@ -227,7 +232,7 @@ def select_mask(masks: torch.Tensor):
     return m, (x0, y0, x1 - x0 + 1, y1 - y0 + 1)
 
 
-def predict(arch, fw, frames_bgr_u8: torch.Tensor, conf=0.5, iou=0.7, max_det=300):
+def predict(arch, fw, frames_bgr_u8: torch.Tensor, conf=0.5, iou=0.7, max_det=300, max_nms=30000):
     """Full segmentation stage for a batch: -> list of (det [k, 38], masks [k, H, W] bool)."""
     B, H, W, _ = frames_bgr_u8.shape
     x = preprocess(frames_bgr_u8)
@@ -235,7 +240,7 @@ def predict(arch, fw, frames_bgr_u8: torch.Tensor, conf=0.5, iou=0.7, max_det=30
     pred = decode(box, cls, H, W)
     out = []
     for b in range(B):
-        det = nms_image(pred[b], coef[b], conf, iou, max_det)
+        det = nms_image(pred[b], coef[b], conf, iou, max_det, max_nms)
         if det.shape[0]:
             masks = process_mask(proto[b], det[:, 6:], det[:, :4], H, W)
         else:

@@ -92,6 +92,38 @@ def test_nms_long_candidate_list_matches_oracle():
     assert torch.allclose(det_gpu[:, 4], det_ref[:, 4], atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("H,max_nms,max_det", [(1280, 20000, 300), (1280, 200, 300), (640, 150, 300),
+                                               (640, 500, 1500)])
+def test_nms_max_nms_truncation_matches_oracle(H, max_nms, max_det):
+    """non_max_suppression's max_nms cut (ops.py:332-333) on long candidate lists: batched sorted path with the
+    cut inside the second batch / inside the first, the cut on a list that fits LDS, and the fallback path
+    (max_det > 1024); same kept detections, in order, as the oracle with the same cut."""
+    from vision_assist_amd.post import PostEngine
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("n")
+    fw = fold(arch, synthetic_state_dict(arch, seed=2, cls_bias=4.0))
+    net = SegNet(arch, fw, dtype="f32")
+    frames = torch.randint(0, 256, (1, H, H, 3), generator=torch.Generator().manual_seed(13), dtype=torch.uint8)
+    out = net.forward(frames.cuda())
+    post = PostEngine(1, H, H, arch.nc, max_det=max_det, max_nms=max_nms)
+    post.run(out.levels, out.proto, select=False)
+    torch.cuda.synchronize()
+    lv = torch.cat([t.cpu().flatten(1, 2) for t in out.levels], 1).permute(0, 2, 1)
+    box, cls, coef = lv[:, :64], lv[:, 64:64 + arch.nc], lv[:, 64 + arch.nc:]
+    pred = Y.decode(box, cls, H, H)
+    n_cand = int((pred[0, 4:].amax(0) > 0.5).sum())
+    assert n_cand > max_nms, n_cand
+    det_ref = Y.nms_image(pred[0], coef[0], max_det=max_det, max_nms=max_nms)
+    assert not torch.equal(det_ref, Y.nms_image(pred[0], coef[0], max_det=max_det, max_nms=10 ** 9)) or \
+        det_ref.shape[0] == max_det, "the cut changes nothing here: pick a smaller max_nms"
+    det_gpu, _ = post.det_tensor(0)
+    assert det_gpu.shape[0] == det_ref.shape[0]
+    assert torch.equal(det_gpu[:, 5], det_ref[:, 5]), "classes / order differ"
+    assert torch.allclose(det_gpu[:, :4], det_ref[:, :4], atol=1e-3, rtol=0)
+    assert torch.allclose(det_gpu[:, 4], det_ref[:, 4], atol=1e-6, rtol=0)
+
+
 def test_pipeline_planted_nav_matches_oracle():
     """Full fused batch (seg + post + nav) with planted corridor masks: the nav outputs are the
     oracle's on the same masks."""
@@ -163,9 +195,9 @@ def test_overlapped_pipelines_match_sequential(depth):
     want = []
     for fr, pc, pr in batches:
         res = seq.run(fr, pc, pr, PLANT_ALWAYS)
-        want.append([[q["path"] for q in res.frame(i).queries] for i in range(B)])
+        want.append([[(q["path"], q["cost"], q["unique"], q["order"]) for q in res.frame(i).queries] for i in range(B)])
     ov = OverlappedPipelines(arch, fw, B, 640, 640, dtype="bf16", depth=depth)
-    got = []
+    got, held = [], []
     ahead = depth - 1
     for s in range(min(ahead, nb)):
         ov.submit(*batches[s], PLANT_ALWAYS)
@@ -173,7 +205,9 @@ def test_overlapped_pipelines_match_sequential(depth):
         if s + ahead < nb:
             ov.submit(*batches[s + ahead], PLANT_ALWAYS)
         res = ov.finish(s)
-        got.append([[q["path"] for q in res.frame(i).queries] for i in range(B)])
+        held.append(res)  # read back only after later batches reuse the pipelines: the records must not change
+    for res in held:
+        got.append([[(q["path"], q["cost"], q["unique"], q["order"]) for q in res.frame(i).queries] for i in range(B)])
     assert got == want
     assert ov.a.seen.keys() == seq.seen.keys()
 

@@ -101,8 +101,12 @@ def nav_dims(H: int, W: int) -> VaNavDims:
     return d
 
 
-def stream_ptr(stream=None) -> int:
-    s = stream if stream is not None else torch.cuda.current_stream()
+def stream_ptr(stream=None, device=None) -> int:
+    """The HIP stream handle to launch on: ``stream``, else the current stream of ``device`` (default: the
+    current device).  Launches go to the current HIP device, so callers run under torch.cuda.device(device)."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    if device is not None and s.device != torch.device(device):
+        raise VaError(f"stream of {s.device} used for work on {device}")
     return int(s.cuda_stream)
 
 

@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 #include "va_fuse.h"
 
 namespace {
@@ -401,12 +402,12 @@ unsigned long long* g_trace = nullptr;
 
 template <class C>
 hipError_t cf_launch(const va_conv_args* a, CfGeom g, int cus, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)c2f_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
             hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     g.tx = (a->W + CF_T - 1) / CF_T;
     g.tpf = g.tx * ((a->H + C::TH - 1) / C::TH);

@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 #include "va_angle_table.h"
 
 #define VA_MAX_LAT 64          // max lattice rows / cols (1280 px)
@@ -878,10 +879,10 @@ __global__ __launch_bounds__(64) void nav_dedupe_kernel(uint8_t* qwork, int64_t 
 }
 
 // ---------------------------------------------------------------------------------------------
-bool g_tables_ready = false;
+DevFlag g_tables_ready;  // the __constant__ tables live in each device's copy of the module
 
 hipError_t ensure_tables() {
-    if (g_tables_ready) return hipSuccess;
+    if (g_tables_ready()) return hipSuccess;
     int8_t prev_idx[49], next_idx[25];
     memset(prev_idx, -1, sizeof prev_idx);
     memset(next_idx, -1, sizeof next_idx);
@@ -891,7 +892,7 @@ hipError_t ensure_tables() {
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_angle_pen), VA_ANGLE_PEN, sizeof VA_ANGLE_PEN)) != hipSuccess) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_prev_idx), prev_idx, sizeof prev_idx)) != hipSuccess) return e;
     if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_next_idx), next_idx, sizeof next_idx)) != hipSuccess) return e;
-    g_tables_ready = true;
+    g_tables_ready() = true;
     return hipSuccess;
 }
 

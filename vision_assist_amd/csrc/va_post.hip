@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 
 namespace {
 
@@ -188,6 +189,46 @@ __device__ inline va_det to_det(const va_cand& k) {
     return d;
 }
 
+// The k-th largest (1-based) of the keys below `hi` (keys unique, at least k of them below hi): an exact
+// 8-pass radix select, one byte per pass, block-wide histograms in LDS.  Every thread of the block calls it.
+__device__ unsigned long long nms_select(const unsigned long long* keys, int n, unsigned long long hi, int k,
+                                         unsigned* s_hist, unsigned long long* s_T, int* s_k) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) {
+        *s_k = k;
+        *s_T = 0;
+    }
+    for (int i = tid; i < 256; i += nt) s_hist[i] = 0;
+    __syncthreads();
+    unsigned long long prefix = 0, mask = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int i = tid; i < n; i += nt) {
+            const unsigned long long kk = keys[i];
+            if (kk < hi && (kk & mask) == prefix) atomicAdd(&s_hist[(kk >> shift) & 255], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int need = *s_k, dsel = 0;
+            for (int dg = 255; dg >= 0; --dg) {
+                const int h = (int)s_hist[dg];
+                if (h >= need) {
+                    dsel = dg;
+                    break;
+                }
+                need -= h;
+            }
+            *s_k = need;
+            *s_T = prefix | ((unsigned long long)dsel << shift);
+        }
+        __syncthreads();
+        prefix = *s_T;
+        mask |= 0xFFull << shift;
+        for (int i = tid; i < 256; i += nt) s_hist[i] = 0;
+        __syncthreads();
+    }
+    return prefix;
+}
+
 // One 1024-thread workgroup per frame.  Sorted path (n <= NMS_CAP, A <= 65536, max_det <= NMS_KEPT_MAX):
 // keys (score bits | ~anchor | list index) bitonic-sorted descending in LDS -- the order the greedy scan
 // visits candidates in (highest score, lowest anchor on ties) -- then 64-candidate chunks: each candidate
@@ -195,8 +236,11 @@ __device__ inline va_det to_det(const va_cand& k) {
 // as one 64-bit ballot per row, and a one-lane scan of the chunk in order.  Same kept set and order as
 // the repeated "highest remaining -> keep -> suppress" loop of the fallback path, which keeps the
 // candidates that do not fit (keys in LDS up to NMS_CAP, else in global scratch).
+// max_nms (ops.py:332-333, 30000): a list longer than that is first cut to its max_nms highest-scoring
+// candidates (ties: lowest anchor first, the order the scan uses) -- the sorted path simply stops taking
+// batches after max_nms keys, the fallback zeroes every key below the max_nms-th.
 __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* cand, const int32_t* count, int A,
-                                                               float iou, int max_det, va_det* dets,
+                                                               float iou, int max_det, int max_nms, va_det* dets,
                                                                int32_t* ndet, unsigned long long* gkeys) {
     extern __shared__ __align__(16) unsigned long long nms_smem[];
     const int b = blockIdx.x, tid = threadIdx.x;
@@ -222,58 +266,28 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
         // lists longer than NMS_CAP run in batches: the NMS_CAP largest keys below the previous batch's
         // smallest (an exact radix select over the keys in global scratch, keys are unique), sorted and
         // scanned like a short list, until max_det boxes are kept or the list is exhausted
-        const bool big = n > NMS_CAP;
+        const bool big = n > NMS_CAP || n > max_nms;  // batches (or the max_nms cut) through global keys
         unsigned long long* gk = gkeys + (int64_t)b * A;
         if (big) {
             for (int i = tid; i < n; i += NMS_THREADS) gk[i] = key_of(i);
         }
         if (tid == 0) s_kept = 0;
         unsigned long long hi = ~0ull;  // exclusive bound of the remaining keys
+        int taken = 0;                  // keys handed to the scan so far (max_nms cap)
         __syncthreads();
         while (true) {
             int nb = n;  // this batch's candidates
             if (big) {
-                if (tid == 0) {
-                    s_m = 0;
-                    s_T = 0;
-                    s_k = NMS_CAP;
-                }
-                for (int i = tid; i < 256; i += NMS_THREADS) s_hist[i] = 0;
+                const int want = min(NMS_CAP, max_nms - taken);
+                if (tid == 0) s_m = 0;
                 __syncthreads();
                 for (int i = tid; i < n; i += NMS_THREADS)
                     if (gk[i] < hi) atomicAdd(&s_m, 1);
                 __syncthreads();
                 const int rem = s_m;
                 __syncthreads();  // everyone has read s_m before it is reused
-                if (rem > NMS_CAP) {  // T = the NMS_CAP-th largest remaining key, 8 bits per pass
-                    unsigned long long prefix = 0, mask = 0;
-                    for (int shift = 56; shift >= 0; shift -= 8) {
-                        for (int i = tid; i < n; i += NMS_THREADS) {
-                            const unsigned long long kk = gk[i];
-                            if (kk < hi && (kk & mask) == prefix) atomicAdd(&s_hist[(kk >> shift) & 255], 1u);
-                        }
-                        __syncthreads();
-                        if (tid == 0) {
-                            int need = s_k, dsel = 0;
-                            for (int dg = 255; dg >= 0; --dg) {
-                                const int h = (int)s_hist[dg];
-                                if (h >= need) {
-                                    dsel = dg;
-                                    break;
-                                }
-                                need -= h;
-                            }
-                            s_k = need;
-                            s_T = prefix | ((unsigned long long)dsel << shift);
-                        }
-                        __syncthreads();
-                        prefix = s_T;
-                        mask |= 0xFFull << shift;
-                        for (int i = tid; i < 256; i += NMS_THREADS) s_hist[i] = 0;
-                        __syncthreads();
-                    }
-                }
-                const unsigned long long T = rem > NMS_CAP ? s_T : 0ull;
+                // T = the want-th largest remaining key
+                const unsigned long long T = rem > want ? nms_select(gk, n, hi, want, s_hist, &s_T, &s_k) : 0ull;
                 if (tid == 0) s_m = 0;
                 __syncthreads();
                 for (int i = tid; i < n; i += NMS_THREADS) {
@@ -283,6 +297,7 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 __syncthreads();
                 nb = s_m;
                 hi = T;
+                taken += nb;
             }
             int P = 2;
             while (P < nb) P <<= 1;
@@ -348,13 +363,16 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
             }
             __syncthreads();
         }
-            if (!big || s_kept >= max_det || hi == 0ull) break;  // uniform
+            if (!big || s_kept >= max_det || hi == 0ull || taken >= max_nms) break;  // uniform
         }
         if (tid == 0) ndet[b] = s_kept;
         return;
     }
     __shared__ unsigned long long red[NMS_THREADS / 64];
     __shared__ int red_i[NMS_THREADS / 64];
+    __shared__ unsigned f_hist[256];
+    __shared__ unsigned long long f_T;
+    __shared__ int f_k;
     // (score bits << 32 | ~anchor): max = highest score, lowest anchor on ties; 0 = kept or suppressed
     unsigned long long* key = n <= NMS_CAP ? nms_smem : gkeys + (int64_t)b * A;
     for (int i = tid; i < n; i += NMS_THREADS) {
@@ -362,6 +380,12 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
         key[i] = ((unsigned long long)sb << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)C[i].anchor);
     }
     __syncthreads();
+    if (n > max_nms) {  // keep the max_nms largest keys (scores > conf > 0, so no key is 0 yet)
+        const unsigned long long T = nms_select(key, n, ~0ull, max_nms, f_hist, &f_T, &f_k);
+        for (int i = tid; i < n; i += NMS_THREADS)
+            if (key[i] < T) key[i] = 0;
+        __syncthreads();
+    }
     int kept = 0;
     while (kept < max_det) {
         unsigned long long best = 0;
@@ -792,15 +816,23 @@ int va_post_run(void* stream, const va_post_args* p) {
     if (p->W / 4 > MASK_STRIP / 2 || mask_lds > 160 * 1024 - 2048 ||
         (p->H / 4 + MASK_STRIP / (p->W / 4) - 2) / (MASK_STRIP / (p->W / 4) - 1) > MASK_MAX_STRIPS)
         return VA_ERR_ARG;  // the strips of the widest window must fit the kernel's tables
-    static size_t mask_attr = 0;
-    if (mask_lds > mask_attr) {
+    static DevVal<size_t> mask_attr;  // per device: the largest dynamic LDS set so far
+    if (mask_lds > mask_attr()) {
         if (hipFuncSetAttribute((const void*)post_mask_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)mask_lds) != hipSuccess)
             return VA_ERR_HIP;
-        mask_attr = mask_lds;
+        mask_attr() = mask_lds;
     }
+    static DevFlag nms_attr;  // post_nms_kernel's 150 KiB of dynamic LDS (set explicitly: graph kernel nodes too)
+    if (!nms_attr()) {
+        if (hipFuncSetAttribute((const void*)post_nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)NMS_LDS) != hipSuccess)
+            return VA_ERR_HIP;
+        nms_attr() = true;
+    }
+    const int max_nms = p->max_nms > 0 ? p->max_nms : VA_MAX_NMS;
     hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), NMS_LDS, st, p->cand, p->cand_count, A, p->iou,
-                       p->max_det, p->dets, p->ndet, p->keys);
+                       p->max_det, max_nms, p->dets, p->ndet, p->keys);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     MaskArgs ma;
     ma.proto = p->proto;

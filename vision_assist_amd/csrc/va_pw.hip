@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 #include "va_fuse.h"
 
 namespace {
@@ -164,12 +165,12 @@ bool va_pw_eligible(const va_conv_args& a) {
 template <int NK, int D>
 hipError_t pw_go(const va_conv_args& a, hipStream_t st, int ntiles, int grid) {
     const int lds = NK * PW_NQ * 1024 + 128 * 4;
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)pw_kernel<NK, D>, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
             hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     hipLaunchKernelGGL((pw_kernel<NK, D>), dim3(grid), dim3(PW_NW * 64), lds, st, a, ntiles);
     return hipGetLastError();

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 #include "va_fuse.h"
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -1721,12 +1722,12 @@ template <int TNS, bool TAIL = false, typename OutT = __bf16>
 hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
     const size_t lds = (size_t)16 * TNS * wstride * 2;
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS, TAIL, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     const int ntiles = (a.M + 63) / 64;
     int blocks = (ntiles + 3) / 4;
@@ -1987,12 +1988,12 @@ bool use_conv3(const va_conv_args& a) {
 
 template <typename OutT, int ABL>
 hipError_t launch_conv3_v(const va_conv_args& a, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv3_kernel<OutT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 C3_LDS) != hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     const int ntm = (a.M + C3_BM - 1) / C3_BM, ntn = (a.Cout + C3_BN - 1) / C3_BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
@@ -2026,12 +2027,12 @@ hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     constexpr int PPI = 64 / CPP, NI = (PW3 * PW3 + PPI - 1) / PPI;
     const int patch_bytes = NI * 1024;
     const size_t lds = (size_t)16 * TNS * wstride * 2 + 2 * (size_t)patch_bytes;
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, ABL>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int tiles_x = (a.Wo + PT - 1) / PT, tiles_y = (a.Ho + PT - 1) / PT;
@@ -2079,12 +2080,12 @@ bool use_wp(const va_conv_args& a) {
 
 template <typename OutT>
 hipError_t launch_conv_wp(const va_conv_args& a, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv_wp_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 WP_LDS) != hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     const int tiles_x = (a.Wo + PT - 1) / PT, tiles_y = (a.Ho + PT - 1) / PT;
     const int ntn = (a.Cout + WP_BN - 1) / WP_BN;
@@ -2109,14 +2110,14 @@ bool use_conv4(const va_conv_args& a) {
 
 template <typename OutT>
 hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
+    static DevFlag attr;
+    if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv4_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * C4_BUF) != hipSuccess ||
             hipFuncSetAttribute((const void*)conv4_kernel<OutT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * C4_BUF) != hipSuccess)
             return hipErrorInvalidValue;
-        attr = true;
+        attr() = true;
     }
     const int ntn = (a.Cout + 255) / 256, ntiles = ntn * ((a.M + 255) / 256);
     if (a.xu)

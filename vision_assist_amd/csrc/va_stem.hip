@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "../../include/va355.h"
+#include "va_dev.h"
 #include "va_fuse.h"
 
 namespace {
@@ -276,13 +277,15 @@ extern "C" int va_seg_stem(void* stream, const va_conv_args* a) {
     const int64_t nt = (int64_t)g.tpf * a->N;
     if (nt > INT32_MAX) return VA_ERR_ARG;
     g.ntiles = (int)nt;
-    if (g_cus == 0) {
+    static DevFlag ready;  // CU count + dynamic-LDS attribute, per device
+    if (!ready()) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
             hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ST_LDS) !=
                 hipSuccess)
             return VA_ERR_HIP;
+        ready() = true;
     }
     int grid = g_cus;
     if (grid > g.ntiles) grid = g.ntiles;

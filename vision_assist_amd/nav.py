@@ -71,21 +71,33 @@ class NavFrame:
 
 
 class NavBatch:
-    def __init__(self, engine: "NavEngine", B: int, rounds: int, queries_off: int):
+    """The records of one va_nav_run.  They are copied to pinned host memory on the stream the run was
+    enqueued on, right behind it (so a later run on the same engine cannot overwrite them first and the host
+    never reads them before the last kernel of the run has finished); ``host()`` waits for that copy."""
+
+    def __init__(self, engine: "NavEngine", B: int, rounds: int, queries_off: int, stream=None):
         self.engine = engine
         self.B = B
         self.rounds = rounds
         self.queries_off = queries_off
+        e = engine
+        st = stream if stream is not None else torch.cuda.current_stream(e.device)
+        nq = B * e.dims.MAXPK * e.dims.query_bytes
+        fr = torch.empty(B * e.dims.frame_bytes, dtype=torch.uint8, pin_memory=True)
+        qs = torch.empty(nq, dtype=torch.uint8, pin_memory=True)
+        with torch.cuda.stream(st):
+            # frames then queries: two contiguous ranges of the workspace
+            fr.copy_(e.work[: B * e.dims.frame_bytes], non_blocking=True)
+            qs.copy_(e.work[queries_off: queries_off + nq], non_blocking=True)
+            self._done = torch.cuda.Event()
+            self._done.record(st)
+        self._pinned = (fr, qs)
         self._host = None
 
     def host(self) -> np.ndarray:
         if self._host is None:
-            e = self.engine
-            # frames then queries: two contiguous ranges of the workspace
-            fr = e.work[: self.B * e.dims.frame_bytes].cpu().numpy()
-            qo = self.queries_off
-            qs = e.work[qo: qo + self.B * e.dims.MAXPK * e.dims.query_bytes].cpu().numpy()
-            self._host = (fr, qs)
+            self._done.synchronize()
+            self._host = (self._pinned[0].numpy(), self._pinned[1].numpy())
         return self._host
 
     def frame(self, i: int) -> NavFrame:
@@ -161,16 +173,19 @@ class NavEngine:
         if tuple(rects.shape) != (B, 4) or rects.dtype != torch.int32 or not rects.is_contiguous():
             raise _lib.VaError("rects must be contiguous int32 [B, 4]")
         rounds = ctypes.c_int32(0)
-        _lib.check(self.lib.va_nav_run(_lib.stream_ptr(stream), cells.data_ptr(), rects.data_ptr(), B, d.H, d.W,
-                                       seen.t.data_ptr(), self.work.data_ptr(), ctypes.byref(rounds)), "va_nav_run")
-        # frame records then query records (16-byte aligned): va_nav.hip work_bytes()
-        return NavBatch(self, B, rounds.value, (B * d.frame_bytes + 15) & ~15)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_nav_run(_lib.stream_ptr(stream, self.device), cells.data_ptr(), rects.data_ptr(),
+                                           B, d.H, d.W, seen.t.data_ptr(), self.work.data_ptr(), ctypes.byref(rounds)),
+                       "va_nav_run")
+            # frame records then query records (16-byte aligned): va_nav.hip work_bytes()
+            return NavBatch(self, B, rounds.value, (B * d.frame_bytes + 15) & ~15, stream)
 
     def sample_cells(self, masks: torch.Tensor, stream=None) -> torch.Tensor:
         """Lattice samples of filled masks uint8 [B, H, W] (FrameProcessor.py:88-97)."""
         B, H, W = masks.shape
         d = self.dims
         cells = torch.empty((B, d.LR, d.LC), dtype=torch.uint8, device=masks.device)
-        _lib.check(self.lib.va_nav_sample_cells(_lib.stream_ptr(stream), masks.data_ptr(), masks.stride(1), B, H, W,
-                                                cells.data_ptr()), "va_nav_sample_cells")
+        with torch.cuda.device(masks.device):
+            _lib.check(self.lib.va_nav_sample_cells(_lib.stream_ptr(stream, masks.device), masks.data_ptr(),
+                                                    masks.stride(1), B, H, W, cells.data_ptr()), "va_nav_sample_cells")
         return cells

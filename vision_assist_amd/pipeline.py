@@ -22,17 +22,26 @@ from .seg import SegNet
 class FramePipeline:
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", conf: float = 0.5,
                  iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None,
-                 seg: SegNet | None = None, tag: int = 0, imgsz: int = 640):
-        """H x W: the frame size.  Frames whose sides are multiples of 32 feed the network as they are (640x640:
-        LetterBox is the identity; 1280x1280 runs the network at 1280, BASELINE.json configs[4]); others are
-        letterboxed to `imgsz` on the device (va_letterbox) as YOLO.predict does, and the mask choice maps
-        back to frame coordinates, so cells / rects / the nav stage stay at H x W."""
+                 seg: SegNet | None = None, tag: int = 0, imgsz: int | None = None):
+        """H x W: the frame size.  ``imgsz`` = YOLO.predict's imgsz: frames are letterboxed to it on the device
+        (va_letterbox; LetterBox(imgsz, auto=True, scaleup=True)) whenever that changes them -- the 640
+        default of the reference's model.predict call -- and the mask choice maps back to frame coordinates,
+        so cells / rects / the nav stage stay at H x W.  ``imgsz=None``: the network runs at the frame's own
+        size when its sides are multiples of 32 (the C5 shape, m-seg at 1280x1280, BASELINE.json configs[4];
+        640x640 is the same either way), else at the 640 letterbox."""
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.B, self.H, self.W = B, H, W
         self.lb = None
         Hn, Wn, frame = H, W, None
-        if H % 32 or W % 32:
-            Hn, Wn, top, left, newh, neww, gain, pad_x, pad_y = letterbox_geometry(H, W, imgsz)
+        geo = None
+        if imgsz is not None:
+            geo = letterbox_geometry(H, W, imgsz)
+            if geo[:2] == (H, W) and geo[4:6] == (H, W):
+                geo = None  # LetterBox is the identity
+        elif H % 32 or W % 32:
+            geo = letterbox_geometry(H, W, 640)
+        if geo is not None:
+            Hn, Wn, top, left, newh, neww, gain, pad_x, pad_y = geo
             self.lb = (Hn, Wn, top, left, newh, neww)
             frame = (H, W, gain, pad_x, pad_y)
         self.Hn, self.Wn = Hn, Wn
@@ -57,8 +66,10 @@ class FramePipeline:
             raise _lib.VaError(f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
         frames = frames.to(self.device, non_blocking=True).contiguous()
         Hn, Wn, top, left, newh, neww = self.lb
-        _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream), frames.data_ptr(), self.B, self.H, self.W,
-                                         self.plan["frames"].data_ptr(), Hn, Wn, top, left, newh, neww), "va_letterbox")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream, self.device), frames.data_ptr(), self.B, self.H,
+                                             self.W, self.plan["frames"].data_ptr(), Hn, Wn, top, left, newh, neww),
+                       "va_letterbox")
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:

@@ -27,6 +27,7 @@ class PostArgs(ctypes.Structure):
         ("cells", VOIDP), ("rects", VOIDP), ("chosen", VOIDP),
         ("H0", ctypes.c_int32), ("W0", ctypes.c_int32), ("pad_x", ctypes.c_int32), ("pad_y", ctypes.c_int32),
         ("gain", ctypes.c_float),
+        ("max_nms", ctypes.c_int32),
     ]
 
 
@@ -53,7 +54,7 @@ class PostEngine:
     """Scratch + outputs for B frames of H x W; one ``run`` per batch."""
 
     def __init__(self, B: int, H: int, W: int, nc: int, conf: float = 0.5, iou: float = 0.7, max_det: int = 300,
-                 device=None, frame=None):
+                 device=None, frame=None, max_nms: int = 30000):
         """H x W: the network input.  frame = (H0, W0, gain, pad_x, pad_y) when it is a letterbox of H0 x W0
         frames: the mask choice then reports cells / rects in frame coordinates."""
         self.lib = _lib.load()
@@ -62,7 +63,7 @@ class PostEngine:
         if A <= 0:
             raise _lib.VaError(f"va_post_anchors({H}, {W}) = {A}")
         self.B, self.H, self.W, self.nc, self.A = B, H, W, nc, A
-        self.conf, self.iou, self.max_det = conf, iou, max_det
+        self.conf, self.iou, self.max_det, self.max_nms = conf, iou, max_det, max_nms
         dev = self.device
         self.cand = torch.empty((B, A, 8), dtype=torch.int32, device=dev)
         self.cand_count = torch.empty(B, dtype=torch.int32, device=dev)
@@ -84,6 +85,7 @@ class PostEngine:
         a.proto = proto.data_ptr()
         a.B, a.H, a.W, a.nc = self.B, self.H, self.W, self.nc
         a.conf, a.iou, a.max_det, a.plant_mode = self.conf, self.iou, self.max_det, plant_mode
+        a.max_nms = self.max_nms
         a.cand, a.cand_count, a.keys = self.cand.data_ptr(), self.cand_count.data_ptr(), self.keys.data_ptr()
         a.dets, a.ndet, a.stats = self.dets.data_ptr(), self.ndet.data_ptr(), self.stats.data_ptr()
         if plant_mode != PLANT_NEVER:
@@ -92,7 +94,8 @@ class PostEngine:
             a.cells, a.rects, a.chosen = self.cells.data_ptr(), self.rects.data_ptr(), self.chosen.data_ptr()
         if self.frame:
             a.H0, a.W0, a.gain, a.pad_x, a.pad_y = self.frame
-        _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream), ctypes.byref(a)), "va_post_run")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream, self.device), ctypes.byref(a)), "va_post_run")
 
     def det_tensor(self, b: int) -> torch.Tensor:
         """Kept detections of frame b as float [k, 6] (x1, y1, x2, y2, score, cls) + anchors [k]."""

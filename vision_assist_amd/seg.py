@@ -491,7 +491,8 @@ class SegNet:
         return p["out"]
 
     def run_plan(self, p, stream=None) -> None:
-        _lib.check(self.lib.va_seg_run(_lib.stream_ptr(stream), p["ops"], p["n"]), "va_seg_run")
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_seg_run(_lib.stream_ptr(stream, self.device), p["ops"], p["n"]), "va_seg_run")
 
     @staticmethod
     def plan_gflop(plan) -> float:

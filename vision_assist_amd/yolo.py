@@ -46,7 +46,7 @@ class Results:
 
 
 class YOLO:
-    def __init__(self, model: str = "yolov8s-seg.pt", task: str | None = None, *, dtype: str = "bf16", nc: int = 80,
+    def __init__(self, model: str = "yolov8s-seg.pt", task: str | None = None, *, dtype: str = "f32", nc: int = 80,
                  seed: int = 0, cls_bias: float | None = None):
         name = os.path.basename(str(model))
         if str(model).endswith(".safetensors") and os.path.exists(model):
@@ -75,25 +75,29 @@ class YOLO:
             self.device = torch.device("cuda", torch.cuda.current_device())
         return self
 
-    def pipeline(self, H: int, W: int, conf: float = 0.5, iou: float = 0.7, max_det: int = 300, seen=None):
-        """The fused single-frame device pipeline for H x W frames (cached)."""
+    def pipeline(self, H: int, W: int, conf: float = 0.5, iou: float = 0.7, max_det: int = 300, seen=None,
+                 imgsz: int | None = 640):
+        """The fused single-frame device pipeline for H x W frames (cached).  imgsz = predict's imgsz (640, the
+        Ultralytics default the reference's model.predict(frame, conf=0.5) uses): frames are letterboxed to it
+        whenever that changes them; None runs the network at the frame's own size (sides multiples of 32)."""
         from .pipeline import FramePipeline
-        key = (H, W, conf, iou, max_det)
+        key = (H, W, conf, iou, max_det, imgsz)
         if key not in self._pipes:
             if self.device is None:
                 self.to("cuda")
             self._pipes[key] = FramePipeline(self.arch, self.folded, 1, H, W, dtype=self.dtype, conf=conf, iou=iou,
-                                             max_det=max_det, device=self.device, seen=seen)
+                                             max_det=max_det, device=self.device, seen=seen, imgsz=imgsz)
         return self._pipes[key]
 
-    def predict(self, source, conf: float = 0.5, verbose: bool = False, iou: float = 0.7, max_det: int = 300):
+    def predict(self, source, conf: float = 0.5, verbose: bool = False, iou: float = 0.7, max_det: int = 300,
+                imgsz: int | None = 640):
         frames = source if isinstance(source, (list, tuple)) else [source]
         out = []
         for fr in frames:
             t = torch.as_tensor(fr) if not isinstance(fr, torch.Tensor) else fr
             H, W = int(t.shape[0]), int(t.shape[1])
-            pipe = self.pipeline(H, W, conf, iou, max_det)
-            pipe.plan["frames"].copy_(t.reshape(1, H, W, 3))
+            pipe = self.pipeline(H, W, conf, iou, max_det, imgsz=imgsz)
+            pipe.load(t.reshape(1, H, W, 3).to(pipe.device))  # letterboxed to the network input if needed
             pipe.seg.run_plan(pipe.plan)
             o = pipe.plan["out"]
             pipe.post.run(o.levels, o.proto, select=True)
