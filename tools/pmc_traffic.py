@@ -23,7 +23,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp)?|c2f|stem|pw)_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp|0_f32)?|c2f|stem|pw)_kernel")
 
 
 def family(name: str) -> str:

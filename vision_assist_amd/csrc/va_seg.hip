@@ -294,19 +294,23 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 //     covers 16 distinct slots of the 256-byte bank row (conflict-free).  Out-of-image / K-tail
 //     chunks are fetched from a zeroed device page.
 constexpr int BK2 = 64;
-constexpr int LDSW2 = BK2 + 8;  // 144-byte rows: ds_read_b128 row groups spread over the banks
 __device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
 typedef __attribute__((address_space(1))) void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
 
-template <int WM, int WN, int TNS, bool GLDS = false>
+// T = element type: __bf16 (K-step 64, v_mfma_f32_16x16x32_bf16) or float (exact-f32 parity mode: K-step 32,
+// four v_mfma_f32_16x16x4_f32 per 16-byte chunk).  A staged row is 128 bytes = 8 chunks of 16 bytes either way,
+// so the LDS layout, the swizzle, the DMA pattern and the im2col bookkeeping are shared.
+template <typename T, int WM, int WN, int TNS, bool GLDS = false>
 struct Conv2Cfg {
-    static constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 16 * TNS * WN, CPR = BK2 / 8;
+    static constexpr int VEC = 16 / (int)sizeof(T);  // elements per 16-byte chunk
+    static constexpr int KS = 8 * VEC;                 // K per stage: 64 bf16 / 32 f32
+    static constexpr int NT = 64 * WM * WN, BM = 64 * WM, BN = 16 * TNS * WN, CPR = 8;
     static constexpr int A_CH = BN * CPR / NT, B_CH = BM * CPR / NT, RSTEP = NT / CPR;
-    static constexpr int RS = GLDS ? BK2 : LDSW2;     // LDS row stride (elements)
-    static constexpr int STAGE = (BN + BM) * RS * 2;  // bytes per stage (A then B)
+    static constexpr int RS = GLDS ? KS : KS + VEC;                  // LDS row stride (elements): 128 / 144 B
+    static constexpr int STAGE = (BN + BM) * RS * (int)sizeof(T);  // bytes per stage (A then B)
     static constexpr int CW = BN + 4;                    // epilogue f32 row (floats)
     static constexpr int EPI = BM * CW * 4;
     static constexpr int LDS = (2 * STAGE > EPI ? 2 * STAGE : EPI);
@@ -411,17 +415,30 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 // after the last barrier), then 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous
 // stores.  Needs BM * (BN + 4) * 4 bytes of LDS.
 // orow(pl): output row of tile row pl (mode 1: the linear GEMM row, scattered below), or -1 when masked
-template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn>
+// RT: element type of the residual (the activations'); bias4 (mode 2): per-row bias from the border table
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename RT = __bf16>
 __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
-                                              int wm, int wn, int tid, int fr, int fq, RowFn orow) {
+                                              int wm, int wn, int tid, int fr, int fq, RowFn orow, int m0 = 0,
+                                              int cls = 0) {
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
+    int brow[4];  // bias row offset per pixel fragment
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        brow[j] = n0;
+        if (a.bias4) {
+            const int m = m0 + wm * 64 + 16 * j + fr;
+            const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
+            const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
+            brow[j] = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
         const int col = wn * 16 * TNS + 16 * i + 4 * fq;
-        const float4 bv = *(const float4*)(a.bias + n0 + col);  // bias is padded to Npad
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            const float4 bv = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
             float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
                   v3 = acc[i][j][3] + bv.w;
             if (a.act) {
@@ -439,7 +456,8 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
     constexpr int OV = 16 / sizeof(OutT);
     constexpr int CPRO = BN / OV;
     OutT* Y = (OutT*)a.y;
-    const __bf16* R = (const __bf16*)a.res;
+    const RT* R = (const RT*)a.res;
+    constexpr int RV = 16 / (int)sizeof(RT);
     for (int c = tid; c < BM * CPRO; c += NT) {
         const int pl = c / CPRO, cl = (c % CPRO) * OV;
         const int co = n0 + cl;
@@ -456,11 +474,11 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
         }
         if (R) {
 #pragma unroll
-            for (int r = 0; r < OV; r += 8) {
+            for (int r = 0; r < OV; r += RV) {
                 const u32x4 rr = *(const u32x4*)(R + orw * a.ldr + co + r);
-                const __bf16* rp = (const __bf16*)&rr;
+                const RT* rp = (const RT*)&rr;
 #pragma unroll
-                for (int e = 0; e < 8 && r + e < OV; ++e) v[r + e] += (float)rp[e];
+                for (int e = 0; e < RV && r + e < OV; ++e) v[r + e] += (float)rp[e];
             }
         }
         OutT* yp;
@@ -490,14 +508,15 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 // UP (FK, 1x1 only): input channels [0, a.cu) come from the half-resolution slice a.xu at (h/2, w/2) -- the
 // FPN's Upsample + Concat read in place (va355.h va_conv_args.xu); a K-step is one 64-channel chunk, so
 // the source is a wave-uniform choice per K-step.
-template <int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false>
+template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
-    using Cfg = Conv2Cfg<WM, WN, TNS, GLDS>;
+    using Cfg = Conv2Cfg<T, WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
     constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, RS = Cfg::RS;
+    constexpr int VEC = Cfg::VEC, KS = Cfg::KS;
     __shared__ __align__(16) unsigned char smem[Cfg::LDS];
-    auto As = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE); };
-    auto Bs = [&](int s) { return (__bf16*)(smem + s * Cfg::STAGE + BN * RS * 2); };
+    auto As = [&](int s) { return (T*)(smem + s * Cfg::STAGE); };
+    auto Bs = [&](int s) { return (T*)(smem + s * Cfg::STAGE + BN * RS * (int)sizeof(T)); };
 
     int bid = blockIdx.x;
     {
@@ -511,8 +530,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
-    const __bf16* __restrict__ X = (const __bf16*)a.x;
-    const __bf16* __restrict__ Wt = (const __bf16*)a.w + (int64_t)cls * a.Npad * a.Kpad;
+    const T* __restrict__ X = (const T*)a.x;
+    const T* __restrict__ Wt = (const T*)a.w + (int64_t)cls * a.Npad * a.Kpad;
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     // fixed 8-element k group of this thread and its first staged row (rows row0 + RSTEP * i); with
     // LDS-DMA, instruction i of wave w covers rows 8 (i NT/64 + w) .. +7, lane l row l >> 3
@@ -521,25 +540,25 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     int b_hi[B_CH], b_wi[B_CH];
     int64_t b_base[B_CH];
-    const __bf16* rowu[UP ? B_CH : 1];  // UP: the pixel's row in the half-resolution source (+ lane's chunk)
+    const T* rowu[UP ? B_CH : 1];  // UP: the pixel's row in the half-resolution source (+ lane's chunk)
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
         const int m = m0 + row0 + RSTEP * i;
-        if constexpr (UP) rowu[i] = (const __bf16*)a.xu + 8 * g;
+        if constexpr (UP) rowu[i] = (const T*)a.xu + VEC * g;
         if (m < a.M) {
             const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
             b_hi[i] = ho * a.stride - pad_y;
             b_wi[i] = wo * a.stride - pad_x;
             b_base[i] = (int64_t)n * a.H * a.W;
             if constexpr (UP)
-                rowu[i] = (const __bf16*)a.xu + (((int64_t)n * (a.H / 2) + (ho >> 1)) * (a.W / 2) + (wo >> 1)) * a.ldu + 8 * g;
+                rowu[i] = (const T*)a.xu + (((int64_t)n * (a.H / 2) + (ho >> 1)) * (a.W / 2) + (wo >> 1)) * a.ldu + VEC * g;
         } else {
             b_hi[i] = -(1 << 28);
             b_wi[i] = 0;
             b_base[i] = 0;
         }
     }
-    int ci = 8 * g, ky = 0, kx = 0;
+    int ci = VEC * g, ky = 0, kx = 0;
     while (ci >= a.Cin) {
         ci -= a.Cin;
         if (++kx == a.kw) {
@@ -547,17 +566,17 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             ++ky;
         }
     }
-    int kcur = 8 * g;
+    int kcur = VEC * g;
     // FK state: per-row base pointers (pixel at tap (0, 0), this lane's 8-channel group) and weight rows
-    const __bf16* rowp[B_CH];
-    const __bf16* wrow[A_CH];
+    const T* rowp[B_CH];
+    const T* wrow[A_CH];
     int fk_ky = 0, fk_kx = 0, fk_c = 0;  // tap and 64-channel chunk of the next K-step (wave-uniform)
     const void* zpage = (const void*)g_zero_page;  // hoisted: the asm waits' memory clobbers force a reload
     if constexpr (FK) {
 #pragma unroll
-        for (int i = 0; i < B_CH; ++i) rowp[i] = X + (b_base[i] + (int64_t)b_hi[i] * a.W + b_wi[i]) * a.ldx + 8 * g;
+        for (int i = 0; i < B_CH; ++i) rowp[i] = X + (b_base[i] + (int64_t)b_hi[i] * a.W + b_wi[i]) * a.ldx + VEC * g;
 #pragma unroll
-        for (int i = 0; i < A_CH; ++i) wrow[i] = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + 8 * g;
+        for (int i = 0; i < A_CH; ++i) wrow[i] = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + VEC * g;
     }
 
     // no lambdas around the staging arrays: captured by reference they become addressable allocas
@@ -565,7 +584,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #define CONV2_LOAD(k0)                                                                                             \
     {                                                                                                              \
         _Pragma("unroll") for (int i = 0; i < A_CH; ++i) ra[i] =                                                   \
-            *(const u32x4*)(Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + 8 * g);                        \
+            *(const u32x4*)(Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g);                        \
         const bool kin = kcur < a.K;                                                                               \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
             const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
@@ -574,8 +593,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             const u32x4 v = *(const u32x4*)(X + off);                                                              \
             rb[i] = ok ? v : (u32x4){0u, 0u, 0u, 0u};                                                              \
         }                                                                                                          \
-        kcur += BK2;                                                                                               \
-        ci += BK2;                                                                                                 \
+        kcur += KS;                                                                                               \
+        ci += KS;                                                                                                 \
         while (ci >= a.Cin) {                                                                                      \
             ci -= a.Cin;                                                                                           \
             if (++kx == a.kw) {                                                                                    \
@@ -586,31 +605,31 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     }
 #define CONV2_STORE(s)                                                                                             \
     {                                                                                                              \
-        __bf16* as_ = As(s);                                                                                       \
-        __bf16* bs_ = Bs(s);                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(as_ + (row0 + RSTEP * i) * LDSW2 + 8 * g) =     \
+        T* as_ = As(s);                                                                                       \
+        T* bs_ = Bs(s);                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(as_ + (row0 + RSTEP * i) * RS + VEC * g) =   \
             ra[i];                                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(bs_ + (row0 + RSTEP * i) * LDSW2 + 8 * g) =     \
+        _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(bs_ + (row0 + RSTEP * i) * RS + VEC * g) =   \
             rb[i];                                                                                                 \
     }
 
     // LDS-DMA form of LOAD+STORE: one 1 KiB DMA per operand row block, zero page for masked chunks
 #define CONV2_DMA(k0, s)                                                                                           \
     if constexpr (FK) {                                                                                            \
-        __bf16* as_ = As(s);                                                                                       \
-        __bf16* bs_ = Bs(s);                                                                                       \
+        T* as_ = As(s);                                                                                       \
+        T* bs_ = Bs(s);                                                                                       \
         _Pragma("unroll") for (int i = 0; i < A_CH; ++i) __builtin_amdgcn_global_load_lds(                         \
-            (gvoid_t*)(wrow[i] + (k0)), (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0, 0);                 \
+            (gvoid_t*)(wrow[i] + (k0)), (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16, 0, 0);                 \
         const int soff = (fk_ky * a.W + fk_kx) * a.ldx + fk_c;                                                     \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
             const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W; \
-            const __bf16* sp_ = rowp[i] + soff;                                                                    \
+            const T* sp_ = rowp[i] + soff;                                                                    \
             if constexpr (UP) sp_ = fk_c < a.cu ? rowu[i] + fk_c : sp_;                                           \
             const void* src = ok ? (const void*)sp_ : zpage;                                                       \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * KS), 16, 0,  \
                                              0);                                                                   \
         }                                                                                                          \
-        fk_c += BK2;                                                                                               \
+        fk_c += KS;                                                                                               \
         if (fk_c == a.Cin) {                                                                                       \
             fk_c = 0;                                                                                              \
             if (++fk_kx == a.kw) {                                                                                 \
@@ -619,11 +638,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             }                                                                                                      \
         }                                                                                                          \
     } else {                                                                                                       \
-        __bf16* as_ = As(s);                                                                                       \
-        __bf16* bs_ = Bs(s);                                                                                       \
+        T* as_ = As(s);                                                                                       \
+        T* bs_ = Bs(s);                                                                                       \
         _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
-            const __bf16* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + 8 * g;                     \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+            const T* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g;                          \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16, 0,  \
                                              0);                                                                   \
         }                                                                                                          \
         const bool kin = kcur < a.K;                                                                               \
@@ -632,11 +651,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
             const void* src = ok ? (const void*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci)            \
                                  : (const void*)g_zero_page;                                                       \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
+            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * KS), 16, 0,  \
                                              0);                                                                   \
         }                                                                                                          \
-        kcur += BK2;                                                                                               \
-        ci += BK2;                                                                                                 \
+        kcur += KS;                                                                                               \
+        ci += KS;                                                                                                 \
         while (ci >= a.Cin) {                                                                                      \
             ci -= a.Cin;                                                                                           \
             if (++kx == a.kw) {                                                                                    \
@@ -652,7 +671,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    const int nk = a.Kpad / BK2;
+    const int nk = a.Kpad / KS;
     if constexpr (GLDS) {
         CONV2_DMA(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -667,31 +686,51 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const bool more = kt + 1 < nk;
         if constexpr (GLDS) {
             if (more) {
-                CONV2_DMA((kt + 1) * BK2, s ^ 1);
+                CONV2_DMA((kt + 1) * KS, s ^ 1);
             }
         } else {
-            if (more) CONV2_LOAD((kt + 1) * BK2);
+            if (more) CONV2_LOAD((kt + 1) * KS);
         }
-        const __bf16* as_ = As(s);
-        const __bf16* bs_ = Bs(s);
+        const T* as_ = As(s);
+        const T* bs_ = Bs(s);
         // all fragments of the K-step first (the second half's reads overlap the first half's MFMAs)
-        bf16x8 af[2][TNS], bfr[2][4];
+        u32x4 af[2][TNS], bfr[2][4];
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
             // chunk 4 kh + fq of the row; GLDS rows are swizzled (slot = chunk ^ (row & 7), row & 7 == fr & 7)
-            const int ch = GLDS ? (((4 * kh + fq) ^ (fr & 7)) * 8) : 32 * kh + 8 * fq;
+            const int ch = GLDS ? (((4 * kh + fq) ^ (fr & 7)) * VEC) : 4 * VEC * kh + VEC * fq;
 #pragma unroll
-            for (int i = 0; i < TNS; ++i) af[kh][i] = *(const bf16x8*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
+            for (int i = 0; i < TNS; ++i) af[kh][i] = *(const u32x4*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[kh][j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
+            for (int j = 0; j < 4; ++j) bfr[kh][j] = *(const u32x4*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
         }
+        if constexpr (sizeof(T) == 2) {
 #pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
+            for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
-            for (int i = 0; i < TNS; ++i)
+                for (int i = 0; i < TNS; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[kh][i]),
+                                                                            __builtin_bit_cast(bf16x8, bfr[kh][j]),
+                                                                            acc[i][j], 0, 0, 0);
+        } else {
+            // f32: element e of lane (fr, fq)'s chunk 4 kh + fq is K index 16 kh + 4 fq + e of the stage -- MFMA
+            // (kh, e) sums over fq, so the four MFMAs of a chunk cover its 16 K values (the same permutation of
+            // K for both operands: an exact f32 fma chain in another order)
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int i = 0; i < TNS; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            // (element e by value: __builtin_bit_cast of a vector-element lvalue reads element 0)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[kh][i][e]),
+                                                                             __uint_as_float(bfr[kh][j][e]),
+                                                                             acc[i][j], 0, 0, 0);
+        }
         if constexpr (GLDS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
@@ -707,13 +746,13 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int m = m0 + pl;
         return m < a.M ? (a.mode == 1 ? (int64_t)m : conv_out_row(a, m, cls)) : -1;
     };
-    if constexpr (BN == 128) {
+    if constexpr (BN == 128 && sizeof(T) == 2) {
         if (a.w2) {
             conv2_tail<NT, BM, TNS, OutT>(a, acc, smem, n0, wm, wn, wid, fr, fq, orow, m0, cls);
             return;
         }
     }
-    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow);
+    conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
 }
 
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
@@ -1737,6 +1776,52 @@ hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------- layer 0, f32
+// Exact-f32 model.0 with the preprocessing folded in (va355.h va_seg_conv0_f32): one output pixel per lane;
+// its 27 inputs (3x3 taps x RGB / 255, zero padding) in registers, every weight a wave-uniform scalar load, so
+// the layer is 27 v_fma per output channel and one 16-byte store per 4 channels -- bound by the f32 output
+// write (128 B per pixel at Cout 32), not by the 8-channel im2col GEMM it replaces.
+template <int NCO>
+__global__ __launch_bounds__(256) void conv0_f32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        float* __restrict__ y, int ldy) {
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    const int64_t total = (int64_t)N * Ho * Wo;
+    for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < total; m += (int64_t)gridDim.x * blockDim.x) {
+        const int wo = (int)(m % Wo);
+        const int64_t t = m / Wo;
+        const int ho = (int)(t % Ho), n = (int)(t / Ho);
+        float x[27];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const int hi = 2 * ho - 1 + ky;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int wi = 2 * wo - 1 + kx;
+                const bool in = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+                const uint8_t* p = frames + (((int64_t)n * H + (in ? hi : 0)) * W + (in ? wi : 0)) * 3;
+#pragma unroll
+                for (int c = 0; c < 3; ++c)  // R, G, B = bytes 2, 1, 0
+                    x[(ky * 3 + kx) * 3 + c] = in ? (float)p[2 - c] / 255.0f : 0.0f;
+            }
+        }
+        float* out = y + m * ldy;
+#pragma unroll
+        for (int co = 0; co < NCO; co += 4) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float* wr = w + (co + r) * 27;
+                float acc = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 27; ++k) acc = fmaf(wr[k], x[k], acc);
+                v[r] = silu_exact(acc + bias[co + r]);
+            }
+            *(float4*)(out + co) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------- layer 0
 // model.0 fused with preprocessing: uint8 BGR frame -> RGB/255 -> Conv(3x3, s2, p1) + folded BN + SiLU
 // -> bf16 NHWC.  K = 3x3x3 = 27 (padded to one 32-deep MFMA step), so instead of materialising an
@@ -1947,28 +2032,29 @@ bool getenv_glds() {
     return v == 1;
 }
 
-template <int WM, int WN, int TNS, typename OutT>
+template <int WM, int WN, int TNS, typename OutT, typename T = __bf16>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
-    using Cfg = Conv2Cfg<WM, WN, TNS>;
+    using Cfg = Conv2Cfg<T, WM, WN, TNS>;
+    constexpr int VEC = Cfg::VEC, KS = Cfg::KS;
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of 8 and a 16-byte aligned base
-    const bool fk = a.Cin % 64 == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
+    // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
+    const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
     if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
-        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a,
-                           ntn, ntiles);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st,
+                           a, ntn, ntiles);
         return hipGetLastError();
     }
-    if (getenv_glds() && a.Cin % 8 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % 8 == 0) {
+    if (getenv_glds() && a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
-            hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a,
-                               ntn, ntiles);
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st,
+                               a, ntn, ntiles);
         else
-            hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
                                ntiles);
     }
     else
-        hipLaunchKernelGGL((conv2_kernel<WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
@@ -2193,6 +2279,17 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
+    if constexpr (sizeof(T) == 4) {
+        // exact-f32 parity mode: conv2 with f32 MFMA (K-step 32); VA_CONV_F32_OLD=1 keeps the register-staged
+        // conv_kernel (A/B timing)
+        if (a.Kpad % 32 == 0 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && (a.mode != 1 || (a.Cout / 4) % 4 == 0) &&
+            getenv("VA_CONV_F32_OLD") == nullptr) {
+            if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float>(a, st) : hipErrorInvalidValue;
+            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float>(a, st);
+            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float>(a, st);
+            return launch_conv2<2, 2, 4, OutT, float>(a, st);
+        }
+    }
     // tile choice: small Cout -> tall pixel tiles
     if (a.Cout <= 64) return launch_conv<T, 4, 1, OutT>(a, st);
     return launch_conv<T, 2, 2, OutT>(a, st);
@@ -2204,18 +2301,19 @@ extern "C" {
 
 int va_seg_conv(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
-    if (a->xu && (a->dtype != VA_DTYPE_BF16 || a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0 ||
-                  a->mode != 0 || a->w2 || a->out_f32 || a->Cin % 64 || a->cu <= 0 || a->cu % 64 || a->cu >= a->Cin ||
-                  a->K != a->Cin || a->Kpad != a->K || a->ldu % 8 || ((uintptr_t)a->xu & 15) || a->H % 2 ||
-                  a->W % 2 || a->ldx % 8 || ((uintptr_t)a->x & 15)))
+    const bool bf = a->dtype == VA_DTYPE_BF16;
+    const int vec = bf ? 8 : 4, ks = 8 * vec;  // elements per 16-byte chunk / per conv2 K-step
+    if (a->xu && (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0 || a->mode != 0 || a->w2 ||
+                  a->out_f32 || a->Cin % ks || a->cu <= 0 || a->cu % ks || a->cu >= a->Cin || a->K != a->Cin ||
+                  a->Kpad != a->K || a->ldu % vec || ((uintptr_t)a->xu & 15) || a->H % 2 || a->W % 2 ||
+                  a->ldx % vec || ((uintptr_t)a->x & 15)))
         return VA_ERR_ARG;
-    const int vec = a->dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
-    if (a->mode == 2 && (a->dtype != VA_DTYPE_BF16 || a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res ||
-                         a->Cout <= 64 || a->Kpad % BK2))
+    if (a->mode == 2 && (a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res || a->Cout <= 64 || a->Kpad % ks))
         return VA_ERR_ARG;
-    if (a->bias4 && (a->mode != 2 || !a->w2 || a->Cout != 128)) return VA_ERR_ARG;  // conv2's fused-tail path only
+    // bias4: mode 2 only -- bf16 through conv2's fused-tail path, f32 through the plain epilogue
+    if (a->bias4 && (a->mode != 2 || (bf ? (!a->w2 || a->Cout != 128) : a->w2 != nullptr))) return VA_ERR_ARG;
     if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode == 1 ||
                   (a->mode == 2 && a->Cout != 128) ||
                   a->res || !a->b2 || a->c2 <= 0 || a->c2 > 16 * (a->Cout == 128 ? TAIL_C2F : DN_TAIL_C2F) ||
@@ -2368,6 +2466,23 @@ int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int3
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const float* w,
+                     const float* bias, int32_t Cout, float* y, int32_t ldy) {
+    if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 4 ||
+        ldy < Cout || ((uintptr_t)y & 15))
+        return VA_ERR_ARG;
+    const int64_t total = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2);
+    const int grid = grid_for(total, 256);
+    hipStream_t st = (hipStream_t)stream;
+    switch (Cout / 16) {
+        case 1: hipLaunchKernelGGL(conv0_f32_kernel<16>, dim3(grid), dim3(256), 0, st, frames, N, H, W, w, bias, y, ldy); break;
+        case 2: hipLaunchKernelGGL(conv0_f32_kernel<32>, dim3(grid), dim3(256), 0, st, frames, N, H, W, w, bias, y, ldy); break;
+        case 3: hipLaunchKernelGGL(conv0_f32_kernel<48>, dim3(grid), dim3(256), 0, st, frames, N, H, W, w, bias, y, ldy); break;
+        default: hipLaunchKernelGGL(conv0_f32_kernel<64>, dim3(grid), dim3(256), 0, st, frames, N, H, W, w, bias, y, ldy);
+    }
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
     if (!ops || n < 0) return VA_ERR_ARG;
     for (int i = 0; i < n; ++i) {
@@ -2389,7 +2504,10 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                 rc = va_seg_preprocess(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.dtype, a.y);
                 break;
             case VA_OP_CONV0:
-                rc = va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
+                rc = a.dtype == VA_DTYPE_F32
+                         ? va_seg_conv0_f32(stream, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w, a.bias,
+                                            a.Cout, (float*)a.y, a.ldy)
+                         : va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             case VA_OP_C2F:
                 rc = va_seg_c2f(stream, &a);

@@ -24,7 +24,7 @@ from .seg_arch import NM, REG_MAX, Arch
 
 VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
-BK = 64  # K padding: the bf16 kernel steps K by 64 (the f32 kernel by 32)
+BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
 
 
@@ -117,12 +117,17 @@ class SegNet:
         w0p = torch.zeros(w0.shape[0], 32, dtype=torch.float32)
         w0p[:, :27] = w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27)
         self.w0 = (w0p.to(self.device, self.tdtype).contiguous(), b0.float().to(self.device).contiguous())
-        self.fuse_first = dtype == "bf16" and w0.shape[0] % 16 == 0 and w0.shape[0] <= 64
-        self.proto_fold = self._fold_proto(folded) if (dtype == "bf16" and arch.npr == 128
-                                                       and os.environ.get("VA_FOLD_PROTO", "1") != "0") else None
+        self.fuse_first = w0.shape[0] % 16 == 0 and w0.shape[0] <= 64 and os.environ.get("VA_CONV0", "1") != "0"
+        if dtype == "f32":  # va_seg_conv0_f32: [Cout][27], k = (ky*3 + kx)*3 + c (RGB)
+            self.w0 = (w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27).float().to(self.device).contiguous(),
+                       b0.float().to(self.device).contiguous())
+        # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
+        fold_ok = arch.npr == 128 if dtype == "bf16" else arch.npr >= 128
+        self.proto_fold = self._fold_proto(folded) if (fold_ok and os.environ.get("VA_FOLD_PROTO", "1") != "0") \
+            else None
         # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
         self.stem = None
-        if self.fuse_first and w0.shape[0] == 32 and os.environ.get("VA_STEM", "1") != "0":
+        if dtype == "bf16" and self.fuse_first and w0.shape[0] == 32 and os.environ.get("VA_STEM", "1") != "0":
             w1, b1 = folded["model.1"]
             if tuple(w1.shape) == (64, 32, 3, 3):
                 self.stem = self._pack_stem(w0p, b0, w1, b1)
@@ -204,7 +209,7 @@ class SegNet:
         wc, wb = wfull[..., :ci], wfull[..., ci]  # weights, per-tap bias contributions [4][O][2][2]
         o = wc.shape[1]
         K = 4 * ci
-        Kpad, Npad = _ceil(K, BK), _ceil(o, NPAD)
+        Kpad, Npad = _ceil(K, self.bk), _ceil(o, NPAD)
         wm = torch.zeros(4, Npad, Kpad, dtype=torch.float64)
         wm[:, :o, :K] = wc.reshape(4, o, K)
         bt = torch.zeros(4, 2, 2, Npad, dtype=torch.float64)
@@ -223,6 +228,11 @@ class SegNet:
         return Packed(wm.to(self.device, self.tdtype).contiguous(),
                       bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
 
+    @property
+    def bk(self) -> int:
+        """K padding of the packed weights: the conv2 K-step (64 bf16 / 32 f32)."""
+        return BK if self.dtype == "bf16" else 32
+
     # ------------------------------------------------------------------ packing
     def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
         if deconv:  # ConvTranspose2d weight [Cin, Cout, 2, 2] -> 1x1 GEMM rows q*Cout + co, q = dy*2 + dx
@@ -237,7 +247,7 @@ class SegNet:
         wp = torch.zeros(cout, kh, kw, cin_p, dtype=torch.float32)
         wp[..., :cin] = w.permute(0, 2, 3, 1)
         K = kh * kw * cin_p
-        Kpad = _ceil(K, BK)
+        Kpad = _ceil(K, self.bk)
         Npad = _ceil(cout, NPAD)
         wm = torch.zeros(Npad, Kpad, dtype=torch.float32)
         wm[:cout, :K] = wp.reshape(cout, K)
@@ -358,7 +368,7 @@ class SegNet:
                                                                w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
                                                                Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)))
                 meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3,
-                             "stride": 2, "bytes": B * H * W * 3 + 2 * B * h1 * w1 * a.c1})
+                             "stride": 2, "bytes": B * H * W * 3 + (2 if self.dtype == "bf16" else 4) * B * h1 * w1 * a.c1})
             else:
                 x0 = new(H, W, 8)
                 ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
@@ -392,8 +402,9 @@ class SegNet:
         P5 = cat20.sub(a.c4, a.c5)
         conv("model.9.cv2", sp, P5, h5, w5)
         # the FPN's Upsample + Concat: read in place by the consumer's 1x1 cv1 (bf16) or materialised
-        fuse_up = self.dtype == "bf16" and os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % 64 == 0 \
-            and a.c4 % 64 == 0 and (a.c5 + a.c4) % 64 == 0 and (a.c4 + a.c3) % 64 == 0
+        ks = 64 if self.dtype == "bf16" else 32  # the conv2 K-step the upsampled prefix must align to
+        fuse_up = os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % ks == 0 \
+            and a.c4 % ks == 0 and (a.c5 + a.c4) % ks == 0 and (a.c4 + a.c3) % ks == 0
         if not fuse_up:
             upsample(P5, cat11.sub(0, a.c5), h5, w5)
         cat17 = new(h4, w4, a.c3 + a.c4)          # [conv16(o3) | h12]
@@ -428,6 +439,27 @@ class SegNet:
                 conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
                 conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False, out_f32=True)
         # Proto
+        if self.proto_fold is not None and self.dtype == "f32":
+            # the sub-pixel fold (mode 2, border bias table) into the 4x map, then cv3 as its own 1x1 GEMM
+            pf = self.proto_fold
+            pr1 = new(h3, w3, a.npr)
+            conv("model.22.proto.cv1", o3, pr1, h3, w3)
+            pr3 = new(h2, w2, a.npr)
+            ops.append(SegOp(kind=VA_OP_CONV, a=ConvArgs(
+                x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
+                w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
+                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1)))
+            meta.append({"name": "model.22.proto.upsample+cv2 (sub-pixel fold)", "kind": "conv",
+                         "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
+                         "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
+                         "bytes": 4 * B * h3 * w3 * pf.cin + 4 * pf.w.numel() + 4 * B * h2 * w2 * pf.cout})
+            proto = new(h2, w2, NM, torch.float32)
+            conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
+            op_arr = (SegOp * len(ops))(*ops)
+            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
+                    "out": SegOutputs(levels=levels, proto=proto.buf)}
+            self._plans[key] = plan
+            return plan
         if self.proto_fold is not None:
             pf = self.proto_fold
             pr1 = new(h3, w3, a.npr)
