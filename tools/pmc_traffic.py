@@ -64,7 +64,7 @@ def agree(trace: str, bench_json: str, out: str, per_fwd: int = 55) -> dict:
     nf = len(rows) // per_fwd
     fwd = [sum(d for _, d in rows[i * per_fwd:(i + 1) * per_fwd]) / per_fwd / 1e3 for i in range(nf)]
     with open(bench_json) as f:
-        b = json.loads(f.read().strip().splitlines()[-1])
+        b = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
     steps, warm = b["steps"], b["warmup"]
     timed = fwd[warm:warm + steps]
     iso = fwd[warm + steps:]
