@@ -196,11 +196,45 @@ class RefRunner:
             "n_lookup": len(fp.grid_lookup),
             "peaks": [[p.x, p.y] for p in peaks],
             "queries": self.queries,
-            "paths": [{"coords": [[q.coords.x, q.coords.y] for q in p.grids],
-                       "cost": _hexf(p.total_cost)} for p in paths],
+            "paths": [dict({"coords": [[q.coords.x, q.coords.y] for q in p.grids],
+                            "cost": _hexf(p.total_cost)}, **path_structure(p)) for p in paths],
             "answer": answer,
         })
         return rec
+
+
+def path_structure(p) -> dict:
+    """models.Path post-init results (models.py:96-99, 160-364): sections (type, cells, total_cost) and corners."""
+    secs = None if p.sections is None else [
+        {"type": q.path_type, "coords": [[g.coords.x, g.coords.y] for g in q.grids], "cost": _hexf(q.total_cost)}
+        for q in p.sections]
+    corners = None if p.corners is None else [
+        {"direction": c.direction, "sharpness": c.sharpness, "shape": c.shape, "start": [c.start.x, c.start.y],
+         "end": [c.end.x, c.end.y], "angle_change": _hexf(c.angle_change), "length": _hexf(c.length)}
+        for c in p.corners]
+    return {"sections": secs, "corners": corners, "angle": _hexf(p.angle), "length": _hexf(p.length)}
+
+
+def path_model_fixtures() -> list:
+    """The 12 hand-captured paths of testing/path_model/grids.py (570 Grid literals, frame 720 x 1280) through the
+    reference's models.Path as testing/path_model/test.py:35-39 builds them (total_cost=100): the cells and the
+    sections / corners the reference computes.  grids.py imports its Grid / Coordinate from `other_models`,
+    aliased here to the reference's own models module."""
+    import importlib.util
+    import vision_assist.models as M
+    sys.modules.setdefault("other_models", M)
+    spec = importlib.util.spec_from_file_location("va_path_model_grids", os.path.join(REF, "testing", "path_model",
+                                                                                     "grids.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = []
+    for path in mod.grids:
+        p = M.Path(grids=path, total_cost=100, path_type="path")
+        out.append(dict({"cells": [{"coords": [g.coords.x, g.coords.y], "centre": [g.centre.x, g.centre.y],
+                                    "penalty": _hexf(g.penalty), "row": g.row, "col": g.col, "empty": g.empty,
+                                    "artificial": g.artificial} for g in path],
+                         "total_cost": "i100"}, **path_structure(p)))
+    return out
 
 
 def load_fixtures() -> dict:
@@ -277,6 +311,8 @@ def main():
     out["sequences"].append(seq)
     # 6) 128-entry angle table computed by the reference's own _angle_between_grids
     out["angle_table"] = angle_table(runner)
+    # 7) models.Path sectioning / corners of the reference's hand-captured paths
+    out["path_model"] = path_model_fixtures()
     quiet.__exit__(None, None, None)
     path = os.path.join(HERE, "nav_goldens.json.gz")
     with gzip.open(path, "wt") as f:

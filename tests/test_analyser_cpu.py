@@ -56,3 +56,60 @@ def test_path_sections_cover_path():
                     assert sc[0] == joined[-1]
                     joined += sc[1:]
                 assert joined == cells
+
+
+def _hx(v):
+    return None if v is None else (("i", int(v)) if isinstance(v, int) else ("f", float(v).hex()))
+
+
+def _structure(p):
+    """Sections and corners of a vision_assist_amd.models.Path in the golden record's form."""
+    secs = None if p.sections is None else [
+        {"type": q.path_type, "coords": [[g.coords.x, g.coords.y] for g in q.grids], "cost": _hx(q.total_cost)}
+        for q in p.sections]
+    corners = None if p.corners is None else [
+        {"direction": c.direction, "sharpness": c.sharpness, "shape": c.shape, "start": [c.start.x, c.start.y],
+         "end": [c.end.x, c.end.y], "angle_change": _hx(c.angle_change), "length": _hx(c.length)}
+        for c in p.corners]
+    return secs, corners
+
+
+def _golden_structure(gp):
+    secs = None if gp["sections"] is None else [dict(s, cost=_hx(unhex(s["cost"]))) for s in gp["sections"]]
+    corners = None if gp["corners"] is None else [
+        dict(c, angle_change=_hx(unhex(c["angle_change"])), length=_hx(unhex(c["length"]))) for c in gp["corners"]]
+    return secs, corners
+
+
+def test_path_sections_and_corners_match_reference_runs():
+    """models.Path post-init (models.py:96-99 sections :160-270, corners :300-364) on every path the reference
+    returned for the golden frames: section types, cells and total_cost (float64 hex) and every corner field
+    (direction, sharpness, shape, start, end, angle_change and length as float64 hex) equal the reference's."""
+    from vision_assist_amd.models import Path
+    n = ncorner = 0
+    for seq in load_goldens()["sequences"]:
+        for fr in seq["frames"]:
+            for gp in fr.get("paths", []):
+                p = Path(grids=[_grid(x, y, {}) for x, y in gp["coords"]], total_cost=unhex(gp["cost"]),
+                         path_type="path")
+                assert _structure(p) == _golden_structure(gp), fr["source"]
+                assert _hx(p.angle) == _hx(unhex(gp["angle"])) and _hx(p.length) == _hx(unhex(gp["length"]))
+                n += 1
+                ncorner += len(gp["corners"] or [])
+    assert n > 300 and ncorner > 300  # 317 paths, every one compared
+
+
+def test_path_model_fixtures_match_reference():
+    """The reference's 12 hand-captured paths (testing/path_model/grids.py, 570 Grid literals, 720 x 1280 frame),
+    built as testing/path_model/test.py:35-39 builds them (total_cost=100): sections and corners equal the
+    reference's models.Path results recorded by tests/golden/gen_goldens.py."""
+    from vision_assist_amd.models import Coordinate, Grid, Path
+    fx = load_goldens()["path_model"]
+    assert len(fx) == 12
+    for k, f in enumerate(fx):
+        cells = [Grid(coords=Coordinate(x=c["coords"][0], y=c["coords"][1]),
+                      centre=Coordinate(x=c["centre"][0], y=c["centre"][1]), penalty=unhex(c["penalty"]),
+                      row=c["row"], col=c["col"], empty=c["empty"], artificial=c["artificial"]) for c in f["cells"]]
+        p = Path(grids=cells, total_cost=100, path_type="path")
+        assert _structure(p) == _golden_structure(f), k
+        assert _hx(p.angle) == _hx(unhex(f["angle"])) and _hx(p.length) == _hx(unhex(f["length"])), k
