@@ -114,13 +114,16 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
         with torch.no_grad():
             out = Y.predict(arch, fw, torch.from_numpy(frames_u8[i:i + 1]))
         det, masks = out[0]
+        stages["network+post"] = stages.get("network+post", 0.0) + time.perf_counter() - tn
+        tm = time.perf_counter()
+        # mask -> polygon -> cells: a pure-python findContours / fillPoly port (cv2's C++ is absent), its own lap
         m, rect = Y.select_mask(masks)
         if m is None:  # planted, as on the GPU
             m = cells_to_mask(plant_cells[i].astype(bool))
             rect = tuple(int(v) for v in plant_rects[i])
         else:
             m = m.numpy()
-        stages["network+post"] = stages.get("network+post", 0.0) + time.perf_counter() - tn
+        stages["mask->cells"] = stages.get("mask->cells", 0.0) + time.perf_counter() - tm
         nav = onav.frame_nav(m, rect, res, res, pf, timings=stages)
         # FrameProcessor.py:246 Path(...) (sections + corners) for every found path and :349 path_analyser on
         # the unique ones: the pure-python host classes the product's FrameProcessor surface also runs per

@@ -287,14 +287,28 @@ int va_prof_enable(int32_t on);
 typedef struct va_cand { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_cand;  /* NMS candidate */
 typedef struct va_det { float x1, y1, x2, y2, score; int32_t cls, anchor, pad; } va_det;    /* kept detection */
 typedef struct va_mask_stat { int32_t count, x0, y0, x1, y1, pad[3]; } va_mask_stat;        /* mask pixels, bbox */
+/* Per instance mask: its Results.masks.xy polygon as FrameProcessor consumes it (masks2segments 'largest' +
+ * scale_coords; oracle/contours.py restates OpenCV's algorithms). */
+typedef struct va_contour_stat {
+    int32_t npts;     /* CHAIN_APPROX_SIMPLE points of the largest external contour (0: empty mask) */
+    int32_t ox, oy;   /* its start pixel in the instance's framed region image */
+    int32_t ncont;    /* external contours found (RETR_EXTERNAL) */
+    int32_t X0, Y0;   /* the region's origin in network pixels (framed image pixel (x, y) = (X0 + x - 1, Y0 + y - 1)) */
+    int32_t status;   /* 0 ok, 1 region too tall for the scan tables */
+    int32_t pad;
+    double area;      /* cv2.contourArea of the float32 scale_coords points */
+} va_contour_stat;
 
 /* Everything YOLO.predict does after the forward, for B frames, plus the mask choice of
- * FrameProcessor.py:67-97 (restated, parity unpinned: OpenCV is absent):
- *   decode (DFL, dist2bbox, sigmoid) -> conf filter -> class-offset greedy NMS (IoU > iou) -> max_det
- *   -> process_mask (coef . proto, crop, bilinear x4, > 0) -> per-instance pixel count / bbox
- *   -> (if cells != NULL) the instance with the most pixels, sampled at the 20-px cell centres, and
- *      its pixel bbox as the boundingRect -> the (cells, rects) input of va_nav_run.
- * plant_mode: 0 = never plant; 1 = use plant_cells/plant_rects for frames with no mask; 2 = always. */
+ * FrameProcessor.py:67-97 with OpenCV's algorithms restated (oracle/contours.py; parity with cv2 unpinned):
+ *   decode (DFL, dist2bbox, sigmoid) -> conf filter -> max_nms cut -> class-offset greedy NMS (IoU > iou) -> max_det
+ *   -> process_mask (coef . proto, crop, bilinear x4, > 0) -> per-instance pixel count / bbox (stats)
+ *   -> (if cells != NULL) per instance the largest external contour (findContours RETR_EXTERNAL,
+ *      CHAIN_APPROX_SIMPLE) and its contourArea over the float32 scale_coords points (cstats); the instance of
+ *      max area (first maximum; a single one as it is), np.int32 of its polygon, boundingRect, and
+ *      fillPoly(LINE_8) sampled at the 20-px cell centres of the H0 x W0 frame -> the (cells, rects) input of
+ *      va_nav_run.
+ * plant_mode: 0 = never plant; 1 = use plant_cells/plant_rects for frames with no detection; 2 = always. */
 typedef struct va_post_args {
     const float* levels[3];     /* float [B][H/s][W/s][64 + nc + 32], s = 8, 16, 32 */
     const float* proto;         /* float [B][H/4][W/4][32] */
@@ -313,11 +327,17 @@ typedef struct va_post_args {
     uint8_t* cells;             /* out [B][H/20][W/20] or NULL (skip the mask choice) */
     int32_t* rects;             /* out [B][4] */
     int32_t* chosen;            /* out [B]: chosen detection, -1 none, -2 planted */
-    /* LetterBox (Ultralytics predict preprocess, replaced by va_letterbox): cells / rects refer to the
-     * H0 x W0 frame, network pixel = frame pixel * gain + (pad_x, pad_y); polygon coordinates are mapped
-     * back as scale_coords does.  H0 = 0: the network input is the frame (identity). */
-    int32_t H0, W0, pad_x, pad_y;
-    float gain;
+    /* The frame the network input was letterboxed from (va_letterbox): cells / rects refer to the H0 x W0
+     * frame; polygon points are mapped back as ops.scale_coords does in float32: (p - pad) / gain, clipped to
+     * [0, W0] x [0, H0], with gain = min(H/H0, W/W0) and pad = ((W - W0 gain) / 2, (H - H0 gain) / 2) rounded
+     * to float32 (numpy's float32 arithmetic).  H0 = 0: the frame is the network input (gain 1, pad 0). */
+    int32_t H0, W0;
+    float sc_gain, sc_padx, sc_pady;
+    /* contour scratch: cslots slots of va_contour_scratch_bytes(H, W, cslots, ccap) bytes each */
+    void* cscratch;
+    int32_t cslots, ccap;
+    va_contour_stat* cstats;    /* out [B][max_det] (required with cells) */
+    int32_t* cstatus;           /* out [B] or NULL: 1 = the chosen contour exceeded ccap points (cells left 0) */
     /* non_max_suppression's max_nms (ops.py:332-333): a candidate list longer than this is cut to its
      * max_nms highest scores before NMS.  <= 0: VA_MAX_NMS (Ultralytics' 30000). */
     int32_t max_nms;
@@ -336,8 +356,40 @@ int va_letterbox(void* stream, const uint8_t* src, int32_t B, int32_t H, int32_t
 int va_post_anchors(int32_t H, int32_t W);
 int va_post_run(void* stream, const va_post_args* p);
 
+/* Bytes of one contour scratch slot for an H x W network input with point capacity cap, and the offsets of its
+ * image and point areas.  The caller allocates nslots x *slot_bytes. */
+int va_contour_scratch_bytes(int32_t H, int32_t W, int32_t nslots, int32_t cap, int64_t* slot_bytes, int64_t* img_off,
+                             int64_t* pts_off);
+
+/* The same mask -> polygon -> cells boundary for given binary masks (test / harness entry point): masks uint8
+ * [B][maxn][Hn][Wn] (non-zero = set), nmask[b] masks for frame b.  polys (optional) [B][maxn][poly_cap][2] float
+ * receives each mask's Results.masks.xy polygon (poly_n[b * maxn + k] points). */
+typedef struct va_mask_select_args {
+    const uint8_t* masks;
+    const int32_t* nmask;
+    int32_t B, maxn, Hn, Wn, H0, W0;
+    float gain, padx, pady;
+    void* scratch;
+    int32_t nslots, cap;
+    va_contour_stat* cstats;    /* out [B][maxn] */
+    uint8_t* cells;             /* out [B][H0/20][W0/20] or NULL */
+    int32_t* rects;             /* out [B][4] */
+    int32_t* chosen;            /* out [B] */
+    int32_t* status;            /* out [B] or NULL */
+    float* polys;               /* out or NULL */
+    int32_t* poly_n;
+    int32_t poly_cap, pad_;
+} va_mask_select_args;
+int va_post_select_masks(void* stream, const va_mask_select_args* m);
+
+/* Results.masks.xy for the detections of the last va_post_run on the same buffers (p as passed to it, with
+ * cstats): per detection its largest external contour in frame coordinates, float [B][max_det][poly_cap][2],
+ * poly_n [B][max_det] points (truncated to poly_cap). */
+int va_post_polygons(void* stream, const va_post_args* p, float* polys, int32_t* poly_n, int32_t poly_cap);
+
 /* ABI self-check: writes sizeof() of va_nav_dims, va_frame_hdr, va_query_hdr, va_conv_args, va_seg_op,
- * va_cand, va_det, va_mask_stat, va_post_args (in that order) into out[0..n-1]; returns how many. */
+ * va_cand, va_det, va_mask_stat, va_post_args, va_contour_stat, va_mask_select_args (in that order) into
+ * out[0..n-1]; returns how many. */
 int va_abi_struct_sizes(int64_t* out, int32_t n);
 
 /* Library version / build info string. */

@@ -15,11 +15,9 @@ vendored spec copies in the reference:
   NMS             testing/old/segmenting_using_tflite/ops.py:214-363 (+ torchvision.ops.nms:
                   greedy, IoU > iou_thres suppresses; ties kept in index order here)
   process_mask    ops.py:707-737 (coef @ proto, crop to box/4, bilinear x4, > 0)
-  mask -> grid    FrameProcessor.py:67-86 via Results.masks.xy (ops.py:837-859 'largest').
-                  PARITY UNPINNED: cv2.findContours / contourArea / fillPoly are not available.
-                  Restated as: instance with the most mask pixels (first wins), its whole
-                  mask as the filled polygon, its pixel bounding box as boundingRect.  Exact
-                  for single hole-free components.
+  mask -> grid    FrameProcessor.py:67-97 via Results.masks.xy (ops.py:837-859 'largest'):
+                  oracle/contours.py restates cv2.findContours / contourArea / boundingRect /
+                  fillPoly (PARITY WITH cv2 UNPINNED: OpenCV is not installed).
 """
 from __future__ import annotations
 
@@ -217,19 +215,30 @@ def process_mask(proto: torch.Tensor, coef: torch.Tensor, boxes: torch.Tensor, H
     return masks.gt_(0.0)
 
 
-def select_mask(masks: torch.Tensor):
-    """Restated FrameProcessor.py:67-86 (see module docstring: parity unpinned vs OpenCV).
-    -> (filled uint8 [H, W] or None, rect (x, y, w, h))."""
+def select_mask(masks: torch.Tensor, frame_hw: tuple[int, int] | None = None):
+    """FrameProcessor.py:67-97 on the instance masks of one frame (network resolution): the instance of max
+    contourArea of its Results.masks.xy polygon, np.int32, boundingRect, fillPoly -- oracle/contours.py.
+    -> (uint8 [H0, W0] image whose cell centres hold the filled polygon's samples, or None when there is no
+    detection; rect (x, y, w, h)); frame_hw = the frame the network input was letterboxed from (default: the same)."""
+    import numpy as np
+    from oracle import contours as C
+    H, W = masks.shape[1:] if masks.dim() == 3 else (0, 0)
+    frame_hw = frame_hw or (H, W)
     if masks.shape[0] == 0:
         return None, (0, 0, 0, 0)
-    counts = masks.flatten(1).sum(1)
-    i = int(torch.argmax(counts))  # first maximum
-    if counts[i] == 0:
-        return None, (0, 0, 0, 0)
-    m = masks[i].to(torch.uint8)
-    ys, xs = torch.nonzero(m, as_tuple=True)
-    x0, x1, y0, y1 = int(xs.min()), int(xs.max()), int(ys.min()), int(ys.max())
-    return m, (x0, y0, x1 - x0 + 1, y1 - y0 + 1)
+    k, pts, rect, cells = C.select_cells(masks.numpy().astype(np.uint8), frame_hw)
+    img = np.kron(cells, np.ones((20, 20), dtype=np.uint8))
+    return torch.from_numpy(img), rect
+
+
+def select_cells(masks: torch.Tensor, frame_hw: tuple[int, int] | None = None):
+    """-> (chosen index or -1, int32 polygon, rect, cells [H0/20, W0/20]) (oracle/contours.select_cells)."""
+    import numpy as np
+    from oracle import contours as C
+    frame_hw = frame_hw or tuple(masks.shape[1:])
+    if masks.shape[0] == 0:
+        return -1, np.zeros((0, 2), np.int32), (0, 0, 0, 0), np.zeros((frame_hw[0] // 20, frame_hw[1] // 20), np.uint8)
+    return C.select_cells(masks.numpy().astype(np.uint8), frame_hw)
 
 
 def predict(arch, fw, frames_bgr_u8: torch.Tensor, conf=0.5, iou=0.7, max_det=300, max_nms=30000):

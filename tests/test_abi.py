@@ -68,12 +68,14 @@ def test_struct_layouts_match_python_mirrors():
     import numpy as np
     from vision_assist_amd import _lib
     from vision_assist_amd.nav import FRAME_HDR, QUERY_HDR
-    from vision_assist_amd.post import PostArgs
+    from vision_assist_amd.post import CSTAT_DTYPE, ContourStat, MaskSelectArgs, PostArgs
     from vision_assist_amd.seg import ConvArgs, SegOp
     lib = _lib.load()
-    out = (ctypes.c_int64 * 9)()
-    assert lib.va_abi_struct_sizes(out, 9) == 9
+    out = (ctypes.c_int64 * 11)()
+    assert lib.va_abi_struct_sizes(out, 11) == 11
     want = [ctypes.sizeof(_lib.VaNavDims), FRAME_HDR.itemsize, QUERY_HDR.itemsize, ctypes.sizeof(ConvArgs),
-            ctypes.sizeof(SegOp), 32, 32, 32, ctypes.sizeof(PostArgs)]
+            ctypes.sizeof(SegOp), 32, 32, 32, ctypes.sizeof(PostArgs), ctypes.sizeof(ContourStat),
+            ctypes.sizeof(MaskSelectArgs)]
+    assert np.dtype(CSTAT_DTYPE).itemsize == ctypes.sizeof(ContourStat)
     assert list(out) == want
     del np

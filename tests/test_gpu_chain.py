@@ -22,6 +22,7 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import contours as C
 from oracle import nav as onav
 from oracle import yolo_ref as Y
 
@@ -71,13 +72,12 @@ def _oracle_chain(regime, cls_bias):
         with torch.no_grad():
             for i in range(B):
                 det, masks = Y.predict(arch, fw, frames[i:i + 1])[0]
-                m, rect = Y.select_mask(masks)
-                rec = {"det": det[:, :6].clone(), "chosen": -1, "rect": None, "cells": None, "paths": None}
-                if m is not None:
-                    rec["chosen"] = int(torch.argmax(masks.flatten(1).sum(1)))
+                k, _pts, rect, cells = Y.select_cells(masks)
+                rec = {"det": det[:, :6].clone(), "chosen": k, "rect": None, "cells": None, "paths": None}
+                if k >= 0:
                     rec["rect"] = tuple(int(v) for v in rect)
-                    mn = m.numpy()
-                    rec["cells"] = mn[10::20, 10::20].copy()
+                    rec["cells"] = cells
+                    mn = np.kron(cells, np.ones((20, 20), np.uint8))
                     nav = onav.frame_nav(mn, rect, 640, 640, pf)
                     rec["paths"] = [[(c.coords.x, c.coords.y) for c in q[2]] for q in nav["queries"]]
                 out.append(rec)
@@ -223,21 +223,18 @@ def test_predict_720x1280_letterboxed_matches_oracle():
         x = Y.letterbox_np(frame, Hn, Wn, top, left, newh, neww)
         with torch.no_grad():
             det, masks = Y.predict(model.arch, model.folded, torch.from_numpy(x[None]))[0]
-        m, rect = Y.select_mask(masks)
-        assert (r.masks is None) == (m is None)
-        if m is None:
+        k, pts, rect, want = Y.select_cells(masks, (H0, W0))
+        assert (r.masks is None) == (k < 0)
+        if k < 0:
             continue
         cells = r.masks.cells.cpu().numpy()
         assert cells.shape == (H0 // 20, W0 // 20)
-        mn = m.numpy()
-        ys = np.clip(np.floor((np.arange(H0 // 20) * 20 + 10) * gain + py).astype(int), 0, Hn - 1)
-        xs = np.clip(np.floor((np.arange(W0 // 20) * 20 + 10) * gain + px).astype(int), 0, Wn - 1)
-        want = mn[ys][:, xs]
         assert int((cells != want).sum()) <= 1
-        x0, y0, w, h = rect
-        fx = lambda v: int(min(max((v - px) / gain, 0), W0))  # noqa: E731
-        fy = lambda v: int(min(max((v - py) / gain, 0), H0))  # noqa: E731
-        wr = (fx(x0), fy(y0), fx(x0 + w - 1) - fx(x0) + 1, fy(y0 + h - 1) - fy(y0) + 1)
-        assert max(abs(a - b) for a, b in zip(r.masks.rect, wr)) <= 2, (r.masks.rect, wr)
+        assert max(abs(a - b) for a, b in zip(r.masks.rect, rect)) <= 2, (r.masks.rect, rect)
+        assert len(r.masks.xy) == det.shape[0]
+        assert r.masks.chosen == k
+        # the chosen polygon of masks.xy is the one the cells / rect came from (np.int32 -> boundingRect)
+        assert r.masks.xy[k].dtype == np.float32
+        assert C.bounding_rect(r.masks.xy[k].astype(np.int32)) == tuple(r.masks.rect)
         checked += 1
     assert checked >= 1

@@ -1,0 +1,43 @@
+"""The mask -> polygon -> cells boundary on the GPU (va_post_select_masks: post_contour_kernel + post_fill_kernel)
+against oracle/contours.py, bit for bit, on the same binary masks (tests/contour_cases.py): holes, several
+components, islands behind one- and three-pixel walls, thin lines, single pixels, empty masks, masks at the
+network input's edges and seeded random blobs; frames equal to the network input (640 x 640), letterboxed
+720 x 1280 camera frames (gain 0.5, pad 12: integer scale_coords) and 500 x 880 frames (gain 0.7272..., pad
+10.18: fractional float32 scale_coords).
+
+Per frame: the chosen instance (max contourArea, first maximum), boundingRect, the fillPoly samples at every cell
+centre; per instance: the point count of its largest external contour, the number of external contours, its
+contourArea (float64, exact) and the Results.masks.xy polygon (float32, exact).  Parity with cv2 itself is
+unpinned (OpenCV is absent): the oracle is the restatement.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import contours as C
+from tests.contour_cases import frames_of
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("Hn,Wn,H0,W0", [(640, 640, 640, 640), (384, 640, 720, 1280), (384, 640, 500, 880)])
+def test_select_masks_matches_oracle(Hn, Wn, H0, W0):
+    from vision_assist_amd.post import select_masks
+    masks, n = frames_of(Hn, Wn, seed=Hn + W0)
+    got = select_masks(torch.from_numpy(masks).cuda(), torch.from_numpy(n), H0, W0)
+    assert (got["status"] == 0).all()
+    for b in range(masks.shape[0]):
+        ms = masks[b, :n[b]]
+        xy = C.masks_xy(ms, (H0, W0))
+        for k in range(n[b]):
+            segs = C.find_contours_external(ms[k])
+            st = got["cstats"][b, k]
+            assert st["ncont"] == len(segs), (b, k)
+            assert st["npts"] == (max(len(s) for s in segs) if segs else 0), (b, k)
+            assert st["area"] == C.contour_area(xy[k]), (b, k, st["area"], C.contour_area(xy[k]))
+            assert np.array_equal(got["polys"][b][k], xy[k]), (b, k)
+        kk, pts, rect, cells = C.select_cells(ms, (H0, W0))
+        assert got["chosen"][b] == kk, (b, got["chosen"][b], kk)
+        assert tuple(got["rects"][b]) == rect, (b, tuple(got["rects"][b]), rect)
+        assert np.array_equal(got["cells"][b], cells), (b, int((got["cells"][b] != cells).sum()))
+

@@ -1,0 +1,54 @@
+"""HIP-graph capture of the network + post-processing of a FramePipeline (FramePipeline.seg_post: letterbox-free
+preprocess, the forward, decode, NMS, masks, contours, the mask choice), replayed once and compared bit for bit
+with the eager run -- the round-1 capture faulted on replay (post_nms_kernel's 150 KiB of dynamic LDS was never
+set on the function for a graph kernel node; va_post.hip now sets it explicitly, per device)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("scale,dtype,B,regime", [("n", "bf16", 1, "dense"), ("s", "f32", 2, "mid")])
+def test_graph_replay_equals_eager(scale, dtype, B, regime):
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_NEVER
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch(scale)
+    bias = {"mid": 0.0, "dense": 4.0}[regime]
+    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=bias)), B, 640, 640,
+                         dtype=dtype)
+    pipe.frames.copy_(torch.randint(0, 256, pipe.frames.shape, generator=torch.Generator().manual_seed(2),
+                                    dtype=torch.uint8).cuda())
+
+    def outs():
+        p = pipe.post
+        return [p.ndet, p.cells, p.rects, p.chosen, pipe.plan["out"].proto] + list(pipe.plan["out"].levels)
+
+    def per_det():  # rows past a frame's ndet are not written
+        p = pipe.post
+        n = p.ndet.tolist()
+        return [t[b, :n[b]].clone() for t in (p.dets, p.stats, p.cstats) for b in range(B)]
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            pipe.seg_post(plant_mode=PLANT_NEVER)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in outs()]
+    ref_det = per_det()
+    assert int(ref[0].sum()) > 0, "the regime produced no detection"
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        pipe.seg_post(plant_mode=PLANT_NEVER)
+    torch.cuda.synchronize()
+    for t in outs() + [pipe.post.dets, pipe.post.stats, pipe.post.cstats]:
+        t.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    same = [bool(torch.equal(a, b)) for a, b in zip(outs(), ref)]
+    assert all(same), same
+    same = [bool(torch.equal(a, b)) for a, b in zip(per_det(), ref_det)]
+    assert all(same), same

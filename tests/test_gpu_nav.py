@@ -111,3 +111,24 @@ def test_nav_sample_cells_matches_lattice():
     eng = _engine(640, 640, 3)
     got = eng.sample_cells(torch.tensor(masks).cuda()).cpu().numpy()
     assert np.array_equal(got, masks[:, 10::20, 10::20])
+
+
+@pytest.mark.parametrize("rect,err", [((600, 100, 41, 100), True), ((100, 600, 100, 41), True),
+                                      ((0, 40, 641, 200), False), ((20, 0, 600, 640), False)])
+def test_nav_rect_past_the_frame(rect, err):
+    """FrameProcessor.py:79-97: the snapped rect's cell centres index mask_img; a rect reaching past the frame
+    (a polygon clipped onto x = W0 / y = H0, rounded up to whole cells) raises numpy's IndexError there -- the
+    device frame status is VA_FRAME_INDEX_ERROR; w alone is clamped to the frame width (no error)."""
+    H = W = 640
+    g = corridor_cells(4242, H // 20, W // 20)
+    eng = _engine(H, W, 1)
+    res = eng.run(torch.tensor(g[None].astype(np.uint8)).cuda(), torch.tensor([rect], dtype=torch.int32).cuda(),
+                  _seen())
+    nf = res.frame(0)
+    if err:
+        with pytest.raises(IndexError):
+            onav.frame_nav(cells_to_mask(g), rect, H, W, onav.PathFinderOracle())
+        assert nf.status == 2  # VA_FRAME_INDEX_ERROR
+    else:
+        out = onav.frame_nav(cells_to_mask(g), rect, H, W, onav.PathFinderOracle())
+        _oracle_compare(nf, out, set(), [q[4] for q in out["queries"]], str(rect))

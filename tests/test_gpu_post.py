@@ -61,19 +61,15 @@ def test_post_matches_oracle(regime, cls_bias):
         cnt_gpu = st[:, 0].long()
         tol = torch.clamp((cnt_ref.float() * 5e-4).long(), min=2)
         assert ((cnt_gpu - cnt_ref).abs() <= tol).all(), (cnt_gpu - cnt_ref).abs().max()
-        m, rect = Y.select_mask(masks)
+        k_ref, _pts, rect, cells_ref = Y.select_cells(masks)
         chosen = int(post.chosen[b])
-        if m is None:
-            assert chosen < 0
-            continue
-        k_ref = int(torch.argmax(cnt_ref))
         assert chosen == k_ref
+        if k_ref < 0:
+            continue
         got_rect = tuple(int(v) for v in post.rects[b].cpu())
         assert max(abs(g - r) for g, r in zip(got_rect, rect)) <= 1, (got_rect, rect)
-        cells_ref = m[10::20, 10::20].numpy()
         cells_gpu = post.cells[b].cpu().numpy()
         assert (cells_ref != cells_gpu).sum() <= 1
-
 
 def test_nms_long_candidate_list_matches_oracle():
     """1280 x 1280 dense regime: > 16384 candidates per frame, so the NMS takes its batched path (exact radix
@@ -232,8 +228,8 @@ def test_letterbox_kernel_matches_restatement(H0, W0):
 
 def test_letterboxed_mask_choice_in_frame_coordinates():
     """720 x 1280 frame -> 384 x 640 network input: the chosen mask's cells and boundingRect come back in frame
-    coordinates (cell centre (X, Y) -> network pixel (X * gain + pad_x, Y * gain + pad_y); rect corners
-    (v - pad) / gain, clipped, truncated -- scale_coords), against the oracle on the same head outputs."""
+    coordinates (the chosen polygon scale_coords'd to the frame, np.int32, boundingRect, fillPoly sampled at the
+    frame's cell centres), against the oracle on the same head outputs."""
     from vision_assist_amd import _lib
     from vision_assist_amd.post import PostEngine, letterbox_geometry
     from vision_assist_amd.seg import SegNet
@@ -259,23 +255,14 @@ def test_letterboxed_mask_choice_in_frame_coordinates():
     det = Y.nms_image(pred[0], coef[0])
     assert det.shape[0] > 0, "regime produced no detection"
     masks = Y.process_mask(proto[0], det[:, 6:], det[:, :4], Hn, Wn)
-    m, (rx, ry, rw, rh) = Y.select_mask(masks)
-    assert m is not None
-    LR, LC = H0 // 20, W0 // 20
-    yy = np.floor((np.arange(LR) * 20 + 10) * gain + py).astype(int)
-    xx = np.floor((np.arange(LC) * 20 + 10) * gain + px).astype(int)
-    cells_ref = m.numpy()[yy][:, xx]
+    k_ref, _pts, rect, cells_ref = Y.select_cells(masks, (H0, W0))
+    assert k_ref >= 0
+    assert int(post.chosen[0]) == k_ref
     cells_gpu = post.cells[0].cpu().numpy()
-    assert cells_gpu.shape == (LR, LC)
+    assert cells_gpu.shape == (H0 // 20, W0 // 20)
     assert (cells_ref != cells_gpu).sum() <= 1
-
-    def fx(v, pad, lim):
-        return int(min(max((v - pad) / gain, 0.0), lim))
-    x0, x1 = fx(rx, px, W0), fx(rx + rw - 1, px, W0)
-    y0, y1 = fx(ry, py, H0), fx(ry + rh - 1, py, H0)
-    got = [int(v) for v in post.rects[0].cpu()]
-    want = [x0, y0, x1 - x0 + 1, y1 - y0 + 1]
-    assert max(abs(g - w) for g, w in zip(got, want)) <= 2, (got, want)
+    got = tuple(int(v) for v in post.rects[0].cpu())
+    assert max(abs(g - w) for g, w in zip(got, rect)) <= 2, (got, rect)
 
 
 def test_pipeline_720x1280_frames_letterboxed_nav_matches_oracle():

@@ -1,8 +1,9 @@
-"""Single-frame latency (BASELINE.json configs[1], C2: YOLOv8n-seg 640x640 bf16 on 1 MI355X): one frame
-resident in HBM -> segmentation forward (+ post-processing + grid/penalty/protrusion/A* for `end_to_end`),
-synchronised after every frame; median and p90 over --iters runs after a warm-up, planted corridor masks so
-the nav stage always runs.  Prints one JSON line.
-    python tools/latency.py [--scale n] [--res 640] [--iters 200]"""
+"""Single-frame latency (BASELINE.json configs[1], C2: YOLOv8n-seg 640x640 on 1 MI355X; exact f32 by default,
+the reference's precision): one frame resident in HBM -> segmentation forward (+ post-processing +
+grid/penalty/protrusion/A* for `end_to_end`), synchronised after every frame; median and p90 over --iters runs
+after a warm-up, planted corridor masks so the nav stage always runs.  `*_graph`: the frame copy, network and
+post-processing replayed as one captured HIP graph.  Prints one JSON line.
+    python tools/latency.py [--scale n] [--res 640] [--iters 200] [--dtype f32|bf16]"""
 import argparse
 import json
 import os
@@ -20,6 +21,7 @@ def main():
     ap.add_argument("--scale", default="n")
     ap.add_argument("--res", type=int, default=640)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     args = ap.parse_args()
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_ALWAYS
@@ -27,14 +29,37 @@ def main():
     from workloads.corridors import cells_rect, corridor_cells
     H = W = args.res
     arch = Arch(args.scale)
-    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0)), 1, H, W, dtype="bf16")
+    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0)), 1, H, W, dtype=args.dtype)
     g = corridor_cells(11, H // 20, W // 20)
     pc = torch.tensor(g[None].astype(np.uint8)).cuda()
     pr = torch.tensor(np.array([cells_rect(g)], dtype=np.int32)).cuda()
     frame = torch.randint(0, 256, (1, H, W, 3), generator=torch.Generator().manual_seed(1), dtype=torch.uint8).cuda()
-    out = {"config": f"C2 shape: YOLOv8{args.scale}-seg {H}x{W} bf16, batch 1, 1 MI355X", "iters": args.iters}
+    out = {"config": f"C2 shape: YOLOv8{args.scale}-seg {H}x{W} {args.dtype}, batch 1, 1 MI355X", "iters": args.iters}
+    # the frame copy + network + post-processing captured once as a HIP graph (the nav stage reads a device flag
+    # on the host per speculative A* round, so it stays eager)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            pipe.load(frame)
+            pipe.seg_post(pc, pr, PLANT_ALWAYS)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        pipe.load(frame)
+        pipe.seg_post(pc, pr, PLANT_ALWAYS)
+    torch.cuda.synchronize()
+    out["ndet"] = int(pipe.post.ndet[0])
+
+    def graph_e2e():
+        graph.replay()
+        pipe.nav_run()
+
     for name, fn in (("seg_only", lambda: pipe.run_seg_only()),
-                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS))):
+                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS)),
+                     ("seg_post_graph", graph.replay),
+                     ("end_to_end_graph", graph_e2e)):
         for _ in range(20):
             fn()
         torch.cuda.synchronize()

@@ -68,6 +68,9 @@ SIGNATURES = [
     ("va_prof_enable", I32, [I32]),
     ("va_post_anchors", I32, [I32, I32]),
     ("va_post_run", I32, [P, P]),
+    ("va_contour_scratch_bytes", I32, [I32, I32, I32, I32, P, P, P]),
+    ("va_post_select_masks", I32, [P, P]),
+    ("va_post_polygons", I32, [P, P, P, P, I32]),
     ("va_letterbox", I32, [P, P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_abi_struct_sizes", I32, [P, I32]),
     ("va_version", ctypes.c_char_p, []),

@@ -223,7 +223,10 @@ __global__ __launch_bounds__(VA_NAV_THREADS) void nav_grid_kernel(GridArgs a) {
         w = (w % VA_GRID != 0) ? w + (VA_GRID - w % VA_GRID) : w;
         w = w > d.W ? d.W : w;
         h = (h % VA_GRID != 0) ? h + (VA_GRID - h % VA_GRID) : h;
-        if (status == VA_FRAME_OK && (x < 0 || y < 0 || x + w > d.W || y + h > d.H)) status = VA_FRAME_NO_MASK;
+        // :94-97 index mask_img at every cell centre of the snapped rect: a centre past the frame (a polygon
+        // clipped onto x = W0 / y = H0 by scale_coords, then rounded up to whole cells) is numpy's IndexError
+        if (status == VA_FRAME_OK && (x < 0 || y < 0)) status = VA_FRAME_NO_MASK;  // (never: points are >= 0)
+        if (status == VA_FRAME_OK && (x + w > d.W || y + h > d.H)) status = VA_FRAME_INDEX_ERROR;
         sh[S_STATUS] = status;
         sh[S_X0] = x;
         sh[S_Y0] = y;
@@ -1067,7 +1070,8 @@ int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen
 int va_abi_struct_sizes(int64_t* out, int32_t n) {
     const int64_t sz[] = {(int64_t)sizeof(va_nav_dims), (int64_t)sizeof(va_frame_hdr), (int64_t)sizeof(va_query_hdr),
                           (int64_t)sizeof(va_conv_args), (int64_t)sizeof(va_seg_op),    (int64_t)sizeof(va_cand),
-                          (int64_t)sizeof(va_det),       (int64_t)sizeof(va_mask_stat), (int64_t)sizeof(va_post_args)};
+                          (int64_t)sizeof(va_det),       (int64_t)sizeof(va_mask_stat), (int64_t)sizeof(va_post_args),
+                          (int64_t)sizeof(va_contour_stat), (int64_t)sizeof(va_mask_select_args)};
     int k = (int)(sizeof sz / sizeof sz[0]);
     if (!out) return k;
     for (int i = 0; i < n && i < k; ++i) out[i] = sz[i];

@@ -11,14 +11,15 @@
 //   post_mask_kernel     process_mask(upsample=True) (ops.py:707-737): coef . proto over the cropped
 //                        low-res box region into LDS, bilinear x4 (align_corners=False), > 0; per
 //                        instance pixel count and pixel bounding box.  One workgroup per detection.
-//   post_select_kernel   FrameProcessor.py:67-97 restated (cv2 absent, parity unpinned): the instance
-//                        with the most mask pixels (first wins), its pixel bbox as boundingRect, its
-//                        mask sampled at the 20-px cell centres -> the nav stage's (cells, rect);
-//                        optional planted masks (bench / tests) when the network yields none.
+//   mask choice          FrameProcessor.py:67-97 with OpenCV's findContours / contourArea / boundingRect /
+//                        fillPoly restated (va_contour.hip, checked against oracle/contours.py; cv2 parity
+//                        unpinned) -> the nav stage's (cells, rect); optional planted masks (bench / tests) when
+//                        the network yields no detection.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/va355.h"
+#include "va_contour.h"
 #include "va_dev.h"
 
 namespace {
@@ -233,7 +234,8 @@ __device__ unsigned long long nms_select(const unsigned long long* keys, int n, 
 // keys (score bits | ~anchor | list index) bitonic-sorted descending in LDS -- the order the greedy scan
 // visits candidates in (highest score, lowest anchor on ties) -- then 64-candidate chunks: each candidate
 // tested against every box kept so far (16 threads per candidate), the chunk's own pairwise suppression
-// as one 64-bit ballot per row, and a one-lane scan of the chunk in order.  Same kept set and order as
+// as one 64-bit ballot per row, and the chunk scanned in order on one wave (take the lowest live candidate,
+// drop the candidates its row suppresses: one iteration per kept box, the kept boxes written in parallel).  Same kept set and order as
 // the repeated "highest remaining -> keep -> suppress" loop of the fallback path, which keeps the
 // candidates that do not fit (keys in LDS up to NMS_CAP, else in global scratch).
 // max_nms (ops.py:332-333, 30000): a list longer than that is first cut to its max_nms highest-scoring
@@ -281,8 +283,11 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 const int want = min(NMS_CAP, max_nms - taken);
                 if (tid == 0) s_m = 0;
                 __syncthreads();
-                for (int i = tid; i < n; i += NMS_THREADS)
-                    if (gk[i] < hi) atomicAdd(&s_m, 1);
+                for (int i0 = 0; i0 < n; i0 += NMS_THREADS) {  // one LDS atomic per wave
+                    const int i = i0 + tid;
+                    const unsigned long long bal = __ballot(i < n && gk[i] < hi);
+                    if ((tid & 63) == 0 && bal) atomicAdd(&s_m, __popcll(bal));
+                }
                 __syncthreads();
                 const int rem = s_m;
                 __syncthreads();  // everyone has read s_m before it is reused
@@ -290,9 +295,15 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 const unsigned long long T = rem > want ? nms_select(gk, n, hi, want, s_hist, &s_T, &s_k) : 0ull;
                 if (tid == 0) s_m = 0;
                 __syncthreads();
-                for (int i = tid; i < n; i += NMS_THREADS) {
-                    const unsigned long long kk = gk[i];
-                    if (kk >= T && kk < hi) sk[atomicAdd(&s_m, 1)] = kk;
+                for (int i0 = 0; i0 < n; i0 += NMS_THREADS) {  // wave-aggregated compaction (sorted below)
+                    const int i = i0 + tid, lane = tid & 63;
+                    const unsigned long long kk = i < n ? gk[i] : 0ull;
+                    const bool in = i < n && kk >= T && kk < hi;
+                    const unsigned long long bal = __ballot(in);
+                    int base = 0;
+                    if (lane == 0 && bal) base = atomicAdd(&s_m, __popcll(bal));
+                    base = __shfl(base, 0, 64);
+                    if (in) sk[base + __popcll(bal & ((1ull << lane) - 1ull))] = kk;
                 }
                 __syncthreads();
                 nb = s_m;
@@ -348,18 +359,26 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                 }
             }
             __syncthreads();
-            if (tid == 0) {
+            if (tid < 64) {  // the in-order scan on wave 0: lowest live candidate -> keep -> drop the rows it hits
+                const unsigned long long row = cm[tid];
+                unsigned long long live = __ballot(tid < m && !sup[tid]), keep = 0;
                 int kk = kept;
-                unsigned long long removed = 0;
-                for (int t = 0; t < m && kk < max_det; ++t) {
-                    if (sup[t] || ((removed >> t) & 1ull)) continue;
-                    removed |= cm[t];
-                    kb[kk] = cb[t];
-                    ka[kk] = ca[t];
-                    D[kk] = to_det(C[sk[c0 + t] & 0xFFFF]);
+                while (live && kk < max_det) {  // wave-uniform
+                    const int t = __builtin_ctzll(live);
+                    keep |= 1ull << t;
                     ++kk;
+                    const unsigned long long rt =
+                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(row >> 32), t) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)row, t);
+                    live &= ~(rt | (1ull << t));
                 }
-                s_kept = kk;
+                if ((keep >> tid) & 1ull) {
+                    const int r = kept + __popcll(keep & ((1ull << tid) - 1ull));
+                    kb[r] = cb[tid];
+                    ka[r] = ca[tid];
+                    D[r] = to_det(C[sk[c0 + tid] & 0xFFFF]);
+                }
+                if (tid == 0) s_kept = kk;
             }
             __syncthreads();
         }
@@ -444,8 +463,6 @@ struct MaskArgs {
     const va_det* dets;
     const int32_t* ndet;
     va_mask_stat* stats;  // [B][max_det]
-    int H0, W0, pad_x, pad_y;  // letterbox (va_post_args): H0 = 0 identity
-    float gain;
 };
 
 __device__ inline const float* coef_of(const MaskArgs& a, int b, int anchor) {
@@ -641,85 +658,6 @@ __global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
     if (tid == 0) *st = va_mask_stat{s_cnt, s_x0, s_y0, s_x1, s_y1, {0, 0, 0}};
 }
 
-__device__ float mask_value_at(const MaskArgs& a, int b, const va_det& d, const float* coef, int X, int Y) {
-    int rx0, rx1, ry0, ry1;
-    crop_window(d, a.W, a.H, a.mw, a.mh, &rx0, &rx1, &ry0, &ry1);
-    const float sx = (float)a.mw / (float)a.W, sy = (float)a.mh / (float)a.H;
-    int xa, xb, ya, yb;
-    float wx0, wx1, wy0, wy1;
-    taps(X, sx, a.mw, &xa, &xb, &wx0, &wx1);
-    taps(Y, sy, a.mh, &ya, &yb, &wy0, &wy1);
-    auto val = [&](int yy, int xx) -> float {
-        if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
-        const float* p = a.proto + (((int64_t)b * a.mh + yy) * a.mw + xx) * NMC;
-        float s = 0.f;
-        for (int c = 0; c < NMC; ++c) s += coef[c] * p[c];
-        return s;
-    };
-    return wy0 * (wx0 * val(ya, xa) + wx1 * val(ya, xb)) + wy1 * (wx0 * val(yb, xa) + wx1 * val(yb, xb));
-}
-
-__global__ void post_select_kernel(MaskArgs a, const uint8_t* plant_cells, const int32_t* plant_rects,
-                                   int plant_mode, uint8_t* cells, int32_t* rects, int32_t* chosen) {
-    const int b = blockIdx.x, tid = threadIdx.x;
-    const bool lb = a.H0 > 0;  // letterboxed: cells / rects in frame coordinates
-    const int H0 = lb ? a.H0 : a.H, W0 = lb ? a.W0 : a.W;
-    const float gain = lb ? a.gain : 1.0f, px = lb ? (float)a.pad_x : 0.0f, py = lb ? (float)a.pad_y : 0.0f;
-    const int LR = H0 / VA_GRID, LC = W0 / VA_GRID;
-    __shared__ int s_k;
-    __shared__ float coef[NMC];
-    if (tid == 0) {
-        int best = -1;
-        long long bc = 0;
-        int n = a.ndet[b];
-        for (int k = 0; k < n; ++k) {
-            int c = a.stats[(int64_t)b * a.max_det + k].count;
-            if (c > bc) {  // strict: the first maximum wins
-                bc = c;
-                best = k;
-            }
-        }
-        if (plant_mode == 2 || (best < 0 && plant_mode == 1)) best = -2;  // planted
-        s_k = best;
-        chosen[b] = best;
-    }
-    __syncthreads();
-    const int k = s_k;
-    uint8_t* out = cells + (int64_t)b * LR * LC;
-    if (k == -2) {
-        for (int i = tid; i < LR * LC; i += blockDim.x) out[i] = plant_cells[(int64_t)b * LR * LC + i];
-        if (tid < 4) rects[4 * b + tid] = plant_rects[4 * b + tid];
-        return;
-    }
-    if (k < 0) {
-        for (int i = tid; i < LR * LC; i += blockDim.x) out[i] = 0;
-        if (tid < 4) rects[4 * b + tid] = 0;  // no mask: w = h = 0
-        return;
-    }
-    const va_det d = a.dets[(int64_t)b * a.max_det + k];
-    if (tid < NMC) coef[tid] = coef_of(a, b, d.anchor)[tid];
-    __syncthreads();
-    for (int i = tid; i < LR * LC; i += blockDim.x) {
-        int r = i / LC, c = i % LC;
-        // the cell centre in network pixels (identity without letterbox)
-        const int X = min(a.W - 1, max(0, (int)floorf((float)(VA_GRID * c + VA_GRID / 2) * gain + px)));
-        const int Y = min(a.H - 1, max(0, (int)floorf((float)(VA_GRID * r + VA_GRID / 2) * gain + py)));
-        out[i] = mask_value_at(a, b, d, coef, X, Y) > 0.f;
-    }
-    if (tid == 0) {
-        const va_mask_stat s = a.stats[(int64_t)b * a.max_det + k];
-        // scale_coords: (network - pad) / gain, clipped to the frame, then np.int32 truncation
-        auto fx = [&](int v) { return (int)fminf(fmaxf(((float)v - px) / gain, 0.0f), (float)W0); };
-        auto fy = [&](int v) { return (int)fminf(fmaxf(((float)v - py) / gain, 0.0f), (float)H0); };
-        const int x0 = lb ? fx(s.x0) : s.x0, x1 = lb ? fx(s.x1) : s.x1;
-        const int y0 = lb ? fy(s.y0) : s.y0, y1 = lb ? fy(s.y1) : s.y1;
-        rects[4 * b + 0] = x0;
-        rects[4 * b + 1] = y0;
-        rects[4 * b + 2] = x1 - x0 + 1;
-        rects[4 * b + 3] = y1 - y0 + 1;
-    }
-}
-
 // LetterBox: one thread per destination pixel (3 bytes).  Resize = cv2.INTER_LINEAR on uint8 in its
 // fixed-point form: per axis src = (d + 0.5) / scale - 0.5, clamped at the borders, weights rounded to
 // 11 bits (w0 = round((1 - f) * 2048), w1 = 2048 - w0); the two passes combine as
@@ -775,6 +713,38 @@ __global__ void letterbox_kernel(const uint8_t* __restrict__ src, int H, int W, 
 }
 
 int grid1(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+// The mask choice of FrameProcessor.py:67-97 (cells != NULL) and / or Results.masks.xy (polys) for the detections
+// of the post-processing buffers p: va_contour.hip.
+int contours(hipStream_t st, const va_post_args* p, float* polys, int32_t* poly_n, int poly_cap, bool fill) {
+    const bool lb = p->H0 > 0;
+    const int H0 = lb ? p->H0 : p->H, W0 = lb ? p->W0 : p->W;
+    if (!p->cscratch || p->cslots <= 0 || p->ccap <= 0 || !p->cstats || H0 % VA_GRID || W0 % VA_GRID ||
+        H0 / VA_GRID > 64 || W0 / VA_GRID > 64 || p->H + 2 > 4096 || (lb && !(p->sc_gain > 0.0f)))
+        return VA_ERR_ARG;
+    if (fill && (!p->cells || !p->rects || !p->chosen || (p->plant_mode && (!p->plant_cells || !p->plant_rects))))
+        return VA_ERR_ARG;
+    CtSrc src{};
+    src.proto = p->proto;
+    for (int l = 0; l < 3; ++l) src.lv[l] = p->levels[l];
+    src.dets = p->dets;
+    src.nc = p->nc;
+    src.max_det = p->max_det;
+    src.ndet = p->ndet;
+    src.B = p->B;
+    src.Hn = p->H;
+    src.Wn = p->W;
+    src.mh = p->H / 4;
+    src.mw = p->W / 4;
+    CtFrame f{H0, W0, lb ? p->sc_gain : 1.0f, lb ? p->sc_padx : 0.0f, lb ? p->sc_pady : 0.0f};
+    CtScratch sc{(unsigned char*)p->cscratch, 0, 0, 0, p->cslots, p->ccap};
+    if (va_contour_scratch_bytes(p->H, p->W, p->cslots, p->ccap, &sc.slot_bytes, &sc.img_off, &sc.pts_off) != VA_OK)
+        return VA_ERR_ARG;
+    const hipError_t e = va_contour_launch(src, f, sc, p->cstats, p->max_det, p->plant_cells, p->plant_rects,
+                                           p->plant_mode, fill ? p->cells : nullptr, p->rects, p->chosen, p->cstatus,
+                                           polys, poly_n, poly_cap, st);
+    return e == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
 
 }  // namespace
 
@@ -849,21 +819,15 @@ int va_post_run(void* stream, const va_post_args* p) {
     ma.dets = p->dets;
     ma.ndet = p->ndet;
     ma.stats = p->stats;
-    ma.H0 = p->H0;
-    ma.W0 = p->W0;
-    ma.pad_x = p->pad_x;
-    ma.pad_y = p->pad_y;
-    ma.gain = p->gain;
     hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), mask_lds, st, ma);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    if (p->cells) {
-        if (p->H0 > 0 ? (p->H0 % VA_GRID || p->W0 % VA_GRID || !(p->gain > 0.0f)) : (p->H % VA_GRID || p->W % VA_GRID))
-            return VA_ERR_ARG;
-        hipLaunchKernelGGL(post_select_kernel, dim3(B), dim3(256), 0, st, ma, p->plant_cells, p->plant_rects,
-                           p->plant_mode, p->cells, p->rects, p->chosen);
-        if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    }
+    if (p->cells) return contours(st, p, nullptr, nullptr, 0, true);
     return VA_OK;
+}
+
+int va_post_polygons(void* stream, const va_post_args* p, float* polys, int32_t* poly_n, int32_t poly_cap) {
+    if (!p || !polys || !poly_n || poly_cap <= 0) return VA_ERR_ARG;
+    return contours((hipStream_t)stream, p, polys, poly_n, poly_cap, false);
 }
 
 }  // extern "C"

@@ -25,10 +25,47 @@ class PostArgs(ctypes.Structure):
         ("dets", VOIDP), ("ndet", VOIDP), ("stats", VOIDP),
         ("plant_cells", VOIDP), ("plant_rects", VOIDP),
         ("cells", VOIDP), ("rects", VOIDP), ("chosen", VOIDP),
-        ("H0", ctypes.c_int32), ("W0", ctypes.c_int32), ("pad_x", ctypes.c_int32), ("pad_y", ctypes.c_int32),
-        ("gain", ctypes.c_float),
+        ("H0", ctypes.c_int32), ("W0", ctypes.c_int32),
+        ("sc_gain", ctypes.c_float), ("sc_padx", ctypes.c_float), ("sc_pady", ctypes.c_float),
+        ("cscratch", VOIDP), ("cslots", ctypes.c_int32), ("ccap", ctypes.c_int32),
+        ("cstats", VOIDP), ("cstatus", VOIDP),
         ("max_nms", ctypes.c_int32),
     ]
+
+
+class ContourStat(ctypes.Structure):  # va_contour_stat
+    _fields_ = [(n, ctypes.c_int32) for n in ("npts", "ox", "oy", "ncont", "X0", "Y0", "status", "pad")] + \
+               [("area", ctypes.c_double)]
+
+
+class MaskSelectArgs(ctypes.Structure):  # va_mask_select_args
+    _fields_ = [("masks", VOIDP), ("nmask", VOIDP)] + \
+               [(n, ctypes.c_int32) for n in ("B", "maxn", "Hn", "Wn", "H0", "W0")] + \
+               [(n, ctypes.c_float) for n in ("gain", "padx", "pady")] + \
+               [("scratch", VOIDP), ("nslots", ctypes.c_int32), ("cap", ctypes.c_int32), ("cstats", VOIDP),
+                ("cells", VOIDP), ("rects", VOIDP), ("chosen", VOIDP), ("status", VOIDP), ("polys", VOIDP),
+                ("poly_n", VOIDP), ("poly_cap", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+CSTAT_DTYPE = [("npts", "<i4"), ("ox", "<i4"), ("oy", "<i4"), ("ncont", "<i4"), ("X0", "<i4"), ("Y0", "<i4"),
+               ("status", "<i4"), ("pad", "<i4"), ("area", "<f8")]
+CONTOUR_SLOTS = 1024   # contour scratch slots: one wave each, 4 per CU
+CONTOUR_CAP = 16384    # points of the chosen contour per frame (the fill kernel's buffer)
+
+
+def scale_coords_params(H: int, W: int, H0: int, W0: int) -> tuple[float, float, float]:
+    """ops.scale_coords(img1_shape=(H, W), ., img0_shape=(H0, W0)): gain and pad in double, as Ultralytics computes
+    them; the kernels use them rounded to float32 (numpy's float32 arithmetic on the float32 polygon)."""
+    gain = min(H / H0, W / W0)
+    return gain, (W - W0 * gain) / 2, (H - H0 * gain) / 2
+
+
+def contour_scratch(H: int, W: int, slots: int = CONTOUR_SLOTS, cap: int = CONTOUR_CAP, device=None) -> torch.Tensor:
+    lib = _lib.load()
+    sb, io, po = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(lib.va_contour_scratch_bytes(H, W, slots, cap, ctypes.byref(sb), ctypes.byref(io), ctypes.byref(po)),
+               "va_contour_scratch_bytes")
+    return torch.empty(slots * sb.value, dtype=torch.uint8, device=device)
 
 
 def letterbox_geometry(H: int, W: int, imgsz: int = 640, stride: int = 32):
@@ -73,9 +110,13 @@ class PostEngine:
         self.stats = torch.empty((B, max_det, 8), dtype=torch.int32, device=dev)
         self.frame = frame
         H0, W0 = (frame[0], frame[1]) if frame else (H, W)
+        self.H0, self.W0 = H0, W0
         self.cells = torch.empty((B, H0 // 20, W0 // 20), dtype=torch.uint8, device=dev)
         self.rects = torch.empty((B, 4), dtype=torch.int32, device=dev)
         self.chosen = torch.empty(B, dtype=torch.int32, device=dev)
+        self.cstats = torch.empty((B, max_det, ctypes.sizeof(ContourStat)), dtype=torch.uint8, device=dev)
+        self.cstatus = torch.empty(B, dtype=torch.int32, device=dev)
+        self.cscratch = contour_scratch(H, W, device=dev)
 
     def run(self, levels, proto, plant_cells=None, plant_rects=None, plant_mode=PLANT_NEVER, select=True,
             stream=None) -> None:
@@ -92,10 +133,39 @@ class PostEngine:
             a.plant_cells, a.plant_rects = plant_cells.data_ptr(), plant_rects.data_ptr()
         if select:
             a.cells, a.rects, a.chosen = self.cells.data_ptr(), self.rects.data_ptr(), self.chosen.data_ptr()
-        if self.frame:
-            a.H0, a.W0, a.gain, a.pad_x, a.pad_y = self.frame
+        self._fill_frame_args(a)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream, self.device), ctypes.byref(a)), "va_post_run")
+        self._last = (a, levels, proto)  # Results.masks.xy re-reads these buffers (polygons())
+
+    def _fill_frame_args(self, a: PostArgs) -> None:
+        if self.frame:
+            a.H0, a.W0 = self.H0, self.W0
+            a.sc_gain, a.sc_padx, a.sc_pady = scale_coords_params(self.H, self.W, self.H0, self.W0)
+        a.cscratch, a.cslots, a.ccap = self.cscratch.data_ptr(), CONTOUR_SLOTS, CONTOUR_CAP
+        a.cstats, a.cstatus = self.cstats.data_ptr(), self.cstatus.data_ptr()
+
+    def polygons(self, b: int, cap: int = 4096, stream=None) -> list:
+        """Results.masks.xy of frame b of the last run: per kept detection its largest external contour in frame
+        coordinates (float32 [k, 2], masks2segments 'largest' + scale_coords)."""
+        import numpy as np
+        a, _levels, _proto = self._last
+        polys = torch.empty((self.B, self.max_det, cap, 2), dtype=torch.float32, device=self.device)
+        pn = torch.zeros((self.B, self.max_det), dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_post_polygons(_lib.stream_ptr(stream, self.device), ctypes.byref(a), polys.data_ptr(),
+                                                 pn.data_ptr(), cap), "va_post_polygons")
+        n = int(self.ndet[b])
+        cnt = pn[b, :n].cpu().numpy()
+        if (cnt > cap).any():  # the kernel reports the full count: rerun with room for the longest
+            return self.polygons(b, cap=int(cnt.max()), stream=stream)
+        pts = polys[b, :n].cpu().numpy()
+        return [np.ascontiguousarray(pts[k, :cnt[k]]) for k in range(n)]
+
+    def contour_stats(self, b: int):
+        import numpy as np
+        n = int(self.ndet[b])
+        return self.cstats[b, :n].cpu().numpy().view(np.dtype(CSTAT_DTYPE)).reshape(n)
 
     def det_tensor(self, b: int) -> torch.Tensor:
         """Kept detections of frame b as float [k, 6] (x1, y1, x2, y2, score, cls) + anchors [k]."""
@@ -104,3 +174,38 @@ class PostEngine:
         f = raw.view(torch.float32)
         out = torch.cat([f[:, :5], raw[:, 5:6].float()], 1)
         return out, raw[:, 6].clone()
+
+
+def select_masks(masks: torch.Tensor, nmask: torch.Tensor, H0: int, W0: int, poly_cap: int = 4096, stream=None):
+    """The mask -> polygon -> cells boundary (va_post_select_masks) on given binary masks uint8 [B, maxn, Hn, Wn]
+    (device) with nmask[b] masks in frame b, mapped onto an H0 x W0 frame as scale_coords does.
+    -> dict(cells [B, H0/20, W0/20], rects [B, 4], chosen [B], status [B], cstats [B, maxn], polys list per frame)."""
+    import numpy as np
+    lib = _lib.load()
+    dev = masks.device
+    B, maxn, Hn, Wn = masks.shape
+    gain, padx, pady = scale_coords_params(Hn, Wn, H0, W0)
+    scratch = contour_scratch(Hn, Wn, device=dev)
+    cstats = torch.empty((B, maxn, ctypes.sizeof(ContourStat)), dtype=torch.uint8, device=dev)
+    cells = torch.empty((B, H0 // 20, W0 // 20), dtype=torch.uint8, device=dev)
+    rects = torch.empty((B, 4), dtype=torch.int32, device=dev)
+    chosen = torch.empty(B, dtype=torch.int32, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    polys = torch.empty((B, maxn, poly_cap, 2), dtype=torch.float32, device=dev)
+    pn = torch.zeros((B, maxn), dtype=torch.int32, device=dev)
+    nm = nmask.to(dev, torch.int32).contiguous()
+    m = masks.contiguous()
+    a = MaskSelectArgs(masks=m.data_ptr(), nmask=nm.data_ptr(), B=B, maxn=maxn, Hn=Hn, Wn=Wn, H0=H0, W0=W0,
+                       gain=gain, padx=padx, pady=pady, scratch=scratch.data_ptr(), nslots=CONTOUR_SLOTS,
+                       cap=CONTOUR_CAP, cstats=cstats.data_ptr(), cells=cells.data_ptr(), rects=rects.data_ptr(),
+                       chosen=chosen.data_ptr(), status=status.data_ptr(), polys=polys.data_ptr(), poly_n=pn.data_ptr(),
+                       poly_cap=poly_cap)
+    with torch.cuda.device(dev):
+        _lib.check(lib.va_post_select_masks(_lib.stream_ptr(stream, dev), ctypes.byref(a)), "va_post_select_masks")
+    torch.cuda.synchronize(dev)
+    cs = cstats.cpu().numpy().view(np.dtype(CSTAT_DTYPE)).reshape(B, maxn)
+    pnh, ph = pn.cpu().numpy(), polys.cpu().numpy()
+    nmh = nm.cpu().numpy()
+    return {"cells": cells.cpu().numpy(), "rects": rects.cpu().numpy(), "chosen": chosen.cpu().numpy(),
+            "status": status.cpu().numpy(), "cstats": cs,
+            "polys": [[ph[b, k, :pnh[b, k]] for k in range(nmh[b])] for b in range(B)]}

@@ -4,7 +4,8 @@
 does.  The network is YOLOv8-seg (n / s / m) running on the MI355X MFMA kernels
 of libva355.so; ``predict`` returns per-frame ``Results`` whose mask has already
 been reduced on the device to what FrameProcessor consumes (FrameProcessor.py:67-97):
-the chosen instance's cell-lattice samples and bounding rect.
+the chosen instance's cell-lattice samples and bounding rect, plus ``masks.xy`` (the
+per-detection polygons, traced on the device as findContours does).
 
 Weights: a ``.safetensors`` file with Ultralytics state-dict names (export one
 with ``safetensors.torch.save_file(model.model.state_dict(), path)`` where
@@ -25,17 +26,13 @@ from .seg_arch import Arch, fold, synthetic_state_dict
 
 
 class Masks:
-    """Device mask summary of one frame (the input of the grid stage)."""
+    """Device mask summary of one frame (the input of the grid stage) + Results.masks.xy."""
 
-    def __init__(self, cells: torch.Tensor, rect: tuple[int, int, int, int], chosen: int):
-        self.cells = cells      # uint8 [H/20, W/20] on the device
-        self.rect = rect        # boundingRect (x, y, w, h) of the chosen mask
-        self.chosen = chosen    # index of the chosen detection, -2 = planted
-
-    @property
-    def xy(self):
-        raise NotImplementedError("mask polygons (cv2.findContours) are not produced: the chosen mask is reduced to "
-                                  "cell samples + boundingRect on the GPU (see vision_assist_amd/csrc/va_post.hip)")
+    def __init__(self, cells: torch.Tensor, rect: tuple[int, int, int, int], chosen: int, xy: list | None = None):
+        self.cells = cells      # uint8 [H/20, W/20] on the device: fillPoly of the chosen polygon at cell centres
+        self.rect = rect        # boundingRect (x, y, w, h) of the chosen polygon
+        self.chosen = chosen    # index of the chosen detection (max contourArea), -2 = planted
+        self.xy = xy            # per detection: largest external contour in frame pixels, float32 [k, 2] (None: given cells)
 
 
 class Results:
@@ -105,6 +102,7 @@ class YOLO:
             chosen = int(pipe.post.chosen[0])
             masks = None
             if chosen >= 0:
-                masks = Masks(pipe.post.cells[0].clone(), tuple(int(v) for v in pipe.post.rects[0].cpu()), chosen)
+                masks = Masks(pipe.post.cells[0].clone(), tuple(int(v) for v in pipe.post.rects[0].cpu()), chosen,
+                              pipe.post.polygons(0))
             out.append(Results((H, W), det.numpy(), masks))
         return out
