@@ -38,8 +38,9 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # dense MFMA peaks, MI355X_MICROARCH.md chip table
-DEFAULT_BATCH = {"f32": 256, "bf16": 384}     # per-GPU batch (sweeps: DESIGN.md §5)
+# dense MFMA peaks, MI355X_MICROARCH.md chip table (fp8: the block-scaled e4m3 MFMA the fp8 convs run on)
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}
+DEFAULT_BATCH = {"f32": 256, "bf16": 384, "fp8": 8}  # per-GPU batch (sweeps: DESIGN.md §5; fp8: C5's 64 / 8 GPUs)
 PROF_KINDS = 8
 CONV_KINDS = (1, 5, 6, 7)  # va355.h VA_OP_CONV, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM
 
@@ -49,14 +50,16 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"], help="network arithmetic of the headline")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16", "fp8"],
+                   help="network arithmetic of the headline (fp8: the convs on e4m3 MFMA, BASELINE configs[4])")
     p.add_argument("--batch", type=int, default=0, help="frames per step per GPU (0 = the dtype's default)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
     p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
-    p.add_argument("--extras", default="bf16,dense",
+    p.add_argument("--extras", default="bf16,dense,c5",
                    help="comma list of extra measurements in the same run: bf16 (the bf16 MFMA pipeline), "
-                        "dense (300 detections per frame); 'none' to skip")
+                        "dense (300 detections per frame), c5 (YOLOv8m-seg 1280 on fp8 MFMA, batch 8); "
+                        "'none' to skip")
     p.add_argument("--cpu-sample", type=int, default=256,
                    help="frames timed for the CPU baseline (0 = skip; 256 = ~10-20 s)")
     p.add_argument("--no-prof", action="store_true", help="skip the HIP-event timing of the isolated forwards")
@@ -144,14 +147,15 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
 class Run:
     """One measured configuration: pipelines, resident inputs and the timed steps."""
 
-    def __init__(self, args, dev, rank, dtype, B, regime):
+    def __init__(self, args, dev, rank, dtype, B, regime, scale=None, res=None):
         from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
         from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
         self.args, self.dtype, self.B, self.regime = args, dtype, B, regime
+        self.scale, self.res = scale or args.scale, res or args.res
         cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0}[regime]
-        self.arch = Arch(args.scale)
+        self.arch = Arch(self.scale)
         self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, cls_bias=cls_bias))
-        H = W = args.res
+        H = W = self.res
         self.overlap = not args.no_overlap
         if self.overlap:
             self.opipe = OverlappedPipelines(self.arch, self.fw, B, H, W, dtype=dtype, device=dev,
@@ -165,7 +169,7 @@ class Run:
         for j in range(self.P):
             rng = np.random.default_rng(1000 * rank + j)
             self.frames.append(torch.from_numpy(rng.integers(0, 256, (B, H, W, 3), dtype=np.uint8)).to(dev))
-            c, r = planted_pool(B, args.res, 1000 * rank + j)
+            c, r = planted_pool(B, self.res, 1000 * rank + j)
             self.pcs.append(torch.from_numpy(c).to(dev))
             self.prs.append(torch.from_numpy(r).to(dev))
         torch.cuda.synchronize()
@@ -194,7 +198,7 @@ class Run:
     def measure(self, steps, warmup, world, prof=True) -> dict:
         from vision_assist_amd import _lib
         from vision_assist_amd.shard import timed
-        args, B, H = self.args, self.B, self.args.res
+        args, B, H = self.args, self.B, self.res
         self.steps(warmup)
         torch.cuda.synchronize()
         if self.overlap:
@@ -235,7 +239,7 @@ class Run:
         achieved = fl_exec / avg_s / 1e12
         rl = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
               "frac": round(achieved / peak, 5), "traffic": None,
-              "kernel": f"the {launches:.0f} conv-family launches of one YOLOv8{self.args.scale}-seg forward "
+              "kernel": f"the {launches:.0f} conv-family launches of one YOLOv8{self.scale}-seg forward "
                         f"({self.dtype} MFMA GEMM kernels: conv/conv2/conv4/conv_dn/conv_patch/pw/c2f/stem)",
               "flops_per_launch": round(fl_exec), "flops_per_launch_def": "executed GEMM FLOPs of the plan / launch",
               "avg_launch_us": round(avg_s * 1e6, 3),
@@ -251,7 +255,7 @@ class Run:
         if os.path.exists(traffic_file):
             with open(traffic_file) as f:
                 tr = json.load(f)
-            key = f"{self.args.scale}-{self.args.res}-b{B}-{self.dtype}"
+            key = f"{self.scale}-{self.res}-b{B}-{self.dtype}"
             if key in tr:
                 rl["traffic"] = tr[key]["hbm_bytes_per_launch"]
                 rl["traffic_source"] = f"profiles/conv_traffic.json[{key}] (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)"
@@ -308,13 +312,21 @@ def main():
             dt_, B_, reg_ = "bf16", args.batch or DEFAULT_BATCH["bf16"], args.regime
         elif ex == "dense" and args.regime != "dense":
             dt_, B_, reg_ = args.dtype, B, "dense"
+        elif ex == "c5" and not (args.scale == "m" and args.res == 1280 and args.dtype == "fp8"):
+            dt_, B_, reg_ = "fp8", DEFAULT_BATCH["fp8"], args.regime
         else:
             continue
-        r = Run(args, dev, rank, dt_, B_, reg_)
+        sc_, rs_ = ("m", 1280) if ex == "c5" else (None, None)
+        r = Run(args, dev, rank, dt_, B_, reg_, scale=sc_, res=rs_)
         m = r.measure(args.steps, min(args.warmup, 3), world, prof)
         r.release()
         e = {"value": round(m["value"], 2), "ms_per_step": round(m["ms_per_step"], 3), "dtype": dt_,
              "batch_per_gpu": B_, "regime": reg_}
+        if ex == "c5":
+            e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU: YOLOv8m-seg 1280x1280, convs on e4m3 MFMA "
+                             "(per-channel weight scales, static activation scales), batch 8 = 64 across 8 GPUs, "
+                             "post-processing + grid / A* on GPU")
+            e["parity"] = "tests/test_gpu_fp8.py: op vs the same quantized operands; forward rel. L2 vs fp32"
         if prof:
             rl = m["roofline"]
             e["roofline"] = {k: rl[k] for k in ("achieved", "peak", "frac", "avg_launch_us", "traffic")}
@@ -324,7 +336,7 @@ def main():
         extras[ex] = e
 
     if rank == 0:
-        tag = {("s", 640): "C3", ("m", 1280): "C5 shape (bf16 / f32 weights)",
+        tag = {("s", 640): "C3", ("m", 1280): "C5 (fp8 MFMA)" if args.dtype == "fp8" else "C5 shape (bf16 / f32)",
                ("n", 640): "C2 shape (batched)"}.get((args.scale, args.res), "custom")
         H = W = args.res
         line = {

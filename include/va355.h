@@ -153,6 +153,8 @@ int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen
 /* ---------------------------------------------------------------- segmentation (YOLOv8-seg) */
 #define VA_DTYPE_BF16 1
 #define VA_DTYPE_F32 2
+#define VA_DTYPE_FP8 3   /* va_seg_conv only: e4m3 weights + per-channel scales, bf16 activations quantized to e4m3
+                          * on the fly, block-scaled fp8 MFMA (va_conv_args.wscale / xscale) */
 
 /* One Conv2d (+ folded BN bias, optional SiLU, optional residual add) as an implicit GEMM on MFMA.
  * Replaces the Conv / Bottleneck / C2f / SPPF / Detect / Proto convolutions Ultralytics runs inside
@@ -201,6 +203,12 @@ typedef struct va_conv_args {
     const void* xu;
     int32_t ldu;
     int32_t cu;
+    /* VA_DTYPE_FP8: w is e4m3 [Npad][Kpad] (Kpad % 128 == 0), the bf16 input is quantized as sat(x * xscale) and
+     * the accumulator dequantized by wscale[co] (= the weights' per-channel scale / xscale) before bias and act;
+     * mode 0 / 1, Cin % 16 == 0, no tail / xu / bias4 (BASELINE.json configs[4]: "fp8 MFMA weights") */
+    const float* wscale;    /* [Npad] */
+    float xscale;
+    int32_t pad8_;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);
@@ -294,17 +302,18 @@ typedef struct va_contour_stat {
     int32_t ox, oy;   /* its start pixel in the instance's framed region image */
     int32_t ncont;    /* external contours found (RETR_EXTERNAL) */
     int32_t X0, Y0;   /* the region's origin in network pixels (framed image pixel (x, y) = (X0 + x - 1, Y0 + y - 1)) */
-    int32_t status;   /* 0 ok, 1 region too tall for the scan tables */
-    int32_t pad;
+    int32_t status;   /* 0 ok */
+    int32_t half;     /* which half of the instance's point buffer (cpts) holds that contour */
     double area;      /* cv2.contourArea of the float32 scale_coords points */
 } va_contour_stat;
 
 /* Everything YOLO.predict does after the forward, for B frames, plus the mask choice of
  * FrameProcessor.py:67-97 with OpenCV's algorithms restated (oracle/contours.py; parity with cv2 unpinned):
  *   decode (DFL, dist2bbox, sigmoid) -> conf filter -> max_nms cut -> class-offset greedy NMS (IoU > iou) -> max_det
- *   -> process_mask (coef . proto, crop, bilinear x4, > 0) -> per-instance pixel count / bbox (stats)
- *   -> (if cells != NULL) per instance the largest external contour (findContours RETR_EXTERNAL,
- *      CHAIN_APPROX_SIMPLE) and its contourArea over the float32 scale_coords points (cstats); the instance of
+ *   -> process_mask (coef . proto, crop, bilinear x4, > 0) -> per-instance pixel count / bbox (stats), the
+ *      largest external contour (findContours RETR_EXTERNAL, CHAIN_APPROX_SIMPLE) and its contourArea over
+ *      the float32 scale_coords points (cstats)
+ *   -> (if cells != NULL) the instance of
  *      max area (first maximum; a single one as it is), np.int32 of its polygon, boundingRect, and
  *      fillPoly(LINE_8) sampled at the 20-px cell centres of the H0 x W0 frame -> the (cells, rects) input of
  *      va_nav_run.
@@ -336,11 +345,15 @@ typedef struct va_post_args {
     /* contour scratch: cslots slots of va_contour_scratch_bytes(H, W, cslots, ccap) bytes each */
     void* cscratch;
     int32_t cslots, ccap;
-    va_contour_stat* cstats;    /* out [B][max_det] (required with cells) */
+    va_contour_stat* cstats;    /* out [B][max_det] */
     int32_t* cstatus;           /* out [B] or NULL: 1 = the chosen contour exceeded ccap points (cells left 0) */
+    /* per instance two buffers of cpts_cap contour points (network pixel x | y << 16): the contour being
+     * followed and the longest so far; a longer contour is followed again from the image instead */
+    uint32_t* cpts;             /* scratch [B][max_det][2][cpts_cap] */
     /* non_max_suppression's max_nms (ops.py:332-333): a candidate list longer than this is cut to its
      * max_nms highest scores before NMS.  <= 0: VA_MAX_NMS (Ultralytics' 30000). */
     int32_t max_nms;
+    int32_t cpts_cap;
 } va_post_args;
 
 #define VA_MAX_NMS 30000
@@ -378,7 +391,8 @@ typedef struct va_mask_select_args {
     int32_t* status;            /* out [B] or NULL */
     float* polys;               /* out or NULL */
     int32_t* poly_n;
-    int32_t poly_cap, pad_;
+    uint32_t* cpts;             /* scratch [B][maxn][2][cpts_cap] (va_post_args.cpts) */
+    int32_t poly_cap, cpts_cap;
 } va_mask_select_args;
 int va_post_select_masks(void* stream, const va_mask_select_args* m);
 

@@ -41,3 +41,27 @@ def test_select_masks_matches_oracle(Hn, Wn, H0, W0):
         assert tuple(got["rects"][b]) == rect, (b, tuple(got["rects"][b]), rect)
         assert np.array_equal(got["cells"][b], cells), (b, int((got["cells"][b] != cells).sum()))
 
+
+
+def test_select_masks_small_frames_lds_image():
+    """80 x 160 masks: the framed image fits the small LDS instantiation (the 640-pixel cases use the large one)."""
+    from tests.contour_cases import blob
+    from vision_assist_amd.post import select_masks
+    rng = np.random.default_rng(11)
+    Hn, Wn = 80, 160
+    masks = np.stack([np.stack([blob(rng, Hn, Wn, sigma=float(rng.uniform(2, 4)), thr=0.52) for _ in range(3)])
+                      for _ in range(6)])
+    masks[0, 1] = 0  # an empty mask
+    n = np.array([3, 3, 2, 3, 1, 3], np.int32)
+    got = select_masks(torch.from_numpy(masks).cuda(), torch.from_numpy(n), Hn, Wn)
+    assert (got["status"] == 0).all()
+    for b in range(masks.shape[0]):
+        ms = masks[b, :n[b]]
+        xy = C.masks_xy(ms, (Hn, Wn))
+        for k in range(n[b]):
+            st = got["cstats"][b, k]
+            assert st["area"] == C.contour_area(xy[k]), (b, k)
+            assert np.array_equal(got["polys"][b][k], xy[k]), (b, k)
+        kk, pts, rect, cells = C.select_cells(ms, (Hn, Wn))
+        assert got["chosen"][b] == kk and tuple(got["rects"][b]) == rect
+        assert np.array_equal(got["cells"][b], cells)

@@ -1,0 +1,150 @@
+"""The fp8 convolution path (va_fp8.hip, BASELINE.json configs[4] "YOLOv8m-seg 1280x1280 fp8 MFMA weights").
+
+* one conv op against torch on the SAME quantized operands: e4m3 weights with their per-channel scales as packed,
+  the bf16 input scaled by a power of two, saturated to +-448 and rounded to e4m3 (torch.float8_e4m3fn), f32
+  accumulation, then the dequant scale, bias, SiLU, residual -- the kernel differs only by summation order, its
+  fast SiLU and the bf16 output rounding: within 2e-2 of the output's scale (3x3 / 1x1 / stride 2 / residual / channel slices /
+  ConvTranspose / float output), which also pins the MFMA operand lane map;
+* the YOLOv8m-seg 1280 x 1280 forward against the fp32 oracle: e4m3 keeps 3 mantissa bits, so the bar is a
+  relative L2 error (stated per output below), not the f32 mode's 1e-3;
+* the fused batch at 1280 with planted corridor masks: grid / A* bit-exact (the nav stage does not see the
+  network's precision).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+FP8_L2 = {"box": 0.25, "cls": 0.25, "coef": 0.25, "proto": 0.25}  # relative L2 vs the fp32 oracle (measured 0.15-0.20)
+
+
+def _conv8(cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, out_f32=False, act=True):
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    from vision_assist_amd.seg_arch import Arch
+    g = torch.Generator().manual_seed(cin * 1000 + cout + k + 7 * stride)
+    B = 2
+    if deconv:
+        w = torch.randn(cin, cout, 2, 2, generator=g) * 0.2
+    else:
+        w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    x = torch.randn(B, cin, H, W, generator=g) * 1.7
+    net = S.SegNet.__new__(S.SegNet)
+    net.arch, net.dtype, net.device = Arch("n"), "fp8", torch.device("cuda")
+    net.tdtype, net.va_dtype, net.vec = torch.bfloat16, S.VA_DTYPE_BF16, 8
+    net.lib = _lib.load()
+    p = net._pack(w, b, deconv=deconv)
+    w8, sw, Kp = net._pack_fp8(p)
+    ld_in = cin + slice_in + 16
+    xin = torch.zeros(B, H, W, ld_in, dtype=torch.bfloat16, device="cuda")
+    xin[..., slice_in:slice_in + cin] = x.permute(0, 2, 3, 1).to(torch.bfloat16).cuda()
+    xb = xin[..., slice_in:slice_in + cin].float().cpu()  # NHWC, what the kernel reads
+    xs = 2.0 ** np.floor(np.log2(S.F8_MAX / float(xb.abs().max())))  # a power of two, as calibrate_fp8 picks
+    pad = k // 2 if not deconv else 0
+    if deconv:
+        Ho, Wo, oh, ow = H, W, 2 * H, 2 * W
+    else:
+        Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+        oh, ow = Ho, Wo
+    odt = torch.float32 if out_f32 else torch.bfloat16
+    ld_out = cout + 16
+    y = torch.zeros(B, oh, ow, ld_out, dtype=odt, device="cuda")
+    res = torch.randn(B, oh, ow, cout, generator=g).to(torch.bfloat16).cuda() if residual else None
+    ws = (sw / xs).contiguous()
+    args = S.ConvArgs(x=xin.data_ptr() + slice_in * 2, N=B, H=H, W=W, Cin=p.cin, ldx=ld_in, kh=p.k, kw=p.k,
+                      stride=stride if not deconv else 1, pad=pad, Ho=Ho, Wo=Wo, w=w8.data_ptr(), bias=p.b.data_ptr(),
+                      Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=Kp, y=y.data_ptr() + 8 * y.element_size(), ldy=ld_out,
+                      res=res.data_ptr() if res is not None else None, ldr=cout, act=1 if act else 0,
+                      mode=1 if deconv else 0, M=B * Ho * Wo, dtype=S.VA_DTYPE_FP8, out_f32=1 if out_f32 else 0,
+                      wscale=ws.data_ptr(), xscale=xs)
+    _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(args)), "va_seg_conv")
+    torch.cuda.synchronize()
+    got = y[..., 8:8 + cout].float().cpu()
+    # the reference on the same quantized operands
+    xq = (xb * xs).clamp(-S.F8_MAX, S.F8_MAX).to(torch.float8_e4m3fn).float().permute(0, 3, 1, 2)
+    wq = w8.cpu().view(torch.float8_e4m3fn).float()[:, :p.K]  # [Npad][K], K = (ky, kx, ci)
+    rows = 4 * cout if deconv else cout
+    wq = wq[:rows].reshape(rows, p.k, p.k, p.cin).permute(0, 3, 1, 2)
+    acc = F.conv2d(xq, wq, None, 1 if deconv else stride, pad)  # [B, rows, Ho, Wo]
+    acc = acc * ws.cpu()[:rows].view(1, rows, 1, 1) + p.b.cpu()[:rows].view(1, rows, 1, 1)
+    if deconv:  # rows q * cout + co, q = 2 dy + dx -> pixel (2 ho + dy, 2 wo + dx)
+        acc = acc.view(B, 2, 2, cout, Ho, Wo).permute(0, 3, 4, 1, 5, 2).reshape(B, cout, 2 * Ho, 2 * Wo)
+    if act:
+        acc = F.silu(acc)
+    ref = acc.permute(0, 2, 3, 1)
+    if residual:
+        ref = ref + res.float().cpu()
+    return got, ref
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,deconv,slice_in,out_f32", [
+    (64, 128, 3, 1, 20, 24, False, False, 0, False),
+    (96, 192, 3, 2, 33, 40, False, False, 16, False),  # stride 2, ragged M, channel slice
+    (128, 64, 1, 1, 17, 19, True, False, 0, False),    # 1x1 + residual
+    (48, 96, 3, 1, 40, 40, True, False, 0, False),     # K = 432 (not a multiple of 128), residual
+    (192, 256, 3, 1, 10, 10, False, False, 0, False),  # two channel tiles
+    (64, 32, 2, 1, 12, 10, False, True, 0, False),     # ConvTranspose2d(2, 2) as mode 1
+    (96, 80, 1, 1, 13, 13, False, False, 0, True),     # head-like: float output, no activation
+])
+def test_fp8_conv_op(cin, cout, k, stride, H, W, residual, deconv, slice_in, out_f32):
+    got, ref = _conv8(cin, cout, k, stride, H, W, residual, deconv, slice_in, out_f32,
+                      act=not (deconv or out_f32))
+    assert got.shape == ref.shape
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
+
+
+def _frames(B, H, W, seed):
+    return torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(seed), dtype=torch.uint8)
+
+
+def test_fp8_forward_medium_1280_vs_fp32_oracle():
+    from oracle import yolo_ref as Y
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    torch.set_num_threads(8)
+    arch = Arch("m")
+    fw = fold(arch, synthetic_state_dict(arch, seed=4))
+    frames = _frames(1, 1280, 1280, 6)
+    box, cls, coef, proto = Y.forward(arch, fw, Y.preprocess(frames))
+    net = SegNet(arch, fw, dtype="fp8")
+    out = net.forward(frames.cuda())
+    torch.cuda.synchronize()
+    n_fp8 = sum(1 for m in net.plan(1, 1280, 1280)["meta"] if m.get("fp8"))
+    assert n_fp8 >= 60, n_fp8  # every conv but model.0 (3 input channels) runs on the fp8 kernel
+    lv = torch.cat([t.float().cpu().flatten(1, 2) for t in out.levels], 1).permute(0, 2, 1)
+    nc = arch.nc
+    got = (lv[:, :64], lv[:, 64:64 + nc], lv[:, 64 + nc:], out.proto.float().cpu().permute(0, 3, 1, 2))
+    errs = {}
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, (box, cls, coef, proto)):
+        assert torch.isfinite(g).all(), name
+        errs[name] = ((g - r).norm() / r.norm()).item()
+    print("fp8 relative L2 vs fp32:", errs)
+    for name, e in errs.items():
+        assert e < FP8_L2[name], (name, e)
+
+
+def test_fp8_pipeline_1280_planted_nav_matches_oracle():
+    from oracle import nav as onav
+    from workloads.corridors import cells_rect, cells_to_mask, corridor_cells
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("m")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0))
+    B, H, W = 2, 1280, 1280
+    pipe = FramePipeline(arch, fw, B, H, W, dtype="fp8")
+    grids = [corridor_cells(7400 + i, H // 20, W // 20) for i in range(B)]
+    pc = torch.tensor(np.stack(grids).astype(np.uint8)).cuda()
+    pr = torch.tensor(np.array([cells_rect(g) for g in grids], dtype=np.int32)).cuda()
+    res = pipe.run(_frames(B, H, W, 17).cuda(), pc, pr, PLANT_ALWAYS)
+    pf = onav.PathFinderOracle()
+    for i, g in enumerate(grids):
+        out = onav.frame_nav(cells_to_mask(g), cells_rect(g), H, W, pf)
+        nf = res.frame(i)
+        assert [q["path"] for q in nf.queries] == [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]]

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--res", type=int, default=640)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--graph", action="store_true", help="also time the captured-graph variants")
     args = ap.parse_args()
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_ALWAYS
@@ -35,31 +36,32 @@ def main():
     pr = torch.tensor(np.array([cells_rect(g)], dtype=np.int32)).cuda()
     frame = torch.randint(0, 256, (1, H, W, 3), generator=torch.Generator().manual_seed(1), dtype=torch.uint8).cuda()
     out = {"config": f"C2 shape: YOLOv8{args.scale}-seg {H}x{W} {args.dtype}, batch 1, 1 MI355X", "iters": args.iters}
-    # the frame copy + network + post-processing captured once as a HIP graph (the nav stage reads a device flag
-    # on the host per speculative A* round, so it stays eager)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(3):
+    variants = [("seg_only", lambda: pipe.run_seg_only()),
+                ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS))]
+    if args.graph:
+        # the frame copy + network + post-processing captured once as a HIP graph (the nav stage reads a device
+        # flag on the host per speculative A* round, so it stays eager)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                pipe.load(frame)
+                pipe.seg_post(pc, pr, PLANT_ALWAYS)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
             pipe.load(frame)
             pipe.seg_post(pc, pr, PLANT_ALWAYS)
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        pipe.load(frame)
-        pipe.seg_post(pc, pr, PLANT_ALWAYS)
-    torch.cuda.synchronize()
-    out["ndet"] = int(pipe.post.ndet[0])
+        torch.cuda.synchronize()
 
-    def graph_e2e():
-        graph.replay()
-        pipe.nav_run()
+        def graph_e2e():
+            graph.replay()
+            pipe.nav_run()
 
-    for name, fn in (("seg_only", lambda: pipe.run_seg_only()),
-                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS)),
-                     ("seg_post_graph", graph.replay),
-                     ("end_to_end_graph", graph_e2e)):
+        variants += [("seg_post_graph", graph.replay), ("end_to_end_graph", graph_e2e)]
+    for name, fn in variants:
+        print(name, file=sys.stderr, flush=True)
         for _ in range(20):
             fn()
         torch.cuda.synchronize()
@@ -70,6 +72,7 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         ts = np.array(ts) * 1e3
+        out["ndet"] = int(pipe.post.ndet[0])
         out[name] = {"median_ms": round(float(np.median(ts)), 3), "p90_ms": round(float(np.percentile(ts, 90)), 3)}
     print(json.dumps(out), flush=True)
 

@@ -1,5 +1,5 @@
 // va_contour.h -- shared between va_post.hip (the pipeline's post-processing) and va_contour.hip (the mask ->
-// polygon -> cells boundary): where the instance masks come from, the frame mapping and the slot scratch.
+// polygon -> cells boundary): where the instance masks come from, the frame mapping and the scratch.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,6 +17,7 @@ struct CtSrc {  // where the instance masks come from
     int maxn;
     const int32_t* ndet;  // detections (masks) per frame
     int B, Hn, Wn, mh, mw;
+    va_mask_stat* stats;  // out [B][max_det] or NULL: pixel count / bbox of each mask (head source)
 };
 
 struct CtFrame {  // scale_coords of the network's Hn x Wn onto the H0 x W0 frame (float32, as numpy computes it)
@@ -25,13 +26,15 @@ struct CtFrame {  // scale_coords of the network's Hn x Wn onto the H0 x W0 fram
 };
 
 struct CtScratch {
-    unsigned char* base;
+    unsigned char* base;  // nslots slots: low-res strip | framed 2-bit image | int32 point pairs
     int64_t slot_bytes, img_off, pts_off;
-    int nslots, cap;  // cap: int32 point pairs per slot (post_fill_kernel)
+    int nslots, cap;      // cap: int32 point pairs per slot (post_fill_kernel)
+    uint32_t* cpts;       // [B][max_det][2][capd] packed contour points
+    int capd;
 };
 
-// Launch the contour kernel for every detection (cstats, optional polygons) and, with cells, the per-frame choice
-// + fill (va_contour.hip).
+// Launch the contour kernels for every detection (stats, cstats, optional polygons) and, with cells, the
+// per-frame choice + fill (va_contour.hip).
 hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch& sc, va_contour_stat* cstats,
                              int max_det, const uint8_t* plant_cells, const int32_t* plant_rects, int plant_mode,
                              uint8_t* cells, int32_t* rects, int32_t* chosen, int32_t* status, float* polys,

@@ -6,27 +6,31 @@
 // absent here; its published algorithms are restated exactly as oracle/contours.py restates them (that module is
 // the checker; the cv2 parity itself is unpinned):
 //
-//   post_contour_kernel  one wave per detection (persistent over slots): the instance mask -- bilinear x4 of the
-//                        cropped coef . proto, > 0 (or a given binary mask) -- as a framed byte image in the slot's
-//                        scratch (global memory: a few KiB to 400 KiB, L2-resident while it is followed; a
-//                        generic pointer that may point into LDS faulted on gfx950 under the atomics below); the
-//                        raster scan of cvFindNextContour and Suzuki-Abe border following (icvFetchContour) for
-//                        every outer border RETR_EXTERNAL keeps; the contour with the most CHAIN_APPROX_SIMPLE
-//                        points, re-followed once for its cv2.contourArea over the float32 scale_coords points
-//                        (double shoelace in OpenCV's order).  -> va_contour_stat.
+//   post_contour_kernel  one wave per detection (persistent over the detections): the instance mask --
+//                        bilinear x4 of the cropped coef . proto, > 0 (process_mask), or a given binary mask --
+//                        as a framed image of three bit planes (mask, traced, traced "right") in LDS, built in strips
+//                        of low-res rows; its pixel count and bbox (va_mask_stat); the raster scan of
+//                        cvFindNextContour over the rows that hold an unmarked 0 -> 1 transition (no other row
+//                        can start an outer border) and Suzuki-Abe border following (icvFetchContour) for every
+//                        outer border RETR_EXTERNAL keeps, each contour's CHAIN_APPROX_SIMPLE points written to
+//                        one of the instance's two point buffers (the longest stays); cv2.contourArea of the
+//                        longest over its float32 scale_coords points (double shoelace in OpenCV's order, the
+//                        terms in parallel, summed in order).  -> va_contour_stat.  Three instantiations by
+//                        image size: 32 KiB of LDS (several waves per CU), 156 KiB (one per CU), and the
+//                        global-memory form for larger regions (full-frame boxes, 1280-pixel inputs).
 //   post_fill_kernel     one workgroup per frame: the instance max(area) picks (first maximum; a single detection
-//                        is taken as it is), its best contour followed again into int32 frame points
-//                        (np.int32 of the float32 scale_coords), boundingRect, and cv2.fillPoly(LINE_8) evaluated
-//                        only at the cell centres: a centre is set when an edge's 8-connected Bresenham line
-//                        (LineIterator + clipLine) passes through it, or when it lies in a FillEdgeCollection span --
-//                        with a = #active edges left of the pixel and b = #active edges left of its right neighbour
-//                        (16.16 edge x at that row), the pixel is inside a pair iff b > a or a is odd, an
-//                        order-free count the threads accumulate with LDS atomics.
+//                        is taken as it is), its points as int32 frame points (np.int32 of the float32
+//                        scale_coords), boundingRect, and cv2.fillPoly(LINE_8) evaluated only at the cell centres:
+//                        a centre is set when an edge's 8-connected Bresenham line (LineIterator + clipLine) passes
+//                        through it, or when it lies in a FillEdgeCollection span -- with a = #active edges left of
+//                        the pixel and b = #active edges left of its right neighbour (16.16 edge x at that row),
+//                        the pixel is inside a pair iff b > a or a is odd, an order-free count the threads
+//                        accumulate with LDS atomics.
 //
-// Pixel states of the byte image: bit 0 = non-zero mask pixel, bit 1 = traced border pixel (OpenCV's nbd = 2),
-// bit 2 = traced "right" border pixel (OpenCV's nbd | -128).  A border visit ORs its bit in (atomicOr on the
-// pixel's word): OpenCV's per-visit update "cond ? -126 : (v == 1 ? 2 : v)" reaches the same final value in any
-// visit order, so a trace never has to read back its own marks.
+// The image lives in LDS through a pointer the compiler sees as LDS (each size class is its own instantiation): an
+// earlier form that selected between an LDS and a global image at run time faulted on gfx950.  The border
+// following runs with wave-uniform scalar state (every lane the same pixel): a step is instruction-bound (one
+// wave issues at most one instruction per 4 cycles), so the step's work is kept to a few dozen scalar ops.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,10 +42,17 @@ namespace {
 
 constexpr int NMC = 32;
 constexpr int REG_MAX = 16;
-constexpr int CT_THREADS = 64;       // one wave per detection: the scan and the border following are serial
+constexpr int CT_THREADS = 64;             // one wave per detection: the scan and the border following are serial
 constexpr int FILL_THREADS = 256;
-__constant__ int c_dx[8] = {1, 1, 0, -1, -1, -1, 0, 1};
-__constant__ int c_dy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+constexpr int CT_STRIP = 2048;             // floats of one strip of low-res rows (8 KiB)
+constexpr int CT_LDS_SMALL = 32 * 1024;    // dynamic LDS of the small instantiation
+constexpr int CT_LDS_LARGE = 156 * 1024;   // of the large one (one wave per CU: regions up to ~560 x 560)
+// chain-code moves (0 = right, counter-clockwise), as 2-bit fields of (d + 1): register arithmetic, not a table
+// load (a per-step table load with a lane-varying index is a memory round trip on the trace's critical path)
+__device__ __forceinline__ int dir_dx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }  // 1 1 0 -1 -1 -1 0 1
+__device__ __forceinline__ int dir_dy(int s) { return (int)((0xA901u >> (2 * s)) & 3u) - 1; }  // 0 -1 -1 -1 0 1 1 1
+// every lane of the wave holds the same value: make it scalar (uniform branches, SALU arithmetic)
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Bounds-checked debug build (-DVA_CT_CHECK, tools/ct_check.py): an out-of-range access is skipped and the first
 // one recorded as (code, v0, v1) for va_contour_debug instead of faulting.
@@ -55,8 +66,16 @@ __device__ inline bool ct_ok(bool c, int code, long long v0, long long v1) {
     return c;
 }
 #define CT_OK(c, code, v0, v1) ct_ok((c), (code), (long long)(v0), (long long)(v1))
+// per-detection phase clocks of the contour kernel (s_memtime): build, scan, area; counts: contours, rows
+// scanned, positions visited, trace steps
+constexpr int CT_PROF_ITEMS = 4096;
+__device__ unsigned long long g_ct_prof[CT_PROF_ITEMS][8];
+#define CT_PROF(...) __VA_ARGS__
+#define CT_STEPS (&nsteps)
 #else
 #define CT_OK(c, code, v0, v1) true
+#define CT_PROF(...)
+#define CT_STEPS nullptr
 #endif
 
 // ------------------------------------------------------------------------------------------ geometry
@@ -106,7 +125,7 @@ __device__ inline void taps(int o, float scale, int in, int* i0, int* i1, float*
 // around (cv::findContours' border).  Empty (w = 0) when the mask cannot have a positive pixel.
 struct Region {
     int X0, Y0, w, h;  // network pixels covered
-    int rW, rH, ww;    // framed size in pixels, words per row
+    int rW, rH, ww;    // framed size in pixels, 32-bit words per plane row (32 pixels each)
     int rx0, rx1, ry0, ry1;
 };
 
@@ -119,7 +138,7 @@ __device__ inline Region region_of(const Src& s, int b, int k) {
         crop_window(d, s, &r.rx0, &r.rx1, &r.ry0, &r.ry1);
         if (r.rx1 < r.rx0 || r.ry1 < r.ry0) return r;  // w = 0: an all-zero mask
         const float sx = (float)s.mw / (float)s.Wn, sy = (float)s.mh / (float)s.Hn;
-        // full-res pixels whose taps can touch the window (post_mask_kernel's footprint)
+        // full-res pixels whose taps can touch the window
         r.X0 = max(0, (int)((r.rx0 - 1) / sx) - 2);
         const int X1 = min(s.Wn - 1, (int)((r.rx1 + 1) / sx) + 2);
         r.Y0 = max(0, (int)((r.ry0 - 1) / sy) - 2);
@@ -129,175 +148,292 @@ __device__ inline Region region_of(const Src& s, int b, int k) {
     }
     r.rW = r.w + 2;
     r.rH = r.h + 2;
-    r.ww = (r.rW + 3) / 4;
+    r.ww = (r.rW + 31) >> 5;
     return r;
 }
 
-// ------------------------------------------------------------------------------------------ the byte image
-// word i holds pixels 4 (i % ww) .. +3 of row i / ww (byte j = pixel 4 (i % ww) + j)
-struct Img {
-    uint32_t* p;
-    int ww, nw;  // words per row, words
-    __device__ inline bool in(int x, int y, int code) const {
-        return CT_OK(x >= 0 && y >= 0 && (x >> 2) < ww && y * ww + (x >> 2) < nw, code, x, y);
-    }
-    __device__ inline int nz(int x, int y) const {  // bit 0 never changes: plain load
-        if (!in(x, y, 1)) return 0;
-        return (p[y * ww + (x >> 2)] >> (8 * (x & 3))) & 1;
-    }
-    __device__ inline int val(int x, int y) const {  // OpenCV's value of the pixel (marks: coherent load)
-        if (!in(x, y, 2)) return 0;
-        const uint32_t w = __hip_atomic_load(p + y * ww + (x >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int v = (int)((w >> (8 * (x & 3))) & 0xFF);
-        return (v & 4) ? -126 : (v & 2) ? 2 : (v & 1);
-    }
-    __device__ inline void mark(int x, int y, bool right) const {
-        if (!in(x, y, 3)) return;
-        atomicOr(p + y * ww + (x >> 2), (right ? 4u : 2u) << (8 * (x & 3)));
-    }
-};
+// 32-bit words of the image: three bit planes per row (+ one spare word, read past by the trace windows)
+__device__ inline int64_t image_words(const Region& r) { return (int64_t)r.rH * 3 * r.ww + 1; }
 
-// Build the framed image of detection (b, k) into img (region r) with nt threads of the calling block.
-// lowres: scratch of (ry1 - ry0 + 1) x (rx1 - rx0 + 1) floats (head source only).
-__device__ void build_image(const Src& s, int b, int k, const Region& r, Img img, float* lowres, int tid, int nt) {
-    const int nwords = r.rH * r.ww;
-    if (s.masks) {
-        const uint8_t* m = s.masks + ((int64_t)b * s.maxn + k) * s.Hn * s.Wn;
-        for (int i = tid; i < nwords; i += nt) {
-            const int y = i / r.ww, x4 = 4 * (i % r.ww);
-            uint32_t w = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int x = x4 + j;
-                if (y >= 1 && y <= r.h && x >= 1 && x <= r.w && m[(int64_t)(y - 1) * s.Wn + (x - 1)]) w |= 1u << (8 * j);
-            }
-            if (CT_OK(i < img.nw, 4, i, img.nw)) img.p[i] = w;
-        }
-        __syncthreads();
-        return;
-    }
-    // low-res window of coef . proto: 8 lanes per pixel, one 16-byte run of its 32 channels each (the dot of
-    // post_mask_kernel, same partial sums and reduction order)
-    const int anchor = s.dets[(int64_t)b * s.max_det + k].anchor;
-    [[maybe_unused]] const int na = (s.Hn / 8) * (s.Wn / 8) + (s.Hn / 16) * (s.Wn / 16) + (s.Hn / 32) * (s.Wn / 32);
-    if (!CT_OK(anchor >= 0 && anchor < na, 13, anchor, na)) return;  // (debug build only)
-    const float* coef = coef_row(s, b, anchor);
-    const int tw = r.rx1 - r.rx0 + 1, th = r.ry1 - r.ry0 + 1;
-    const int sub = tid & 7;
-    const float4 cq = *(const float4*)(coef + 4 * sub);
-    for (int i = tid >> 3; i < tw * th; i += nt / 8) {
-        const int y = r.ry0 + i / tw, x = r.rx0 + i % tw;
-        if (!CT_OK(y >= 0 && y < s.mh && x >= 0 && x < s.mw, 5, x, y)) continue;  // (debug build only)
-        const float4 v = *(const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC + 4 * sub);
-        float sdot = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
-        sdot += __shfl_xor(sdot, 1, 8);
-        sdot += __shfl_xor(sdot, 2, 8);
-        sdot += __shfl_xor(sdot, 4, 8);
-        if (sub == 0 && CT_OK(i < s.mh * s.mw, 6, i, tw)) lowres[i] = sdot;
-    }
-    __syncthreads();
-    const float sx = (float)s.mw / (float)s.Wn, sy = (float)s.mh / (float)s.Hn;
-    auto val = [&](int yy, int xx) -> float {
-        if (xx < r.rx0 || xx > r.rx1 || yy < r.ry0 || yy > r.ry1) return 0.f;
-        const int li = (yy - r.ry0) * tw + (xx - r.rx0);
-        if (!CT_OK(li >= 0 && li < s.mh * s.mw, 7, li, tw)) return 0.f;
-        return lowres[li];
-    };
-    for (int i = tid; i < nwords; i += nt) {
-        const int y = i / r.ww, x4 = 4 * (i % r.ww);
-        uint32_t w = 0;
-        if (y >= 1 && y <= r.h) {
-            const int Y = r.Y0 + y - 1;
-            int ya, yb;
-            float wy0, wy1;
-            taps(Y, sy, s.mh, &ya, &yb, &wy0, &wy1);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int x = x4 + j;
-                if (x < 1 || x > r.w) continue;
-                const int X = r.X0 + x - 1;
-                int xa, xb;
-                float wx0, wx1;
-                taps(X, sx, s.mw, &xa, &xb, &wx0, &wx1);
-                const float A = val(ya, xa), B = val(ya, xb), C = val(yb, xa), D = val(yb, xb);
-                const float ha = wx0 * A + wx1 * B, hb = wx0 * C + wx1 * D;
-                if (wy0 * ha + wy1 * hb > 0.f) w |= 1u << (8 * j);
-            }
-        }
-        if (CT_OK(i < img.nw, 8, i, img.nw)) img.p[i] = w;
-    }
-    __syncthreads();
-}
-
-// ------------------------------------------------------------------------------------------ border following
-// icvFetchContour (CHAIN_APPROX_SIMPLE) from the outer-border start (x0, y0) of the framed image, executed by the
-// whole wave in lock step (lanes 0-7 fetch the 8 neighbours of the current pixel).  emit(x, y) gets every kept
-// point in order; mark = whether to write the traced pixels' marks.  Returns the number of points.
-template <typename Emit>
-__device__ int fetch_contour(Img img, int x0, int y0, bool mark, Emit emit) {
-    const int lane = threadIdx.x & 63;
-    const int ld = lane & 7;
-    auto nbrs = [&](int x, int y) -> unsigned {  // bit d = neighbour in direction d is non-zero
-        const int nzv = lane < 8 ? img.nz(x + c_dx[ld], y + c_dy[ld]) : 0;
-        return (unsigned)(__ballot(nzv != 0) & 0xFFull);
-    };
-    unsigned nb = nbrs(x0, y0);
-    int s = 4;  // outer border: s_end = s = 4
-    const int s_end0 = 4;
-    do {
-        s = (s - 1) & 7;
-    } while (!((nb >> s) & 1) && s != s_end0);
-    if (s == s_end0) {  // single pixel domain
-        if (mark && lane == 0) img.mark(x0, y0, true);
-        emit(x0, y0);
-        return 1;
-    }
-    const int x1 = x0 + c_dx[s], y1 = y0 + c_dy[s];  // i1
-    int x3 = x0, y3 = y0;
-    int prev_s = s ^ 4, n = 0;
-    int px = x0, py = y0;
-    unsigned nb3 = nb;
-    while (true) {
-        const int s_end = s;
-        // counter-clockwise from s_end + 1 to the first non-zero neighbour
-        int t = s_end + 1;
-        while (!((nb3 >> (t & 7)) & 1)) ++t;
-        s = t & 7;
-        const int x4 = x3 + c_dx[s], y4 = y3 + c_dy[s];
-        if (mark && lane == 0) img.mark(x3, y3, (unsigned)(s - 1) < (unsigned)s_end);
-        if (s != prev_s) {
-            emit(px, py);
-            ++n;
-            prev_s = s;
-        }
-        px += c_dx[s];
-        py += c_dy[s];
-        if (x4 == x0 && y4 == y0 && x3 == x1 && y3 == y1) break;
-        x3 = x4;
-        y3 = y4;
-        s = (s + 4) & 7;
-        nb3 = nbrs(x3, y3);
-    }
-    return n;
-}
-
-// The first position >= x of row y whose value differs from prev (OpenCV's skip loop), or width.  Wave-wide.
-__device__ inline int next_stop(Img img, int y, int x, int width, int prev) {
-    const int lane = threadIdx.x & 63;
-    while (x < width) {
-        const int xx = x + lane;
-        const bool d = xx < width && img.val(xx, y) != prev;
-        const unsigned long long m = __ballot(d);
-        if (m) return x + __builtin_ctzll(m);
-        x += 64;
-    }
-    return width;
+// bytes an instance needs: the image, plus the low-res strip for a head-source mask
+__device__ inline int64_t region_need(const Src& s, const Region& r) {
+    if (r.w <= 0) return 0;
+    return ((image_words(r) * 4 + 15) & ~15ll) + (s.masks ? 0 : CT_STRIP * 4);
 }
 
 // float32 scale_coords of a network point (ops.py:784-816)
 __device__ inline void scale_pt(const Frame& f, int X, int Y, float* xs, float* ys) {
     *xs = fminf(fmaxf(((float)X - f.padx) / f.gain, 0.0f), (float)f.W0);
     *ys = fminf(fmaxf(((float)Y - f.pady) / f.gain, 0.0f), (float)f.H0);
+}
+
+// ------------------------------------------------------------------------------------------ the image
+// Three bit planes per framed row y, 32 pixels per word: NZ (plane 0, the mask), N (1: visited by a border trace,
+// OpenCV's nbd) and R (2: visited as a "right" border pixel, OpenCV's nbd | -128).  OpenCV's per-visit update
+// ("right" -> -126, else 1 -> 2) reaches the value R ? -126 : N ? 2 : NZ in any visit order, so a visit just ORs
+// its bit in -- one LDS (or global) atomic OR from lane 0, no read.
+__device__ __forceinline__ uint32_t* plane(uint32_t* img, int ww, int y, int p) { return img + (3 * y + p) * ww; }
+__device__ __forceinline__ const uint32_t* plane(const uint32_t* img, int ww, int y, int p) {
+    return img + (3 * y + p) * ww;
+}
+
+// N / R words: the scan reads what the traces wrote.  LDS: plain (one wave, in order); global: coherent.
+template <bool LDS>
+__device__ __forceinline__ uint32_t ldm(const uint32_t* p) {
+    if constexpr (LDS) {
+        return *p;
+    } else {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// OpenCV's value of a pixel from its three bits
+__device__ __forceinline__ int val_bits(uint32_t nz, uint32_t n, uint32_t r) { return r ? -126 : (n ? 2 : (int)nz); }
+
+template <bool LDS>
+__device__ __forceinline__ int val_at(const uint32_t* img, int ww, int x, int y) {
+    if (!CT_OK(x >= 0 && y >= 0 && (x >> 5) < ww, 2, x, y)) return 0;
+    const int w = x >> 5, b = x & 31;
+    return val_bits((plane(img, ww, y, 0)[w] >> b) & 1u, (ldm<LDS>(plane(img, ww, y, 1) + w) >> b) & 1u,
+                    (ldm<LDS>(plane(img, ww, y, 2) + w) >> b) & 1u);
+}
+
+// the value planes of a word: hi = any mark, lo = "right" mark or an unmarked non-zero pixel (value codes
+// 0 / 1 / 2 / 3 for 0 / 1 / 2 / -126)
+__device__ __forceinline__ void code_planes(uint32_t nz, uint32_t n, uint32_t r, uint32_t& hi, uint32_t& lo) {
+    hi = n | r;
+    lo = r | (nz & ~n);
+}
+
+// Whether row y holds a non-zero, unmarked pixel right of a zero pixel: the only rows where cvFindNextContour can
+// start an outer border (traces only mark, so the answer at the row's start holds through the row).  Wave-wide.
+template <bool LDS>
+__device__ __forceinline__ bool row_has_start(const uint32_t* img, int ww, int y) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t* nzr = plane(img, ww, y, 0);
+    bool any = false;
+    for (int w0 = 0; w0 < ww; w0 += 64) {
+        const int wi = w0 + lane;
+        if (wi < ww) {
+            const uint32_t nz = nzr[wi], pnz = wi >= 1 ? nzr[wi - 1] : 0u;
+            const uint32_t mk = ldm<LDS>(plane(img, ww, y, 1) + wi) | ldm<LDS>(plane(img, ww, y, 2) + wi);
+            const uint32_t left0 = ~((nz << 1) | (pnz >> 31));
+            any |= (nz & ~mk & left0) != 0u;
+        }
+    }
+    return __ballot(any) != 0ull;
+}
+
+// ------------------------------------------------------------------------------------------ building
+struct MaskStat {
+    int cnt, x0, x1, y0, y1;
+};
+
+// The framed image of detection (b, k) into img (region r), by nt threads of the calling block; the mask pixel
+// count and bbox accumulate per thread in ms.  Head source: strips of the low-res window of coef . proto in
+// `strip`, each evaluating the full-res rows whose taps it holds with the exact per-pixel expression
+// wy0 (wx0 v(ya, xa) + wx1 v(ya, xb)) + wy1 (wx0 v(yb, xa) + wx1 v(yb, xb)) > 0.
+__device__ __forceinline__ void build_image(const Src& s, int b, int k, const Region& r, uint32_t* img, float* strip,
+                                            int tid, int nt, MaskStat& ms) {
+    auto account = [&](uint32_t w, int x32, int yy) {
+        if (!w) return;
+        ms.cnt += __builtin_popcount(w);
+        const int X = r.X0 + x32 - 1, Y = r.Y0 + yy - 1;
+        ms.x0 = min(ms.x0, X + __builtin_ctz(w));
+        ms.x1 = max(ms.x1, X + 31 - __builtin_clz(w));
+        ms.y0 = min(ms.y0, Y);
+        ms.y1 = max(ms.y1, Y);
+    };
+    // the mark planes and the frame rows start at zero
+    for (int i = tid; i < r.rH * r.ww; i += nt) {
+        const int y = i / r.ww, w = i % r.ww;
+        plane(img, r.ww, y, 1)[w] = 0u;
+        plane(img, r.ww, y, 2)[w] = 0u;
+        if (y == 0 || y == r.rH - 1) plane(img, r.ww, y, 0)[w] = 0u;
+    }
+    if (tid == 0) img[image_words(r) - 1] = 0u;
+    if (s.masks) {
+        const uint8_t* m = s.masks + ((int64_t)b * s.maxn + k) * s.Hn * s.Wn;
+        for (int i = tid; i < r.h * r.ww; i += nt) {
+            const int y = 1 + i / r.ww, x32 = 32 * (i % r.ww);
+            uint32_t w = 0;
+#pragma unroll 8
+            for (int j = 0; j < 32; ++j) {
+                const int x = x32 + j;
+                if (x >= 1 && x <= r.w && m[(int64_t)(y - 1) * s.Wn + (x - 1)]) w |= 1u << j;
+            }
+            account(w, x32, y);
+            plane(img, r.ww, y, 0)[x32 >> 5] = w;
+        }
+        __syncthreads();
+        return;
+    }
+    const int anchor = s.dets[(int64_t)b * s.max_det + k].anchor;
+    const float4* coef4 = (const float4*)coef_row(s, b, anchor);
+    float4 cq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cq[q] = coef4[q];
+    const int tw = r.rx1 - r.rx0 + 1;
+    const int S = CT_STRIP / tw;  // >= 6: tw <= mw <= 320
+    const float sx = (float)s.mw / (float)s.Wn, sy = (float)s.mh / (float)s.Hn;
+    int next = 1, s0 = r.ry0;     // next framed row to produce; first low-res row of the strip
+    while (next <= r.h) {         // block-uniform
+        const int s1 = min(s0 + S - 1, r.ry1);
+        // one low-res pixel per lane: its 128 bytes of proto as 8 loads in flight; the partial sums per 4
+        // channels and their pairwise tree are post-processing's 8-lane dot (same order, same result)
+        for (int i = tid; i < (s1 - s0 + 1) * tw; i += nt) {
+            const int y = s0 + i / tw, x = r.rx0 + i % tw;
+            const float4* pp = (const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC);
+            float part[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const float4 v = pp[q];
+                part[q] = (cq[q].x * v.x + cq[q].y * v.y) + (cq[q].z * v.z + cq[q].w * v.w);
+            }
+            strip[i] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+        }
+        __syncthreads();
+        // the rows whose taps inside the window all lie in s0 .. s1 (taps are non-decreasing in the row)
+        int end = next;
+        while (end <= r.h) {
+            int ya, yb;
+            float w0, w1;
+            taps(r.Y0 + end - 1, sy, s.mh, &ya, &yb, &w0, &w1);
+            const int hi = (yb >= r.ry0 && yb <= r.ry1) ? yb : ((ya >= r.ry0 && ya <= r.ry1) ? ya : -1);
+            if (hi > s1) break;
+            ++end;
+        }
+        auto val = [&](int yy, int xx) -> float {
+            if (xx < r.rx0 || xx > r.rx1 || yy < r.ry0 || yy > r.ry1) return 0.f;
+            const int li = (yy - s0) * tw + (xx - r.rx0);
+            if (!CT_OK(li >= 0 && li < CT_STRIP, 7, li, tw)) return 0.f;
+            return strip[li];
+        };
+        for (int i = tid; i < (end - next) * r.ww; i += nt) {
+            const int yy = next + i / r.ww, x32 = 32 * (i % r.ww);
+            int ya, yb;
+            float wy0, wy1;
+            taps(r.Y0 + yy - 1, sy, s.mh, &ya, &yb, &wy0, &wy1);
+            uint32_t w = 0;
+#pragma unroll 4
+            for (int j = 0; j < 32; ++j) {
+                const int x = x32 + j;
+                if (x < 1 || x > r.w) continue;
+                int xa, xb;
+                float wx0, wx1;
+                taps(r.X0 + x - 1, sx, s.mw, &xa, &xb, &wx0, &wx1);
+                const float A = val(ya, xa), B = val(ya, xb), C = val(yb, xa), D = val(yb, xb);
+                const float ha = wx0 * A + wx1 * B, hb = wx0 * C + wx1 * D;
+                if (wy0 * ha + wy1 * hb > 0.f) w |= 1u << j;
+            }
+            account(w, x32, yy);
+            plane(img, r.ww, yy, 0)[x32 >> 5] = w;
+        }
+        next = end;
+        s0 = s1;  // a later row may need s1 and s1 + 1
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------ border following
+// The trace's view of the NZ plane: the two-word windows (from word c0 = (x - 1) / 32) of rows cy - 1, cy, cy + 1,
+// held as wave-uniform scalars.  A step to a neighbour keeps c0 31 times in 32 and shifts the rows on a vertical
+// move, so most steps load one row or none (the NZ plane never changes).
+struct TraceWin {
+    unsigned long long up, md, dn;
+    int c0, cy;
+};
+
+__device__ __forceinline__ unsigned long long load_win(const uint32_t* img, int ww, int y, int c0) {
+    const uint32_t* p = plane(img, ww, y, 0) + c0;
+    const uint32_t lo = p[0], hi = p[1];
+    return (unsigned long long)(unsigned)uni((int)lo) | ((unsigned long long)(unsigned)uni((int)hi) << 32);
+}
+
+__device__ __forceinline__ void win_at(const uint32_t* img, int ww, int x, int y, TraceWin& w) {
+    const int c0 = (x - 1) >> 5;
+    if (c0 == w.c0 && y == w.cy) return;
+    if (c0 == w.c0 && y == w.cy + 1) {
+        w.up = w.md, w.md = w.dn, w.dn = load_win(img, ww, y + 1, c0);
+    } else if (c0 == w.c0 && y == w.cy - 1) {
+        w.dn = w.md, w.md = w.up, w.up = load_win(img, ww, y - 1, c0);
+    } else {
+        const uint32_t* p = plane(img, ww, y - 1, 0) + c0;
+        const int st = 3 * ww;  // one row down, same plane
+        const uint32_t a0 = p[0], a1 = p[1], b0 = p[st], b1 = p[st + 1], d0 = p[2 * st], d1 = p[2 * st + 1];
+        w.up = (unsigned long long)(unsigned)uni((int)a0) | ((unsigned long long)(unsigned)uni((int)a1) << 32);
+        w.md = (unsigned long long)(unsigned)uni((int)b0) | ((unsigned long long)(unsigned)uni((int)b1) << 32);
+        w.dn = (unsigned long long)(unsigned)uni((int)d0) | ((unsigned long long)(unsigned)uni((int)d1) << 32);
+    }
+    w.c0 = c0, w.cy = y;
+}
+
+// bit d = the neighbour in direction d (0 = right, counter-clockwise) is non-zero
+__device__ __forceinline__ unsigned win_nbrs(const TraceWin& w, int x) {
+    const int sh = (x - 1) & 31;
+    const unsigned up = (unsigned)(w.up >> sh) & 7u, m = (unsigned)(w.md >> sh) & 7u, dn = (unsigned)(w.dn >> sh) & 7u;
+    // up: x-1, x, x+1 -> directions 3, 2, 1 (bit-reversed); md: x+1 -> 0, x-1 -> 4; dn: x-1, x, x+1 -> 5, 6, 7
+    return ((m >> 2) & 1u) | (__builtin_bitreverse32(up) >> 28) | ((m & 1u) << 4) | (dn << 5);
+}
+
+// the visit's mark of (x, y): "right" -> R, else N (lane 0, one atomic OR)
+__device__ __forceinline__ void mark_at(uint32_t* img, int ww, int x, int y, bool right) {
+    if ((threadIdx.x & 63) != 0) return;
+    if (!CT_OK(x >= 0 && y >= 0 && (x >> 5) < ww, 3, x, y)) return;
+    atomicOr(plane(img, ww, y, right ? 2 : 1) + (x >> 5), 1u << (x & 31));
+}
+
+// icvFetchContour (CHAIN_APPROX_SIMPLE) from the outer-border start (x0, y0) of the framed image, executed by the
+// whole wave in lock step (every lane the same pixel, scalar state; marks by lane 0).  emit(x, y) gets every kept
+// point in order; mark = whether to write the traced pixels' marks.  Returns the number of points.
+template <typename Emit>
+__device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int y0, bool mark, Emit emit,
+                                             int* steps = nullptr) {
+    TraceWin w{0ull, 0ull, 0ull, -1, -1};
+    win_at(img, ww, x0, y0, w);
+    const unsigned nb = win_nbrs(w, x0);
+    int s = 4;  // outer border: s_end = s = 4
+    const int s_end0 = 4;
+    do {
+        s = (s - 1) & 7;
+    } while (!((nb >> s) & 1) && s != s_end0);
+    if (s == s_end0) {  // single pixel domain
+        if (mark) mark_at(img, ww, x0, y0, true);
+        emit(x0, y0);
+        return 1;
+    }
+    const int x1 = x0 + dir_dx(s), y1 = y0 + dir_dy(s);  // i1
+    int x3 = x0, y3 = y0;
+    int prev_s = s ^ 4, n = 0;
+    unsigned nb3 = nb;
+    while (true) {
+        const int s_end = s;
+        // counter-clockwise from s_end + 1 to the first non-zero neighbour (one exists: i1 at the latest)
+        const unsigned rot = ((nb3 | (nb3 << 8)) >> ((s_end + 1) & 7)) & 0xFFu;
+        s = (s_end + 1 + __builtin_ctz(rot)) & 7;
+        const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
+        if (mark) mark_at(img, ww, x3, y3, (unsigned)(s - 1) < (unsigned)s_end);
+        if (s != prev_s) {
+            emit(x3, y3);
+            ++n;
+            prev_s = s;
+        }
+        if (x4 == x0 && y4 == y0 && x3 == x1 && y3 == y1) break;
+        x3 = x4;
+        y3 = y4;
+        s = (s + 4) & 7;
+        win_at(img, ww, x3, y3, w);
+        nb3 = win_nbrs(w, x3);
+        CT_PROF(if (steps) ++*steps);
+    }
+    return n;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long bits = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // ------------------------------------------------------------------------------------------ per detection
@@ -312,53 +448,136 @@ struct CtArgs {
     int poly_cap;
 };
 
+// MODE 0 / 1: image in LDS (CT_LDS_SMALL / CT_LDS_LARGE bytes); MODE 2: in the block's scratch slot.  Every
+// instantiation walks all detections and takes the ones of its size class.
+template <int MODE>
 __global__ __launch_bounds__(CT_THREADS) void post_contour_kernel(CtArgs a) {
-    __shared__ unsigned char rowflag[4096];
-    const int tid = threadIdx.x;
+    constexpr bool LDS = MODE < 2;
+    constexpr int64_t lo = MODE == 0 ? -1 : (MODE == 1 ? CT_LDS_SMALL : CT_LDS_LARGE);
+    constexpr int64_t hi = MODE == 0 ? CT_LDS_SMALL : (MODE == 1 ? CT_LDS_LARGE : INT64_MAX);
+    extern __shared__ __align__(16) uint32_t ct_lds[];
+    __shared__ int s_red[5];
+    const int tid = threadIdx.x, lane = tid & 63;
     const Src& s = a.s;
     unsigned char* slot = a.sc.base + (int64_t)blockIdx.x * a.sc.slot_bytes;
     const int total = s.B * a.max_det;
     for (int item = blockIdx.x; item < total; item += gridDim.x) {
         const int b = item / a.max_det, k = item % a.max_det;
-        const int nd = s.ndet[b];
-        if (k >= nd) continue;  // block-uniform
+        if (k >= s.ndet[b]) continue;  // block-uniform
+        const Region r = region_of(s, b, k);
+        const int64_t need = region_need(s, r);
+        if (need <= lo || need > hi) continue;
         va_contour_stat st{};
         st.ox = st.oy = -1;
-        const Region r = region_of(s, b, k);
-        if (r.w > 0 && r.rH <= 4096) {
-            Img img{(uint32_t*)(slot + a.sc.img_off), r.ww, r.rH * r.ww};
-            build_image(s, b, k, r, img, (float*)slot, tid, CT_THREADS);
-            // rows with a 0 -> 1 transition (no other row can start a border): per word, bit 0 of each byte
-            // against the byte before it
-            for (int y = tid; y < r.rH; y += CT_THREADS) rowflag[y] = 0;
-            __syncthreads();
-            for (int i = tid; i < r.rH * r.ww; i += CT_THREADS) {
-                const int y = i / r.ww, wx = i % r.ww;
-                const uint32_t cur = img.p[i] & 0x01010101u;
-                const uint32_t before = (cur << 8) | (wx ? (img.p[i - 1] >> 24) & 1u : 0u);
-                if (cur & ~before) rowflag[y] = 1;
+        st.X0 = r.X0, st.Y0 = r.Y0;
+        const int64_t di = (int64_t)b * a.max_det + k;
+        float* poly = a.polys ? a.polys + di * a.poly_cap * 2 : nullptr;
+        if (r.w <= 0) {
+            if (tid == 0) {
+                if (s.stats) s.stats[di] = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
+                if (a.poly_n) a.poly_n[di] = 0;
+                a.cstats[di] = st;
+            }
+            continue;
+        }
+        uint32_t* img;
+        float* strip;
+        if constexpr (LDS) {
+            img = ct_lds;
+            strip = (float*)(ct_lds + ((image_words(r) + 3) & ~3ll));
+        } else {
+            img = (uint32_t*)(slot + a.sc.img_off);
+            strip = (float*)slot;
+        }
+        MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+        CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime(); unsigned long long nrows = 0, npos = 0;
+                int nsteps = 0; unsigned long long ttr = 0);
+        build_image(s, b, k, r, img, strip, tid, CT_THREADS, ms);
+        CT_PROF(const unsigned long long t1 = __builtin_amdgcn_s_memtime());
+        if (s.stats) {  // pixel count and bbox (process_mask's instance mask)
+            if (tid == 0) {
+                s_red[0] = 0;
+                s_red[1] = s.Wn;
+                s_red[2] = -1;
+                s_red[3] = s.Hn;
+                s_red[4] = -1;
             }
             __syncthreads();
-            // cvFindNextContour's raster scan (RETR_EXTERNAL); best = the contour with the most points
-            int best_n = 0, bx = -1, by = -1, blx = 0, bly = 0, ncont = 0;
-            for (int y = 1; y < r.rH - 1; ++y) {
-                if (!rowflag[y]) continue;
-                int x = 1, prev = 0, lnbd = 0;
+            atomicAdd(&s_red[0], ms.cnt);
+            if (ms.x1 >= 0) {
+                atomicMin(&s_red[1], ms.x0);
+                atomicMax(&s_red[2], ms.x1);
+                atomicMin(&s_red[3], ms.y0);
+                atomicMax(&s_red[4], ms.y1);
+            }
+            __syncthreads();
+            if (tid == 0) s.stats[di] = va_mask_stat{s_red[0], s_red[1], s_red[3], s_red[2], s_red[4], {0, 0, 0}};
+        }
+        if constexpr (!LDS) __threadfence();  // the image before the coherent reads of the scan
+        // cvFindNextContour's raster scan (RETR_EXTERNAL); the contour with the most points stays in its half of
+        // the instance's point buffer
+        uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
+        int best_n = 0, best_half = 0, bx = -1, by = -1, ncont = 0, alt = 0;
+        for (int y = 1; y < r.rH - 1; ++y) {
+            if (!row_has_start<LDS>(img, r.ww, y)) continue;
+            CT_PROF(++nrows);
+            // OpenCV's skip loop visits the positions whose value differs from their left neighbour's (the
+            // scan's prev is always the value at x - 1): per 2048-pixel chunk each lane holds its word's change
+            // flags and value planes, and the positions are taken in order from registers; a trace changes marks,
+            // so the chunk is re-read after one
+            const uint32_t* nzr = plane(img, r.ww, y, 0);
+            const uint32_t* nr = plane(img, r.ww, y, 1);
+            const uint32_t* rr = plane(img, r.ww, y, 2);
+            int prev = 0, lnbd = 0;
+            for (int w0 = 0; w0 < r.ww; w0 += 64) {
+                const int wi = w0 + lane;
+                uint32_t chi = 0u, clo = 0u, dm = 0u;
+                auto load = [&](int from) {  // value planes + change flags at positions >= from
+                    uint32_t phi = 0u, plo = 0u;
+                    chi = clo = 0u;
+                    if (wi < r.ww) code_planes(nzr[wi], ldm<LDS>(nr + wi), ldm<LDS>(rr + wi), chi, clo);
+                    if (wi >= 1 && wi <= r.ww)
+                        code_planes(nzr[wi - 1], ldm<LDS>(nr + wi - 1), ldm<LDS>(rr + wi - 1), phi, plo);
+                    dm = (chi ^ ((chi << 1) | (phi >> 31))) | (clo ^ ((clo << 1) | (plo >> 31)));
+                    const int fw = from >> 5;
+                    if (wi < fw || wi >= r.ww) dm = 0u;
+                    else if (wi == fw) dm &= ~0u << (from & 31);
+                };
+                load(0);
                 while (true) {
-                    x = next_stop(img, y, x, r.rW, prev);
-                    if (x >= r.rW) break;
-                    const int p = img.val(x, y);
+                    const unsigned long long bal = __ballot(dm != 0u);
+                    if (!bal) break;
+                    const int l = __builtin_ctzll(bal);
+                    const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)dm, l);
+                    const int j = __builtin_ctz(dl);
+                    const int x = 32 * (w0 + l) + j;
+                    const uint32_t vh = ((uint32_t)__builtin_amdgcn_readlane((int)chi, l) >> j) & 1u;
+                    const uint32_t vl = ((uint32_t)__builtin_amdgcn_readlane((int)clo, l) >> j) & 1u;
+                    const int p = vh ? (vl ? -126 : 2) : (int)vl;
+                    if (lane == l) dm &= ~(1u << j);
+                    CT_PROF(++npos);
                     if (prev == 0 && p == 1) {
-                        if (img.val(lnbd, y) <= 0) {
-                            int lx = 0, ly = 0;
-                            const int n = fetch_contour(img, x, y, true, [&](int px, int py) { lx = px, ly = py; });
+                        if (uni(val_at<LDS>(img, r.ww, lnbd, y)) <= 0) {
+                            uint32_t* dst = cp + alt * a.sc.capd;
+                            int i = 0;
+                            CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
+                            const int n = fetch_contour(
+                                img, r.ww, x, y, true,
+                                [&](int px, int py) {
+                                    if (lane == 0 && i < a.sc.capd)
+                                        dst[i] = (uint32_t)(r.X0 + px - 1) | ((uint32_t)(r.Y0 + py - 1) << 16);
+                                    ++i;
+                                },
+                                CT_STEPS);
+                            CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
                             ++ncont;
                             if (n > best_n) {
-                                best_n = n, bx = x, by = y, blx = lx, bly = ly;
+                                best_n = n, best_half = alt, bx = x, by = y;
+                                alt ^= 1;
                             }
-                            __threadfence();  // the marks (atomics at L2) before the scan reads on
-                            prev = img.val(x, y);
-                            ++x;
+                            if constexpr (!LDS) __threadfence();  // the marks before the scan reads on
+                            prev = uni(val_at<LDS>(img, r.ww, x, y));
+                            load(x + 1);
                             continue;
                         }
                     } else if (p == 0 && prev >= 1) {
@@ -366,42 +585,70 @@ __global__ __launch_bounds__(CT_THREADS) void post_contour_kernel(CtArgs a) {
                     }
                     prev = p;
                     if (p & -2) lnbd = x;
-                    ++x;
                 }
             }
-            st.npts = best_n;
-            st.ncont = ncont;
-            if (best_n > 0) {
-                st.ox = bx, st.oy = by;
-                // cv2.contourArea of the float32 scale_coords points, from the last point on (OpenCV's order)
+        }
+        st.npts = best_n;
+        st.ncont = ncont;
+        st.half = best_half;
+        CT_PROF(const unsigned long long t2 = __builtin_amdgcn_s_memtime());
+        if (best_n > 0) {
+            st.ox = bx, st.oy = by;
+            // cv2.contourArea of the float32 scale_coords points: a00 += prev.x * y - prev.y * x from the last
+            // point on, in order (terms in parallel, summed in order); the polygon itself if asked for
+            double acc = 0.0;
+            if (best_n <= a.sc.capd) {
+                __threadfence();  // lane 0's point stores before every lane reads them
+                const uint32_t* P = cp + best_half * a.sc.capd;
+                const uint32_t plast = P[best_n - 1];
+                for (int b0 = 0; b0 < best_n; b0 += 64) {
+                    const int i = b0 + lane;
+                    double term = 0.0;
+                    if (i < best_n) {
+                        const uint32_t q = P[i], pq = i == 0 ? plast : P[i - 1];
+                        float xs, ys, pxs, pys;
+                        scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
+                        scale_pt(a.f, (int)(pq & 0xFFFFu), (int)(pq >> 16), &pxs, &pys);
+                        term = (double)pxs * (double)ys - (double)pys * (double)xs;
+                        if (poly && i < a.poly_cap) {
+                            poly[2 * i] = xs;
+                            poly[2 * i + 1] = ys;
+                        }
+                    }
+                    const int m = min(64, best_n - b0);
+                    for (int j = 0; j < m; ++j) acc += readlane_f64(term, j);
+                }
+            } else {  // longer than the buffer: followed again from the image (marks off)
+                int lx = 0, ly = 0;
+                fetch_contour(img, r.ww, bx, by, false, [&](int px, int py) { lx = px, ly = py; });
                 float pxs, pys;
-                scale_pt(a.f, r.X0 + blx - 1, r.Y0 + bly - 1, &pxs, &pys);
-                double a00 = 0.0;
-                float* poly = a.polys ? a.polys + ((int64_t)b * a.max_det + k) * a.poly_cap * 2 : nullptr;
+                scale_pt(a.f, r.X0 + lx - 1, r.Y0 + ly - 1, &pxs, &pys);
                 int i = 0;
-                fetch_contour(img, bx, by, false, [&](int qx, int qy) {
+                fetch_contour(img, r.ww, bx, by, false, [&](int qx, int qy) {
                     float xs, ys;
                     scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
-                    a00 += (double)pxs * (double)ys - (double)pys * (double)xs;
+                    acc += (double)pxs * (double)ys - (double)pys * (double)xs;
                     pxs = xs, pys = ys;
-                    if (poly && i < a.poly_cap && tid == 0) {
+                    if (poly && i < a.poly_cap && lane == 0) {
                         poly[2 * i] = xs;
                         poly[2 * i + 1] = ys;
                     }
                     ++i;
                 });
-                st.area = fabs(a00 * 0.5);
-                if (a.poly_n && tid == 0) a.poly_n[(int64_t)b * a.max_det + k] = best_n;
-            } else if (a.poly_n && tid == 0) {
-                a.poly_n[(int64_t)b * a.max_det + k] = 0;
             }
-            st.X0 = r.X0, st.Y0 = r.Y0;
-        } else {
-            st.status = r.w > 0 ? 1 : 0;  // 1: region taller than the row-flag table
-            if (a.poly_n && tid == 0) a.poly_n[(int64_t)b * a.max_det + k] = 0;
+            st.area = fabs(acc * 0.5);
         }
-        if (tid == 0) a.cstats[(int64_t)b * a.max_det + k] = st;
-        __syncthreads();  // the slot image is reused by the next item
+        if (tid == 0) {
+            if (a.poly_n) a.poly_n[di] = best_n;
+            a.cstats[di] = st;
+            CT_PROF(if (item < CT_PROF_ITEMS) {
+                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                unsigned long long* pr = g_ct_prof[item];
+                pr[0] = t1 - t0, pr[1] = t2 - t1, pr[2] = t3 - t2, pr[3] = (unsigned long long)ncont;
+                pr[4] = nrows, pr[5] = npos, pr[6] = (unsigned long long)nsteps, pr[7] = ttr;
+            });
+        }
+        __syncthreads();  // the image is reused by the next item
     }
 }
 
@@ -510,25 +757,37 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
             __syncthreads();
             continue;
         }
-        const va_contour_stat st = a.cstats[(int64_t)b * a.max_det + k];
+        const int64_t di = (int64_t)b * a.max_det + k;
+        const va_contour_stat st = a.cstats[di];
         if (st.npts > a.sc.cap) {
             if (tid == 0 && a.status) a.status[b] = 1;
             if (tid < 4) a.rects[4 * b + tid] = 0;
             __syncthreads();
             continue;
         }
-        // the chosen instance's best contour, followed again into int32 frame points (np.int32 of scale_coords)
-        if (st.npts > 0) {
+        // the chosen instance's best contour as int32 frame points (np.int32 of scale_coords: truncation, >= 0)
+        if (st.npts > 0 && st.npts <= a.sc.capd) {
+            const uint32_t* P = a.sc.cpts + (di * 2 + st.half) * a.sc.capd;
+            for (int i = tid; i < st.npts; i += nt) {
+                const uint32_t q = P[i];
+                float xs, ys;
+                scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
+                pts[2 * i] = (int)xs;
+                pts[2 * i + 1] = (int)ys;
+            }
+            if (tid == 0) s_n = st.npts;
+        } else if (st.npts > 0) {  // longer than the buffer: the image rebuilt in the slot and followed again
             const Region r = region_of(s, b, k);
-            Img img{(uint32_t*)(slot + a.sc.img_off), r.ww, r.rH * r.ww};
-            build_image(s, b, k, r, img, (float*)slot, tid, nt);
+            uint32_t* img = (uint32_t*)(slot + a.sc.img_off);
+            MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+            build_image(s, b, k, r, img, (float*)slot, tid, nt, ms);
             if (tid < 64) {
                 int i = 0;
-                fetch_contour(img, st.ox, st.oy, false, [&](int qx, int qy) {
+                fetch_contour(img, r.ww, st.ox, st.oy, false, [&](int qx, int qy) {
                     float xs, ys;
                     scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
-                    if (tid == 0 && i < a.sc.cap && CT_OK(xs >= 0.f && ys >= 0.f, 9, xs, ys)) {
-                        pts[2 * i] = (int)xs;  // np.int32: truncation (the values are >= 0)
+                    if (tid == 0 && i < a.sc.cap) {
+                        pts[2 * i] = (int)xs;
                         pts[2 * i + 1] = (int)ys;
                     }
                     ++i;
@@ -547,7 +806,6 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
             s_eymin = INT32_MAX;
             s_eymax = INT32_MIN;
         }
-        __threadfence_block();
         __syncthreads();
         const int n = s_n;
         // boundingRect + the edges: lines through cell centres, span counts at the sampled rows
@@ -586,9 +844,8 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                     long long x = lx1, y = ly1;
                     for (long long st2 = 0; st2 <= dx; ++st2) {
                         if (x % VA_GRID == VA_GRID / 2 && y % VA_GRID == VA_GRID / 2 && x >= 0 && y >= 0 && x < W0 &&
-                            y < H0)
-                            if (CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
-                                hit[(y / VA_GRID) * LC + x / VA_GRID] = 1;
+                            y < H0 && CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
+                            hit[(y / VA_GRID) * LC + x / VA_GRID] = 1;
                         const bool minor = err < 0;
                         err += minus + (minor ? plus : 0);
                         if (vert) {
@@ -640,8 +897,8 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                     const long long xi = xx >> 16;
                     const long long qa = xi - VA_GRID / 2, qb = xi - VA_GRID / 2 - 1;
                     const long long ca = qa < 0 ? 0 : qa / VA_GRID + 1, cb = qb < 0 ? 0 : qb / VA_GRID + 1;
-                    if (ca < LC && CT_OK(ca >= 0, 11, ca, rr)) atomicAdd(&cnt_a[rr * (LC + 1) + ca], 1);
-                    if (cb < LC && CT_OK(cb >= 0, 12, cb, rr)) atomicAdd(&cnt_b[rr * (LC + 1) + cb], 1);
+                    if (ca < LC) atomicAdd(&cnt_a[rr * (LC + 1) + ca], 1);
+                    if (cb < LC) atomicAdd(&cnt_b[rr * (LC + 1) + cb], 1);
                 }
             }
         }
@@ -682,6 +939,13 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
                              const uint8_t* plant_cells, const int32_t* plant_rects, int plant_mode, uint8_t* cells,
                              int32_t* rects, int32_t* chosen, int32_t* status, float* polys, int32_t* poly_n,
                              int poly_cap, hipStream_t st) {
+    static DevFlag large_attr;  // per device: the large instantiation's dynamic LDS
+    if (!large_attr()) {
+        if (hipFuncSetAttribute((const void*)post_contour_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                CT_LDS_LARGE) != hipSuccess)
+            return hipErrorInvalidValue;
+        large_attr() = true;
+    }
     CtArgs ca;
     ca.s = src;
     ca.f = f;
@@ -693,7 +957,9 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     ca.poly_cap = poly_cap;
     const int64_t items = (int64_t)src.B * max_det;
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
-    hipLaunchKernelGGL(post_contour_kernel, dim3(grid), dim3(CT_THREADS), 0, st, ca);
+    hipLaunchKernelGGL(post_contour_kernel<0>, dim3(grid), dim3(CT_THREADS), CT_LDS_SMALL, st, ca);
+    hipLaunchKernelGGL(post_contour_kernel<1>, dim3(grid), dim3(CT_THREADS), CT_LDS_LARGE, st, ca);
+    hipLaunchKernelGGL(post_contour_kernel<2>, dim3(grid), dim3(CT_THREADS), 0, st, ca);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     if (!cells) return hipSuccess;
     FillArgs fa;
@@ -726,23 +992,20 @@ extern "C" {
 int va_contour_scratch_bytes(int32_t Hn, int32_t Wn, int32_t nslots, int32_t cap, int64_t* slot_bytes,
                              int64_t* img_off, int64_t* pts_off) {
     if (Hn <= 0 || Wn <= 0 || Hn % 4 || Wn % 4 || nslots <= 0 || cap <= 0) return VA_ERR_ARG;
-    const int64_t lowres = ((int64_t)(Hn / 4) * (Wn / 4) * 4 + 255) & ~255ll;
-    const int64_t img = ((int64_t)(Hn + 2) * (((Wn + 2) + 3) / 4) * 4 + 255) & ~255ll;
+    const int64_t strip = (int64_t)CT_STRIP * 4;
+    const int64_t img = (((int64_t)(Hn + 2) * 3 * (((Wn + 2) + 31) / 32) + 1) * 4 + 255) & ~255ll;
     const int64_t pts = (int64_t)cap * 8;
-    *img_off = lowres;
-    *pts_off = lowres + img;
-    *slot_bytes = lowres + img + pts;
+    *img_off = strip;
+    *pts_off = strip + img;
+    *slot_bytes = strip + img + pts;
     return VA_OK;
 }
-
-}  // extern "C"
-
-extern "C" {
 
 int va_post_select_masks(void* stream, const va_mask_select_args* m) {
     if (!m || !m->masks || !m->nmask || m->B <= 0 || m->maxn <= 0 || m->Hn <= 0 || m->Wn <= 0 || !m->scratch ||
         m->nslots <= 0 || m->cap <= 0 || !m->cstats || !frame_ok(m->H0, m->W0) || !(m->gain > 0.0f) ||
-        (m->cells && (!m->rects || !m->chosen)) || m->Hn + 2 > 4096 || m->Hn % 4 || m->Wn % 4)
+        (m->cells && (!m->rects || !m->chosen)) || m->Hn % 4 || m->Wn % 4 || m->Hn > 65535 || m->Wn > 65535 ||
+        !m->cpts || m->cpts_cap <= 0 || m->cpts_cap > m->cap)
         return VA_ERR_ARG;
     Src src{};
     src.masks = m->masks;
@@ -755,7 +1018,7 @@ int va_post_select_masks(void* stream, const va_mask_select_args* m) {
     src.mw = m->Wn / 4;
     src.max_det = m->maxn;
     Frame f{m->H0, m->W0, m->gain, m->padx, m->pady};
-    Scratch sc{(unsigned char*)m->scratch, 0, 0, 0, m->nslots, m->cap};
+    Scratch sc{(unsigned char*)m->scratch, 0, 0, 0, m->nslots, m->cap, m->cpts, m->cpts_cap};
     if (va_contour_scratch_bytes(m->Hn, m->Wn, m->nslots, m->cap, &sc.slot_bytes, &sc.img_off, &sc.pts_off) != VA_OK)
         return VA_ERR_ARG;
     const hipError_t e = va_contour_launch(src, f, sc, m->cstats, m->maxn, nullptr, nullptr, 0, m->cells, m->rects,
@@ -767,6 +1030,14 @@ int va_post_select_masks(void* stream, const va_mask_select_args* m) {
 }  // extern "C"
 
 #ifdef VA_CT_CHECK
+extern "C" int va_contour_prof(unsigned long long* out, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return VA_ERR_HIP;
+    if (n > CT_PROF_ITEMS) n = CT_PROF_ITEMS;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ct_prof), sizeof(unsigned long long) * 8 * n) != hipSuccess)
+        return VA_ERR_HIP;
+    return VA_OK;
+}
+
 extern "C" int va_contour_debug(unsigned int* out4, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return VA_ERR_HIP;
     if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_ct_err), sizeof(unsigned int) * 4) != hipSuccess) return VA_ERR_HIP;

@@ -539,11 +539,14 @@ __global__ __launch_bounds__(VA_NAV_THREADS) void nav_grid_kernel(GridArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// A*: one wave64 per query.  LDS layout per node: g f64 | key f64 | parent u16 | hist u16 | state u8 plus the
-// open list (u16 node ids): 23 B per node, 23.5 KiB at 640x640.  The node penalties stay in global memory
-// (8 KiB per frame, L1/L2-resident): with them in LDS (31 KiB) a query wave sharing a CU with two
-// conv2 workgroups (2 x 67.5 KiB) would not fit beside them, and the ~100 query waves of a batch,
-// overlapping the next batch's network, would halve conv occupancy on the CUs they land on.
+// A*: one wave64 per query.  LDS: the angle tables (1.1 KiB), then per node g f64 | parent u16 | hist u16 |
+// state u8, and per open-list slot its node u16, push-time f (key bits, u64) and (x, y) tie key u32: 27 B per
+// node, 28.7 KiB at 640x640.  The node penalties stay in global memory (8 KiB per frame, L1/L2-resident; a
+// query wave sharing a CU with two conv2 workgroups must fit beside them): a pop issues the four neighbours'
+// penalty loads first, so their latency runs under the pop's LDS work.  One wave per workgroup: no block
+// barrier is needed between the lanes' LDS accesses (a wave's LDS operations complete in order), only a
+// compiler-level ordering point (WAVE_SYNC).
+constexpr int ASTAR_TABLES = 128 * 8 + 64 + 32;  // angle penalties f64, prev / next index tables
 #define ST_EXISTS 1u
 #define ST_MULT_SHIFT 1  // bits 1-2
 #define ST_HASG 8u
@@ -564,6 +567,12 @@ struct AstarArgs {
     int slot0;                  // first slot to (re)run
     const uint64_t* seen;       // base seen set of this round
 };
+
+#define WAVE_SYNC()                                            \
+    do {                                                       \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                       \
+    } while (0)
 
 extern "C" __device__ __attribute__((const)) unsigned long long __ockl_wfred_min_u64(unsigned long long);
 extern "C" __device__ __attribute__((const)) unsigned int __ockl_wfred_min_u32(unsigned int);
@@ -590,14 +599,21 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     const double* npen = (const double*)((const uint8_t*)a.node_pen + (int64_t)fr * a.node_stride);
 
     extern __shared__ __align__(16) uint8_t smem[];
-    double* g = (double*)smem;
-    double* fk = g + N;
-    const double* __restrict__ pen = npen;  // global (see above)
-    uint16_t* par = (uint16_t*)(fk + N);
+    double* apen = (double*)smem;                 // [128] angle penalties
+    int8_t* pidx = (int8_t*)(apen + 128);         // [49] (+ pad)
+    int8_t* nidx = pidx + 64;                     // [25] (+ pad)
+    double* g = (double*)(smem + ASTAR_TABLES);
+    unsigned long long* okey = (unsigned long long*)(g + N);  // per open slot: push-time f bits
+    uint32_t* osec = (uint32_t*)(okey + N);       // per open slot: x << 24 | y << 16
+    uint16_t* par = (uint16_t*)(osec + N);
     uint16_t* hd = par + N;
     uint16_t* open = hd + N;
     uint8_t* st = (uint8_t*)(open + N);
+    const double* __restrict__ pen = npen;  // global (see above)
 
+    for (int i = lane; i < 128; i += 64) apen[i] = c_angle_pen[i];
+    if (lane < 49) pidx[lane] = c_prev_idx[lane];
+    if (lane < 25) nidx[lane] = c_next_idx[lane];
     for (int i = lane; i < N; i += 64) {
         uint8_t fl = nflags[i];
         uint8_t v = 0;
@@ -608,18 +624,19 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     unsigned long long seen0 = a.seen[0], seen1 = a.seen[1];
     unsigned long long miss0 = 0, miss1 = 0;
     const int ex = e % LC, ey = e / LC;
-    __syncthreads();
+    WAVE_SYNC();
     if (lane == 0) {
         g[s] = 0.0;
         int sx = s % LC, sy = s / LC;
-        fk[s] = (double)(VA_GRID * (abs(sx - ex) + abs(sy - ey)));
         hd[s] = 0;
         st[s] |= ST_HASG | ST_INOPEN;
         open[0] = (uint16_t)s;
+        okey[0] = (unsigned long long)__double_as_longlong((double)(VA_GRID * (abs(sx - ex) + abs(sy - ey))));
+        osec[0] = ((unsigned)sx << 24) | ((unsigned)sy << 16);
     }
     int open_n = 1;
     int found = 0, expansions = 0;
-    __syncthreads();
+    WAVE_SYNC();
     // neighbour order of FrameProcessor.py:195-200: right, left, down, up
     const int ndx = lane == 0 ? 1 : lane == 1 ? -1 : 0;
     const int ndy = lane == 2 ? 1 : lane == 3 ? -1 : 0;
@@ -628,9 +645,8 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         unsigned long long fb = ~0ull;
         unsigned sec = ~0u;
         for (int i = lane; i < open_n; i += 64) {
-            int nd = open[i];
-            unsigned long long kb = (unsigned long long)__double_as_longlong(fk[nd]);
-            unsigned ks = ((unsigned)(nd % LC) << 24) | ((unsigned)(nd / LC) << 16) | (unsigned)i;
+            const unsigned long long kb = okey[i];
+            const unsigned ks = osec[i] | (unsigned)i;
             if (kb < fb || (kb == fb && ks < sec)) {
                 fb = kb;
                 sec = ks;
@@ -639,31 +655,37 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         wave_argmin(fb, sec);
         const int slot = (int)(sec & 0xFFFFu);
         const int cur = (int)open[slot];
-        __syncthreads();
-        if (lane == 0) open[slot] = open[open_n - 1];
+        const int cx = cur % LC, cy = cur / LC;
+        // the neighbours (lanes 0..3) and their penalties, loaded now and consumed by the relaxation
+        int nb = -1;
+        if (lane < 4) {
+            const int nx = cx + ndx, ny = cy + ndy;
+            if (nx >= 0 && nx < LC && ny >= 0 && ny < a.LR) nb = ny * LC + nx;
+        }
+        const double pnb = pen[nb >= 0 ? nb : cur];  // unconditional: the wait lands at the use
+        WAVE_SYNC();
+        if (lane == 0) {
+            const int last = open_n - 1;
+            open[slot] = open[last];
+            okey[slot] = okey[last];
+            osec[slot] = osec[last];
+        }
         --open_n;
         ++expansions;
         if (cur == e) {
             found = 1;
             break;
         }
-        const int cx = cur % LC, cy = cur / LC;
         const double gcur = g[cur];
         const unsigned hcur = hd[cur];
         const unsigned mult = (st[cur] >> ST_MULT_SHIFT) & 3u;
-        __syncthreads();
+        WAVE_SYNC();
         if (lane == 0) st[cur] |= ST_CLOSED;
-        __syncthreads();
-        // ---- neighbours (lanes 0..3)
-        int nb = -1;
+        WAVE_SYNC();
         bool valid = false;
-        if (lane < 4) {
-            int nx = cx + ndx, ny = cy + ndy;
-            if (nx >= 0 && nx < LC && ny >= 0 && ny < a.LR) {
-                nb = ny * LC + nx;
-                uint8_t sv = st[nb];
-                valid = (sv & ST_EXISTS) && !(sv & ST_CLOSED);
-            }
+        if (nb >= 0) {
+            const uint8_t sv = st[nb];
+            valid = (sv & ST_EXISTS) && !(sv & ST_CLOSED);
         }
         unsigned long long vb = __ballot(valid);
         // angle penalty of the first non-closed neighbour (newest-window rule, Q3)
@@ -677,14 +699,14 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
                 m5 = (hcur >> 10) & 3;
             int nxv = mvx(m0) + mvx(m1), nyv = mvy(m0) + mvy(m1);
             int pxv = mvx(m3) + mvx(m4) + mvx(m5), pyv = mvy(m3) + mvy(m4) + mvy(m5);
-            int pi = c_prev_idx[(pxv + 3) * 7 + (pyv + 3)];
-            int ni = c_next_idx[(nxv + 2) * 5 + (nyv + 2)];
+            int pi = pidx[(pxv + 3) * 7 + (pyv + 3)];
+            int ni = nidx[(nxv + 2) * 5 + (nyv + 2)];
             if (pi >= 0 && ni >= 0) {
                 int key = pi * 8 + ni;
                 unsigned long long bit = 1ull << (key & 63);
                 bool hit = key < 64 ? (seen0 & bit) : (seen1 & bit);
                 if (!hit) {
-                    ap = c_angle_pen[key];
+                    ap = apen[key];
                     if (key < 64) {
                         seen0 |= bit;
                         miss0 |= bit;
@@ -698,10 +720,11 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         const int first = vb ? __ffsll((long long)vb) - 1 : -1;
         for (unsigned pass = 0; pass < mult; ++pass) {
             bool push = false;
-            double t = 0.0;
+            double t = 0.0, fnew = 0.0;
+            unsigned secn = 0;
             if (valid) {
                 double apj = (pass == 0 && lane == first) ? ap : 0.0;
-                double pm = (1.0 + (0.5 * pen[nb])) + (apj * 1.5);
+                double pm = (1.0 + (0.5 * pnb)) + (apj * 1.5);
                 t = gcur + (20.0 * pm);
                 uint8_t sv = st[nb];
                 if (!(sv & ST_HASG) || t < g[nb]) {
@@ -711,8 +734,9 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
                     hd[nb] = (uint16_t)((dnew << HD_DEPTH_SHIFT) | (((hcur << 2) | (unsigned)lane) & 0xFFFu));
                     if (!(sv & ST_INOPEN)) {
                         push = true;
-                        int nx = nb % LC, ny = nb / LC;
-                        fk[nb] = t + (double)(VA_GRID * (abs(nx - ex) + abs(ny - ey)));
+                        const int nx = nb % LC, ny = nb / LC;
+                        fnew = t + (double)(VA_GRID * (abs(nx - ex) + abs(ny - ey)));
+                        secn = ((unsigned)nx << 24) | ((unsigned)ny << 16);
                         st[nb] = sv | ST_HASG | ST_INOPEN;
                     } else {
                         st[nb] = sv | ST_HASG;
@@ -721,11 +745,13 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
             }
             unsigned long long pb = __ballot(push);
             if (push) {
-                int before = __popcll(pb & ((1ull << lane) - 1ull));
-                open[open_n + before] = (uint16_t)nb;
+                const int pos = open_n + __popcll(pb & ((1ull << lane) - 1ull));
+                open[pos] = (uint16_t)nb;
+                okey[pos] = (unsigned long long)__double_as_longlong(fnew);
+                osec[pos] = secn;
             }
             open_n += __popcll(pb);
-            __syncthreads();
+            WAVE_SYNC();
         }
     }
     // ---- result
@@ -899,7 +925,7 @@ hipError_t ensure_tables() {
     return hipSuccess;
 }
 
-size_t astar_lds(int nodes) { return (size_t)nodes * (8 + 8 + 2 + 2 + 2 + 1) + 16; }
+size_t astar_lds(int nodes) { return ASTAR_TABLES + (size_t)nodes * (8 + 8 + 4 + 2 + 2 + 2 + 1) + 16; }
 
 // speculative rounds over `nslots` query slots
 int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out) {

@@ -8,13 +8,12 @@
 //                        max_det cap (ops.py:318-330): one 1024-thread workgroup per frame, candidates
 //                        bitonic-sorted in LDS and scanned greedily in 64-candidate chunks (fallback for
 //                        lists that do not fit: repeated "highest remaining -> keep -> suppress")
-//   post_mask_kernel     process_mask(upsample=True) (ops.py:707-737): coef . proto over the cropped
-//                        low-res box region into LDS, bilinear x4 (align_corners=False), > 0; per
-//                        instance pixel count and pixel bounding box.  One workgroup per detection.
-//   mask choice          FrameProcessor.py:67-97 with OpenCV's findContours / contourArea / boundingRect /
-//                        fillPoly restated (va_contour.hip, checked against oracle/contours.py; cv2 parity
-//                        unpinned) -> the nav stage's (cells, rect); optional planted masks (bench / tests) when
-//                        the network yields no detection.
+//   masks + choice       process_mask (ops.py:707-737: coef . proto over the cropped low-res box region,
+//                        bilinear x4, > 0) with each instance's pixel count / bbox, and FrameProcessor.py:67-97
+//                        with OpenCV's findContours / contourArea / boundingRect / fillPoly restated
+//                        (va_contour.hip, checked against oracle/contours.py; cv2 parity unpinned) -> the nav
+//                        stage's (cells, rect); optional planted masks (bench / tests) when the network yields
+//                        no detection.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -159,6 +158,7 @@ __global__ __launch_bounds__(DEC_THREADS) void post_decode_kernel(LevelPtrs lv, 
 // ------------------------------------------------------------------------------------------- NMS
 constexpr int NMS_THREADS = 1024;
 constexpr int NMS_CAP = 16384;       // candidates whose keys fit LDS (128 KiB)
+constexpr int NMS_BATCH = 2048;      // longer lists: sorted and scanned in batches of their largest keys
 constexpr int NMS_KEPT_MAX = 1024;   // max_det of the sorted path (kept boxes in LDS)
 constexpr int NMS_CH = 64;           // candidates per greedy-scan chunk (one ballot per row)
 constexpr size_t NMS_LDS = (size_t)NMS_CAP * 8 + (size_t)NMS_KEPT_MAX * 20 + NMS_CH * 32;
@@ -208,18 +208,31 @@ __device__ unsigned long long nms_select(const unsigned long long* keys, int n, 
             if (kk < hi && (kk & mask) == prefix) atomicAdd(&s_hist[(kk >> shift) & 255], 1u);
         }
         __syncthreads();
-        if (tid == 0) {
-            int need = *s_k, dsel = 0;
-            for (int dg = 255; dg >= 0; --dg) {
-                const int h = (int)s_hist[dg];
-                if (h >= need) {
-                    dsel = dg;
-                    break;
-                }
-                need -= h;
+        if (tid < 64) {  // the digit: suffix sums over the 256 bins, 4 per lane, on wave 0
+            const int need = *s_k;
+            const unsigned h0 = s_hist[4 * tid], h1 = s_hist[4 * tid + 1], h2 = s_hist[4 * tid + 2],
+                           h3 = s_hist[4 * tid + 3];
+            const unsigned own = h0 + h1 + h2 + h3;
+            unsigned suf = own;  // this lane's bins and every higher lane's
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned t = __shfl_down(suf, o, 64);
+                if (tid + o < 64) suf += t;
             }
-            *s_k = need;
-            *s_T = prefix | ((unsigned long long)dsel << shift);
+            const unsigned above = suf - own;
+            if (suf >= (unsigned)need && above < (unsigned)need) {  // exactly one lane
+                int left = need - (int)above, dsel = 4 * tid;
+                if ((int)h3 >= left) {
+                    dsel += 3;
+                } else if ((int)(h3 + h2) >= left) {
+                    dsel += 2, left -= (int)h3;
+                } else if ((int)(h3 + h2 + h1) >= left) {
+                    dsel += 1, left -= (int)(h3 + h2);
+                } else {
+                    left -= (int)(h3 + h2 + h1);
+                }
+                *s_k = left;
+                *s_T = prefix | ((unsigned long long)dsel << shift);
+            }
         }
         __syncthreads();
         prefix = *s_T;
@@ -230,7 +243,8 @@ __device__ unsigned long long nms_select(const unsigned long long* keys, int n, 
     return prefix;
 }
 
-// One 1024-thread workgroup per frame.  Sorted path (n <= NMS_CAP, A <= 65536, max_det <= NMS_KEPT_MAX):
+// One 1024-thread workgroup per frame.  Sorted path (A <= 65536, max_det <= NMS_KEPT_MAX; lists longer than
+// NMS_BATCH in batches of their largest keys, so a frame sorts 2048 keys at a time, not all of them):
 // keys (score bits | ~anchor | list index) bitonic-sorted descending in LDS -- the order the greedy scan
 // visits candidates in (highest score, lowest anchor on ties) -- then 64-candidate chunks: each candidate
 // tested against every box kept so far (16 threads per candidate), the chunk's own pairwise suppression
@@ -265,10 +279,10 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
             return ((unsigned long long)__float_as_uint(C[i].score) << 32) |
                    ((unsigned long long)(0xFFFFu - (unsigned)C[i].anchor) << 16) | (unsigned long long)i;
         };
-        // lists longer than NMS_CAP run in batches: the NMS_CAP largest keys below the previous batch's
+        // lists longer than NMS_BATCH run in batches: the NMS_BATCH largest keys below the previous batch's
         // smallest (an exact radix select over the keys in global scratch, keys are unique), sorted and
         // scanned like a short list, until max_det boxes are kept or the list is exhausted
-        const bool big = n > NMS_CAP || n > max_nms;  // batches (or the max_nms cut) through global keys
+        const bool big = n > NMS_BATCH || n > max_nms;  // batches (or the max_nms cut) through global keys
         unsigned long long* gk = gkeys + (int64_t)b * A;
         if (big) {
             for (int i = tid; i < n; i += NMS_THREADS) gk[i] = key_of(i);
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
         while (true) {
             int nb = n;  // this batch's candidates
             if (big) {
-                const int want = min(NMS_CAP, max_nms - taken);
+                const int want = min(NMS_BATCH, max_nms - taken);
                 if (tid == 0) s_m = 0;
                 __syncthreads();
                 for (int i0 = 0; i0 < n; i0 += NMS_THREADS) {  // one LDS atomic per wave
@@ -455,209 +469,6 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
     if (tid == 0) ndet[b] = kept;
 }
 
-// ------------------------------------------------------------------------------------------- masks
-struct MaskArgs {
-    const float* proto;  // [B][mh][mw][32]
-    const float* lv[3];
-    int B, H, W, nc, max_det, mh, mw;
-    const va_det* dets;
-    const int32_t* ndet;
-    va_mask_stat* stats;  // [B][max_det]
-};
-
-__device__ inline const float* coef_of(const MaskArgs& a, int b, int anchor) {
-    int local;
-    Level L = level_of(a.lv, a.H, a.W, anchor, &local);
-    const int no = 4 * REG_MAX + a.nc + NMC;
-    return L.p + ((int64_t)b * L.h * L.w + local) * no + 4 * REG_MAX + a.nc;
-}
-
-// low-res crop window of a detection: r >= x1*mw/W && r < x2*mw/W (crop_mask), clipped to the map
-__device__ inline void crop_window(const va_det& d, int W, int H, int mw, int mh, int* rx0, int* rx1, int* ry0,
-                                   int* ry1) {
-    float fx1 = d.x1 * ((float)mw / (float)W), fx2 = d.x2 * ((float)mw / (float)W);
-    float fy1 = d.y1 * ((float)mh / (float)H), fy2 = d.y2 * ((float)mh / (float)H);
-    int a0 = (int)ceilf(fx1), a1 = (int)ceilf(fx2) - 1;  // integer r with fx1 <= r < fx2
-    int b0 = (int)ceilf(fy1), b1 = (int)ceilf(fy2) - 1;
-    *rx0 = max(a0, 0);
-    *rx1 = min(a1, mw - 1);
-    *ry0 = max(b0, 0);
-    *ry1 = min(b1, mh - 1);
-}
-
-// bilinear tap positions of F.interpolate(align_corners=False) for output index o (scale in/out)
-__device__ inline void taps(int o, float scale, int in, int* i0, int* i1, float* l0, float* l1) {
-    float src = scale * ((float)o + 0.5f) - 0.5f;
-    if (src < 0.f) src = 0.f;
-    int x0 = (int)src;
-    int p = x0 < in - 1 ? 1 : 0;
-    *l1 = src - (float)x0;
-    *l0 = 1.0f - *l1;
-    *i0 = x0;
-    *i1 = x0 + p;
-}
-
-constexpr int MASK_THREADS = 256;
-constexpr int MASK_STRIP = 6144;    // low-res window values in LDS per strip (24 KiB)
-constexpr int MASK_MAX_STRIPS = 128;
-
-// One workgroup per detection.  The low-res crop window of coef . proto is built in LDS one strip of rows
-// at a time (S rows + the next one, S = MASK_STRIP / width - 1), and each strip upsamples the full-res
-// rows whose upper tap falls in it.  Work unit = one BLOCK of full-res pixels sharing their four low-res
-// taps (the run of columns with one horizontal tap pair x the run of rows with one vertical pair: 4 x 4
-// inside the map at the x4 upsample).  With one weight of each pair >= 1/2 and both >= 0, four tap values
-// >= 2^-98 blend to > 0 at every pixel of the block and four values <= 0 to <= 0, so a one-sign block is
-// counted whole; only mixed blocks evaluate wy0 * (wx0 * v(ya, xa) + wx1 * v(ya, xb)) + wy1 * (wx0 *
-// v(yb, xa) + wx1 * v(yb, xb)) per pixel, the per-pixel form's exact expression.  Small LDS (strip + run
-// tables, ~27 KiB at 640 x 640) keeps several workgroups per CU: the work per detection is short and
-// latency-bound, so concurrency is what counts.
-__global__ __launch_bounds__(MASK_THREADS) void post_mask_kernel(MaskArgs a) {
-    const int k = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-    if (k >= a.ndet[b]) return;
-    const va_det d = a.dets[(int64_t)b * a.max_det + k];
-    int rx0, rx1, ry0, ry1;
-    crop_window(d, a.W, a.H, a.mw, a.mh, &rx0, &rx1, &ry0, &ry1);
-    va_mask_stat* st = a.stats + (int64_t)b * a.max_det + k;
-    __shared__ float coef[NMC];
-    __shared__ int s_cnt, s_x0, s_x1, s_y0, s_y1;
-    extern __shared__ __align__(16) int mask_smem_i[];
-    const int MC = a.mw + 4, MR = a.mh + 4;  // run-table capacities (low-res columns / rows)
-    int* cs = mask_smem_i;                   // [MC]: first full-res column whose left tap is xa0 + i
-    int* ce = cs + MC;                       //       one past its last
-    int* rs = ce + MC;                       // [MR]: the same for full-res rows (offsets from Y0)
-    int* re = rs + MR;
-    float* tile = (float*)(re + MR);         // [S + 1][tw]: one strip of the crop window
-    if (rx1 < rx0 || ry1 < ry0) {
-        if (tid == 0) *st = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
-        return;
-    }
-    const int tw = rx1 - rx0 + 1, th = ry1 - ry0 + 1;
-    const int S = MASK_STRIP / tw - 1;  // >= 1: the launcher checks mw <= MASK_STRIP / 2
-    const int nstrips = (th + S - 1) / S;
-    if (tid < NMC) coef[tid] = coef_of(a, b, d.anchor)[tid];
-    if (tid == 0) {
-        s_cnt = 0;
-        s_x0 = a.W;
-        s_x1 = -1;
-        s_y0 = a.H;
-        s_y1 = -1;
-    }
-    const float sx = (float)a.mw / (float)a.W, sy = (float)a.mh / (float)a.H;
-    // full-res pixels whose taps can touch the window
-    const int X0 = max(0, (int)((rx0 - 1) / sx) - 2), X1 = min(a.W - 1, (int)((rx1 + 1) / sx) + 2);
-    const int Y0 = max(0, (int)((ry0 - 1) / sy) - 2), Y1 = min(a.H - 1, (int)((ry1 + 1) / sy) + 2);
-    const int ow = X1 - X0 + 1, oh = Y1 - Y0 + 1;
-    int xa0, ya0, xal, yal, u_;
-    float w0_, w1_;
-    taps(X0, sx, a.mw, &xa0, &u_, &w0_, &w1_);
-    taps(Y0, sy, a.mh, &ya0, &u_, &w0_, &w1_);
-    taps(X1, sx, a.mw, &xal, &u_, &w0_, &w1_);
-    taps(Y1, sy, a.mh, &yal, &u_, &w0_, &w1_);
-    const int ncol = xal - xa0 + 1, nrow = yal - ya0 + 1;  // left / upper taps are non-decreasing in X / Y
-    // run tables: the full-res columns (rows) whose left (upper) tap is xa0 + i (ya0 + j)
-    for (int i = tid; i < ncol; i += MASK_THREADS) cs[i] = ce[i] = 0;
-    for (int j = tid; j < nrow; j += MASK_THREADS) rs[j] = re[j] = 0;
-    __syncthreads();
-    for (int x = tid; x < ow; x += MASK_THREADS) {
-        int t0, tp = -1, tn = -1, u;
-        float f0, f1;
-        taps(X0 + x, sx, a.mw, &t0, &u, &f0, &f1);
-        if (x > 0) taps(X0 + x - 1, sx, a.mw, &tp, &u, &f0, &f1);
-        if (x + 1 < ow) taps(X0 + x + 1, sx, a.mw, &tn, &u, &f0, &f1);
-        if (tp != t0) cs[t0 - xa0] = X0 + x;
-        if (tn != t0) ce[t0 - xa0] = X0 + x + 1;
-    }
-    for (int y = tid; y < oh; y += MASK_THREADS) {
-        int t0, tp = -1, tn = -1, u;
-        float f0, f1;
-        taps(Y0 + y, sy, a.mh, &t0, &u, &f0, &f1);
-        if (y > 0) taps(Y0 + y - 1, sy, a.mh, &tp, &u, &f0, &f1);
-        if (y + 1 < oh) taps(Y0 + y + 1, sy, a.mh, &tn, &u, &f0, &f1);
-        if (tp != t0) rs[t0 - ya0] = y;
-        if (tn != t0) re[t0 - ya0] = y + 1;
-    }
-    const int sub = tid & 7;
-    const float4 cq = make_float4(coef[4 * sub], coef[4 * sub + 1], coef[4 * sub + 2], coef[4 * sub + 3]);
-    int cnt = 0, bx0 = a.W, bx1 = -1, by0 = a.H, by1 = -1;
-    constexpr float POS4 = 3.155443620884047e-30f;  // 2^-98: blended twice it stays >= 2^-100 > 0
-    for (int ks = 0; ks < nstrips; ++ks) {
-        const int s0 = ry0 + ks * S, s1 = min(s0 + S, ry1);  // crop rows held: s0 .. s1
-        __syncthreads();  // previous strip consumed; run tables / coef visible
-        // the strip of coef . proto: 8 lanes per low-res pixel, each one 16-byte run of its 32 channels
-        // (a wave reads 8 whole 128-byte pixels, coalesced), partial dots reduced across the 8 lanes
-        for (int i = tid >> 3; i < (s1 - s0 + 1) * tw; i += MASK_THREADS / 8) {
-            const int y = s0 + i / tw, x = rx0 + i % tw;
-            const float4 v = *(const float4*)(a.proto + (((int64_t)b * a.mh + y) * a.mw + x) * NMC + 4 * sub);
-            float sdot = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
-            sdot += __shfl_xor(sdot, 1, 8);
-            sdot += __shfl_xor(sdot, 2, 8);
-            sdot += __shfl_xor(sdot, 4, 8);
-            if (sub == 0) tile[i] = sdot;
-        }
-        __syncthreads();
-        auto val = [&](int yy, int xx) -> float {
-            if (xx < rx0 || xx > rx1 || yy < ry0 || yy > ry1) return 0.f;
-            return tile[(yy - s0) * tw + (xx - rx0)];
-        };
-        // upper taps this strip owns: s0 .. s0 + S - 1 (strip 0 also the rows above the crop); blocks whose
-        // taps all miss the crop are 0 everywhere (never counted)
-        const int jlo = ks == 0 ? 0 : s0 - ya0, jhi = min(nrow, s0 + S - ya0);
-        const int nj = max(0, jhi - jlo);
-        for (int it = tid; it < ncol * nj; it += MASK_THREADS) {
-            const int i = it % ncol, j = jlo + it / ncol;
-            const int xa = xa0 + i, ya = ya0 + j;
-            const int c0 = cs[i], c1 = ce[i], r0 = rs[j], r1 = re[j];
-            if (c1 <= c0 || r1 <= r0) continue;
-            const int xb = min(xa + 1, a.mw - 1), yb = min(ya + 1, a.mh - 1);
-            if (ya > ry1 || yb < ry0) continue;
-            const float A = val(ya, xa), B = val(ya, xb), C = val(yb, xa), D = val(yb, xb);
-            int c = 0, fx = a.W, lx = -1, fy = a.H, ly = -1;
-            if (A >= POS4 && B >= POS4 && C >= POS4 && D >= POS4) {
-                c = (c1 - c0) * (r1 - r0);
-                fx = c0;
-                lx = c1 - 1;
-                fy = Y0 + r0;
-                ly = Y0 + r1 - 1;
-            } else if (!(A <= 0.f && B <= 0.f && C <= 0.f && D <= 0.f)) {
-                for (int X = c0; X < c1; ++X) {
-                    int ta, tb;
-                    float wx0, wx1;
-                    taps(X, sx, a.mw, &ta, &tb, &wx0, &wx1);
-                    const float ha = wx0 * A + wx1 * B, hb = wx0 * C + wx1 * D;
-                    for (int r = r0; r < r1; ++r) {
-                        int tc, td;
-                        float wy0, wy1;
-                        taps(Y0 + r, sy, a.mh, &tc, &td, &wy0, &wy1);
-                        if (wy0 * ha + wy1 * hb > 0.f) {
-                            ++c;
-                            fx = min(fx, X);
-                            lx = max(lx, X);
-                            fy = min(fy, Y0 + r);
-                            ly = max(ly, Y0 + r);
-                        }
-                    }
-                }
-            }
-            if (c) {
-                cnt += c;
-                bx0 = min(bx0, fx);
-                bx1 = max(bx1, lx);
-                by0 = min(by0, fy);
-                by1 = max(by1, ly);
-            }
-        }
-    }
-    atomicAdd(&s_cnt, cnt);
-    if (bx1 >= 0) {
-        atomicMin(&s_x0, bx0);
-        atomicMax(&s_x1, bx1);
-        atomicMin(&s_y0, by0);
-        atomicMax(&s_y1, by1);
-    }
-    __syncthreads();
-    if (tid == 0) *st = va_mask_stat{s_cnt, s_x0, s_y0, s_x1, s_y1, {0, 0, 0}};
-}
-
 // LetterBox: one thread per destination pixel (3 bytes).  Resize = cv2.INTER_LINEAR on uint8 in its
 // fixed-point form: per axis src = (d + 0.5) / scale - 0.5, clamped at the borders, weights rounded to
 // 11 bits (w0 = round((1 - f) * 2048), w1 = 2048 - w0); the two passes combine as
@@ -720,7 +531,8 @@ int contours(hipStream_t st, const va_post_args* p, float* polys, int32_t* poly_
     const bool lb = p->H0 > 0;
     const int H0 = lb ? p->H0 : p->H, W0 = lb ? p->W0 : p->W;
     if (!p->cscratch || p->cslots <= 0 || p->ccap <= 0 || !p->cstats || H0 % VA_GRID || W0 % VA_GRID ||
-        H0 / VA_GRID > 64 || W0 / VA_GRID > 64 || p->H + 2 > 4096 || (lb && !(p->sc_gain > 0.0f)))
+        H0 / VA_GRID > 64 || W0 / VA_GRID > 64 || p->H > 65535 || p->W > 65535 || (lb && !(p->sc_gain > 0.0f)) ||
+        !p->cpts || p->cpts_cap <= 0 || p->cpts_cap > p->ccap)
         return VA_ERR_ARG;
     if (fill && (!p->cells || !p->rects || !p->chosen || (p->plant_mode && (!p->plant_cells || !p->plant_rects))))
         return VA_ERR_ARG;
@@ -736,8 +548,9 @@ int contours(hipStream_t st, const va_post_args* p, float* polys, int32_t* poly_
     src.Wn = p->W;
     src.mh = p->H / 4;
     src.mw = p->W / 4;
+    src.stats = p->stats;
     CtFrame f{H0, W0, lb ? p->sc_gain : 1.0f, lb ? p->sc_padx : 0.0f, lb ? p->sc_pady : 0.0f};
-    CtScratch sc{(unsigned char*)p->cscratch, 0, 0, 0, p->cslots, p->ccap};
+    CtScratch sc{(unsigned char*)p->cscratch, 0, 0, 0, p->cslots, p->ccap, p->cpts, p->cpts_cap};
     if (va_contour_scratch_bytes(p->H, p->W, p->cslots, p->ccap, &sc.slot_bytes, &sc.img_off, &sc.pts_off) != VA_OK)
         return VA_ERR_ARG;
     const hipError_t e = va_contour_launch(src, f, sc, p->cstats, p->max_det, p->plant_cells, p->plant_rects,
@@ -782,17 +595,6 @@ int va_post_run(void* stream, const va_post_args* p) {
     hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, DEC_APB), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
                        p->nc, A, p->conf, p->cand, p->cand_count);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    const size_t mask_lds = (size_t)2 * (p->W / 4 + 4 + p->H / 4 + 4) * 4 + (size_t)MASK_STRIP * 4;
-    if (p->W / 4 > MASK_STRIP / 2 || mask_lds > 160 * 1024 - 2048 ||
-        (p->H / 4 + MASK_STRIP / (p->W / 4) - 2) / (MASK_STRIP / (p->W / 4) - 1) > MASK_MAX_STRIPS)
-        return VA_ERR_ARG;  // the strips of the widest window must fit the kernel's tables
-    static DevVal<size_t> mask_attr;  // per device: the largest dynamic LDS set so far
-    if (mask_lds > mask_attr()) {
-        if (hipFuncSetAttribute((const void*)post_mask_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)mask_lds) != hipSuccess)
-            return VA_ERR_HIP;
-        mask_attr() = mask_lds;
-    }
     static DevFlag nms_attr;  // post_nms_kernel's 150 KiB of dynamic LDS (set explicitly: graph kernel nodes too)
     if (!nms_attr()) {
         if (hipFuncSetAttribute((const void*)post_nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -804,25 +606,7 @@ int va_post_run(void* stream, const va_post_args* p) {
     hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), NMS_LDS, st, p->cand, p->cand_count, A, p->iou,
                        p->max_det, max_nms, p->dets, p->ndet, p->keys);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    MaskArgs ma;
-    ma.proto = p->proto;
-    ma.lv[0] = p->levels[0];
-    ma.lv[1] = p->levels[1];
-    ma.lv[2] = p->levels[2];
-    ma.B = B;
-    ma.H = p->H;
-    ma.W = p->W;
-    ma.nc = p->nc;
-    ma.max_det = p->max_det;
-    ma.mh = p->H / 4;
-    ma.mw = p->W / 4;
-    ma.dets = p->dets;
-    ma.ndet = p->ndet;
-    ma.stats = p->stats;
-    hipLaunchKernelGGL(post_mask_kernel, dim3(p->max_det, B), dim3(MASK_THREADS), mask_lds, st, ma);
-    if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-    if (p->cells) return contours(st, p, nullptr, nullptr, 0, true);
-    return VA_OK;
+    return contours(st, p, nullptr, nullptr, 0, p->cells != nullptr);
 }
 
 int va_post_polygons(void* stream, const va_post_args* p, float* polys, int32_t* poly_n, int32_t poly_cap) {

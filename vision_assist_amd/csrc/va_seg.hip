@@ -33,6 +33,8 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 // va_pw.hip: the streaming pointwise kernel for 1x1 / Cout-128 layers
 bool va_pw_eligible(const va_conv_args& a);
 hipError_t va_pw_launch(const va_conv_args& a, hipStream_t st);
+bool va_fp8_conv_ok(const va_conv_args& a);
+hipError_t va_fp8_conv_launch(const va_conv_args& a, hipStream_t st);
 
 namespace {
 
@@ -2301,6 +2303,10 @@ extern "C" {
 
 int va_seg_conv(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
+    if (a->dtype == VA_DTYPE_FP8) {  // va_fp8.hip
+        if (!va_fp8_conv_ok(*a) || a->Npad < a->Cout || a->K > a->Kpad) return VA_ERR_ARG;
+        return va_fp8_conv_launch(*a, (hipStream_t)stream) == hipSuccess ? VA_OK : VA_ERR_HIP;
+    }
     const bool bf = a->dtype == VA_DTYPE_BF16;
     const int vec = bf ? 8 : 4, ks = 8 * vec;  // elements per 16-byte chunk / per conv2 K-step
     if (a->xu && (a->kh != 1 || a->kw != 1 || a->stride != 1 || a->pad != 0 || a->mode != 0 || a->w2 ||

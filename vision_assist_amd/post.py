@@ -28,13 +28,13 @@ class PostArgs(ctypes.Structure):
         ("H0", ctypes.c_int32), ("W0", ctypes.c_int32),
         ("sc_gain", ctypes.c_float), ("sc_padx", ctypes.c_float), ("sc_pady", ctypes.c_float),
         ("cscratch", VOIDP), ("cslots", ctypes.c_int32), ("ccap", ctypes.c_int32),
-        ("cstats", VOIDP), ("cstatus", VOIDP),
-        ("max_nms", ctypes.c_int32),
+        ("cstats", VOIDP), ("cstatus", VOIDP), ("cpts", VOIDP),
+        ("max_nms", ctypes.c_int32), ("cpts_cap", ctypes.c_int32),
     ]
 
 
 class ContourStat(ctypes.Structure):  # va_contour_stat
-    _fields_ = [(n, ctypes.c_int32) for n in ("npts", "ox", "oy", "ncont", "X0", "Y0", "status", "pad")] + \
+    _fields_ = [(n, ctypes.c_int32) for n in ("npts", "ox", "oy", "ncont", "X0", "Y0", "status", "half")] + \
                [("area", ctypes.c_double)]
 
 
@@ -44,13 +44,14 @@ class MaskSelectArgs(ctypes.Structure):  # va_mask_select_args
                [(n, ctypes.c_float) for n in ("gain", "padx", "pady")] + \
                [("scratch", VOIDP), ("nslots", ctypes.c_int32), ("cap", ctypes.c_int32), ("cstats", VOIDP),
                 ("cells", VOIDP), ("rects", VOIDP), ("chosen", VOIDP), ("status", VOIDP), ("polys", VOIDP),
-                ("poly_n", VOIDP), ("poly_cap", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("poly_n", VOIDP), ("cpts", VOIDP), ("poly_cap", ctypes.c_int32), ("cpts_cap", ctypes.c_int32)]
 
 
 CSTAT_DTYPE = [("npts", "<i4"), ("ox", "<i4"), ("oy", "<i4"), ("ncont", "<i4"), ("X0", "<i4"), ("Y0", "<i4"),
-               ("status", "<i4"), ("pad", "<i4"), ("area", "<f8")]
+               ("status", "<i4"), ("half", "<i4"), ("area", "<f8")]
 CONTOUR_SLOTS = 1024   # contour scratch slots: one wave each, 4 per CU
 CONTOUR_CAP = 16384    # points of the chosen contour per frame (the fill kernel's buffer)
+CONTOUR_PTS = 1024     # points kept per instance and buffer half (va_post_args.cpts_cap); longer: followed again
 
 
 def scale_coords_params(H: int, W: int, H0: int, W0: int) -> tuple[float, float, float]:
@@ -117,6 +118,7 @@ class PostEngine:
         self.cstats = torch.empty((B, max_det, ctypes.sizeof(ContourStat)), dtype=torch.uint8, device=dev)
         self.cstatus = torch.empty(B, dtype=torch.int32, device=dev)
         self.cscratch = contour_scratch(H, W, device=dev)
+        self.cpts = torch.empty((B, max_det, 2, CONTOUR_PTS), dtype=torch.int32, device=dev)
 
     def run(self, levels, proto, plant_cells=None, plant_rects=None, plant_mode=PLANT_NEVER, select=True,
             stream=None) -> None:
@@ -144,6 +146,7 @@ class PostEngine:
             a.sc_gain, a.sc_padx, a.sc_pady = scale_coords_params(self.H, self.W, self.H0, self.W0)
         a.cscratch, a.cslots, a.ccap = self.cscratch.data_ptr(), CONTOUR_SLOTS, CONTOUR_CAP
         a.cstats, a.cstatus = self.cstats.data_ptr(), self.cstatus.data_ptr()
+        a.cpts, a.cpts_cap = self.cpts.data_ptr(), CONTOUR_PTS
 
     def polygons(self, b: int, cap: int = 4096, stream=None) -> list:
         """Results.masks.xy of frame b of the last run: per kept detection its largest external contour in frame
@@ -193,13 +196,14 @@ def select_masks(masks: torch.Tensor, nmask: torch.Tensor, H0: int, W0: int, pol
     status = torch.empty(B, dtype=torch.int32, device=dev)
     polys = torch.empty((B, maxn, poly_cap, 2), dtype=torch.float32, device=dev)
     pn = torch.zeros((B, maxn), dtype=torch.int32, device=dev)
+    cpts = torch.empty((B, maxn, 2, CONTOUR_PTS), dtype=torch.int32, device=dev)
     nm = nmask.to(dev, torch.int32).contiguous()
     m = masks.contiguous()
     a = MaskSelectArgs(masks=m.data_ptr(), nmask=nm.data_ptr(), B=B, maxn=maxn, Hn=Hn, Wn=Wn, H0=H0, W0=W0,
                        gain=gain, padx=padx, pady=pady, scratch=scratch.data_ptr(), nslots=CONTOUR_SLOTS,
                        cap=CONTOUR_CAP, cstats=cstats.data_ptr(), cells=cells.data_ptr(), rects=rects.data_ptr(),
                        chosen=chosen.data_ptr(), status=status.data_ptr(), polys=polys.data_ptr(), poly_n=pn.data_ptr(),
-                       poly_cap=poly_cap)
+                       cpts=cpts.data_ptr(), poly_cap=poly_cap, cpts_cap=CONTOUR_PTS)
     with torch.cuda.device(dev):
         _lib.check(lib.va_post_select_masks(_lib.stream_ptr(stream, dev), ctypes.byref(a)), "va_post_select_masks")
     torch.cuda.synchronize(dev)

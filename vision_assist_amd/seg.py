@@ -14,6 +14,7 @@ proto masks float32 [B, H/4, W/4, 32].
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from dataclasses import dataclass
 
@@ -22,7 +23,9 @@ import torch
 from . import _lib
 from .seg_arch import NM, REG_MAX, Arch
 
-VA_DTYPE_BF16, VA_DTYPE_F32 = 1, 2
+VA_DTYPE_BF16, VA_DTYPE_F32, VA_DTYPE_FP8 = 1, 2, 3
+F8_KS = 128        # K-step of the fp8 kernel (va_fp8.hip): fp8 weights are padded to it
+F8_MAX = 448.0     # largest OCP e4m3 value
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -43,6 +46,7 @@ class ConvArgs(ctypes.Structure):
         ("out_f32", ctypes.c_int32), ("bias4", ctypes.c_int32),
         ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("c2", ctypes.c_int32), ("act2", ctypes.c_int32),
         ("xu", ctypes.c_void_p), ("ldu", ctypes.c_int32), ("cu", ctypes.c_int32),
+        ("wscale", ctypes.c_void_p), ("xscale", ctypes.c_float), ("pad8_", ctypes.c_int32),
     ]
 
 
@@ -97,10 +101,12 @@ class SegNet:
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
+        if dtype not in ("bf16", "f32", "fp8"):
+            raise ValueError(f"dtype {dtype!r}: bf16, f32 or fp8")
         self.dtype = dtype
-        self.tdtype = torch.bfloat16 if dtype == "bf16" else torch.float32
-        self.va_dtype = VA_DTYPE_BF16 if dtype == "bf16" else VA_DTYPE_F32
-        self.vec = 8 if dtype == "bf16" else 4
+        self.tdtype = torch.bfloat16 if self.store == "bf16" else torch.float32
+        self.va_dtype = VA_DTYPE_BF16 if self.store == "bf16" else VA_DTYPE_F32
+        self.vec = 8 if self.store == "bf16" else 4
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.w = {}
         for prefix, kind, ci, co, k in arch.conv_specs():
@@ -122,7 +128,7 @@ class SegNet:
             self.w0 = (w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27).float().to(self.device).contiguous(),
                        b0.float().to(self.device).contiguous())
         # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
-        fold_ok = arch.npr == 128 if dtype == "bf16" else arch.npr >= 128
+        fold_ok = arch.npr == 128 if dtype == "bf16" else (arch.npr >= 128 and dtype == "f32")
         self.proto_fold = self._fold_proto(folded) if (fold_ok and os.environ.get("VA_FOLD_PROTO", "1") != "0") \
             else None
         # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
@@ -138,6 +144,51 @@ class SegNet:
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
         self._plans = {}
+        # fp8: e4m3 weights with per-output-channel scales (the convs whose input channels come in 16s), and
+        # the per-conv activation scales of calibrate_fp8
+        self.w8 = {}
+        self.xscale = None
+        if dtype == "fp8":
+            for prefix, p in self.w.items():
+                if p.cin % 16 == 0:
+                    self.w8[prefix] = self._pack_fp8(p)
+
+    def _pack_fp8(self, p: Packed):
+        """(e4m3 bytes [Npad][Kpad128], per-output-channel scale float [Npad]) of a packed bf16 conv: the
+        channel's largest |w| maps to 448, values rounded to nearest even (torch.float8_e4m3fn)."""
+        wf = p.w.float().cpu()
+        Kp = _ceil(p.K, F8_KS)
+        amax = wf.abs().amax(1)
+        sw = torch.where(amax > 0, amax / F8_MAX, torch.ones_like(amax))
+        w8 = torch.zeros(p.Npad, Kp, dtype=torch.float32)
+        w8[:, :p.K] = (wf[:, :p.K] / sw[:, None]).clamp(-F8_MAX, F8_MAX)
+        q = w8.to(torch.float8_e4m3fn).view(torch.uint8)
+        return q.to(self.device).contiguous(), sw.to(self.device).contiguous(), Kp
+
+    def calibrate_fp8(self, H: int, W: int, frames_u8: torch.Tensor | None = None, seed: int = 0) -> dict:
+        """Static activation scales of the fp8 convs: one forward of this network in bf16 (same weights) on
+        `frames_u8` (default: 2 seeded uniform uint8 frames, the bench's input distribution); each fp8 conv's
+        input is quantized as sat(x * s), s the power of two with amax * s in [224, 448], amax the largest |x|
+        of its input there."""
+        if frames_u8 is None:
+            g = torch.Generator().manual_seed(seed)
+            frames_u8 = torch.randint(0, 256, (2, H, W, 3), generator=g, dtype=torch.uint8)
+        B = frames_u8.shape[0]
+        p = self.plan(B, H, W, tag=-1, _calib=True)
+        p["frames"].copy_(frames_u8.to(self.device), non_blocking=True)
+        self.run_plan(p)
+        torch.cuda.synchronize(self.device)
+        xs = {}
+        for m in p["meta"]:
+            src = m.get("src")
+            if src is None or m["prefix"] not in self.w8:
+                continue
+            amax = float(src.buf[..., src.off:src.off + src.c].float().abs().max())
+            # a power of two (va_fp8.hip's conversion takes it exactly): amax lands in [224, 448]
+            xs[m["prefix"]] = 2.0 ** math.floor(math.log2(F8_MAX / amax)) if amax > 0 else 1.0
+        self.xscale = xs
+        del self._plans[(B, H, W, -1, True)]
+        return xs
 
     def _pack_stem(self, w0p: torch.Tensor, b0: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
         """Weight blob + bias vector of va_seg_stem: bf16 MFMA A fragments (see _pack_c2f) W0 = model.0
@@ -229,9 +280,15 @@ class SegNet:
                       bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
 
     @property
+    def store(self) -> str:
+        """Activation storage: f32 in the f32 mode, else bf16 (fp8, BASELINE.json configs[4], runs its convs on
+        e4m3 MFMA -- va_fp8.hip -- and keeps activations in bf16)."""
+        return "f32" if self.dtype == "f32" else "bf16"
+
+    @property
     def bk(self) -> int:
         """K padding of the packed weights: the conv2 K-step (64 bf16 / 32 f32)."""
-        return BK if self.dtype == "bf16" else 32
+        return BK if self.store == "bf16" else 32
 
     # ------------------------------------------------------------------ packing
     def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
@@ -260,12 +317,16 @@ class SegNet:
     def _buf(self, B, h, w, c, dtype=None):
         return torch.empty((B, h, w, c), dtype=dtype or self.tdtype, device=self.device)
 
-    def plan(self, B: int, H: int, W: int, tag: int = 0):
+    def plan(self, B: int, H: int, W: int, tag: int = 0, _calib: bool = False):
         """Op list + buffers for B frames of H x W (``tag`` gives independent buffer sets, e.g. for
-        double-buffered batches that overlap on two streams)."""
-        key = (B, H, W, tag)
+        double-buffered batches that overlap on two streams).  fp8: calibrated on first use (calibrate_fp8);
+        _calib = the bf16 plan that calibration runs."""
+        key = (B, H, W, tag, _calib)
         if key in self._plans:
             return self._plans[key]
+        fp8 = self.dtype == "fp8" and not _calib
+        if fp8 and self.xscale is None:
+            self.calibrate_fp8(H, W)
         if H % 32 or W % 32:
             raise _lib.VaError(f"frame {H}x{W}: the network needs multiples of 32 (pad/letterbox first)")
         a = self.arch
@@ -296,7 +357,16 @@ class SegNet:
                 w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
                 y=dst.ptr, ldy=dst.ld, res=res.ptr if res is not None else None, ldr=res.ld if res is not None else 0,
                 act=1 if act else 0, mode=1 if p.deconv else 0, M=B * ho * wo, dtype=self.va_dtype,
-                out_f32=1 if (out_f32 and self.dtype == "bf16") else 0)
+                out_f32=1 if (out_f32 and self.store == "bf16") else 0)
+            on_fp8 = fp8 and prefix in self.w8 and tail is None and up is None and self._fp8_fits(p, src, dst, res,
+                                                                                                  out_f32)
+            if on_fp8:  # va_fp8.hip: e4m3 weights, the bf16 input quantized with its calibrated scale
+                w8, sw, Kp = self.w8[prefix]
+                xs = self.xscale[prefix]
+                ws = (sw / xs).contiguous()
+                keep.append(ws)
+                args.dtype, args.w, args.Kpad, args.wscale, args.xscale = VA_DTYPE_FP8, w8.data_ptr(), Kp, \
+                    ws.data_ptr(), xs
             if up is not None:
                 args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
             cout = p.cout
@@ -310,12 +380,13 @@ class SegNet:
             if dst.c != (cout // 4 if p.deconv else cout):
                 raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {cout}")
             ops.append(SegOp(kind=VA_OP_CONV, a=args))
-            es = 2 if self.dtype == "bf16" else 4
+            es = 2 if self.store == "bf16" else 4
             flops = 2 * B * ho * wo * p.cout * k * k * src.c + (2 * B * ho * wo * p.cout * cout if p2 else 0)
             meta.append({"name": prefix + (f"+{tail}" if tail else ""), "kind": "conv", "M": B * ho * wo,
                          "N": p.cout, "K": k * k * src.c, "k": k, "stride": stride, "flops": flops,
-                         "bytes": es * B * h * w * src.c + es * p.cout * k * k * src.c
-                         + B * ho * wo * cout * (4 if out_f32 else es)})
+                         "bytes": es * B * h * w * src.c + (1 if on_fp8 else es) * p.cout * k * k * src.c
+                         + B * ho * wo * cout * (4 if out_f32 else es),
+                         "prefix": prefix, "src": src, "fp8": on_fp8})
             return ho, wo
 
         def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None):
@@ -368,7 +439,7 @@ class SegNet:
                                                                w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
                                                                Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)))
                 meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3,
-                             "stride": 2, "bytes": B * H * W * 3 + (2 if self.dtype == "bf16" else 4) * B * h1 * w1 * a.c1})
+                             "stride": 2, "bytes": B * H * W * 3 + (2 if self.store == "bf16" else 4) * B * h1 * w1 * a.c1})
             else:
                 x0 = new(H, W, 8)
                 ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
@@ -403,7 +474,7 @@ class SegNet:
         conv("model.9.cv2", sp, P5, h5, w5)
         # the FPN's Upsample + Concat: read in place by the consumer's 1x1 cv1 (bf16) or materialised
         ks = 64 if self.dtype == "bf16" else 32  # the conv2 K-step the upsampled prefix must align to
-        fuse_up = os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % ks == 0 \
+        fuse_up = self.dtype != "fp8" and os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % ks == 0 \
             and a.c4 % ks == 0 and (a.c5 + a.c4) % ks == 0 and (a.c4 + a.c3) % ks == 0
         if not fuse_up:
             upsample(P5, cat11.sub(0, a.c5), h5, w5)
@@ -499,6 +570,17 @@ class SegNet:
                 "out": SegOutputs(levels=levels, proto=proto.buf)}
         self._plans[key] = plan
         return plan
+
+    @staticmethod
+    def _fp8_fits(p: Packed, src: Slice, dst: Slice, res, out_f32: bool) -> bool:
+        """va_fp8.hip's operand rules (va_fp8_conv_ok): bf16 input rows in 16-byte runs, outputs in 8-element
+        runs (4 for a float output, which takes no residual)."""
+        ok = src.ld % 8 == 0 and (src.off * 2) % 16 == 0
+        if out_f32:
+            return ok and p.cout % 4 == 0 and dst.ld % 4 == 0 and res is None
+        cd = p.cout // 4 if p.deconv else p.cout
+        return ok and cd % 8 == 0 and dst.ld % 8 == 0 and (dst.off * 2) % 16 == 0 and \
+            (res is None or (res.ld % 8 == 0 and (res.off * 2) % 16 == 0))
 
     def _can_fuse_tail(self, prefix: str, tail: str) -> bool:
         """Whether the 1x1 conv ``tail`` (sole consumer of ``prefix``) can run in prefix's epilogue: bf16,
