@@ -30,6 +30,7 @@ def test_bench_contract_line():
     assert c["value"] > 0 and c["kind"] == "port" and c["cores"] >= 1
     assert d["config"]["workload"].startswith("C3")
     assert d["dtype"] == "f32" and r["peak"] == 157.3  # the reference's precision (args.yaml half: false)
-    assert set(d["extras"]) == {"bf16", "dense"}
+    assert set(d["extras"]) == {"bf16", "dense", "c5"}
     assert d["extras"]["bf16"]["roofline"]["peak"] == 2500.0 and d["extras"]["dense"]["dtype"] == "f32"
+    assert d["extras"]["c5"]["dtype"] == "fp8" and d["extras"]["c5"]["roofline"]["peak"] == 5000.0
     assert "grid_stage_ms_per_frame" in c and "path+analyser" in c["stage_ms_per_frame"]
