@@ -153,8 +153,8 @@ def test_forward_f32_nano_1280():
     ref = _ref_heads(arch, fw, frames)
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
-        err = ((g - r).abs() / (1.0 + r.abs())).max().item()
-        assert err <= 1e-3, f"{name}: max rel err {err}"
+        err = (g - r).abs().max().item()
+        assert err <= 1e-3, f"{name}: max |gpu - torch fp32| = {err}"
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
@@ -607,8 +607,8 @@ def test_forward_f32_medium_1280_within_1e3():
     got = _gpu_heads(SegNet(c["arch"], c["fw"], dtype="f32"), c["frames"])
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, c["ref"]):
         assert g.shape == r.shape, name
-        err = ((g - r).abs() / (1.0 + r.abs())).max().item()
-        assert err <= 1e-3, f"{name}: max rel err {err}"
+        err = (g - r).abs().max().item()
+        assert err <= 1e-3, f"{name}: max |gpu - torch fp32| = {err}"
 
 
 def test_forward_bf16_medium_1280_close():
