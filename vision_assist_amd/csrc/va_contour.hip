@@ -33,6 +33,8 @@
 // wave issues at most one instruction per 4 cycles), so the step's work is kept to a few dozen scalar ops.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
 
 #include "../../include/va355.h"
 #include "va_contour.h"
@@ -44,9 +46,15 @@ constexpr int NMC = 32;
 constexpr int REG_MAX = 16;
 constexpr int CT_THREADS = 64;             // one wave per detection: the scan and the border following are serial
 constexpr int FILL_THREADS = 256;
-constexpr int CT_STRIP = 2048;             // floats of one strip of low-res rows (8 KiB)
-constexpr int CT_LDS_SMALL = 32 * 1024;    // dynamic LDS of the small instantiation
-constexpr int CT_LDS_LARGE = 156 * 1024;   // of the large one (one wave per CU: regions up to ~560 x 560)
+constexpr int CT_STRIP = 1024;             // floats of one strip of low-res rows (4 KiB; >= 2 rows of a 2048-px input)
+// The LDS form: 16 waves per workgroup, one workgroup per CU, each wave an independent worker over the detections
+// with its image in pages of a shared 160 KiB pool (a 32-bit page map, CAS-allocated), so a CU holds as many
+// images as fit instead of one fixed size class per launch.
+constexpr int CP_WAVES = 16;
+constexpr int CP_THREADS = 64 * CP_WAVES;
+constexpr int CP_PAGES = 32;
+constexpr int CP_PAGE = 5104;              // bytes (16-aligned): 32 pages + the pool's bookkeeping fit in 160 KiB
+constexpr int CP_POOL = CP_PAGES * CP_PAGE;
 // chain-code moves (0 = right, counter-clockwise), as 2-bit fields of (d + 1): register arithmetic, not a table
 // load (a per-step table load with a lane-varying index is a memory round trip on the trace's critical path)
 __device__ __forceinline__ int dir_dx(int s) { return (int)((0x901Au >> (2 * s)) & 3u) - 1; }  // 1 1 0 -1 -1 -1 0 1
@@ -70,12 +78,33 @@ __device__ inline bool ct_ok(bool c, int code, long long v0, long long v1) {
 // scanned, positions visited, trace steps
 constexpr int CT_PROF_ITEMS = 4096;
 __device__ unsigned long long g_ct_prof[CT_PROF_ITEMS][8];
+// per frame of the fill kernel: choice + points, edges, fill (s_memtime cycles), the point count, fallback flag
+constexpr int CT_FILL_FRAMES = 1024;
+__device__ unsigned long long g_ct_fill[CT_FILL_FRAMES][8];
 #define CT_PROF(...) __VA_ARGS__
 #define CT_STEPS (&nsteps)
 #else
 #define CT_OK(c, code, v0, v1) true
 #define CT_PROF(...)
 #define CT_STEPS nullptr
+#endif
+#if defined(VA_CT_CHECK) && !defined(VA_CT_WATCH)
+#define VA_CT_WATCH
+#endif
+#ifdef VA_CT_WATCH
+// hang watch: per (block, wave) of the pool kernel {item, phase, y, counter} in host-mapped memory (system-scope
+// stores), readable by the host while a kernel runs (tools/ct_watch.py)
+constexpr int CT_WATCH_SLOTS = 256 * 16;
+__device__ int* g_ct_watch;
+__device__ inline void ct_watch(int f, int v) {
+    int* w = g_ct_watch;
+    if (!w || (threadIdx.x & 63) != 0) return;
+    const int slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (slot < CT_WATCH_SLOTS) __hip_atomic_store(w + 4 * slot + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define CT_WATCH(f, v) ct_watch((f), (int)(v))
+#else
+#define CT_WATCH(f, v)
 #endif
 
 // ------------------------------------------------------------------------------------------ geometry
@@ -150,6 +179,15 @@ __device__ inline Region region_of(const Src& s, int b, int k) {
     r.rH = r.h + 2;
     r.ww = (r.rW + 31) >> 5;
     return r;
+}
+
+// the region's fields as scalars (every lane computed the same values from the same loads): scalar branches
+__device__ __forceinline__ Region uni_region(const Region& r) {
+    Region u;
+    u.X0 = uni(r.X0), u.Y0 = uni(r.Y0), u.w = uni(r.w), u.h = uni(r.h);
+    u.rW = uni(r.rW), u.rH = uni(r.rH), u.ww = uni(r.ww);
+    u.rx0 = uni(r.rx0), u.rx1 = uni(r.rx1), u.ry0 = uni(r.ry0), u.ry1 = uni(r.ry1);
+    return u;
 }
 
 // 32-bit words of the image: three bit planes per row (+ one spare word, read past by the trace windows)
@@ -233,6 +271,18 @@ struct MaskStat {
 // count and bbox accumulate per thread in ms.  Head source: strips of the low-res window of coef . proto in
 // `strip`, each evaluating the full-res rows whose taps it holds with the exact per-pixel expression
 // wy0 (wx0 v(ya, xa) + wx1 v(ya, xb)) + wy1 (wx0 v(yb, xa) + wx1 v(yb, xb)) > 0.
+// the threads building an image: one wave (the contour kernels) or the whole block (post_fill_kernel)
+template <bool WAVE>
+__device__ __forceinline__ void ct_sync() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
+template <bool WAVE>
 __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Region& r, uint32_t* img, float* strip,
                                             int tid, int nt, MaskStat& ms) {
     auto account = [&](uint32_t w, int x32, int yy) {
@@ -265,34 +315,34 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
             account(w, x32, y);
             plane(img, r.ww, y, 0)[x32 >> 5] = w;
         }
-        __syncthreads();
+        ct_sync<WAVE>();
         return;
     }
     const int anchor = s.dets[(int64_t)b * s.max_det + k].anchor;
     const float4* coef4 = (const float4*)coef_row(s, b, anchor);
-    float4 cq[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) cq[q] = coef4[q];
+    const float4 cq = coef4[tid & 7];  // this lane's 4 of the 32 coefficients (nt is a multiple of 8)
     const int tw = r.rx1 - r.rx0 + 1;
-    const int S = CT_STRIP / tw;  // >= 6: tw <= mw <= 320
+    const int S = CT_STRIP / tw;  // >= 2: tw <= mw <= CT_STRIP / 2 (va_contour_launch)
     const float sx = (float)s.mw / (float)s.Wn, sy = (float)s.mh / (float)s.Hn;
     int next = 1, s0 = r.ry0;     // next framed row to produce; first low-res row of the strip
     while (next <= r.h) {         // block-uniform
         const int s1 = min(s0 + S - 1, r.ry1);
-        // one low-res pixel per lane: its 128 bytes of proto as 8 loads in flight; the partial sums per 4
-        // channels and their pairwise tree are post-processing's 8-lane dot (same order, same result)
-        for (int i = tid; i < (s1 - s0 + 1) * tw; i += nt) {
-            const int y = s0 + i / tw, x = r.rx0 + i % tw;
-            const float4* pp = (const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC);
-            float part[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const float4 v = pp[q];
-                part[q] = (cq[q].x * v.x + cq[q].y * v.y) + (cq[q].z * v.z + cq[q].w * v.w);
-            }
-            strip[i] = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
+        // eight lanes per low-res pixel (its 128 bytes of proto in one coalesced run): lane q's partial sum of 4
+        // channels, then the pairwise tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) by xor shuffles --
+        // post-processing's 8-lane dot (same order, same result)
+        const int npx = (s1 - s0 + 1) * tw;
+#pragma unroll 1
+        for (int i = tid; i < npx * 8; i += nt) {  // whole 8-lane groups are active together
+            const int px = i >> 3;
+            const int y = s0 + px / tw, x = r.rx0 + px % tw;
+            const float4 v = ((const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC))[tid & 7];
+            float part = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
+            part += __shfl_xor(part, 1);
+            part += __shfl_xor(part, 2);
+            part += __shfl_xor(part, 4);
+            if ((tid & 7) == 0) strip[px] = part;
         }
-        __syncthreads();
+        ct_sync<WAVE>();
         // the rows whose taps inside the window all lie in s0 .. s1 (taps are non-decreasing in the row)
         int end = next;
         while (end <= r.h) {
@@ -309,6 +359,7 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
             if (!CT_OK(li >= 0 && li < CT_STRIP, 7, li, tw)) return 0.f;
             return strip[li];
         };
+#pragma unroll 1
         for (int i = tid; i < (end - next) * r.ww; i += nt) {
             const int yy = next + i / r.ww, x32 = 32 * (i % r.ww);
             int ya, yb;
@@ -331,7 +382,7 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
         }
         next = end;
         s0 = s1;  // a later row may need s1 and s1 + 1
-        __syncthreads();
+        ct_sync<WAVE>();
     }
 }
 
@@ -446,209 +497,300 @@ struct CtArgs {
     float* polys;             // optional [B][max_det][poly_cap][2]: the best contour in frame coordinates
     int32_t* poly_n;
     int poly_cap;
+    int gate;                 // pool kernel: hold new claims while a wave waits for pages
 };
 
-// MODE 0 / 1: image in LDS (CT_LDS_SMALL / CT_LDS_LARGE bytes); MODE 2: in the block's scratch slot.  Every
-// instantiation walks all detections and takes the ones of its size class.
-template <int MODE>
-__global__ __launch_bounds__(CT_THREADS) void post_contour_kernel(CtArgs a) {
-    constexpr bool LDS = MODE < 2;
-    constexpr int64_t lo = MODE == 0 ? -1 : (MODE == 1 ? CT_LDS_SMALL : CT_LDS_LARGE);
-    constexpr int64_t hi = MODE == 0 ? CT_LDS_SMALL : (MODE == 1 ? CT_LDS_LARGE : INT64_MAX);
-    extern __shared__ __align__(16) uint32_t ct_lds[];
-    __shared__ int s_red[5];
-    const int tid = threadIdx.x, lane = tid & 63;
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Detection (b, k) with region r, by one wave, its image at img (LDS: a pool page run; else the wave's global
+// scratch slot) and, for a head-source mask, the low-res strip at strip.  LDS = the image is in LDS (the
+// compiler sees the pointer's address space through the inlining).
+template <bool LDS>
+__device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, const Region& r, uint32_t* img,
+                                             float* strip, int item) {
+    const int lane = threadIdx.x & 63;
+    const Src& s = a.s;
+    va_contour_stat st{};
+    st.ox = st.oy = -1;
+    st.X0 = r.X0, st.Y0 = r.Y0;
+    const int64_t di = (int64_t)b * a.max_det + k;
+    float* poly = a.polys ? a.polys + di * a.poly_cap * 2 : nullptr;
+    MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+    CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime(); unsigned long long nrows = 0, npos = 0;
+            int nsteps = 0; unsigned long long ttr = 0);
+    CT_WATCH(1, 10);
+    build_image<true>(s, b, k, r, img, strip, lane, 64, ms);
+    CT_WATCH(1, 11);
+    CT_PROF(const unsigned long long t1 = __builtin_amdgcn_s_memtime());
+    if (s.stats) {  // pixel count and bbox (process_mask's instance mask)
+        const int cnt = wave_sum(ms.cnt);
+        const int x0 = wave_min(ms.x1 >= 0 ? ms.x0 : s.Wn), x1 = wave_max(ms.x1);
+        const int y0 = wave_min(ms.x1 >= 0 ? ms.y0 : s.Hn), y1 = wave_max(ms.x1 >= 0 ? ms.y1 : -1);
+        if (lane == 0) s.stats[di] = va_mask_stat{cnt, x0, y0, x1, y1, {0, 0, 0}};
+    }
+    if constexpr (!LDS) __threadfence();  // the image before the coherent reads of the scan
+    // cvFindNextContour's raster scan (RETR_EXTERNAL); the contour with the most points stays in its half of
+    // the instance's point buffer
+    uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
+    int best_n = 0, best_half = 0, bx = -1, by = -1, ncont = 0, alt = 0;
+    for (int y = 1; y < r.rH - 1; ++y) {
+        CT_WATCH(2, y);
+        if (!row_has_start<LDS>(img, r.ww, y)) continue;
+        CT_PROF(++nrows);
+        // OpenCV's skip loop visits the positions whose value differs from their left neighbour's (the
+        // scan's prev is always the value at x - 1): per 2048-pixel chunk each lane holds its word's change
+        // flags and value planes, and the positions are taken in order from registers; a trace changes marks,
+        // so the chunk is re-read after one
+        const uint32_t* nzr = plane(img, r.ww, y, 0);
+        const uint32_t* nr = plane(img, r.ww, y, 1);
+        const uint32_t* rr = plane(img, r.ww, y, 2);
+        int prev = 0, lnbd = 0;
+        for (int w0 = 0; w0 < r.ww; w0 += 64) {
+            const int wi = w0 + lane;
+            uint32_t chi = 0u, clo = 0u, dm = 0u;
+            auto load = [&](int from) {  // value planes + change flags at positions >= from
+                uint32_t phi = 0u, plo = 0u;
+                chi = clo = 0u;
+                if (wi < r.ww) code_planes(nzr[wi], ldm<LDS>(nr + wi), ldm<LDS>(rr + wi), chi, clo);
+                if (wi >= 1 && wi <= r.ww)
+                    code_planes(nzr[wi - 1], ldm<LDS>(nr + wi - 1), ldm<LDS>(rr + wi - 1), phi, plo);
+                dm = (chi ^ ((chi << 1) | (phi >> 31))) | (clo ^ ((clo << 1) | (plo >> 31)));
+                const int fw = from >> 5;
+                if (wi < fw || wi >= r.ww) dm = 0u;
+                else if (wi == fw) dm &= ~0u << (from & 31);
+            };
+            load(0);
+            while (true) {
+                const unsigned long long bal = __ballot(dm != 0u);
+                if (!bal) break;
+                const int l = __builtin_ctzll(bal);
+                const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)dm, l);
+                const int j = __builtin_ctz(dl);
+                const int x = 32 * (w0 + l) + j;
+                const uint32_t vh = ((uint32_t)__builtin_amdgcn_readlane((int)chi, l) >> j) & 1u;
+                const uint32_t vl = ((uint32_t)__builtin_amdgcn_readlane((int)clo, l) >> j) & 1u;
+                const int p = vh ? (vl ? -126 : 2) : (int)vl;
+                if (lane == l) dm &= ~(1u << j);
+                CT_PROF(++npos);
+                if (prev == 0 && p == 1) {
+                    if (uni(val_at<LDS>(img, r.ww, lnbd, y)) <= 0) {
+                        uint32_t* dst = cp + alt * a.sc.capd;
+                        int i = 0;
+                        CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
+                        const int n = fetch_contour(
+                            img, r.ww, x, y, true,
+                            [&](int px, int py) {
+                                if (lane == 0 && i < a.sc.capd)
+                                    dst[i] = (uint32_t)(r.X0 + px - 1) | ((uint32_t)(r.Y0 + py - 1) << 16);
+                                ++i;
+                            },
+                            CT_STEPS);
+                        CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
+                        ++ncont;
+                        CT_WATCH(3, ncont);
+                        if (n > best_n) {
+                            best_n = n, best_half = alt, bx = x, by = y;
+                            alt ^= 1;
+                        }
+                        if constexpr (!LDS) __threadfence();  // the marks before the scan reads on
+                        prev = uni(val_at<LDS>(img, r.ww, x, y));
+                        load(x + 1);
+                        continue;
+                    }
+                } else if (p == 0 && prev >= 1) {
+                    if (prev & -2) lnbd = x - 1;
+                }
+                prev = p;
+                if (p & -2) lnbd = x;
+            }
+        }
+    }
+    st.npts = best_n;
+    st.ncont = ncont;
+    st.half = best_half;
+    CT_PROF(const unsigned long long t2 = __builtin_amdgcn_s_memtime());
+    if (best_n > 0) {
+        st.ox = bx, st.oy = by;
+        // cv2.contourArea of the float32 scale_coords points: a00 += prev.x * y - prev.y * x from the last
+        // point on, in order (terms in parallel, summed in order); the polygon itself if asked for
+        double acc = 0.0;
+        if (best_n <= a.sc.capd) {
+            __threadfence();  // lane 0's point stores before every lane reads them
+            const uint32_t* P = cp + best_half * a.sc.capd;
+            const uint32_t plast = P[best_n - 1];
+            for (int b0 = 0; b0 < best_n; b0 += 64) {
+                const int i = b0 + lane;
+                double term = 0.0;
+                if (i < best_n) {
+                    const uint32_t q = P[i], pq = i == 0 ? plast : P[i - 1];
+                    float xs, ys, pxs, pys;
+                    scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
+                    scale_pt(a.f, (int)(pq & 0xFFFFu), (int)(pq >> 16), &pxs, &pys);
+                    term = (double)pxs * (double)ys - (double)pys * (double)xs;
+                    if (poly && i < a.poly_cap) {
+                        poly[2 * i] = xs;
+                        poly[2 * i + 1] = ys;
+                    }
+                }
+                const int m = min(64, best_n - b0);
+                for (int j = 0; j < m; ++j) acc += readlane_f64(term, j);
+            }
+        } else {  // longer than the buffer: followed again from the image (marks off)
+            int lx = 0, ly = 0;
+            fetch_contour(img, r.ww, bx, by, false, [&](int px, int py) { lx = px, ly = py; });
+            float pxs, pys;
+            scale_pt(a.f, r.X0 + lx - 1, r.Y0 + ly - 1, &pxs, &pys);
+            int i = 0;
+            fetch_contour(img, r.ww, bx, by, false, [&](int qx, int qy) {
+                float xs, ys;
+                scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
+                acc += (double)pxs * (double)ys - (double)pys * (double)xs;
+                pxs = xs, pys = ys;
+                if (poly && i < a.poly_cap && lane == 0) {
+                    poly[2 * i] = xs;
+                    poly[2 * i + 1] = ys;
+                }
+                ++i;
+            });
+        }
+        st.area = fabs(acc * 0.5);
+    }
+    if (lane == 0) {
+        if (a.poly_n) a.poly_n[di] = best_n;
+        a.cstats[di] = st;
+        CT_PROF(if (item < CT_PROF_ITEMS) {
+            const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+            unsigned long long* pr = g_ct_prof[item];
+            pr[0] = t1 - t0, pr[1] = t2 - t1, pr[2] = t3 - t2, pr[3] = (unsigned long long)ncont;
+            pr[4] = nrows, pr[5] = npos, pr[6] = (unsigned long long)nsteps, pr[7] = ttr;
+        });
+    }
+    CT_PROF((void)item);
+}
+
+// the empty record of a detection whose crop window holds no low-res pixel
+__device__ __forceinline__ void contour_empty(const CtArgs& a, int b, int k, const Region& r) {
+    if ((threadIdx.x & 63) != 0) return;
+    const int64_t di = (int64_t)b * a.max_det + k;
+    va_contour_stat st{};
+    st.ox = st.oy = -1;
+    st.X0 = r.X0, st.Y0 = r.Y0;
+    if (a.s.stats) a.s.stats[di] = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
+    if (a.poly_n) a.poly_n[di] = 0;
+    a.cstats[di] = st;
+}
+
+// The LDS form.  Block g takes detections g, g + G, ...; its 16 waves claim them one at a time from an LDS counter
+// and each runs its own detection in a page run of the pool (first fit on the page map, CAS).  A wave that finds
+// no free run raises the gate, and no wave claims a new detection while the gate is up, so the pool drains towards
+// the waiting wave (which holds no pages: no deadlock); it lowers the gate once it has its run.  Detections
+// needing more than the pool are left to post_contour_global_kernel.
+__global__ __launch_bounds__(CP_THREADS) void post_contour_pool_kernel(CtArgs a) {
+    extern __shared__ __align__(16) uint32_t cp_pool[];
+    __shared__ unsigned s_map;
+    __shared__ int s_next, s_gate;
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) s_map = 0u, s_next = 0, s_gate = 0;
+    __syncthreads();
+    const Src& s = a.s;
+    const int total = s.B * a.max_det;
+    const int G = gridDim.x;
+    int spins = 0;
+    // Every lane runs the bookkeeping (no lane-0-only regions): the claim adds 1 from lane 0 and 0 from the others
+    // (lane 0 gets the claim), the page-map CAS is issued by all lanes with the same operands (one succeeds), the
+    // release and the gate are idempotent.  An earlier form with `if (lane == 0)` regions and `continue` was
+    // compiled into a loop that re-ran a skipped detection without claiming a new one (hung).
+    for (int item = 0; item < total;) {
+        while (uni(__hip_atomic_load(&s_gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0)
+            __builtin_amdgcn_s_sleep(2);
+        item = blockIdx.x + uni(atomicAdd(&s_next, lane == 0 ? 1 : 0)) * G;
+        CT_WATCH(0, item);
+        CT_WATCH(1, 1);
+        bool run_it = false;
+        Region r{};
+        int b = 0, k = 0;
+        if (item < total) {
+            b = item / a.max_det, k = item % a.max_det;
+            if (k < uni(s.ndet[b])) {
+                r = uni_region(region_of(s, b, k));
+                if (r.w <= 0) contour_empty(a, b, k, r);
+                else run_it = region_need(s, r) <= CP_POOL;  // else the global kernel's
+            }
+        }
+        if (run_it) {
+            const int np = (int)((region_need(s, r) + CP_PAGE - 1) / CP_PAGE);
+            const unsigned run = np >= 32 ? ~0u : ((1u << np) - 1u);
+            CT_WATCH(1, 2);
+            int page = -1;
+            bool gated = false;
+            while (true) {
+                const unsigned cur = uni((int)__hip_atomic_load(&s_map, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                int q = -1;
+                for (int t = 0; t + np <= CP_PAGES; ++t)
+                    if (!(cur & (run << t))) {
+                        q = t;
+                        break;
+                    }
+                if (q >= 0) {  // a failed CAS (the map changed under us) looks again at once
+                    const unsigned old = atomicCAS(&s_map, cur, cur | (run << q));
+                    if (__ballot(old == cur) != 0ull) {
+                        page = q;
+                        break;
+                    }
+                } else {
+                    if (!gated && a.gate) {
+                        __hip_atomic_store(&s_gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        gated = true;
+                    }
+                    ++spins;
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            if (gated) __hip_atomic_store(&s_gate, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            CT_WATCH(1, 3);
+            CT_WATCH(2, page);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint32_t* img = cp_pool + page * (CP_PAGE / 4);
+            float* strip = (float*)(img + ((image_words(r) + 3) & ~3ll));
+            contour_item<true>(a, b, k, r, img, strip, item);
+            CT_WATCH(1, 4);
+            ct_sync<true>();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's image accesses before the release
+            atomicAnd(&s_map, ~(run << page));
+        }
+    }
+    CT_WATCH(1, 5);
+    CT_WATCH(3, spins);
+    (void)spins;
+}
+
+// The global-memory form for the regions the pool cannot hold (full-frame boxes of 1280-pixel inputs): one wave
+// per block, the image in the block's scratch slot.
+__global__ __launch_bounds__(CT_THREADS) void post_contour_global_kernel(CtArgs a) {
     const Src& s = a.s;
     unsigned char* slot = a.sc.base + (int64_t)blockIdx.x * a.sc.slot_bytes;
     const int total = s.B * a.max_det;
     for (int item = blockIdx.x; item < total; item += gridDim.x) {
         const int b = item / a.max_det, k = item % a.max_det;
-        if (k >= s.ndet[b]) continue;  // block-uniform
-        const Region r = region_of(s, b, k);
-        const int64_t need = region_need(s, r);
-        if (need <= lo || need > hi) continue;
-        va_contour_stat st{};
-        st.ox = st.oy = -1;
-        st.X0 = r.X0, st.Y0 = r.Y0;
-        const int64_t di = (int64_t)b * a.max_det + k;
-        float* poly = a.polys ? a.polys + di * a.poly_cap * 2 : nullptr;
-        if (r.w <= 0) {
-            if (tid == 0) {
-                if (s.stats) s.stats[di] = va_mask_stat{0, 0, 0, -1, -1, {0, 0, 0}};
-                if (a.poly_n) a.poly_n[di] = 0;
-                a.cstats[di] = st;
-            }
-            continue;
-        }
-        uint32_t* img;
-        float* strip;
-        if constexpr (LDS) {
-            img = ct_lds;
-            strip = (float*)(ct_lds + ((image_words(r) + 3) & ~3ll));
-        } else {
-            img = (uint32_t*)(slot + a.sc.img_off);
-            strip = (float*)slot;
-        }
-        MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
-        CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime(); unsigned long long nrows = 0, npos = 0;
-                int nsteps = 0; unsigned long long ttr = 0);
-        build_image(s, b, k, r, img, strip, tid, CT_THREADS, ms);
-        CT_PROF(const unsigned long long t1 = __builtin_amdgcn_s_memtime());
-        if (s.stats) {  // pixel count and bbox (process_mask's instance mask)
-            if (tid == 0) {
-                s_red[0] = 0;
-                s_red[1] = s.Wn;
-                s_red[2] = -1;
-                s_red[3] = s.Hn;
-                s_red[4] = -1;
-            }
-            __syncthreads();
-            atomicAdd(&s_red[0], ms.cnt);
-            if (ms.x1 >= 0) {
-                atomicMin(&s_red[1], ms.x0);
-                atomicMax(&s_red[2], ms.x1);
-                atomicMin(&s_red[3], ms.y0);
-                atomicMax(&s_red[4], ms.y1);
-            }
-            __syncthreads();
-            if (tid == 0) s.stats[di] = va_mask_stat{s_red[0], s_red[1], s_red[3], s_red[2], s_red[4], {0, 0, 0}};
-        }
-        if constexpr (!LDS) __threadfence();  // the image before the coherent reads of the scan
-        // cvFindNextContour's raster scan (RETR_EXTERNAL); the contour with the most points stays in its half of
-        // the instance's point buffer
-        uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
-        int best_n = 0, best_half = 0, bx = -1, by = -1, ncont = 0, alt = 0;
-        for (int y = 1; y < r.rH - 1; ++y) {
-            if (!row_has_start<LDS>(img, r.ww, y)) continue;
-            CT_PROF(++nrows);
-            // OpenCV's skip loop visits the positions whose value differs from their left neighbour's (the
-            // scan's prev is always the value at x - 1): per 2048-pixel chunk each lane holds its word's change
-            // flags and value planes, and the positions are taken in order from registers; a trace changes marks,
-            // so the chunk is re-read after one
-            const uint32_t* nzr = plane(img, r.ww, y, 0);
-            const uint32_t* nr = plane(img, r.ww, y, 1);
-            const uint32_t* rr = plane(img, r.ww, y, 2);
-            int prev = 0, lnbd = 0;
-            for (int w0 = 0; w0 < r.ww; w0 += 64) {
-                const int wi = w0 + lane;
-                uint32_t chi = 0u, clo = 0u, dm = 0u;
-                auto load = [&](int from) {  // value planes + change flags at positions >= from
-                    uint32_t phi = 0u, plo = 0u;
-                    chi = clo = 0u;
-                    if (wi < r.ww) code_planes(nzr[wi], ldm<LDS>(nr + wi), ldm<LDS>(rr + wi), chi, clo);
-                    if (wi >= 1 && wi <= r.ww)
-                        code_planes(nzr[wi - 1], ldm<LDS>(nr + wi - 1), ldm<LDS>(rr + wi - 1), phi, plo);
-                    dm = (chi ^ ((chi << 1) | (phi >> 31))) | (clo ^ ((clo << 1) | (plo >> 31)));
-                    const int fw = from >> 5;
-                    if (wi < fw || wi >= r.ww) dm = 0u;
-                    else if (wi == fw) dm &= ~0u << (from & 31);
-                };
-                load(0);
-                while (true) {
-                    const unsigned long long bal = __ballot(dm != 0u);
-                    if (!bal) break;
-                    const int l = __builtin_ctzll(bal);
-                    const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)dm, l);
-                    const int j = __builtin_ctz(dl);
-                    const int x = 32 * (w0 + l) + j;
-                    const uint32_t vh = ((uint32_t)__builtin_amdgcn_readlane((int)chi, l) >> j) & 1u;
-                    const uint32_t vl = ((uint32_t)__builtin_amdgcn_readlane((int)clo, l) >> j) & 1u;
-                    const int p = vh ? (vl ? -126 : 2) : (int)vl;
-                    if (lane == l) dm &= ~(1u << j);
-                    CT_PROF(++npos);
-                    if (prev == 0 && p == 1) {
-                        if (uni(val_at<LDS>(img, r.ww, lnbd, y)) <= 0) {
-                            uint32_t* dst = cp + alt * a.sc.capd;
-                            int i = 0;
-                            CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
-                            const int n = fetch_contour(
-                                img, r.ww, x, y, true,
-                                [&](int px, int py) {
-                                    if (lane == 0 && i < a.sc.capd)
-                                        dst[i] = (uint32_t)(r.X0 + px - 1) | ((uint32_t)(r.Y0 + py - 1) << 16);
-                                    ++i;
-                                },
-                                CT_STEPS);
-                            CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
-                            ++ncont;
-                            if (n > best_n) {
-                                best_n = n, best_half = alt, bx = x, by = y;
-                                alt ^= 1;
-                            }
-                            if constexpr (!LDS) __threadfence();  // the marks before the scan reads on
-                            prev = uni(val_at<LDS>(img, r.ww, x, y));
-                            load(x + 1);
-                            continue;
-                        }
-                    } else if (p == 0 && prev >= 1) {
-                        if (prev & -2) lnbd = x - 1;
-                    }
-                    prev = p;
-                    if (p & -2) lnbd = x;
-                }
-            }
-        }
-        st.npts = best_n;
-        st.ncont = ncont;
-        st.half = best_half;
-        CT_PROF(const unsigned long long t2 = __builtin_amdgcn_s_memtime());
-        if (best_n > 0) {
-            st.ox = bx, st.oy = by;
-            // cv2.contourArea of the float32 scale_coords points: a00 += prev.x * y - prev.y * x from the last
-            // point on, in order (terms in parallel, summed in order); the polygon itself if asked for
-            double acc = 0.0;
-            if (best_n <= a.sc.capd) {
-                __threadfence();  // lane 0's point stores before every lane reads them
-                const uint32_t* P = cp + best_half * a.sc.capd;
-                const uint32_t plast = P[best_n - 1];
-                for (int b0 = 0; b0 < best_n; b0 += 64) {
-                    const int i = b0 + lane;
-                    double term = 0.0;
-                    if (i < best_n) {
-                        const uint32_t q = P[i], pq = i == 0 ? plast : P[i - 1];
-                        float xs, ys, pxs, pys;
-                        scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
-                        scale_pt(a.f, (int)(pq & 0xFFFFu), (int)(pq >> 16), &pxs, &pys);
-                        term = (double)pxs * (double)ys - (double)pys * (double)xs;
-                        if (poly && i < a.poly_cap) {
-                            poly[2 * i] = xs;
-                            poly[2 * i + 1] = ys;
-                        }
-                    }
-                    const int m = min(64, best_n - b0);
-                    for (int j = 0; j < m; ++j) acc += readlane_f64(term, j);
-                }
-            } else {  // longer than the buffer: followed again from the image (marks off)
-                int lx = 0, ly = 0;
-                fetch_contour(img, r.ww, bx, by, false, [&](int px, int py) { lx = px, ly = py; });
-                float pxs, pys;
-                scale_pt(a.f, r.X0 + lx - 1, r.Y0 + ly - 1, &pxs, &pys);
-                int i = 0;
-                fetch_contour(img, r.ww, bx, by, false, [&](int qx, int qy) {
-                    float xs, ys;
-                    scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
-                    acc += (double)pxs * (double)ys - (double)pys * (double)xs;
-                    pxs = xs, pys = ys;
-                    if (poly && i < a.poly_cap && lane == 0) {
-                        poly[2 * i] = xs;
-                        poly[2 * i + 1] = ys;
-                    }
-                    ++i;
-                });
-            }
-            st.area = fabs(acc * 0.5);
-        }
-        if (tid == 0) {
-            if (a.poly_n) a.poly_n[di] = best_n;
-            a.cstats[di] = st;
-            CT_PROF(if (item < CT_PROF_ITEMS) {
-                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-                unsigned long long* pr = g_ct_prof[item];
-                pr[0] = t1 - t0, pr[1] = t2 - t1, pr[2] = t3 - t2, pr[3] = (unsigned long long)ncont;
-                pr[4] = nrows, pr[5] = npos, pr[6] = (unsigned long long)nsteps, pr[7] = ttr;
-            });
-        }
-        __syncthreads();  // the image is reused by the next item
+        if (k >= uni(s.ndet[b])) continue;
+        const Region r = uni_region(region_of(s, b, k));
+        if (r.w <= 0 || region_need(s, r) <= CP_POOL) continue;
+        contour_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, item);
+        __syncthreads();  // the slot is reused by the next item
     }
 }
 
@@ -670,6 +812,7 @@ struct FillArgs {
 
 constexpr int FILL_MAX_CELLS = 64 * 64;  // lattice of a 1280 x 1280 frame
 constexpr int FILL_MAX_ROWS = 64, FILL_MAX_COLS = 64;
+constexpr int FILL_LDS = 120 * 1024;  // dynamic LDS of the fill kernel (its static arrays take ~37 KiB)
 
 // cv::clipLine(Size(W, H), pt1, pt2): false when the segment misses the image
 __device__ bool clip_line(int W, int H, long long& x1, long long& y1, long long& x2, long long& y2) {
@@ -709,6 +852,7 @@ __device__ bool clip_line(int W, int H, long long& x1, long long& y1, long long&
 }
 
 __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
+    extern __shared__ __align__(16) uint32_t fill_lds[];  // FILL_LDS bytes: the chosen instance's image
     __shared__ int s_k, s_n, s_edges;
     __shared__ int s_minx, s_miny, s_maxx, s_maxy;
     __shared__ unsigned long long s_exmin, s_exmax;  // edge x extremes, biased by 2^62
@@ -741,6 +885,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
         }
         __syncthreads();
         const int k = s_k;
+        CT_PROF(const unsigned long long f0 = __builtin_amdgcn_s_memtime(); int fb = 0);
         if (k == -2) {
             for (int i = tid; i < LR * LC; i += nt) out[i] = a.plant_cells[(int64_t)b * LR * LC + i];
             if (tid < 4) a.rects[4 * b + tid] = a.plant_rects[4 * b + tid];
@@ -776,24 +921,28 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                 pts[2 * i + 1] = (int)ys;
             }
             if (tid == 0) s_n = st.npts;
-        } else if (st.npts > 0) {  // longer than the buffer: the image rebuilt in the slot and followed again
-            const Region r = region_of(s, b, k);
-            uint32_t* img = (uint32_t*)(slot + a.sc.img_off);
+        } else if (st.npts > 0) {  // longer than the buffer: the image rebuilt (in LDS if it fits) and followed again
+            const Region r = uni_region(region_of(s, b, k));
             MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
-            build_image(s, b, k, r, img, (float*)slot, tid, nt, ms);
-            if (tid < 64) {
-                int i = 0;
-                fetch_contour(img, r.ww, st.ox, st.oy, false, [&](int qx, int qy) {
-                    float xs, ys;
-                    scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
-                    if (tid == 0 && i < a.sc.cap) {
-                        pts[2 * i] = (int)xs;
-                        pts[2 * i + 1] = (int)ys;
-                    }
-                    ++i;
-                });
-                if (tid == 0) s_n = i;
-            }
+            auto retrace = [&](uint32_t* img, float* strip) {
+                build_image<false>(s, b, k, r, img, strip, tid, nt, ms);
+                if (tid < 64) {
+                    int i = 0;
+                    fetch_contour(img, r.ww, st.ox, st.oy, false, [&](int qx, int qy) {
+                        float xs, ys;
+                        scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
+                        if (tid == 0 && i < a.sc.cap) {
+                            pts[2 * i] = (int)xs;
+                            pts[2 * i + 1] = (int)ys;
+                        }
+                        ++i;
+                    });
+                    if (tid == 0) s_n = i;
+                }
+            };
+            // two call sites, each with its own pointer (an LDS / global select would make the accesses flat)
+            if (region_need(s, r) <= FILL_LDS) retrace(fill_lds, (float*)(fill_lds + ((image_words(r) + 3) & ~3ll)));
+            else retrace((uint32_t*)(slot + a.sc.img_off), (float*)slot);
         } else if (tid == 0) {
             s_n = 0;
         }
@@ -808,6 +957,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
         }
         __syncthreads();
         const int n = s_n;
+        CT_PROF(const unsigned long long f1 = __builtin_amdgcn_s_memtime(); fb = st.npts > a.sc.capd);
         // boundingRect + the edges: lines through cell centres, span counts at the sampled rows
         for (int i = tid; i < n; i += nt) {
             const int x1i = pts[2 * i], y1i = pts[2 * i + 1];
@@ -903,6 +1053,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
             }
         }
         __syncthreads();
+        CT_PROF(const unsigned long long f2 = __builtin_amdgcn_s_memtime());
         // FillEdgeCollection's early outs: fewer than 2 edges, or all edges outside the image
         constexpr unsigned long long BIAS = 1ull << 62;
         const long long exmin = (long long)(s_exmin - BIAS), exmax = (long long)(s_exmax - BIAS);
@@ -926,6 +1077,11 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                 a.rects[4 * b + 2] = s_maxx - s_minx + 1;
                 a.rects[4 * b + 3] = s_maxy - s_miny + 1;
             }
+            CT_PROF(if (b < CT_FILL_FRAMES) {
+                unsigned long long* pr = g_ct_fill[b];
+                pr[0] = f1 - f0, pr[1] = f2 - f1, pr[2] = __builtin_amdgcn_s_memtime() - f2;
+                pr[3] = (unsigned long long)n, pr[4] = (unsigned long long)fb;
+            });
         }
         __syncthreads();
     }
@@ -939,13 +1095,16 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
                              const uint8_t* plant_cells, const int32_t* plant_rects, int plant_mode, uint8_t* cells,
                              int32_t* rects, int32_t* chosen, int32_t* status, float* polys, int32_t* poly_n,
                              int poly_cap, hipStream_t st) {
-    static DevFlag large_attr;  // per device: the large instantiation's dynamic LDS
-    if (!large_attr()) {
-        if (hipFuncSetAttribute((const void*)post_contour_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                CT_LDS_LARGE) != hipSuccess)
+    static DevFlag pool_attr;  // per device: the pool and fill kernels' dynamic LDS
+    if (!pool_attr()) {
+        if (hipFuncSetAttribute((const void*)post_contour_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                CP_POOL) != hipSuccess ||
+            hipFuncSetAttribute((const void*)post_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                FILL_LDS) != hipSuccess)
             return hipErrorInvalidValue;
-        large_attr() = true;
+        pool_attr() = true;
     }
+    if (src.mw > CT_STRIP / 2) return hipErrorInvalidValue;  // a strip holds >= 2 low-res rows
     CtArgs ca;
     ca.s = src;
     ca.f = f;
@@ -955,11 +1114,21 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     ca.polys = polys;
     ca.poly_n = poly_n;
     ca.poly_cap = poly_cap;
+    static const int gate_env = getenv("VA_CT_GATE") ? atoi(getenv("VA_CT_GATE")) : 1;  // A/B knob
+    ca.gate = gate_env;
     const int64_t items = (int64_t)src.B * max_det;
+    static DevVal<int> n_cu;  // per device: one pool block per CU
+    if (n_cu() <= 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return hipErrorInvalidValue;
+        n_cu() = cus;
+    }
+    const int pgrid = (int)(items < n_cu() ? items : n_cu());
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
-    hipLaunchKernelGGL(post_contour_kernel<0>, dim3(grid), dim3(CT_THREADS), CT_LDS_SMALL, st, ca);
-    hipLaunchKernelGGL(post_contour_kernel<1>, dim3(grid), dim3(CT_THREADS), CT_LDS_LARGE, st, ca);
-    hipLaunchKernelGGL(post_contour_kernel<2>, dim3(grid), dim3(CT_THREADS), 0, st, ca);
+    hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), CP_POOL, st, ca);
+    hipLaunchKernelGGL(post_contour_global_kernel, dim3(grid), dim3(CT_THREADS), 0, st, ca);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     if (!cells) return hipSuccess;
     FillArgs fa;
@@ -976,7 +1145,7 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     fa.chosen = chosen;
     fa.status = status;
     const int fgrid = src.B < sc.nslots ? src.B : sc.nslots;
-    hipLaunchKernelGGL(post_fill_kernel, dim3(fgrid), dim3(FILL_THREADS), 0, st, fa);
+    hipLaunchKernelGGL(post_fill_kernel, dim3(fgrid), dim3(FILL_THREADS), FILL_LDS, st, fa);
     return hipGetLastError();
 }
 
@@ -1038,6 +1207,14 @@ extern "C" int va_contour_prof(unsigned long long* out, int n) {
     return VA_OK;
 }
 
+extern "C" int va_contour_fill_prof(unsigned long long* out, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return VA_ERR_HIP;
+    if (n > CT_FILL_FRAMES) n = CT_FILL_FRAMES;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ct_fill), sizeof(unsigned long long) * 8 * n) != hipSuccess)
+        return VA_ERR_HIP;
+    return VA_OK;
+}
+
 extern "C" int va_contour_debug(unsigned int* out4, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return VA_ERR_HIP;
     if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_ct_err), sizeof(unsigned int) * 4) != hipSuccess) return VA_ERR_HIP;
@@ -1045,6 +1222,23 @@ extern "C" int va_contour_debug(unsigned int* out4, int reset) {
         const unsigned int z[4] = {0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_ct_err), z, sizeof(z)) != hipSuccess) return VA_ERR_HIP;
     }
+    return VA_OK;
+}
+#endif
+
+#ifdef VA_CT_WATCH
+extern "C" int va_contour_watch(void** host) {
+    static int* h = nullptr;
+    if (!h) {
+        if (hipHostMalloc((void**)&h, sizeof(int) * 4 * CT_WATCH_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess)
+            return VA_ERR_HIP;
+        memset(h, 0xFF, sizeof(int) * 4 * CT_WATCH_SLOTS);
+        int* d = nullptr;
+        if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return VA_ERR_HIP;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ct_watch), &d, sizeof(d)) != hipSuccess) return VA_ERR_HIP;
+    }
+    *host = h;
     return VA_OK;
 }
 #endif
