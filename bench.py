@@ -324,7 +324,7 @@ def main():
              "batch_per_gpu": B_, "regime": reg_}
         if ex == "c5":
             e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU: YOLOv8m-seg 1280x1280, convs on e4m3 MFMA "
-                             "(per-channel weight scales, static activation scales), batch 8 = 64 across 8 GPUs, "
+                             "(per-channel weight scales; activations stored as e4m3 with one calibrated power-of-two scale per buffer), batch 8 = 64 across 8 GPUs, "
                              "post-processing + grid / A* on GPU")
             e["parity"] = "tests/test_gpu_fp8.py: op vs the same quantized operands; forward rel. L2 vs fp32"
         if prof:

@@ -153,8 +153,9 @@ int va_astar_run(void* stream, const uint8_t* node_flags, const double* node_pen
 /* ---------------------------------------------------------------- segmentation (YOLOv8-seg) */
 #define VA_DTYPE_BF16 1
 #define VA_DTYPE_F32 2
-#define VA_DTYPE_FP8 3   /* va_seg_conv only: e4m3 weights + per-channel scales, bf16 activations quantized to e4m3
-                          * on the fly, block-scaled fp8 MFMA (va_conv_args.wscale / xscale) */
+#define VA_DTYPE_FP8 3   /* e4m3 MFMA convolutions (va_seg_conv: e4m3 weights + per-channel scales, e4m3 or bf16
+                            activations, va_conv_args.xscale...); va_seg_sppf_pool / va_seg_upsample2x: e4m3 byte
+                            buffers (one power-of-two scale per buffer, unchanged by max and copy) */
 
 /* One Conv2d (+ folded BN bias, optional SiLU, optional residual add) as an implicit GEMM on MFMA.
  * Replaces the Conv / Bottleneck / C2f / SPPF / Detect / Proto convolutions Ultralytics runs inside
@@ -203,12 +204,17 @@ typedef struct va_conv_args {
     const void* xu;
     int32_t ldu;
     int32_t cu;
-    /* VA_DTYPE_FP8: w is e4m3 [Npad][Kpad] (Kpad % 128 == 0), the bf16 input is quantized as sat(x * xscale) and
-     * the accumulator dequantized by wscale[co] (= the weights' per-channel scale / xscale) before bias and act;
-     * mode 0 / 1, Cin % 16 == 0, no tail / xu / bias4 (BASELINE.json configs[4]: "fp8 MFMA weights") */
+    /* VA_DTYPE_FP8: w is e4m3 [Npad][Kpad] (Kpad % 128 == 0); the input holds sat(x * xscale) as e4m3 bytes
+     * (x8 = 1: an fp8 activation buffer, ldx % 16 == 0) or is bf16 quantized so on the fly (x8 = 0); the
+     * accumulator is dequantized by wscale[co] (= the weights' per-channel scale / xscale) before bias and act.
+     * Output: e4m3 sat(y * yscale) when yscale > 0 (ldy % 8 == 0), else bf16 (or float with out_f32); an e4m3
+     * residual holds r * rscale (rscale > 0), else bf16.  Scales are powers of two.  Mode 0 / 1, Cin % 16 == 0,
+     * no tail / xu / bias4 (BASELINE.json configs[4]: "fp8 MFMA weights"). */
     const float* wscale;    /* [Npad] */
     float xscale;
-    int32_t pad8_;
+    int32_t x8;
+    float yscale;
+    float rscale;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);
@@ -254,7 +260,8 @@ int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, 
                      const float* bias, int32_t Cout, float* y, int32_t ldy);
 
 /* SPPF (block.py SPPF): slice 0 (c channels) of an NHWC buffer of channel stride ld >= 4c -> slices 1..3
- * = MaxPool2d(5, 1, 2) applied once, twice, three times. */
+ * = MaxPool2d(5, 1, 2) applied once, twice, three times (dtype F32 / BF16 / FP8: e4m3 bytes, ordered as the
+ * values they encode). */
 int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld, int32_t dtype);
 
 /* nn.Upsample(scale_factor=2, mode="nearest") from a slice into a concat slice. */

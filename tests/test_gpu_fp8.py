@@ -1,6 +1,7 @@
 """The fp8 convolution path (va_fp8.hip, BASELINE.json configs[4] "YOLOv8m-seg 1280x1280 fp8 MFMA weights").
 
-* one conv op against torch on the SAME quantized operands: e4m3 weights with their per-channel scales as packed,
+* one conv op against torch on the SAME quantized operands (bf16 or e4m3 input, bf16 / float / e4m3 output, bf16
+  or e4m3 residual -- the fp8 mode keeps its activations as e4m3 bytes): e4m3 weights with their per-channel scales as packed,
   the bf16 input scaled by a power of two, saturated to +-448 and rounded to e4m3 (torch.float8_e4m3fn), f32
   accumulation, then the dequant scale, bias, SiLU, residual -- the kernel differs only by summation order, its
   fast SiLU and the bf16 output rounding: within 2e-2 of the output's scale (3x3 / 1x1 / stride 2 / residual / channel slices /
@@ -22,7 +23,21 @@ pytestmark = pytest.mark.gpu
 FP8_L2 = {"box": 0.25, "cls": 0.25, "coef": 0.25, "proto": 0.25}  # relative L2 vs the fp32 oracle (measured 0.15-0.20)
 
 
-def _conv8(cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, out_f32=False, act=True):
+def _e4m3(t: torch.Tensor, s: float) -> torch.Tensor:
+    """sat(t * s) as e4m3 bytes (uint8), round to nearest even."""
+    from vision_assist_amd import seg as S
+    return (t.float() * s).clamp(-S.F8_MAX, S.F8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def _pow2_scale(amax: float) -> float:
+    from vision_assist_amd import seg as S
+    return 2.0 ** np.floor(np.log2(S.F8_MAX / amax))
+
+
+def _conv8(cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, out_f32=False, act=True,
+           x8=False, y8=False, r8=False):
+    """One va_seg_conv fp8 op and its reference.  x8 / y8 / r8: input / output / residual as e4m3 bytes (the fp8
+    mode's activation buffers); y8 returns (got, ref) both scaled by the output scale (e4m3 units)."""
     from vision_assist_amd import _lib
     from vision_assist_amd import seg as S
     from vision_assist_amd.seg_arch import Arch
@@ -41,32 +56,41 @@ def _conv8(cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0,
     p = net._pack(w, b, deconv=deconv)
     w8, sw, Kp = net._pack_fp8(p)
     ld_in = cin + slice_in + 16
-    xin = torch.zeros(B, H, W, ld_in, dtype=torch.bfloat16, device="cuda")
-    xin[..., slice_in:slice_in + cin] = x.permute(0, 2, 3, 1).to(torch.bfloat16).cuda()
-    xb = xin[..., slice_in:slice_in + cin].float().cpu()  # NHWC, what the kernel reads
-    xs = 2.0 ** np.floor(np.log2(S.F8_MAX / float(xb.abs().max())))  # a power of two, as calibrate_fp8 picks
+    xb = x.permute(0, 2, 3, 1).to(torch.bfloat16).float()  # NHWC, the bf16 values
+    xs = _pow2_scale(float(xb.abs().max()))  # a power of two, as calibrate_fp8 picks
+    if x8:  # the e4m3 buffer holds sat(x * xs)
+        xin = torch.zeros(B, H, W, ld_in, dtype=torch.uint8, device="cuda")
+        xin[..., slice_in:slice_in + cin] = _e4m3(xb, xs).cuda()
+    else:
+        xin = torch.zeros(B, H, W, ld_in, dtype=torch.bfloat16, device="cuda")
+        xin[..., slice_in:slice_in + cin] = xb.to(torch.bfloat16).cuda()
     pad = k // 2 if not deconv else 0
     if deconv:
         Ho, Wo, oh, ow = H, W, 2 * H, 2 * W
     else:
         Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
         oh, ow = Ho, Wo
-    odt = torch.float32 if out_f32 else torch.bfloat16
+    odt = torch.float32 if out_f32 else (torch.uint8 if y8 else torch.bfloat16)
     ld_out = cout + 16
     y = torch.zeros(B, oh, ow, ld_out, dtype=odt, device="cuda")
-    res = torch.randn(B, oh, ow, cout, generator=g).to(torch.bfloat16).cuda() if residual else None
+    res, rs = None, 0.0
+    if residual:
+        rf = torch.randn(B, oh, ow, cout, generator=g).to(torch.bfloat16).float()
+        if r8:
+            rs = _pow2_scale(float(rf.abs().max()))
+            res = _e4m3(rf, rs).cuda()
+        else:
+            res = rf.to(torch.bfloat16).cuda()
     ws = (sw / xs).contiguous()
-    args = S.ConvArgs(x=xin.data_ptr() + slice_in * 2, N=B, H=H, W=W, Cin=p.cin, ldx=ld_in, kh=p.k, kw=p.k,
+    args = S.ConvArgs(x=xin.data_ptr() + slice_in * xin.element_size(), N=B, H=H, W=W, Cin=p.cin, ldx=ld_in, kh=p.k,
+                      kw=p.k,
                       stride=stride if not deconv else 1, pad=pad, Ho=Ho, Wo=Wo, w=w8.data_ptr(), bias=p.b.data_ptr(),
                       Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=Kp, y=y.data_ptr() + 8 * y.element_size(), ldy=ld_out,
                       res=res.data_ptr() if res is not None else None, ldr=cout, act=1 if act else 0,
                       mode=1 if deconv else 0, M=B * Ho * Wo, dtype=S.VA_DTYPE_FP8, out_f32=1 if out_f32 else 0,
-                      wscale=ws.data_ptr(), xscale=xs)
-    _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(args)), "va_seg_conv")
-    torch.cuda.synchronize()
-    got = y[..., 8:8 + cout].float().cpu()
+                      wscale=ws.data_ptr(), xscale=xs, x8=1 if x8 else 0, rscale=rs)
     # the reference on the same quantized operands
-    xq = (xb * xs).clamp(-S.F8_MAX, S.F8_MAX).to(torch.float8_e4m3fn).float().permute(0, 3, 1, 2)
+    xq = _e4m3(xb, xs).view(torch.float8_e4m3fn).float().permute(0, 3, 1, 2)
     wq = w8.cpu().view(torch.float8_e4m3fn).float()[:, :p.K]  # [Npad][K], K = (ky, kx, ci)
     rows = 4 * cout if deconv else cout
     wq = wq[:rows].reshape(rows, p.k, p.k, p.cin).permute(0, 3, 1, 2)
@@ -78,8 +102,17 @@ def _conv8(cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0,
         acc = F.silu(acc)
     ref = acc.permute(0, 2, 3, 1)
     if residual:
-        ref = ref + res.float().cpu()
-    return got, ref
+        ref = ref + (res.cpu().view(torch.float8_e4m3fn).float() / rs if r8 else res.float().cpu())
+    ys = 0.0
+    if y8:
+        ys = _pow2_scale(float(ref.abs().max()))
+        args.yscale = ys
+        args.y = y.data_ptr() + 8
+    _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(args)), "va_seg_conv")
+    torch.cuda.synchronize()
+    if y8:  # e4m3 units
+        return y[..., 8:8 + cout].cpu().view(torch.float8_e4m3fn).float(), ref * ys
+    return y[..., 8:8 + cout].float().cpu(), ref
 
 
 @pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,deconv,slice_in,out_f32", [
@@ -97,6 +130,64 @@ def test_fp8_conv_op(cin, cout, k, stride, H, W, residual, deconv, slice_in, out
     assert got.shape == ref.shape
     err = ((got - ref).abs().max() / ref.abs().max()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,deconv,slice_in,x8,y8,r8", [
+    (64, 128, 3, 1, 20, 24, False, False, 0, True, True, False),    # e4m3 in and out
+    (96, 192, 3, 2, 33, 40, False, False, 16, True, True, False),   # stride 2, ragged M, 16-channel slice
+    (128, 64, 1, 1, 17, 19, True, False, 0, True, True, True),      # 1x1 + e4m3 residual (C2f bottleneck)
+    (48, 96, 3, 1, 40, 40, True, False, 0, False, True, True),      # bf16 in (model.1), e4m3 out + residual
+    (64, 32, 2, 1, 12, 10, False, True, 0, True, True, False),      # ConvTranspose2d(2, 2) into e4m3
+    (96, 80, 1, 1, 13, 13, False, False, 0, True, False, False),    # head-like: e4m3 in, float out
+])
+def test_fp8_conv_op_e4m3_buffers(cin, cout, k, stride, H, W, residual, deconv, slice_in, x8, y8, r8):
+    """The fp8 mode's ops on e4m3 activation buffers: e4m3 output within one e4m3 step of the exact value (the
+    kernel rounds its float result) plus 1e-4 of the output's scale (float summation order, where partial sums
+    cancel)."""
+    out_f32 = not y8 and cout == 80
+    got, ref = _conv8(cin, cout, k, stride, H, W, residual, deconv, slice_in, out_f32,
+                      act=not (deconv or out_f32), x8=x8, y8=y8, r8=r8)
+    assert got.shape == ref.shape
+    if y8:
+        r = ref.clamp(-448, 448)
+        ulp = torch.where(r.abs() >= 2.0 ** -6, 2.0 ** (torch.floor(torch.log2(r.abs().clamp_min(1e-30))) - 3),
+                          torch.full_like(r, 2.0 ** -9))
+        # one e4m3 step, plus the float sums' own error where large partial sums cancel (1e-4 of the output's
+        # scale: the kernel and torch add in different orders)
+        badm = (got - r).abs() > ulp * 1.0001 + 1e-4 * r.abs().max()
+        bad = int(badm.sum().item())
+        assert bad == 0, (bad, (got - r).abs().max().item(), got[badm][:8].tolist(), r[badm][:8].tolist(),
+                          badm.nonzero()[:8].tolist())
+    else:
+        err = ((got - ref).abs().max() / ref.abs().max()).item()
+        assert err < 2e-2, err
+
+
+def test_fp8_sppf_and_upsample_on_e4m3_bytes():
+    """SPPF maxima and the FPN upsample copy on e4m3 bytes equal the same ops on the decoded values."""
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(3)
+    B, H, W, c = 2, 20, 20, 64
+    v = torch.randn(B, H, W, c, generator=g) * 30
+    buf = torch.zeros(B, H, W, 4 * c, dtype=torch.uint8)
+    buf[..., :c] = _e4m3(v, 4.0)
+    d = buf.cuda()
+    _lib.check(lib.va_seg_sppf_pool(_lib.stream_ptr(), d.data_ptr(), B, H, W, c, 4 * c, S.VA_DTYPE_FP8), "sppf")
+    torch.cuda.synchronize()
+    got = d.cpu().view(torch.float8_e4m3fn).float()
+    x = got[..., :c].permute(0, 3, 1, 2)
+    want = []
+    for _ in range(3):
+        x = F.max_pool2d(x, 5, 1, 2)
+        want.append(x.permute(0, 2, 3, 1))
+    assert torch.equal(got[..., c:], torch.cat(want, -1))
+    up = torch.zeros(B, 2 * H, 2 * W, c + 16, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.va_seg_upsample2x(_lib.stream_ptr(), d.data_ptr(), 4 * c, up.data_ptr() + 16, c + 16, B, H, W, c,
+                                     S.VA_DTYPE_FP8), "upsample")
+    torch.cuda.synchronize()
+    assert torch.equal(up[..., 16:].cpu(), d[..., :c].cpu().repeat_interleave(2, 1).repeat_interleave(2, 2))
 
 
 def _frames(B, H, W, seed):

@@ -1,20 +1,23 @@
 // va_fp8.hip -- the convolutions of YOLOv8-seg on block-scaled fp8 MFMA (gfx950 v_mfma_scale_f32_16x16x128_f8f6f4,
 // OCP e4m3 operands): BASELINE.json configs[4], "YOLOv8m-seg 1280x1280 fp8 MFMA weights".
 //
-// Weights are e4m3 with one scale per output channel (seg.py packs them); activations stay bf16 in HBM (every
-// other op of the network -- upsample, concat, SPPF, residuals, the heads' post-processing -- is unchanged) and are
-// quantized to e4m3 while a tile is staged into LDS, with one static power-of-two scale per conv input (calibrated
-// once on a bf16 forward, seg.py SegNet.calibrate_fp8).  With x_q = sat(x * xscale) and W_q = W / sw[co]:
-//     y[co] = act(sum_k W_q[co][k] x_q[k] * wscale[co] + bias[co]) (+ residual),  wscale[co] = sw[co] / xscale,
+// Weights are e4m3 with one scale per output channel (seg.py packs them).  Activations live in HBM as e4m3 bytes
+// with one static power-of-two scale per buffer (seg.py SegNet.calibrate_fp8: a concat buffer, and the buffers an
+// upsample copies between, share one): every conv reads its input bytes as they are (X8) -- or, for the one bf16
+// map (model.0's output), quantizes it while staging -- and writes its output already quantized with the output
+// buffer's scale, so SPPF's maxima and the FPN's upsample copies work on the bytes.  With x_q = sat(x * xs),
+// W_q = W / sw[co]:
+//     y[co] = act(sum_k W_q[co][k] x_q[k] * wscale[co] + bias[co]) (+ r_q / rs),  wscale[co] = sw[co] / xs,
+//     stored as sat(y * ys) (e4m3), or bf16 / float,
 // the instruction's own E8M0 block scales held at 1.0 (127).  The K order inside a 128-deep step is whatever the
 // instruction's lane map is -- the same bytes of a lane feed A and B, so the sum is over the same K either way.
 //
-//   conv8_kernel  implicit GEMM, 128 pixels x 128 output channels per 256-thread workgroup (2 x 2 waves of
-//                 64 x 64, 16 accumulators each), K-steps of 128 bytes, two LDS stages with register staging
-//                 (weights: 16-byte loads; activations: two 16-byte bf16 loads per 16 fp8, clamped in the bf16
-//                 domain and converted by v_cvt_scalef32_pk_fp8_bf16), XCD-aware tile order, the bias / SiLU /
-//                 residual epilogue of the bf16 kernels (mode 0 and the ConvTranspose2d scatter of mode 1; bf16 or
-//                 f32 output).
+//   conv8_kernel<X8>  implicit GEMM, 128 pixels x 128 output channels per 256-thread workgroup (2 x 2 waves of
+//                     64 x 64, 16 accumulators each), K-steps of 128 bytes, two LDS stages with register staging
+//                     (weights and e4m3 activations: 16-byte loads; bf16 activations: two 16-byte loads per 16
+//                     values, clamped in the bf16 domain and converted by v_cvt_scalef32_pk_fp8_bf16),
+//                     XCD-aware tile order, the bias / SiLU / residual epilogue (mode 0 and the ConvTranspose2d
+//                     scatter of mode 1) with e4m3, bf16 or float output and an e4m3 or bf16 residual.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -75,6 +78,28 @@ __device__ __forceinline__ unsigned quant_lim2(float s) {
     return b | (b << 16);
 }
 
+// 8 floats -> 8 e4m3 bytes: sat(v * ys), round to nearest even
+__device__ __forceinline__ uint2 pack8_e4m3(const float* v, float ys) {
+    float c[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c[e] = fminf(fmaxf(v[e] * ys, -F8_MAX), F8_MAX);
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+    return make_uint2((unsigned)lo, (unsigned)hi);
+}
+
+// 8 e4m3 bytes -> 8 floats times inv (exact: e4m3 values and power-of-two scales)
+__device__ __forceinline__ void unpack8_e4m3(uint2 q, float inv, float* v) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.x, true);
+    const f2 c = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)q.y, true);
+    v[0] = a[0] * inv, v[1] = a[1] * inv, v[2] = b[0] * inv, v[3] = b[1] * inv;
+    v[4] = c[0] * inv, v[5] = c[1] * inv, v[6] = d[0] * inv, v[7] = d[1] * inv;
+}
+
+template <bool X8>
 __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, int ntiles) {
     __shared__ __align__(16) unsigned char smem[F8_LDS];
     int bid = blockIdx.x;
@@ -88,6 +113,7 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
     const int m0 = tm * F8_BM, n0 = tn * F8_BN;
     const uint8_t* __restrict__ Wq = (const uint8_t*)a.w;
     const __bf16* __restrict__ X = (const __bf16*)a.x;
+    const uint8_t* __restrict__ X8p = (const uint8_t*)a.x;
     const float inv = 1.0f / a.xscale;  // xscale is a power of two (va_fp8_conv_ok)
     const unsigned lim2 = quant_lim2(a.xscale);
     // staging: chunk c = tid + 256 q (q < 4): row c / 8, 16-byte column g = c % 8 (the same g for all four)
@@ -127,8 +153,13 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
             const int hi = b_hi[q] + ky, wi = b_wi[q] + kx;
             const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
             const int64_t off = ok ? (b_base[q] + (int64_t)hi * a.W + wi) * a.ldx + ci : 0;
-            const u32x4 lo = *(const u32x4*)(X + off), hi8 = *(const u32x4*)(X + off + 8);
-            rb[q] = ok ? quant16(lo, hi8, inv, lim2) : (u32x4){0u, 0u, 0u, 0u};
+            if constexpr (X8) {  // already e4m3 with this scale
+                const u32x4 v = *(const u32x4*)(X8p + off);
+                rb[q] = ok ? v : (u32x4){0u, 0u, 0u, 0u};
+            } else {
+                const u32x4 lo = *(const u32x4*)(X + off), hi8 = *(const u32x4*)(X + off + 8);
+                rb[q] = ok ? quant16(lo, hi8, inv, lim2) : (u32x4){0u, 0u, 0u, 0u};
+            }
         }
         kcur += F8_KS;
         ci += F8_KS;
@@ -209,9 +240,11 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
         }
     }
     __syncthreads();
-    const bool of32 = a.out_f32 != 0;
+    const bool of32 = a.out_f32 != 0, o8 = a.yscale > 0.0f, r8 = a.rscale > 0.0f;
     const int OV = of32 ? 4 : 8, CPRO = F8_BN / OV;
     const __bf16* R = (const __bf16*)a.res;
+    const uint8_t* R8 = (const uint8_t*)a.res;
+    const float rinv = r8 ? 1.0f / a.rscale : 0.0f;
     for (int c = tid; c < F8_BM * CPRO; c += F8_NT) {
         const int pl = c / CPRO, cl = (c % CPRO) * OV;
         const int m = m0 + pl, co = n0 + cl;
@@ -224,8 +257,13 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
                 v[r] = t.x, v[r + 1] = t.y, v[r + 2] = t.z, v[r + 3] = t.w;
             }
         }
-        if (R) {
-            if (of32) {
+        if (a.res) {
+            if (r8) {  // e4m3 residual (8 channels; not with a float output)
+                float rv[8];
+                unpack8_e4m3(*(const uint2*)(R8 + (int64_t)m * a.ldr + co), rinv, rv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += rv[e];
+            } else if (of32) {
                 const uint2 rr = *(const uint2*)(R + (int64_t)m * a.ldr + co);
                 const __bf16* rp = (const __bf16*)&rr;
 #pragma unroll
@@ -247,6 +285,8 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
         }
         if (of32) {
             *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+        } else if (o8) {
+            *(uint2*)((uint8_t*)a.y + yo) = pack8_e4m3(v, a.yscale);
         } else {
             bf16x8 o;
 #pragma unroll
@@ -262,19 +302,36 @@ __global__ __launch_bounds__(F8_NT) void conv8_kernel(va_conv_args a, int ntn, i
 hipError_t va_fp8_conv_launch(const va_conv_args& a, hipStream_t st) {
     const int ntm = (a.M + F8_BM - 1) / F8_BM, ntn = a.Npad / F8_BN;
     const int ntiles = ntm * ntn;
-    hipLaunchKernelGGL(conv8_kernel, dim3(ntiles), dim3(F8_NT), 0, st, a, ntn, ntiles);
+    if (a.x8) hipLaunchKernelGGL(conv8_kernel<true>, dim3(ntiles), dim3(F8_NT), 0, st, a, ntn, ntiles);
+    else hipLaunchKernelGGL(conv8_kernel<false>, dim3(ntiles), dim3(F8_NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
 bool va_fp8_conv_ok(const va_conv_args& a) {
-    // 16 channels of one tap per staged chunk; bf16 input rows 16-byte aligned; outputs in 8 (4) element runs
-    uint32_t xb;
-    memcpy(&xb, &a.xscale, sizeof xb);
-    return a.wscale && a.xscale > 0.0f && (xb & 0x7FFFFFu) == 0 && a.Cin % 16 == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 &&
-           a.Kpad % F8_KS == 0 && a.Npad % F8_BN == 0 && (a.mode == 0 || a.mode == 1) && !a.w2 && !a.xu &&
-           !a.bias4 && (a.out_f32 ? (a.Cout % 4 == 0 && a.ldy % 4 == 0 && !a.res)
-                                 : (a.Cout % 8 == 0 && a.ldy % 8 == 0 && (!a.res || a.ldr % 8 == 0))) &&
-           (a.mode != 1 || (a.Cout / 4) % 8 == 0);
+    // 16 channels of one tap per staged chunk (16 e4m3 bytes, or two 16-byte bf16 runs); outputs in 8-element runs
+    // (e4m3: 8 bytes, bf16: 16 bytes; 4 floats for a float output, which takes no residual); power-of-two scales
+    auto pow2 = [](float f) {
+        uint32_t b;
+        memcpy(&b, &f, sizeof b);
+        return f > 0.0f && (b & 0x7FFFFFu) == 0;
+    };
+    const bool in_ok = a.x8 ? (a.ldx % 16 == 0 && ((uintptr_t)a.x & 15) == 0)
+                            : (a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0);
+    const bool o8 = a.yscale > 0.0f, r8 = a.rscale > 0.0f;
+    bool out_ok;
+    if (a.out_f32) {
+        out_ok = !o8 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && !a.res;
+    } else {
+        const int cd = a.mode == 1 ? a.Cout / 4 : a.Cout;
+        const int al = o8 ? 8 : 16;  // bytes of an 8-element run
+        out_ok = a.Cout % 8 == 0 && cd % 8 == 0 && a.ldy % 8 == 0 && ((uintptr_t)a.y & (al - 1)) == 0 &&
+                 (!o8 || pow2(a.yscale));
+        if (a.res)
+            out_ok = out_ok && a.ldr % 8 == 0 && (r8 ? (pow2(a.rscale) && ((uintptr_t)a.res & 7) == 0)
+                                                     : ((uintptr_t)a.res & 15) == 0);
+    }
+    return a.wscale && pow2(a.xscale) && a.Cin % 16 == 0 && in_ok && a.Kpad % F8_KS == 0 && a.Npad % F8_BN == 0 &&
+           (a.mode == 0 || a.mode == 1) && !a.w2 && !a.xu && !a.bias4 && out_ok;
 }
 
 // Test probe of the e4m3 conversions (tests/test_gpu_fp8.py): out[2i], out[2i+1] = the staging path's bytes of

@@ -1930,6 +1930,11 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
 // planes live in LDS ([4][H*W] x 16 B: 25.6 KiB at 20x20, 100 KiB at 40x40).
 constexpr int SPPF_MAXPIX = 40 * 40;  // 1280-px input -> 40x40 at stride 32
 
+// an order key of a stored value: the value itself, or for an e4m3 byte (sign-magnitude) +-magnitude bits
+__device__ inline float ord_key(float v) { return v; }
+__device__ inline float ord_key(__bf16 v) { return (float)v; }
+__device__ inline float ord_key(uint8_t v) { return (v & 0x80) ? -(float)(v & 0x7F) : (float)v; }
+
 template <typename T>
 __device__ inline u32x4 vmax16(u32x4 a, u32x4 b) {
     constexpr int E = 16 / sizeof(T);
@@ -1938,7 +1943,7 @@ __device__ inline u32x4 vmax16(u32x4 a, u32x4 b) {
     u32x4 r;
     T* pr = (T*)&r;
 #pragma unroll
-    for (int e = 0; e < E; ++e) pr[e] = to_f(pa[e]) >= to_f(pb[e]) ? pa[e] : pb[e];
+    for (int e = 0; e < E; ++e) pr[e] = ord_key(pa[e]) >= ord_key(pb[e]) ? pa[e] : pb[e];
     return r;
 }
 
@@ -2355,7 +2360,7 @@ int va_seg_preprocess(void* stream, const uint8_t* frames, int32_t B, int32_t H,
 
 int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, int32_t c, int32_t ld,
                      int32_t dtype) {
-    const int cg = dtype == VA_DTYPE_BF16 ? 8 : 4;
+    const int cg = dtype == VA_DTYPE_FP8 ? 16 : dtype == VA_DTYPE_BF16 ? 8 : 4;  // elements per 16 bytes
     if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % cg || ld % cg || H * W > SPPF_MAXPIX || ((uintptr_t)buf & 15))
         return VA_ERR_ARG;
     // 2 channel groups per workgroup while the four planes fit 52 KiB of LDS (20 x 20 maps: three
@@ -2368,7 +2373,10 @@ int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, i
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, p, H, W, c, ld);
     };
-    if (dtype == VA_DTYPE_BF16) {
+    if (dtype == VA_DTYPE_FP8) {
+        if (cgw == 2) go(sppf_pool_kernel<uint8_t, 2>, (uint8_t*)buf);
+        else go(sppf_pool_kernel<uint8_t, 1>, (uint8_t*)buf);
+    } else if (dtype == VA_DTYPE_BF16) {
         if (cgw == 2) go(sppf_pool_kernel<__bf16, 2>, (__bf16*)buf);
         else go(sppf_pool_kernel<__bf16, 1>, (__bf16*)buf);
     } else {
@@ -2380,11 +2388,14 @@ int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, i
 
 int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, int32_t ld_d, int32_t N, int32_t H,
                       int32_t W, int32_t c, int32_t dtype) {
-    const int vec = dtype == VA_DTYPE_BF16 ? 8 : 4;
+    const int vec = dtype == VA_DTYPE_FP8 ? 16 : dtype == VA_DTYPE_BF16 ? 8 : 4;
     if (!src || !dst || c % vec || ld_s % vec || ld_d % vec) return VA_ERR_ARG;
     int64_t total = (int64_t)N * 4 * H * W * (c / vec);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == VA_DTYPE_BF16)
+    if (dtype == VA_DTYPE_FP8)
+        hipLaunchKernelGGL(upsample2x_kernel<uint8_t>, dim3(grid_for(total, 256)), dim3(256), 0, st,
+                           (const uint8_t*)src, ld_s, (uint8_t*)dst, ld_d, N, H, W, c);
+    else if (dtype == VA_DTYPE_BF16)
         hipLaunchKernelGGL(upsample2x_kernel<__bf16>, dim3(grid_for(total, 256)), dim3(256), 0, st,
                            (const __bf16*)src, ld_s, (__bf16*)dst, ld_d, N, H, W, c);
     else

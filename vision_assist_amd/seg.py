@@ -46,7 +46,8 @@ class ConvArgs(ctypes.Structure):
         ("out_f32", ctypes.c_int32), ("bias4", ctypes.c_int32),
         ("w2", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("c2", ctypes.c_int32), ("act2", ctypes.c_int32),
         ("xu", ctypes.c_void_p), ("ldu", ctypes.c_int32), ("cu", ctypes.c_int32),
-        ("wscale", ctypes.c_void_p), ("xscale", ctypes.c_float), ("pad8_", ctypes.c_int32),
+        ("wscale", ctypes.c_void_p), ("xscale", ctypes.c_float), ("x8", ctypes.c_int32),
+        ("yscale", ctypes.c_float), ("rscale", ctypes.c_float),
     ]
 
 
@@ -87,6 +88,11 @@ class Slice:
 
     def sub(self, off, c):
         return Slice(self.buf, self.off + off, c)
+
+    @property
+    def e4m3(self) -> bool:
+        """An fp8-mode activation buffer: e4m3 bytes (with one power-of-two scale per buffer)."""
+        return self.buf.dtype == torch.uint8
 
 
 @dataclass
@@ -147,7 +153,8 @@ class SegNet:
         # fp8: e4m3 weights with per-output-channel scales (the convs whose input channels come in 16s), and
         # the per-conv activation scales of calibrate_fp8
         self.w8 = {}
-        self.xscale = None
+        self.xscale = None   # per fp8 conv: its input's scale (calibrate_fp8)
+        self.bscale = None   # per activation buffer of the plan, in creation order (calibrate_fp8)
         if dtype == "fp8":
             for prefix, p in self.w.items():
                 if p.cin % 16 == 0:
@@ -166,10 +173,11 @@ class SegNet:
         return q.to(self.device).contiguous(), sw.to(self.device).contiguous(), Kp
 
     def calibrate_fp8(self, H: int, W: int, frames_u8: torch.Tensor | None = None, seed: int = 0) -> dict:
-        """Static activation scales of the fp8 convs: one forward of this network in bf16 (same weights) on
-        `frames_u8` (default: 2 seeded uniform uint8 frames, the bench's input distribution); each fp8 conv's
-        input is quantized as sat(x * s), s the power of two with amax * s in [224, 448], amax the largest |x|
-        of its input there."""
+        """Static scales of the fp8 mode: one forward of this network in bf16 (same weights, the same buffers in
+        the same order) on `frames_u8` (default: 2 seeded uniform uint8 frames, the bench's input distribution).
+        Every activation buffer gets the power of two s with amax * s in [224, 448], amax the largest |x| it held
+        there; buffers an upsample copies between share one scale (the copy moves bytes).  Values are stored as
+        sat(x * s) in e4m3.  -> {conv prefix: its input's scale}."""
         if frames_u8 is None:
             g = torch.Generator().manual_seed(seed)
             frames_u8 = torch.randint(0, 256, (2, H, W, 3), generator=g, dtype=torch.uint8)
@@ -178,17 +186,30 @@ class SegNet:
         p["frames"].copy_(frames_u8.to(self.device), non_blocking=True)
         self.run_plan(p)
         torch.cuda.synchronize(self.device)
-        xs = {}
-        for m in p["meta"]:
-            src = m.get("src")
-            if src is None or m["prefix"] not in self.w8:
-                continue
-            amax = float(src.buf[..., src.off:src.off + src.c].float().abs().max())
-            # a power of two (va_fp8.hip's conversion takes it exactly): amax lands in [224, 448]
-            xs[m["prefix"]] = 2.0 ** math.floor(math.log2(F8_MAX / amax)) if amax > 0 else 1.0
-        self.xscale = xs
+        bufs = p["bufs"]
+        amax = [float(t.float().abs().max()) for t in bufs]
+        parent = list(range(len(bufs)))
+
+        def find(i):
+            while parent[i] != i:
+                parent[i] = parent[parent[i]]
+                i = parent[i]
+            return i
+
+        for i, j in p["links"]:
+            parent[find(i)] = find(j)
+        gmax = {}
+        for i, m in enumerate(amax):
+            r = find(i)
+            gmax[r] = max(gmax.get(r, 0.0), m)
+        # a power of two (exact in the kernels' conversions): amax lands in [224, 448]
+        self.bscale = [2.0 ** math.floor(math.log2(F8_MAX / gmax[find(i)])) if gmax[find(i)] > 0 else 1.0
+                       for i in range(len(bufs))]
+        index = {t.data_ptr(): i for i, t in enumerate(bufs)}
+        self.xscale = {m["prefix"]: self.bscale[index[m["src"].buf.data_ptr()]] for m in p["meta"]
+                       if m.get("src") is not None and m["prefix"] in self.w8}
         del self._plans[(B, H, W, -1, True)]
-        return xs
+        return self.xscale
 
     def _pack_stem(self, w0p: torch.Tensor, b0: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
         """Weight blob + bias vector of va_seg_stem: bf16 MFMA A fragments (see _pack_c2f) W0 = model.0
@@ -281,8 +302,9 @@ class SegNet:
 
     @property
     def store(self) -> str:
-        """Activation storage: f32 in the f32 mode, else bf16 (fp8, BASELINE.json configs[4], runs its convs on
-        e4m3 MFMA -- va_fp8.hip -- and keeps activations in bf16)."""
+        """Activation storage of the f32 / bf16 kernels: f32 in the f32 mode, else bf16.  The fp8 mode
+        (BASELINE.json configs[4], e4m3 MFMA -- va_fp8.hip) keeps its activations as e4m3 bytes with one scale per
+        buffer (plan(), calibrate_fp8); only model.0's output (and its weights' padding) stays bf16."""
         return "f32" if self.dtype == "f32" else "bf16"
 
     @property
@@ -325,7 +347,7 @@ class SegNet:
         if key in self._plans:
             return self._plans[key]
         fp8 = self.dtype == "fp8" and not _calib
-        if fp8 and self.xscale is None:
+        if fp8 and self.bscale is None:
             self.calibrate_fp8(H, W)
         if H % 32 or W % 32:
             raise _lib.VaError(f"frame {H}x{W}: the network needs multiples of 32 (pad/letterbox first)")
@@ -333,11 +355,21 @@ class SegNet:
         ops = []
         meta = []  # per op: name, kind, GEMM M/N/K (algorithmic), bytes moved
         keep = []  # buffers referenced by the op list
+        bufs = []  # activation buffers in creation order (fp8: one scale each, calibrate_fp8)
+        links = []  # (i, j): buffers an upsample copies between (one scale)
+        scale = {}  # fp8: buffer data_ptr -> its scale
 
         def new(h, w, c, dtype=None):
-            t = self._buf(B, h, w, c, dtype)
+            # fp8: activations as e4m3 bytes, except the float outputs and the bf16 map model.0 writes
+            t = self._buf(B, h, w, c, dtype if dtype is not None or not fp8 else torch.uint8)
             keep.append(t)
+            if fp8:
+                scale[t.data_ptr()] = self.bscale[len(bufs)]
+            bufs.append(t)
             return Slice(t, 0, c)
+
+        def bidx(sl: Slice) -> int:
+            return next(i for i, t in enumerate(bufs) if t.data_ptr() == sl.buf.data_ptr())
 
         def conv(prefix, src: Slice, dst: Slice, h, w, stride=1, act=True, res: Slice | None = None,
                  out_f32=False, tail: str | None = None, act2=False, up: Slice | None = None):
@@ -360,13 +392,18 @@ class SegNet:
                 out_f32=1 if (out_f32 and self.store == "bf16") else 0)
             on_fp8 = fp8 and prefix in self.w8 and tail is None and up is None and self._fp8_fits(p, src, dst, res,
                                                                                                   out_f32)
-            if on_fp8:  # va_fp8.hip: e4m3 weights, the bf16 input quantized with its calibrated scale
+            if fp8 and not on_fp8:
+                raise _lib.VaError(f"{prefix}: the fp8 mode's e4m3 buffers need the fp8 kernel's operand rules")
+            if on_fp8:  # va_fp8.hip: e4m3 weights; input, output and residual with their buffers' scales
                 w8, sw, Kp = self.w8[prefix]
-                xs = self.xscale[prefix]
+                xs = scale[src.buf.data_ptr()]
                 ws = (sw / xs).contiguous()
                 keep.append(ws)
                 args.dtype, args.w, args.Kpad, args.wscale, args.xscale = VA_DTYPE_FP8, w8.data_ptr(), Kp, \
                     ws.data_ptr(), xs
+                args.x8 = 1 if src.e4m3 else 0
+                args.yscale = scale[dst.buf.data_ptr()] if dst.e4m3 else 0.0
+                args.rscale = scale[res.buf.data_ptr()] if res is not None and res.e4m3 else 0.0
             if up is not None:
                 args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
             cout = p.cout
@@ -381,11 +418,12 @@ class SegNet:
                 raise _lib.VaError(f"{prefix}: output slice has {dst.c} channels, conv gives {cout}")
             ops.append(SegOp(kind=VA_OP_CONV, a=args))
             es = 2 if self.store == "bf16" else 4
+            xe, ye = src.buf.element_size(), (4 if out_f32 else dst.buf.element_size())
             flops = 2 * B * ho * wo * p.cout * k * k * src.c + (2 * B * ho * wo * p.cout * cout if p2 else 0)
             meta.append({"name": prefix + (f"+{tail}" if tail else ""), "kind": "conv", "M": B * ho * wo,
                          "N": p.cout, "K": k * k * src.c, "k": k, "stride": stride, "flops": flops,
-                         "bytes": es * B * h * w * src.c + (1 if on_fp8 else es) * p.cout * k * k * src.c
-                         + B * ho * wo * cout * (4 if out_f32 else es),
+                         "bytes": xe * B * h * w * src.c + (1 if on_fp8 else es) * p.cout * k * k * src.c
+                         + B * ho * wo * cout * ye,
                          "prefix": prefix, "src": src, "fp8": on_fp8})
             return ho, wo
 
@@ -412,8 +450,10 @@ class SegNet:
             conv(f"model.{i}.cv2", t, dst, h, w)
 
         def upsample(src: Slice, dst: Slice, h, w):
+            links.append((bidx(src), bidx(dst)))
             ops.append(SegOp(kind=VA_OP_UPSAMPLE, a=ConvArgs(x=src.ptr, ldx=src.ld, y=dst.ptr, ldy=dst.ld, N=B, H=h, W=w,
-                                                              Cin=src.c, dtype=self.va_dtype)))
+                                                              Cin=src.c,
+                                                              dtype=VA_DTYPE_FP8 if src.e4m3 else self.va_dtype)))
             meta.append({"name": "upsample", "kind": "upsample"})
 
         frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
@@ -433,7 +473,7 @@ class SegNet:
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
                          "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
         else:
-            a0 = new(h1, w1, a.c1)
+            a0 = new(h1, w1, a.c1, self.tdtype)  # bf16 (fp8 mode: model.1 quantizes it while staging)
             if self.fuse_first:
                 ops.append(SegOp(kind=VA_OP_CONV0, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W,
                                                                w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
@@ -441,7 +481,7 @@ class SegNet:
                 meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3,
                              "stride": 2, "bytes": B * H * W * 3 + (2 if self.store == "bf16" else 4) * B * h1 * w1 * a.c1})
             else:
-                x0 = new(H, W, 8)
+                x0 = new(H, W, 8, self.tdtype)
                 ops.append(SegOp(kind=VA_OP_PREPROCESS, a=ConvArgs(x=frames.data_ptr(), y=x0.ptr, N=B, H=H, W=W,
                                                                     dtype=self.va_dtype)))
                 meta.append({"name": "preprocess", "kind": "preprocess"})
@@ -467,7 +507,8 @@ class SegNet:
         cs = a.c5 // 2
         sp = new(h5, w5, 4 * cs)
         conv("model.9.cv1", b8, sp.sub(0, cs), h5, w5)
-        ops.append(SegOp(kind=VA_OP_SPPF, a=ConvArgs(y=sp.ptr, N=B, H=h5, W=w5, Cin=cs, ldy=sp.ld, dtype=self.va_dtype)))
+        ops.append(SegOp(kind=VA_OP_SPPF, a=ConvArgs(y=sp.ptr, N=B, H=h5, W=w5, Cin=cs, ldy=sp.ld,
+                                                      dtype=VA_DTYPE_FP8 if sp.e4m3 else self.va_dtype)))
         meta.append({"name": "sppf_pool", "kind": "sppf"})
         cat20 = new(h5, w5, a.c4 + a.c5)          # [conv19(o4) | P5]
         P5 = cat20.sub(a.c4, a.c5)
@@ -527,7 +568,8 @@ class SegNet:
             proto = new(h2, w2, NM, torch.float32)
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
             op_arr = (SegOp * len(ops))(*ops)
-            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
+            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
+                    "links": links,
                     "out": SegOutputs(levels=levels, proto=proto.buf)}
             self._plans[key] = plan
             return plan
@@ -549,7 +591,8 @@ class SegNet:
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * (pf.K + p3.cout),
                          "bytes": 2 * B * h3 * w3 * pf.cin + 2 * pf.w.numel() + 4 * B * h2 * w2 * NM})
             op_arr = (SegOp * len(ops))(*ops)
-            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
+            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
+                    "links": links,
                     "out": SegOutputs(levels=levels, proto=proto.buf)}
             self._plans[key] = plan
             return plan
@@ -566,21 +609,27 @@ class SegNet:
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
         op_arr = (SegOp * len(ops))(*ops)
         assert len(meta) == len(ops)
-        plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
+        plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
+                    "links": links,
                 "out": SegOutputs(levels=levels, proto=proto.buf)}
         self._plans[key] = plan
         return plan
 
     @staticmethod
     def _fp8_fits(p: Packed, src: Slice, dst: Slice, res, out_f32: bool) -> bool:
-        """va_fp8.hip's operand rules (va_fp8_conv_ok): bf16 input rows in 16-byte runs, outputs in 8-element
-        runs (4 for a float output, which takes no residual)."""
-        ok = src.ld % 8 == 0 and (src.off * 2) % 16 == 0
+        """va_fp8.hip's operand rules (va_fp8_conv_ok): input rows in 16-byte runs of 16 channels (e4m3 or bf16),
+        outputs and residuals in 8-element runs (4 for a float output, which takes no residual)."""
+        xe = src.buf.element_size()
+        ok = (src.ld * xe) % 16 == 0 and (src.off * xe) % 16 == 0 and p.cin % 16 == 0
         if out_f32:
             return ok and p.cout % 4 == 0 and dst.ld % 4 == 0 and res is None
         cd = p.cout // 4 if p.deconv else p.cout
-        return ok and cd % 8 == 0 and dst.ld % 8 == 0 and (dst.off * 2) % 16 == 0 and \
-            (res is None or (res.ld % 8 == 0 and (res.off * 2) % 16 == 0))
+        ye = dst.buf.element_size()
+        ok = ok and cd % 8 == 0 and dst.ld % 8 == 0 and (dst.off * ye) % (8 * ye) == 0
+        if res is not None:
+            re = res.buf.element_size()
+            ok = ok and res.ld % 8 == 0 and (res.off * re) % (8 * re) == 0
+        return ok
 
     def _can_fuse_tail(self, prefix: str, tail: str) -> bool:
         """Whether the 1x1 conv ``tail`` (sole consumer of ``prefix``) can run in prefix's epilogue: bf16,
