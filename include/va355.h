@@ -256,6 +256,11 @@ int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int3
  * Conv2d(3, Cout, 3, s2, p1) + folded BN bias + SiLU (x / (1 + exp(-x))) -> f32 NHWC [N][H/2][W/2] with channel
  * stride ldy, on the vector ALU (K = 27: one output pixel per lane, the weights wave-uniform).  w: f32 [Cout][27],
  * k = (ky*3 + kx)*3 + c with c in R, G, B order; Cout in {16, 32, 48, 64}; ldy % 4 == 0, y 16-byte aligned. */
+/* va_seg_conv0 with an e4m3 output sat(y * yscale) (the fp8 mode's first activation buffer; bf16 weights and
+ * arithmetic as va_seg_conv0, yscale a power of two). */
+int va_seg_conv0_e4m3(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
+                      const float* bias, int32_t Cout, uint8_t* y, int32_t ldy, float yscale);
+
 int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const float* w,
                      const float* bias, int32_t Cout, float* y, int32_t ldy);
 
@@ -275,7 +280,8 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_UPSAMPLE 3    /* upsample2x: a.x/a.ldx -> a.y/a.ldy, a.N/H/W (source size), a.Cin = c, a.dtype */
 #define VA_OP_PREPROCESS 4  /* preprocess: a.x = uint8 frames, a.y = out, a.N/H/W, a.dtype */
 #define VA_OP_CONV0 5       /* preprocess fused into model.0: a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
-                               a.Cout, a.y, a.ldy, a.dtype -- see va_seg_conv0 / va_seg_conv0_f32 */
+                               a.Cout, a.y, a.ldy, a.dtype (FP8: e4m3 output with a.yscale) -- see va_seg_conv0 /
+                               va_seg_conv0_f32 / va_seg_conv0_e4m3 */
 #define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
 #define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: see va_seg_stem */
 typedef struct va_seg_op {

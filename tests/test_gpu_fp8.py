@@ -190,6 +190,34 @@ def test_fp8_sppf_and_upsample_on_e4m3_bytes():
     assert torch.equal(up[..., 16:].cpu(), d[..., :c].cpu().repeat_interleave(2, 1).repeat_interleave(2, 2))
 
 
+def test_fp8_conv0_e4m3_output_matches_bf16_kernel():
+    """va_seg_conv0_e4m3 (model.0 fused with the preprocess, e4m3 output) = the bf16 kernel's output quantized:
+    within one e4m3 step (the e4m3 form rounds the float result directly, the bf16 one after a bf16 rounding)."""
+    from vision_assist_amd import _lib
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("m")
+    net = SegNet(arch, fold(arch, synthetic_state_dict(arch, seed=2)), dtype="bf16")
+    B, H, W = 2, 160, 192
+    fr = _frames(B, H, W, 9).cuda()
+    c = arch.c1
+    yb = torch.zeros(B, H // 2, W // 2, c, dtype=torch.bfloat16, device="cuda")
+    y8 = torch.zeros(B, H // 2, W // 2, c, dtype=torch.uint8, device="cuda")
+    w, b = net.w0
+    _lib.check(net.lib.va_seg_conv0(_lib.stream_ptr(), fr.data_ptr(), B, H, W, w.data_ptr(), b.data_ptr(), c,
+                                    yb.data_ptr(), c), "conv0")
+    torch.cuda.synchronize()
+    ys = _pow2_scale(float(yb.float().abs().max()))
+    _lib.check(net.lib.va_seg_conv0_e4m3(_lib.stream_ptr(), fr.data_ptr(), B, H, W, w.data_ptr(), b.data_ptr(), c,
+                                         y8.data_ptr(), c, ys), "conv0_e4m3")
+    torch.cuda.synchronize()
+    got = y8.cpu().view(torch.float8_e4m3fn).float()
+    r = (yb.float().cpu() * ys).clamp(-448, 448)
+    ulp = torch.where(r.abs() >= 2.0 ** -6, 2.0 ** (torch.floor(torch.log2(r.abs().clamp_min(1e-30))) - 3),
+                      torch.full_like(r, 2.0 ** -9))
+    assert ((got - r).abs() <= ulp * 1.0001 + 1e-3 * r.abs().max()).all()
+
+
 def _frames(B, H, W, seed):
     return torch.randint(0, 256, (B, H, W, 3), generator=torch.Generator().manual_seed(seed), dtype=torch.uint8)
 

@@ -59,6 +59,7 @@ SIGNATURES = [
     ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
     ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_conv0_f32", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
+    ("va_seg_conv0_e4m3", I32, [P, P, I32, I32, I32, P, P, I32, P, I32, ctypes.c_float]),
     ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_upsample2x", I32, [P, P, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_run", I32, [P, P, I32]),

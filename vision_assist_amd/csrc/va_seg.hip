@@ -299,11 +299,13 @@ constexpr int BK2 = 64;
 __device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((address_space(1))) void gvoid_t;
 typedef __attribute__((address_space(3))) void lvoid_t;
 
-// T = element type: __bf16 (K-step 64, v_mfma_f32_16x16x32_bf16) or float (exact-f32 parity mode: K-step 32,
-// four v_mfma_f32_16x16x4_f32 per 16-byte chunk).  A staged row is 128 bytes = 8 chunks of 16 bytes either way,
+// T = element type: __bf16 (K-step 64, v_mfma_f32_16x16x32_bf16), float (exact-f32 parity mode: K-step 32,
+// four v_mfma_f32_16x16x4_f32 per 16-byte chunk) or uint8_t = e4m3 bytes (the fp8 mode, va355.h
+// VA_DTYPE_FP8 with x8: K-step 128, one block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 per fragment pair).  A staged row is 128 bytes = 8 chunks of 16 bytes either way,
 // so the LDS layout, the swizzle, the DMA pattern and the im2col bookkeeping are shared.
 template <typename T, int WM, int WN, int TNS, bool GLDS = false>
 struct Conv2Cfg {
@@ -418,10 +420,28 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 // stores.  Needs BM * (BN + 4) * 4 bytes of LDS.
 // orow(pl): output row of tile row pl (mode 1: the linear GEMM row, scattered below), or -1 when masked
 // RT: element type of the residual (the activations'); bias4 (mode 2): per-row bias from the border table
+// e4m3 (RT / OutT = uint8_t, the fp8 mode): the accumulator is dequantized by wscale before the bias, the residual
+// holds r * rscale, the output is stored as sat(y * yscale) (va355.h va_conv_args, VA_DTYPE_FP8)
+__device__ __forceinline__ uint2 e4m3_pack8(const float* v, float ys) {
+    float c[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) c[e] = fminf(fmaxf(v[e] * ys, -448.0f), 448.0f);
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+    return make_uint2((unsigned)lo, (unsigned)hi);
+}
+__device__ __forceinline__ void e4m3_unpack4(unsigned q, float inv, float* v) {
+    const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)q, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)q, true);
+    v[0] = a[0] * inv, v[1] = a[1] * inv, v[2] = b[0] * inv, v[3] = b[1] * inv;
+}
+
 template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename RT = __bf16>
 __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
                                               int wm, int wn, int tid, int fr, int fq, RowFn orow, int m0 = 0,
                                               int cls = 0) {
+    constexpr bool F8 = sizeof(RT) == 1;  // the fp8 mode (e4m3 activations)
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
     int brow[4];  // bias row offset per pixel fragment
@@ -441,8 +461,12 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float4 bv = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
-            float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y, v2 = acc[i][j][2] + bv.z,
-                  v3 = acc[i][j][3] + bv.w;
+            f32x4 ac = acc[i][j];
+            if constexpr (F8) {
+                const float4 sv = *(const float4*)(a.wscale + n0 + col);
+                ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
+            }
+            float v0 = ac[0] + bv.x, v1 = ac[1] + bv.y, v2 = ac[2] + bv.z, v3 = ac[3] + bv.w;
             if (a.act) {
                 const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
                 v0 = s01[0];
@@ -475,12 +499,24 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
             v[r + 3] = t.w;
         }
         if (R) {
+            if constexpr (F8) {  // e4m3 residual: OV (16) bytes
+                const float rinv = 1.0f / a.rscale;
+                const u32x4 rr = *(const u32x4*)(R + orw * a.ldr + co);
 #pragma unroll
-            for (int r = 0; r < OV; r += RV) {
-                const u32x4 rr = *(const u32x4*)(R + orw * a.ldr + co + r);
-                const RT* rp = (const RT*)&rr;
+                for (int w = 0; w < 4 && 4 * w < OV; ++w) {
+                    float rv[4];
+                    e4m3_unpack4(rr[w], rinv, rv);
 #pragma unroll
-                for (int e = 0; e < RV && r + e < OV; ++e) v[r + e] += (float)rp[e];
+                    for (int e = 0; e < 4; ++e) v[4 * w + e] += rv[e];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < OV; r += RV) {
+                    const u32x4 rr = *(const u32x4*)(R + orw * a.ldr + co + r);
+                    const RT* rp = (const RT*)&rr;
+#pragma unroll
+                    for (int e = 0; e < RV && r + e < OV; ++e) v[r + e] += (float)rp[e];
+                }
             }
         }
         OutT* yp;
@@ -492,7 +528,10 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
         } else {
             yp = Y + orw * a.ldy + co;
         }
-        if constexpr (sizeof(OutT) == 2) {
+        if constexpr (sizeof(OutT) == 1) {  // 16 e4m3 bytes
+            const uint2 lo = e4m3_pack8(v, a.yscale), hi = e4m3_pack8(v + 8, a.yscale);
+            *(u32x4*)yp = (u32x4){lo.x, lo.y, hi.x, hi.y};
+        } else if constexpr (sizeof(OutT) == 2) {
             bf16x8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
@@ -716,6 +755,21 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[kh][i]),
                                                                             __builtin_bit_cast(bf16x8, bfr[kh][j]),
                                                                             acc[i][j], 0, 0, 0);
+        } else if constexpr (sizeof(T) == 1) {
+            // e4m3: lane (fr, fq) holds chunks fq and 4 + fq of row fr -- 32 of the step's 128 K bytes, the same K
+            // bytes for A and B, which is all the instruction's lane map asks; E8M0 block scales 2^0 (127)
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) {
+                const i32x8 av = {(int)af[0][i][0], (int)af[0][i][1], (int)af[0][i][2], (int)af[0][i][3],
+                                  (int)af[1][i][0], (int)af[1][i][1], (int)af[1][i][2], (int)af[1][i][3]};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const i32x8 bv = {(int)bfr[0][j][0], (int)bfr[0][j][1], (int)bfr[0][j][2], (int)bfr[0][j][3],
+                                      (int)bfr[1][j][0], (int)bfr[1][j][1], (int)bfr[1][j][2], (int)bfr[1][j][3]};
+                    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc[i][j], 0, 0, 0, 127, 0,
+                                                                               127);
+                }
+            }
         } else {
             // f32: element e of lane (fr, fq)'s chunk 4 kh + fq is K index 16 kh + 4 fq + e of the stage -- MFMA
             // (kh, e) sums over fq, so the four MFMAs of a chunk cover its 16 K values (the same permutation of
@@ -1838,10 +1892,12 @@ constexpr int C0_PR = 2 * C0_TH + 1;
 // first window pixel (ix0 = 2 ox0 - 1) sits at byte 13
 constexpr int C0_PP = 400, C0_OFF = 13;
 
-template <int NCO>
+// OUT8: e4m3 output sat(y * yscale) (the fp8 mode's activation buffers), else bf16
+template <int NCO, bool OUT8 = false>
 __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                     const __bf16* __restrict__ w, const float* __restrict__ bias,
-                                                    __bf16* __restrict__ y, int ldy) {
+                                                    void* __restrict__ yv, int ldy, float yscale = 0.0f) {
+    __bf16* __restrict__ y = (__bf16*)yv;
     __shared__ __align__(16) uint8_t patch[C0_PR * C0_PP];
     const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
     const int tx = blockIdx.x, ty = blockIdx.y, n = blockIdx.z;
@@ -1894,6 +1950,28 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
         for (int i = 0; i < NCO; ++i)
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         if (oy >= Ho || ox >= Wo) continue;
+        if constexpr (OUT8) {
+            uint8_t* yp8 = (uint8_t*)yv + (((int64_t)n * Ho + oy) * Wo + ox) * ldy;
+#pragma unroll
+            for (int p = 0; p < NCO / 2; ++p) {
+                const int co = 32 * p + 8 * fq;
+                const float4 b0 = *(const float4*)(bias + co), b1 = *(const float4*)(bias + co + 4);
+                const float v[8] = {silu(acc[2 * p][0] + b0.x),     silu(acc[2 * p][1] + b0.y),
+                                    silu(acc[2 * p][2] + b0.z),     silu(acc[2 * p][3] + b0.w),
+                                    silu(acc[2 * p + 1][0] + b1.x), silu(acc[2 * p + 1][1] + b1.y),
+                                    silu(acc[2 * p + 1][2] + b1.z), silu(acc[2 * p + 1][3] + b1.w)};
+                *(uint2*)(yp8 + co) = e4m3_pack8(v, yscale);
+            }
+            if constexpr (NCO % 2) {
+                const int co = 16 * (NCO - 1) + 4 * fq;
+                const float4 bv = *(const float4*)(bias + co);
+                const f32x4 t = acc[NCO - 1];
+                const float v[8] = {silu(t[0] + bv.x), silu(t[1] + bv.y), silu(t[2] + bv.z), silu(t[3] + bv.w),
+                                    0.f, 0.f, 0.f, 0.f};
+                *(unsigned*)(yp8 + co) = e4m3_pack8(v, yscale).x;
+            }
+            continue;
+        }
         __bf16* yp = y + (((int64_t)n * Ho + oy) * Wo + ox) * ldy;
 #pragma unroll
         for (int p = 0; p < NCO / 2; ++p) {
@@ -2308,9 +2386,30 @@ extern "C" {
 
 int va_seg_conv(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
-    if (a->dtype == VA_DTYPE_FP8) {  // va_fp8.hip
+    if (a->dtype == VA_DTYPE_FP8) {
         if (!va_fp8_conv_ok(*a) || a->Npad < a->Cout || a->K > a->Kpad) return VA_ERR_ARG;
-        return va_fp8_conv_launch(*a, (hipStream_t)stream) == hipSuccess ? VA_OK : VA_ERR_HIP;
+        hipStream_t st = (hipStream_t)stream;
+        // e4m3 input: conv2's LDS-DMA tiles (narrow layers get the tall 256-pixel tiles), e4m3 or float output;
+        // a bf16 input (model.0's map) or a bf16 output / residual: va_fp8.hip's register-staged kernel
+        const bool c2 = a->x8 && (a->out_f32 || a->yscale > 0.0f) && (!a->res || a->rscale > 0.0f) &&
+                        getenv("VA_FP8_CONV8") == nullptr;
+        if (c2) {
+            const int ov = a->out_f32 ? 4 : 16, cd = a->mode == 1 ? a->Cout / 4 : a->Cout;
+            if (a->Cout % ov == 0 && cd % ov == 0 && a->ldy % ov == 0 && ((uintptr_t)a->y & 15) == 0 &&
+                (!a->res || (a->ldr % 16 == 0 && ((uintptr_t)a->res & 15) == 0))) {
+                hipError_t e;
+                if (a->out_f32)
+                    e = a->Cout <= 32   ? launch_conv2<4, 1, 2, float, uint8_t>(*a, st)
+                        : a->Cout <= 64 ? launch_conv2<4, 1, 4, float, uint8_t>(*a, st)
+                                        : launch_conv2<2, 2, 4, float, uint8_t>(*a, st);
+                else
+                    e = a->Cout <= 32   ? launch_conv2<4, 1, 2, uint8_t, uint8_t>(*a, st)
+                        : a->Cout <= 64 ? launch_conv2<4, 1, 4, uint8_t, uint8_t>(*a, st)
+                                        : launch_conv2<2, 2, 4, uint8_t, uint8_t>(*a, st);
+                return e == hipSuccess ? VA_OK : VA_ERR_HIP;
+            }
+        }
+        return va_fp8_conv_launch(*a, st) == hipSuccess ? VA_OK : VA_ERR_HIP;
     }
     const bool bf = a->dtype == VA_DTYPE_BF16;
     const int vec = bf ? 8 : 4, ks = 8 * vec;  // elements per 16-byte chunk / per conv2 K-step
@@ -2483,6 +2582,24 @@ int va_seg_conv0(void* stream, const uint8_t* frames, int32_t N, int32_t H, int3
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+int va_seg_conv0_e4m3(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w,
+                      const float* bias, int32_t Cout, uint8_t* y, int32_t ldy, float yscale) {
+    if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 8 ||
+        (3 * W) % 16 || ((uintptr_t)frames & 15) || ((uintptr_t)y & 7) || !(yscale > 0.0f))
+        return VA_ERR_ARG;
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    dim3 grid((Wo + C0_TW - 1) / C0_TW, (Ho + C0_TH - 1) / C0_TH, N);
+    hipStream_t st = (hipStream_t)stream;
+    const __bf16* wp = (const __bf16*)w;
+    switch (Cout / 16) {
+        case 1: hipLaunchKernelGGL((conv0_kernel<1, true>), grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy, yscale); break;
+        case 2: hipLaunchKernelGGL((conv0_kernel<2, true>), grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy, yscale); break;
+        case 3: hipLaunchKernelGGL((conv0_kernel<3, true>), grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy, yscale); break;
+        default: hipLaunchKernelGGL((conv0_kernel<4, true>), grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy, yscale);
+    }
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
 int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const float* w,
                      const float* bias, int32_t Cout, float* y, int32_t ldy) {
     if (!frames || !w || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 4 ||
@@ -2524,6 +2641,9 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                 rc = a.dtype == VA_DTYPE_F32
                          ? va_seg_conv0_f32(stream, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w, a.bias,
                                             a.Cout, (float*)a.y, a.ldy)
+                     : a.dtype == VA_DTYPE_FP8
+                         ? va_seg_conv0_e4m3(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout,
+                                             (uint8_t*)a.y, a.ldy, a.yscale)
                          : va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             case VA_OP_C2F:

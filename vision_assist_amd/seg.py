@@ -473,11 +473,14 @@ class SegNet:
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
                          "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
         else:
-            a0 = new(h1, w1, a.c1, self.tdtype)  # bf16 (fp8 mode: model.1 quantizes it while staging)
+            # fp8: e4m3 straight from the fused model.0 (else bf16, and model.1 quantizes it while staging)
+            a0 = new(h1, w1, a.c1, None if self.fuse_first else self.tdtype)
             if self.fuse_first:
-                ops.append(SegOp(kind=VA_OP_CONV0, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W,
-                                                               w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
-                                                               Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)))
+                c0 = ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
+                              Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)
+                if a0.e4m3:
+                    c0.dtype, c0.yscale = VA_DTYPE_FP8, scale[a0.buf.data_ptr()]
+                ops.append(SegOp(kind=VA_OP_CONV0, a=c0))
                 meta.append({"name": "model.0", "kind": "conv", "M": B * h1 * w1, "N": a.c1, "K": 27, "k": 3,
                              "stride": 2, "bytes": B * H * W * 3 + (2 if self.store == "bf16" else 4) * B * h1 * w1 * a.c1})
             else:
