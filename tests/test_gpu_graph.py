@@ -52,3 +52,63 @@ def test_graph_replay_equals_eager(scale, dtype, B, regime):
     assert all(same), same
     same = [bool(torch.equal(a, b)) for a, b in zip(per_det(), ref_det)]
     assert all(same), same
+
+
+def test_graph_replay_then_nav_equals_eager():
+    """The batch-1 latency form (tools/latency.py --graph): frame copy + network + post-processing replayed from
+    a graph, then the grid / A* stage eagerly on the replayed cells -- the same paths, costs and angle-cache keys
+    as the eager pipeline, over several replays."""
+    import numpy as np
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_ALWAYS
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    from workloads.corridors import cells_rect, corridor_cells
+    arch = Arch("n")
+    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0)), 1, 640, 640, dtype="bf16")
+    frame = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(1),
+                          dtype=torch.uint8).cuda()
+    runs = []
+    for seed in (11, 12, 13):
+        gc_ = corridor_cells(seed, 32, 32)
+        runs.append((torch.tensor(gc_[None].astype(np.uint8)).cuda(),
+                     torch.tensor(np.array([cells_rect(gc_)], dtype=np.int32)).cuda()))
+    pc = torch.zeros_like(runs[0][0])
+    pr = torch.zeros_like(runs[0][1])
+
+    def summary(res):
+        f = res.frame(0)
+        return [(q["path"], float(q["cost"]).hex() if q["path"] else None) for q in f.queries]
+
+    want = []
+    for c, r in runs:  # eager
+        res = pipe.run(frame, c, r, PLANT_ALWAYS)
+        want.append((summary(res), sorted(pipe.seen.keys())))
+    pipe.seen.clear()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            pipe.load(frame)
+            pipe.seg_post(pc, pr, PLANT_ALWAYS)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        pipe.load(frame)
+        pipe.seg_post(pc, pr, PLANT_ALWAYS)
+    torch.cuda.synchronize()
+    # replay and the eager stage on a stream of their own: on the legacy default stream (handle 0) the replayed
+    # graph was observed not to be ordered before the following launches (illegal address in the nav stage,
+    # gone with AMD_SERIALIZE_KERNEL=3), so graphs are never launched on it here
+    got = []
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for c, r in runs:
+            pc.copy_(c)
+            pr.copy_(r)
+            g.replay()
+            res = pipe.nav_run()
+            got.append((summary(res), sorted(pipe.seen.keys())))
+    torch.cuda.current_stream().wait_stream(st)
+    assert got == want

@@ -38,6 +38,9 @@ def main():
     out = {"config": f"C2 shape: YOLOv8{args.scale}-seg {H}x{W} {args.dtype}, batch 1, 1 MI355X", "iters": args.iters}
     variants = [("seg_only", lambda: pipe.run_seg_only()),
                 ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS))]
+    # every variant runs on a stream of its own: a graph replayed on the legacy default stream was observed not to
+    # be ordered before the following launches there (tests/test_gpu_graph.py)
+    run_stream = torch.cuda.Stream()
     if args.graph:
         # the frame copy + network + post-processing captured once as a HIP graph (the nav stage reads a device
         # flag on the host per speculative A* round, so it stays eager)
@@ -62,15 +65,17 @@ def main():
         variants += [("seg_post_graph", graph.replay), ("end_to_end_graph", graph_e2e)]
     for name, fn in variants:
         print(name, file=sys.stderr, flush=True)
-        for _ in range(20):
-            fn()
-        torch.cuda.synchronize()
-        ts = []
-        for _ in range(args.iters):
-            t0 = time.perf_counter()
-            fn()
+        run_stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(run_stream):
+            for _ in range(20):
+                fn()
             torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t0)
+            ts = []
+            for _ in range(args.iters):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
         ts = np.array(ts) * 1e3
         out["ndet"] = int(pipe.post.ndet[0])
         out[name] = {"median_ms": round(float(np.median(ts)), 3), "p90_ms": round(float(np.percentile(ts, 90)), 3)}

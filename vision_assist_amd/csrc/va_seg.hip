@@ -2008,21 +2008,36 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
 // planes live in LDS ([4][H*W] x 16 B: 25.6 KiB at 20x20, 100 KiB at 40x40).
 constexpr int SPPF_MAXPIX = 40 * 40;  // 1280-px input -> 40x40 at stride 32
 
-// an order key of a stored value: the value itself, or for an e4m3 byte (sign-magnitude) +-magnitude bits
-__device__ inline float ord_key(float v) { return v; }
-__device__ inline float ord_key(__bf16 v) { return (float)v; }
-__device__ inline float ord_key(uint8_t v) { return (v & 0x80) ? -(float)(v & 0x7F) : (float)v; }
+// e4m3 bytes (sign-magnitude) as order keys, four per word: a positive byte b -> b | 0x80, a negative one -> ~b, so
+// the keys compare as unsigned bytes in the order of the values (-0 just below +0); key_e4m3 undoes it
+__device__ inline unsigned e4m3_key(unsigned w) { return w ^ (0x80808080u | (((w >> 7) & 0x01010101u) * 0x7Fu)); }
+__device__ inline unsigned key_e4m3(unsigned k) { return k ^ (0x80808080u | (((~k >> 7) & 0x01010101u) * 0x7Fu)); }
 
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+// byte-wise unsigned max of two words: even and odd bytes as two packed u16 maxima (v_pk_max_u16)
+__device__ inline unsigned bytemax(unsigned a, unsigned b) {
+    const u16x2 e = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a & 0x00FF00FFu),
+                                              __builtin_bit_cast(u16x2, b & 0x00FF00FFu));
+    const u16x2 o = __builtin_elementwise_max(__builtin_bit_cast(u16x2, (a >> 8) & 0x00FF00FFu),
+                                              __builtin_bit_cast(u16x2, (b >> 8) & 0x00FF00FFu));
+    return __builtin_bit_cast(unsigned, e) | (__builtin_bit_cast(unsigned, o) << 8);
+}
+
+// element-wise max of two 16-byte vectors; uint8_t: e4m3 order keys (see e4m3_key)
 template <typename T>
 __device__ inline u32x4 vmax16(u32x4 a, u32x4 b) {
-    constexpr int E = 16 / sizeof(T);
-    const T* pa = (const T*)&a;
-    const T* pb = (const T*)&b;
-    u32x4 r;
-    T* pr = (T*)&r;
+    if constexpr (sizeof(T) == 1) {
+        return (u32x4){bytemax(a[0], b[0]), bytemax(a[1], b[1]), bytemax(a[2], b[2]), bytemax(a[3], b[3])};
+    } else {
+        constexpr int E = 16 / sizeof(T);
+        const T* pa = (const T*)&a;
+        const T* pb = (const T*)&b;
+        u32x4 r;
+        T* pr = (T*)&r;
 #pragma unroll
-    for (int e = 0; e < E; ++e) pr[e] = ord_key(pa[e]) >= ord_key(pb[e]) ? pa[e] : pb[e];
-    return r;
+        for (int e = 0; e < E; ++e) pr[e] = to_f(pa[e]) >= to_f(pb[e]) ? pa[e] : pb[e];
+        return r;
+    }
 }
 
 // CGW channel groups per workgroup, the group index fastest over the threads: with CGW = 4 (bf16) a
@@ -2038,7 +2053,9 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int H, int W, in
     T* base = buf + (int64_t)n * np * ld + cg0 * CG;
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
         const int p = i / CGW, q = i - p * CGW;
-        sp[i] = *(const u32x4*)(base + (int64_t)p * ld + q * CG);
+        u32x4 v = *(const u32x4*)(base + (int64_t)p * ld + q * CG);
+        if constexpr (sizeof(T) == 1) v = (u32x4){e4m3_key(v[0]), e4m3_key(v[1]), e4m3_key(v[2]), e4m3_key(v[3])};
+        sp[i] = v;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
@@ -2068,6 +2085,7 @@ __global__ __launch_bounds__(256) void sppf_pool_kernel(T* buf, int H, int W, in
                 if (y - d >= 0) m = vmax16<T>(m, pl[(y - d) * W * CGW]);
                 if (y + d < H) m = vmax16<T>(m, pl[(y + d) * W * CGW]);
             }
+            if constexpr (sizeof(T) == 1) m = (u32x4){key_e4m3(m[0]), key_e4m3(m[1]), key_e4m3(m[2]), key_e4m3(m[3])};
             *(u32x4*)(base + (int64_t)p * ld + k * c + q * CG) = m;
         }
     }
