@@ -1835,46 +1835,66 @@ hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
 // ----------------------------------------------------------------------------------------- layer 0, f32
 // Exact-f32 model.0 with the preprocessing folded in (va355.h va_seg_conv0_f32): one output pixel per lane;
 // its 27 inputs (3x3 taps x RGB / 255, zero padding) in registers, every weight a wave-uniform scalar load, so
-// the layer is 27 v_fma per output channel and one 16-byte store per 4 channels -- bound by the f32 output
-// write (128 B per pixel at Cout 32), not by the 8-channel im2col GEMM it replaces.
+// the layer is 27 v_fma per output channel.  The results go through LDS: each lane parks its pixel's NCO floats,
+// then the wave writes its 64 consecutive pixels as whole 16-byte runs by consecutive lanes (a lane storing its
+// own pixel's 128 bytes would put 64 scattered 16-byte pieces in every store instruction) -- the layer is bound
+// by that f32 output write (128 B per pixel at Cout 32).
 template <int NCO>
 __global__ __launch_bounds__(256) void conv0_f32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         float* __restrict__ y, int ldy) {
+    constexpr int RS = NCO + 4;  // LDS row (floats): +4 staggers the 64 rows over the banks
+    __shared__ __align__(16) float stage[4][64 * RS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float* sw = stage[wid];
     const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
     const int64_t total = (int64_t)N * Ho * Wo;
-    for (int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; m < total; m += (int64_t)gridDim.x * blockDim.x) {
-        const int wo = (int)(m % Wo);
-        const int64_t t = m / Wo;
-        const int ho = (int)(t % Ho), n = (int)(t / Ho);
-        float x[27];
+    const int64_t nwave = (int64_t)gridDim.x * 4;
+    for (int64_t m0 = ((int64_t)blockIdx.x * 4 + wid) * 64; m0 < total; m0 += nwave * 64) {  // wave-uniform
+        const int64_t m = m0 + lane;
+        if (m < total) {
+            const int wo = (int)(m % Wo);
+            const int64_t t = m / Wo;
+            const int ho = (int)(t % Ho), n = (int)(t / Ho);
+            float x[27];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-            const int hi = 2 * ho - 1 + ky;
+            for (int ky = 0; ky < 3; ++ky) {
+                const int hi = 2 * ho - 1 + ky;
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const int wi = 2 * wo - 1 + kx;
-                const bool in = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-                const uint8_t* p = frames + (((int64_t)n * H + (in ? hi : 0)) * W + (in ? wi : 0)) * 3;
+                for (int kx = 0; kx < 3; ++kx) {
+                    const int wi = 2 * wo - 1 + kx;
+                    const bool in = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+                    const uint8_t* p = frames + (((int64_t)n * H + (in ? hi : 0)) * W + (in ? wi : 0)) * 3;
 #pragma unroll
-                for (int c = 0; c < 3; ++c)  // R, G, B = bytes 2, 1, 0
-                    x[(ky * 3 + kx) * 3 + c] = in ? (float)p[2 - c] / 255.0f : 0.0f;
+                    for (int c = 0; c < 3; ++c)  // R, G, B = bytes 2, 1, 0
+                        x[(ky * 3 + kx) * 3 + c] = in ? (float)p[2 - c] / 255.0f : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int co = 0; co < NCO; co += 4) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float* wr = w + (co + r) * 27;
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < 27; ++k) acc = fmaf(wr[k], x[k], acc);
+                    v[r] = silu_exact(acc + bias[co + r]);
+                }
+                *(float4*)(sw + lane * RS + co) = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
-        float* out = y + m * ldy;
-#pragma unroll
-        for (int co = 0; co < NCO; co += 4) {
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float* wr = w + (co + r) * 27;
-                float acc = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 27; ++k) acc = fmaf(wr[k], x[k], acc);
-                v[r] = silu_exact(acc + bias[co + r]);
-            }
-            *(float4*)(out + co) = make_float4(v[0], v[1], v[2], v[3]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the wave's 64 pixels x NCO floats: 16-byte run c of pixel p by lane (p * NCO / 4 + c) % 64
+        constexpr int RUNS = NCO / 4;
+        for (int i = lane; i < 64 * RUNS; i += 64) {
+            const int p = i / RUNS, c = i - p * RUNS;
+            if (m0 + p < total) *(float4*)(y + (m0 + p) * ldy + 4 * c) = *(const float4*)(sw + p * RS + 4 * c);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
