@@ -435,10 +435,10 @@ __device__ __forceinline__ void mark_at(uint32_t* img, int ww, int x, int y, boo
 }
 
 // icvFetchContour (CHAIN_APPROX_SIMPLE) from the outer-border start (x0, y0) of the framed image, executed by the
-// whole wave in lock step (every lane the same pixel, scalar state; marks by lane 0).  emit(x, y) gets every kept
-// point in order; mark = whether to write the traced pixels' marks.  Returns the number of points.
-template <typename Emit>
-__device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int y0, bool mark, Emit emit,
+// whole wave in lock step (every lane the same pixel, scalar state).  mark(x, y, right) gets every visit's mark,
+// emit(x, y) every kept point in order.  Returns the number of points.
+template <typename Mark, typename Emit>
+__device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int y0, Mark mark, Emit emit,
                                              int* steps = nullptr) {
     TraceWin w{0ull, 0ull, 0ull, -1, -1};
     win_at(img, ww, x0, y0, w);
@@ -449,7 +449,7 @@ __device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int 
         s = (s - 1) & 7;
     } while (!((nb >> s) & 1) && s != s_end0);
     if (s == s_end0) {  // single pixel domain
-        if (mark) mark_at(img, ww, x0, y0, true);
+        mark(x0, y0, true);
         emit(x0, y0);
         return 1;
     }
@@ -463,7 +463,7 @@ __device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int 
         const unsigned rot = ((nb3 | (nb3 << 8)) >> ((s_end + 1) & 7)) & 0xFFu;
         s = (s_end + 1 + __builtin_ctz(rot)) & 7;
         const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
-        if (mark) mark_at(img, ww, x3, y3, (unsigned)(s - 1) < (unsigned)s_end);
+        mark(x3, y3, (unsigned)(s - 1) < (unsigned)s_end);
         if (s != prev_s) {
             emit(x3, y3);
             ++n;
@@ -477,6 +477,49 @@ __device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int 
         nb3 = win_nbrs(w, x3);
         CT_PROF(if (steps) ++*steps);
     }
+    return n;
+}
+
+// the unmarked form (a contour followed again for its points)
+template <typename Emit>
+__device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int y0, Emit emit) {
+    return follow_border(img, ww, x0, y0, [](int, int, bool) {}, emit);
+}
+
+// The scan's form: marks and points are collected one per lane in registers (lane i takes record i)
+// and written 64 at a time -- a mark is 64 lanes' LDS atomic ORs in one instruction, the points one coalesced
+// store -- instead of a lane-0 atomic and a lane-0 store per step on the trace's critical path (the trace reads
+// only the mask plane, never the marks, so deferring them changes nothing it sees).  Points go to dst[0, capd)
+// as network pixels X | Y << 16.  Returns the number of points.
+template <bool LDS>
+__device__ __forceinline__ int trace_marked(uint32_t* img, int ww, int x0, int y0, uint32_t* dst, int capd, int X0,
+                                            int Y0, int* steps = nullptr) {
+    const int lane = threadIdx.x & 63;
+    int mrec = 0, nm = 0;   // lane i: pending mark i (x | y << 16 | right << 31)
+    int prec = 0, np = 0;   // lane i: pending point i
+    auto flush_marks = [&](int cnt) {
+        if (lane < cnt) {
+            const int x = mrec & 0xFFFF, y = (mrec >> 16) & 0x7FFF;
+            if (CT_OK(x >= 0 && y >= 0 && (x >> 5) < ww, 3, x, y))
+                atomicOr(plane(img, ww, y, mrec < 0 ? 2 : 1) + (x >> 5), 1u << (x & 31));
+        }
+    };
+    auto flush_points = [&](int base, int cnt) {
+        if (lane < cnt && base + lane < capd) dst[base + lane] = (uint32_t)prec;
+    };
+    const int n = follow_border(
+        img, ww, x0, y0,
+        [&](int x, int y, bool right) {
+            if (lane == (nm & 63)) mrec = x | (y << 16) | (right ? (int)0x80000000 : 0);
+            if ((++nm & 63) == 0) flush_marks(64);
+        },
+        [&](int x, int y) {
+            if (lane == (np & 63)) prec = (X0 + x - 1) | ((Y0 + y - 1) << 16);
+            if ((++np & 63) == 0) flush_points(np - 64, 64);
+        },
+        steps);
+    flush_marks(nm & 63);
+    flush_points(np & ~63, np & 63);
     return n;
 }
 
@@ -588,17 +631,9 @@ __device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, cons
                 CT_PROF(++npos);
                 if (prev == 0 && p == 1) {
                     if (uni(val_at<LDS>(img, r.ww, lnbd, y)) <= 0) {
-                        uint32_t* dst = cp + alt * a.sc.capd;
-                        int i = 0;
                         CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
-                        const int n = fetch_contour(
-                            img, r.ww, x, y, true,
-                            [&](int px, int py) {
-                                if (lane == 0 && i < a.sc.capd)
-                                    dst[i] = (uint32_t)(r.X0 + px - 1) | ((uint32_t)(r.Y0 + py - 1) << 16);
-                                ++i;
-                            },
-                            CT_STEPS);
+                        const int n = trace_marked<LDS>(img, r.ww, x, y, cp + alt * a.sc.capd, a.sc.capd, r.X0,
+                                                        r.Y0, CT_STEPS);
                         CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
                         ++ncont;
                         CT_WATCH(3, ncont);
@@ -651,11 +686,11 @@ __device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, cons
             }
         } else {  // longer than the buffer: followed again from the image (marks off)
             int lx = 0, ly = 0;
-            fetch_contour(img, r.ww, bx, by, false, [&](int px, int py) { lx = px, ly = py; });
+            fetch_contour(img, r.ww, bx, by, [&](int px, int py) { lx = px, ly = py; });
             float pxs, pys;
             scale_pt(a.f, r.X0 + lx - 1, r.Y0 + ly - 1, &pxs, &pys);
             int i = 0;
-            fetch_contour(img, r.ww, bx, by, false, [&](int qx, int qy) {
+            fetch_contour(img, r.ww, bx, by, [&](int qx, int qy) {
                 float xs, ys;
                 scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
                 acc += (double)pxs * (double)ys - (double)pys * (double)xs;
@@ -928,7 +963,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                 build_image<false>(s, b, k, r, img, strip, tid, nt, ms);
                 if (tid < 64) {
                     int i = 0;
-                    fetch_contour(img, r.ww, st.ox, st.oy, false, [&](int qx, int qy) {
+                    fetch_contour(img, r.ww, st.ox, st.oy, [&](int qx, int qy) {
                         float xs, ys;
                         scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
                         if (tid == 0 && i < a.sc.cap) {
