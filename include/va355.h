@@ -419,6 +419,19 @@ int va_post_polygons(void* stream, const va_post_args* p, float* polys, int32_t*
  * out[0..n-1]; returns how many. */
 int va_abi_struct_sizes(int64_t* out, int32_t n);
 
+/* Device-bound handle.  va_create binds to HIP device `device` (a gfx950; flags must be 0);
+ * the kernels' own entry points stay stateless.  va_frame runs one batch through the whole hot path on the
+ * handle's device (made current for the call, the caller's restored after it): va_seg_run(ops) ->
+ * va_post_run(post) -> va_nav_run(post->cells, post->rects, post->B, H0, W0, seen, nav_work, rounds) -- the
+ * reference's FrameProcessor.__call__ (FrameProcessor.py:301-360) up to the PathAnalyser, for post->B frames of
+ * H0 x W0 (the frame size the cells and rects are in).  Returns the first failing stage's status. */
+typedef struct va_handle_s* va_handle;
+int va_create(int32_t device, uint32_t flags, va_handle* out);
+int va_destroy(va_handle h);
+int va_handle_device(va_handle h, int32_t* device);
+int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
+             int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds);
+
 /* Library version / build info string. */
 const char* va_version(void);
 

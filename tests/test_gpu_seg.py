@@ -602,16 +602,19 @@ def _m1280_ref():
 
 
 def test_forward_f32_medium_1280_within_1e3():
-    """m@1280 in exact f32: within 1e-3 absolute where |logit| <= 1 and 1e-3 relative above (the headline s@640
-    test holds 1e-3 absolute everywhere; here the DFL box logits reach |r| >> 1, and two fp32 summation orders
-    over K up to 5184 then differ by more than 1e-3 absolute -- measured 1.5e-3 on a box logit)."""
+    """m@1280 in exact f32 against the torch fp32 oracle, relative to the logits' scale: max |gpu - r| <= 1e-5 *
+    max |r|.  The headline s@640 and n@1280 tests hold 1e-3 absolute; here the synthetic m weights drive logits to
+    |r| ~ 290, and at that scale fp32 rounding alone moves results by ~1e-3 absolute in any summation order --
+    measured against a float64 forward of the same weights (tools/save_heads.py): torch fp32 CPU differs from it
+    by 6.9e-4 (box) / 5.5e-4 (cls) / 6.3e-4 (coef) / 3.8e-4 (proto), the GPU by 1.5e-3 / 1.3e-3 / 1.2e-3 / 8.2e-4
+    (5e-6 of the scale), the GPU from fp32 CPU by 1.6e-3."""
     from vision_assist_amd.seg import SegNet
     c = _m1280_ref()
     got = _gpu_heads(SegNet(c["arch"], c["fw"], dtype="f32"), c["frames"])
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, c["ref"]):
         assert g.shape == r.shape, name
-        err = ((g - r).abs() / r.abs().clamp_min(1.0)).max().item()
-        assert err <= 1e-3, f"{name}: max |gpu - torch fp32| / max(1, |r|) = {err}"
+        err = ((g - r).abs().max() / r.abs().max()).item()
+        assert err <= 1e-5, f"{name}: max |gpu - torch fp32| / max |r| = {err}"
 
 
 def test_forward_bf16_medium_1280_close():

@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VA355_LIB") or os.path.join(HERE, "libva355.so")
 
 VA_OK = 0
+VA_ERR_ARG, VA_ERR_HIP, VA_ERR_RANGE = -1, -2, -3
 VA_FRAME_OK, VA_FRAME_EMPTY, VA_FRAME_INDEX_ERROR, VA_FRAME_NO_MASK = 0, 1, 2, 3
 VA_QUERY_NONE, VA_QUERY_FOUND, VA_QUERY_NO_PATH = 0, 1, 2
 VA_CELL_EMPTY, VA_CELL_ARTIFICIAL = 1, 2
@@ -60,6 +61,10 @@ SIGNATURES = [
     ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_conv0_f32", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_conv0_e4m3", I32, [P, P, I32, I32, I32, P, P, I32, P, I32, ctypes.c_float]),
+    ("va_create", I32, [I32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    ("va_destroy", I32, [P]),
+    ("va_handle_device", I32, [P, ctypes.POINTER(ctypes.c_int32)]),
+    ("va_frame", I32, [P, P, P, I32, P, I32, I32, P, P, ctypes.POINTER(ctypes.c_int32)]),
     ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_upsample2x", I32, [P, P, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_run", I32, [P, P, I32]),
@@ -118,3 +123,30 @@ def stream_ptr(stream=None, device=None) -> int:
 def require_gpu() -> None:
     if not torch.cuda.is_available():
         raise VaError("vision_assist_amd needs a ROCm GPU (MI355X); torch.cuda.is_available() is False")
+
+
+class Handle:
+    """A va_create handle bound to one HIP device (va355.h: va_frame runs a whole batch on it)."""
+
+    _by_device: dict = {}
+
+    def __init__(self, device: int):
+        lib = load()
+        h = ctypes.c_void_p()
+        check(lib.va_create(int(device), 0, ctypes.byref(h)), f"va_create({device})")
+        self.ptr, self.device, self._lib = h.value, int(device), lib
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.va_destroy(self.ptr)
+            self.ptr = None
+
+    @classmethod
+    def for_device(cls, device) -> "Handle":
+        """The process's handle for `device` (created on first use)."""
+        d = torch.device(device)
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+        if idx not in cls._by_device:
+            cls._by_device[idx] = cls(idx)
+        return cls._by_device[idx]
+

@@ -1,0 +1,70 @@
+// va_handle.hip -- the device-bound handle of the C ABI (va_create / va_destroy and a fused
+// per-batch entry point, va_frame).  The kernels' entry points are stateless (caller-owned buffers, the stream as
+// an argument); the handle binds a caller to one HIP device -- the library is built for gfx950 only, so
+// va_create refuses any other -- and va_frame runs one batch through the whole hot path (forward -> decode / NMS /
+// contours / mask choice -> grid / penalty / protrusion / A*) on that device in one call, with the device made
+// current for the call and restored after it (a process may drive several GPUs).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/va355.h"
+
+struct va_handle_s {
+    int32_t device;
+    uint32_t flags;
+};
+
+namespace {
+// the handle's device current for the call, the caller's restored after it
+struct DeviceScope {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceScope(int d) {
+        ok = hipGetDevice(&prev) == hipSuccess && hipSetDevice(d) == hipSuccess;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+}  // namespace
+
+extern "C" {
+
+int va_create(int32_t device, uint32_t flags, va_handle* out) {
+    if (!out || flags != 0) return VA_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return VA_ERR_HIP;
+    if (device < 0 || device >= n) return VA_ERR_ARG;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess) return VA_ERR_HIP;
+    if (strncmp(p.gcnArchName, "gfx950", 6) != 0) return VA_ERR_ARG;  // the code objects are gfx950 only
+    *out = new va_handle_s{device, flags};
+    return VA_OK;
+}
+
+int va_destroy(va_handle h) {
+    delete h;
+    return VA_OK;
+}
+
+int va_handle_device(va_handle h, int32_t* device) {
+    if (!h || !device) return VA_ERR_ARG;
+    *device = h->device;
+    return VA_OK;
+}
+
+int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
+             int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds) {
+    if (!h || !ops || nops <= 0 || !post || !post->cells || !post->rects || !seen || !nav_work) return VA_ERR_ARG;
+    DeviceScope scope(h->device);
+    if (!scope.ok) return VA_ERR_HIP;
+    int rc = va_seg_run(stream, ops, nops);
+    if (rc != VA_OK) return rc;
+    rc = va_post_run(stream, post);
+    if (rc != VA_OK) return rc;
+    return va_nav_run(stream, post->cells, post->rects, post->B, H0, W0, seen, nav_work, rounds);
+}
+
+}  // extern "C"

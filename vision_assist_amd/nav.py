@@ -162,8 +162,8 @@ class NavEngine:
     def LC(self):
         return self.dims.LC
 
-    def run(self, cells: torch.Tensor, rects: torch.Tensor, seen: AngleSeen, stream=None) -> NavBatch:
-        """cells: uint8 [B, H/20, W/20] (device), rects: int32 [B, 4] (device)."""
+    def check_inputs(self, cells: torch.Tensor, rects: torch.Tensor) -> int:
+        """Validates cells uint8 [B, H/20, W/20] / rects int32 [B, 4]; -> B."""
         B = cells.shape[0]
         d = self.dims
         if B > self.max_batch:
@@ -172,13 +172,24 @@ class NavEngine:
             raise _lib.VaError(f"cells must be contiguous uint8 [B, {d.LR}, {d.LC}], got {tuple(cells.shape)}")
         if tuple(rects.shape) != (B, 4) or rects.dtype != torch.int32 or not rects.is_contiguous():
             raise _lib.VaError("rects must be contiguous int32 [B, 4]")
+        return B
+
+    def batch(self, B: int, rounds: int, stream=None) -> NavBatch:
+        """The records of the va_nav_run just enqueued on `stream` (frame records, then query records)."""
+        d = self.dims
+        return NavBatch(self, B, rounds, (B * d.frame_bytes + 15) & ~15, stream)
+
+    def run(self, cells: torch.Tensor, rects: torch.Tensor, seen: AngleSeen, stream=None) -> NavBatch:
+        """cells: uint8 [B, H/20, W/20] (device), rects: int32 [B, 4] (device)."""
+        B = self.check_inputs(cells, rects)
+        d = self.dims
         rounds = ctypes.c_int32(0)
         with torch.cuda.device(self.device):
             _lib.check(self.lib.va_nav_run(_lib.stream_ptr(stream, self.device), cells.data_ptr(), rects.data_ptr(),
                                            B, d.H, d.W, seen.t.data_ptr(), self.work.data_ptr(), ctypes.byref(rounds)),
                        "va_nav_run")
             # frame records then query records (16-byte aligned): va_nav.hip work_bytes()
-            return NavBatch(self, B, rounds.value, (B * d.frame_bytes + 15) & ~15, stream)
+            return self.batch(B, rounds.value, stream)
 
     def sample_cells(self, masks: torch.Tensor, stream=None) -> torch.Tensor:
         """Lattice samples of filled masks uint8 [B, H, W] (FrameProcessor.py:88-97)."""

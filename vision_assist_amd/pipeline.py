@@ -11,6 +11,8 @@ cache (the batch gives exactly the sequential result, see va_nav.hip).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -73,14 +75,22 @@ class FramePipeline:
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:
+        """One batch through the whole path: frames in, then ONE va_frame call on the device's handle (forward,
+        post-processing and mask choice, grid / penalty / protrusion / A*)."""
         if frames is not None:
             self.load(frames, stream)
-        self.seg.run_plan(self.plan, stream)
         out = self.plan["out"]
         if plant_mode != PLANT_NEVER and plant_cells is None:
             raise ValueError("plant_mode needs plant_cells / plant_rects")
-        self.post.run(out.levels, out.proto, plant_cells, plant_rects, plant_mode, select=True, stream=stream)
-        return self.nav.run(self.post.cells, self.post.rects, self.seen, stream)
+        a = self.post.args(out.levels, out.proto, plant_cells, plant_rects, plant_mode, select=True)
+        B = self.nav.check_inputs(self.post.cells, self.post.rects)
+        rounds = ctypes.c_int32(0)
+        h = _lib.Handle.for_device(self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_frame(h.ptr, _lib.stream_ptr(stream, self.device), self.plan["ops"], self.plan["n"],
+                                         ctypes.byref(a), self.H, self.W, self.seen.t.data_ptr(),
+                                         self.nav.work.data_ptr(), ctypes.byref(rounds)), "va_frame")
+        return self.nav.batch(B, rounds.value, stream)
 
     def run_seg_only(self, stream=None) -> None:
         self.seg.run_plan(self.plan, stream)

@@ -122,6 +122,13 @@ class PostEngine:
 
     def run(self, levels, proto, plant_cells=None, plant_rects=None, plant_mode=PLANT_NEVER, select=True,
             stream=None) -> None:
+        a = self.args(levels, proto, plant_cells, plant_rects, plant_mode, select)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream, self.device), ctypes.byref(a)), "va_post_run")
+
+    def args(self, levels, proto, plant_cells=None, plant_rects=None, plant_mode=PLANT_NEVER,
+             select=True) -> "PostArgs":
+        """The va_post_args of a run on these network outputs (also kept for polygons())."""
         a = PostArgs()
         for i in range(3):
             a.levels[i] = levels[i].data_ptr()
@@ -136,9 +143,8 @@ class PostEngine:
         if select:
             a.cells, a.rects, a.chosen = self.cells.data_ptr(), self.rects.data_ptr(), self.chosen.data_ptr()
         self._fill_frame_args(a)
-        with torch.cuda.device(self.device):
-            _lib.check(self.lib.va_post_run(_lib.stream_ptr(stream, self.device), ctypes.byref(a)), "va_post_run")
         self._last = (a, levels, proto)  # Results.masks.xy re-reads these buffers (polygons())
+        return a
 
     def _fill_frame_args(self, a: PostArgs) -> None:
         if self.frame:
