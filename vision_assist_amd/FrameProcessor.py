@@ -10,8 +10,8 @@
 grid build, penalties, protrusions, start/end selection and A* as one device
 pipeline (vision_assist_amd.pipeline), copies one frame record back and hands
 the unique paths to PathAnalyser.  Same return values: the answer string, ``[]``
-when no grid was built (:328-332), ``(frame, answer)`` in debug mode (debug
-drawing needs OpenCV and is out of scope: the frame is returned undrawn).  The
+when no grid was built (:328-332), ``(frame, answer)`` in debug mode (the frame drawn as the reference draws it:
+penalty-coloured grids, then the paths -- vision_assist_amd.PathVisualiser).  The
 reference's IndexError on masks confined to the last rows is
 raised the same way.
 
@@ -35,6 +35,7 @@ from .config import grid_size
 from .models import Coordinate, Grid, Path
 from .PathAnalyser import path_analyser
 from .PathFinder import path_finder
+from .PathVisualiser import fill_square, path_visualiser
 from .PenaltyCalculator import penalty_calculator
 from .ProtrusionDetector import ProtrusionDetector
 from .utils import get_closest_grid_to_point
@@ -358,7 +359,23 @@ class FrameProcessor:
         self.protrusion_detector.frames_processed += 1
         final_answer = path_analyser(H, W, paths)
         if self.debug:
+            if isinstance(self.frame, torch.Tensor):
+                self.frame = self.frame.cpu().numpy()
+            self._draw_non_path_grids()
+            self.frame = path_visualiser(self.frame, paths)
             return self.frame, final_answer
         return final_answer
+
+    # ------- debug drawing (FrameProcessor.py:273-299; PathVisualiser.py) -------
+    def _draw_grid(self, grid, color) -> None:
+        fill_square(self.frame, grid.coords.x, grid.coords.y, color)
+
+    def _draw_non_path_grids(self) -> None:
+        """Every non-empty grid of self.grids in its penalty colour (the reference's path-grid set is empty)."""
+        for grid_row in self.grids:
+            for grid in grid_row:
+                if grid.empty:
+                    continue
+                self._draw_grid(grid, penalty_calculator.get_penalty_colour(grid.penalty or 0))
 
     process = __call__  # the name BASELINE.json's north_star uses
