@@ -549,7 +549,39 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 // UP (FK, 1x1 only): input channels [0, a.cu) come from the half-resolution slice a.xu at (h/2, w/2) -- the
 // FPN's Upsample + Concat read in place (va355.h va_conv_args.xu); a K-step is one 64-channel chunk, so
 // the source is a wave-uniform choice per K-step.
-template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false>
+// f32 as three bf16 terms: h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (round to nearest even, two elements
+// per v_cvt_pk_bf16_f32), x = h + m + l EXACTLY: x - h is a multiple of x's ulp below half of h's bf16 ulp (<= 16
+// significant bits, an exact f32 subtraction), likewise (x - h) - m (<= 8 bits, so l is exact in bf16).  Elements
+// 0-3 come from c0, 4-7 from c1 -- the same order for both MFMA operands, so the K pairing is kept.
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+__device__ __forceinline__ unsigned cvt_pk_bf16(f32x2 v) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpk_bf16(unsigned p) {
+    return (f32x2){__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3_bf16(const u32x4& c0, const u32x4& c1, bf16x8 (&t)[3]) {
+    unsigned w[3][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const u32x4& c = e < 2 ? c0 : c1;
+        const f32x2 x = {__uint_as_float(c[2 * (e & 1)]), __uint_as_float(c[2 * (e & 1) + 1])};
+        w[0][e] = cvt_pk_bf16(x);
+        const f32x2 r = x - unpk_bf16(w[0][e]);
+        w[1][e] = cvt_pk_bf16(r);
+        w[2][e] = cvt_pk_bf16(r - unpk_bf16(w[1][e]));
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = __builtin_bit_cast(bf16x8, (u32x4){w[k][0], w[k][1], w[k][2], w[k][3]});
+}
+
+// SPL (T = float only): 0 = exact f32 MFMA (v_mfma_f32_16x16x4_f32, 32 cycles per SIMD); 6 or 9 = the f32
+// operands split into three exact bf16 terms (split3_bf16) and multiplied on v_mfma_f32_16x16x32_bf16 (16 cycles
+// per SIMD, 8x the K per instruction): the term products h.h, h.m, m.h, h.l, m.m, l.h (+ m.l, l.m, l.l for 9) are
+// exact in f32 and accumulated in f32; the three left out at 6 are <= 2^-23 of |a b| together, below one f32
+// rounding of the sum.
+template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false,
+          int SPL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
     using Cfg = Conv2Cfg<T, WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
@@ -770,6 +802,24 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                                                                                127);
                 }
             }
+        } else if constexpr (SPL > 0) {
+            static_assert(SPL == 6 || SPL == 9, "term count");
+            // the lane's 8 f32 of a row (chunks fq and 4 + fq) as one 8-deep bf16 operand per term: a 32-deep
+            // K-step is one 16x16x32 MFMA per term pair
+            bf16x8 at[TNS][3], bt[4][3];
+#pragma unroll
+            for (int i = 0; i < TNS; ++i) split3_bf16(af[0][i], af[1][i], at[i]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) split3_bf16(bfr[0][j], bfr[1][j], bt[j]);
+            constexpr int TA[9] = {0, 0, 1, 0, 1, 2, 1, 2, 2}, TB[9] = {0, 1, 0, 2, 1, 0, 2, 1, 2};
+#pragma unroll
+            for (int t = 0; t < SPL; ++t)
+#pragma unroll
+                for (int i = 0; i < TNS; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i][TA[t]], bt[j][TB[t]], acc[i][j], 0,
+                                                                            0, 0);
         } else {
             // f32: element e of lane (fr, fq)'s chunk 4 kh + fq is K index 16 kh + 4 fq + e of the stage -- MFMA
             // (kh, e) sums over fq, so the four MFMAs of a chunk cover its 16 K values (the same permutation of
@@ -2155,7 +2205,7 @@ bool getenv_glds() {
     return v == 1;
 }
 
-template <int WM, int WN, int TNS, typename OutT, typename T = __bf16>
+template <int WM, int WN, int TNS, typename OutT, typename T = __bf16, int SPL = 0>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     using Cfg = Conv2Cfg<T, WM, WN, TNS>;
     constexpr int VEC = Cfg::VEC, KS = Cfg::KS;
@@ -2164,20 +2214,20 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
     const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
     if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st,
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st,
                            a, ntn, ntiles);
         return hipGetLastError();
     }
     if (getenv_glds() && a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true>), dim3(ntiles), dim3(Cfg::NT), 0, st,
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st,
                                a, ntn, ntiles);
         else
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
                                ntiles);
     }
     else
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
     return hipGetLastError();
 }
 
@@ -2346,6 +2396,22 @@ bool getenv_dn() {
     return v == 1;
 }
 
+// f32 mode's MFMA form (conv2_kernel SPL): VA_F32_SPLIT = 0 (exact f32 MFMA), 6 (default) or 9 bf16 term
+// products; read per launch (A/B timing)
+int f32_split() {
+    const char* e = getenv("VA_F32_SPLIT");
+    if (!e) return 6;
+    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
+}
+
+template <int SPL, typename OutT>
+hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
+    if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
+    if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float, SPL>(a, st);
+    if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float, SPL>(a, st);
+    return launch_conv2<2, 2, 4, OutT, float, SPL>(a, st);
+}
+
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2 && sizeof(OutT) == 2) {
@@ -2407,10 +2473,11 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         // conv_kernel (A/B timing)
         if (a.Kpad % 32 == 0 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && (a.mode != 1 || (a.Cout / 4) % 4 == 0) &&
             getenv("VA_CONV_F32_OLD") == nullptr) {
-            if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float>(a, st) : hipErrorInvalidValue;
-            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float>(a, st);
-            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float>(a, st);
-            return launch_conv2<2, 2, 4, OutT, float>(a, st);
+            switch (f32_split()) {
+                case 6: return launch_conv2_f32<6, OutT>(a, st);
+                case 9: return launch_conv2_f32<9, OutT>(a, st);
+                default: return launch_conv2_f32<0, OutT>(a, st);
+            }
         }
     }
     // tile choice: small Cout -> tall pixel tiles
