@@ -8,7 +8,7 @@ shift
 BARGS="$*"
 SQ="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 exec tools/gpu_steps.sh "$OUT" \
-  "300:trace:rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --extras none $BARGS" \
+  "300:trace:rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --extras none --no-ingest $BARGS" \
   "180:fetch:rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --extras none $BARGS" \
   "180:write:rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --extras none $BARGS" \
   "120:sq_f32:rocprofv3 --pmc $SQ --output-format csv -d $OUT/sq_f32 -o run -- python3 tools/pmc_forward.py --dtype f32 --out $OUT/plan_f32" \

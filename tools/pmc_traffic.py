@@ -67,16 +67,17 @@ def agree(trace: str, bench_json: str, out: str, per_fwd: int = 55) -> dict:
         b = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
     steps, warm = b["steps"], b["warmup"]
     timed = fwd[warm:warm + steps]
-    iso = fwd[warm + steps:]
+    iso = fwd[warm + steps:warm + steps + 3]  # bench.py's 3 isolated forwards (an ingest pass may follow them)
     rl = b["roofline"]
     res = {"conv_launches_per_forward": per_fwd, "forwards_in_trace": nf,
            "rocprof_avg_us_per_forward_in_launch_order": [round(x, 1) for x in fwd],
            f"rocprof_avg_us_timed_forwards({warm}..{warm + steps - 1})": round(sum(timed) / max(len(timed), 1), 1),
            "rocprof_avg_us_isolated_forwards": round(sum(iso) / max(len(iso), 1), 1),
-           "bench_avg_launch_us(events, sampled timed forwards)": rl["avg_launch_us"],
+           "bench_avg_launch_us(events, isolated forwards)": rl["avg_launch_us"],
            "bench_isolated_avg_launch_us": rl.get("isolated_avg_launch_us"),
            "note": "forwards 0..warmup-1 warm-up; then the timed region (two network streams overlapping); "
-                   "the tail = the isolated forwards bench.py runs after the timed region; B = "
+                   "then the 3 isolated forwards bench.py runs after the timed region (the roofline's timing), then the "
+                   "ingest pass if any; B = "
                    f"{b['config']['batch_per_gpu']}"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
