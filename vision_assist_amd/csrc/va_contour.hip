@@ -594,63 +594,78 @@ __device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, cons
         CT_WATCH(2, y);
         if (!row_has_start<LDS>(img, r.ww, y)) continue;
         CT_PROF(++nrows);
-        // OpenCV's skip loop visits the positions whose value differs from their left neighbour's (the
-        // scan's prev is always the value at x - 1): per 2048-pixel chunk each lane holds its word's change
-        // flags and value planes, and the positions are taken in order from registers; a trace changes marks,
-        // so the chunk is re-read after one
+        // OpenCV's skip loop, evaluated a 2048-pixel chunk at a time instead of position by position (the scan's
+        // prev is always the value at x - 1, so its stops are the change positions of the current image).  Between
+        // two traces nothing changes the image, so the scan's decisions over a chunk follow from the chunk alone
+        // and the sign of row[lnbd] carried in: a stop x is an outer-border candidate when row[x - 1] == 0 and
+        // row[x] == 1, traced when the last lnbd event before it -- a stop on a mark (lnbd = x), or a hole start
+        // after a mark (row[x] == 0, lnbd = x - 1) -- left a non-positive row[lnbd] (marks only grow, 2 -> -126,
+        // and a -126 or zero pixel never changes again).  The first traced candidate is taken (every lane finds
+        // its word's first by the events below it and the sign carried in from the lanes to its left), then the
+        // chunk is re-read from x + 1 with row[lnbd] <= 0 (a traced start does not move lnbd).
         const uint32_t* nzr = plane(img, r.ww, y, 0);
         const uint32_t* nr = plane(img, r.ww, y, 1);
         const uint32_t* rr = plane(img, r.ww, y, 2);
-        int prev = 0, lnbd = 0;
+        bool lpos = false;  // row[lnbd] > 0 (lnbd starts on the frame: 0)
         for (int w0 = 0; w0 < r.ww; w0 += 64) {
             const int wi = w0 + lane;
-            uint32_t chi = 0u, clo = 0u, dm = 0u;
-            auto load = [&](int from) {  // value planes + change flags at positions >= from
-                uint32_t phi = 0u, plo = 0u;
-                chi = clo = 0u;
+            int from = 32 * w0;
+            while (true) {
+                CT_PROF(++npos);
+                uint32_t chi = 0u, clo = 0u, phi = 0u, plo = 0u;
                 if (wi < r.ww) code_planes(nzr[wi], ldm<LDS>(nr + wi), ldm<LDS>(rr + wi), chi, clo);
                 if (wi >= 1 && wi <= r.ww)
                     code_planes(nzr[wi - 1], ldm<LDS>(nr + wi - 1), ldm<LDS>(rr + wi - 1), phi, plo);
-                dm = (chi ^ ((chi << 1) | (phi >> 31))) | (clo ^ ((clo << 1) | (plo >> 31)));
+                // bit j of a word = pixel 32 wi + j; "shifted" = the pixel to its left
+                const uint32_t shi = (chi << 1) | (phi >> 31), slo = (clo << 1) | (plo >> 31);
+                uint32_t live = 0u;  // positions >= from of this word
                 const int fw = from >> 5;
-                if (wi < fw || wi >= r.ww) dm = 0u;
-                else if (wi == fw) dm &= ~0u << (from & 31);
-            };
-            load(0);
-            while (true) {
-                const unsigned long long bal = __ballot(dm != 0u);
-                if (!bal) break;
-                const int l = __builtin_ctzll(bal);
-                const uint32_t dl = (uint32_t)__builtin_amdgcn_readlane((int)dm, l);
-                const int j = __builtin_ctz(dl);
-                const int x = 32 * (w0 + l) + j;
-                const uint32_t vh = ((uint32_t)__builtin_amdgcn_readlane((int)chi, l) >> j) & 1u;
-                const uint32_t vl = ((uint32_t)__builtin_amdgcn_readlane((int)clo, l) >> j) & 1u;
-                const int p = vh ? (vl ? -126 : 2) : (int)vl;
-                if (lane == l) dm &= ~(1u << j);
-                CT_PROF(++npos);
-                if (prev == 0 && p == 1) {
-                    if (uni(val_at<LDS>(img, r.ww, lnbd, y)) <= 0) {
-                        CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
-                        const int n = trace_marked<LDS>(img, r.ww, x, y, cp + alt * a.sc.capd, a.sc.capd, r.X0,
-                                                        r.Y0, CT_STEPS);
-                        CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
-                        ++ncont;
-                        CT_WATCH(3, ncont);
-                        if (n > best_n) {
-                            best_n = n, best_half = alt, bx = x, by = y;
-                            alt ^= 1;
-                        }
-                        if constexpr (!LDS) __threadfence();  // the marks before the scan reads on
-                        prev = uni(val_at<LDS>(img, r.ww, x, y));
-                        load(x + 1);
-                        continue;
+                if (wi < r.ww && wi >= fw) live = wi == fw ? ~0u << (from & 31) : ~0u;
+                const uint32_t stop = ((chi ^ shi) | (clo ^ slo)) & live;
+                const uint32_t cand = stop & ~chi & clo & ~shi & ~slo;          // 0 -> 1 (unmarked)
+                const uint32_t evA = stop & chi;                                  // a stop on a mark
+                const uint32_t evB = stop & ~chi & ~clo & shi;                    // 0 after a mark
+                const uint32_t ev = evA | evB;
+                const uint32_t evpos = (evA & ~clo) | (evB & ~slo);               // row[lnbd] == 2 after it
+                // the sign carried into this word: the last event of the lanes to the left, else the chunk's
+                const unsigned long long hasb = __ballot(ev != 0u);
+                const int topb = ev ? 31 - __builtin_clz(ev) : 0;
+                const int lastpos = (int)((evpos >> topb) & 1u);
+                const unsigned long long below = hasb & ((1ull << lane) - 1ull);
+                const int src = below ? 63 - __builtin_clzll(below) : lane;
+                const int fromleft = __shfl(lastpos, src);
+                const bool cin = below ? fromleft != 0 : lpos;
+                // this word's first candidate whose last event below it (or cin) leaves row[lnbd] <= 0
+                int okbit = -1;
+                for (uint32_t c = cand; c; c &= c - 1u) {
+                    const int j = __builtin_ctz(c);
+                    const uint32_t eb = ev & ((1u << j) - 1u);
+                    const bool pos = eb ? ((evpos >> (31 - __builtin_clz(eb))) & 1u) != 0u : cin;
+                    if (!pos) {
+                        okbit = j;
+                        break;
                     }
-                } else if (p == 0 && prev >= 1) {
-                    if (prev & -2) lnbd = x - 1;
                 }
-                prev = p;
-                if (p & -2) lnbd = x;
+                const unsigned long long okb = __ballot(okbit >= 0);
+                if (!okb) {  // no trace in the rest of the chunk: carry the last event's sign on
+                    if (hasb) lpos = __builtin_amdgcn_readlane(lastpos, 63 - __builtin_clzll(hasb)) != 0;
+                    break;
+                }
+                const int l = __builtin_ctzll(okb);
+                const int x = 32 * (w0 + l) + __builtin_amdgcn_readlane(okbit, l);
+                CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
+                const int n = trace_marked<LDS>(img, r.ww, x, y, cp + alt * a.sc.capd, a.sc.capd, r.X0, r.Y0,
+                                                CT_STEPS);
+                CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
+                ++ncont;
+                CT_WATCH(3, ncont);
+                if (n > best_n) {
+                    best_n = n, best_half = alt, bx = x, by = y;
+                    alt ^= 1;
+                }
+                if constexpr (!LDS) __threadfence();  // the marks before the scan reads on
+                lpos = false;
+                from = x + 1;
             }
         }
     }
