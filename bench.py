@@ -65,11 +65,12 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="frames per step per GPU (0 = the dtype's default)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
-    p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense"])
-    p.add_argument("--extras", default="bf16,dense,c5",
+    p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense", "dense_box"])
+    p.add_argument("--extras", default="bf16,dense,dense_box,c5",
                    help="comma list of extra measurements in the same run: bf16 (the bf16 MFMA pipeline), "
-                        "dense (300 detections per frame), c5 (YOLOv8m-seg 1280 on fp8 MFMA, batch 8); "
-                        "'none' to skip")
+                        "dense (300 detections per frame, the random weights' noise masks), dense_box (300 "
+                        "detections per frame with solid box masks, one contour each, as a trained model's compact "
+                        "masks), c5 (YOLOv8m-seg 1280 on fp8 MFMA, batch 8); 'none' to skip")
     p.add_argument("--cpu-sample", type=int, default=256,
                    help="frames timed for the CPU baseline (0 = skip; 256 = ~10-20 s)")
     p.add_argument("--no-prof", action="store_true", help="skip the HIP-event timing of the isolated forwards")
@@ -164,9 +165,10 @@ class Run:
         from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
         self.args, self.dtype, self.B, self.regime = args, dtype, B, regime
         self.scale, self.res = scale or args.scale, res or args.res
-        cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0}[regime]
+        cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0, "dense_box": 4.0}[regime]
         self.arch = Arch(self.scale)
-        self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, cls_bias=cls_bias))
+        self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, cls_bias=cls_bias,
+                                                       solid_masks=regime == "dense_box"))
         H = W = self.res
         self.overlap = not args.no_overlap
         if self.overlap:
@@ -362,8 +364,8 @@ def main():
     for ex in [e for e in args.extras.split(",") if e and e != "none"]:
         if ex == "bf16" and args.dtype != "bf16":
             dt_, B_, reg_ = "bf16", args.batch or DEFAULT_BATCH["bf16"], args.regime
-        elif ex == "dense" and args.regime != "dense":
-            dt_, B_, reg_ = args.dtype, B, "dense"
+        elif ex in ("dense", "dense_box") and args.regime != ex:
+            dt_, B_, reg_ = args.dtype, B, ex
         elif ex == "c5" and not (args.scale == "m" and args.res == 1280 and args.dtype == "fp8"):
             dt_, B_, reg_ = "fp8", DEFAULT_BATCH["fp8"], args.regime
         else:

@@ -30,7 +30,8 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 B = 4
-BF16_FLOOR = {"mid": {"chosen": 0.5, "paths": 0.5}, "dense": {"chosen": 0.0, "paths": 0.0}}
+BF16_FLOOR = {"mid": {"chosen": 0.5, "paths": 0.5}, "dense": {"chosen": 0.0, "paths": 0.0},
+              "dense_box": {"chosen": 0.5, "paths": 0.5}}
 _RESULTS = {}
 
 
@@ -50,10 +51,10 @@ def _match(g, r, tol_box=1e-2, tol_score=1e-4):
     return pairs, [i for i in range(g.shape[0]) if i not in pairs], [j for j in range(r.shape[0]) if j not in used]
 
 
-def _weights(cls_bias):
+def _weights(cls_bias, solid_masks=False):
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
     arch = Arch("s")
-    return arch, fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=cls_bias))
+    return arch, fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=cls_bias, solid_masks=solid_masks))
 
 
 def _frames(seed):
@@ -65,7 +66,7 @@ _ORACLE = {}
 
 def _oracle_chain(regime, cls_bias):
     if regime not in _ORACLE:
-        arch, fw = _weights(cls_bias)
+        arch, fw = _weights(cls_bias, solid_masks=regime == "dense_box")
         frames = _frames(21)
         pf = onav.PathFinderOracle()
         out = []
@@ -85,7 +86,7 @@ def _oracle_chain(regime, cls_bias):
     return _ORACLE[regime]
 
 
-@pytest.mark.parametrize("regime,cls_bias", [("mid", 0.0), ("dense", 4.0)])
+@pytest.mark.parametrize("regime,cls_bias", [("mid", 0.0), ("dense", 4.0), ("dense_box", 4.0)])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_chain_vs_fp32_oracle(dtype, regime, cls_bias):
     from vision_assist_amd.pipeline import FramePipeline

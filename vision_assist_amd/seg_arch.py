@@ -165,11 +165,14 @@ def learnable_params(arch: Arch) -> int:
     return n
 
 
-def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = None) -> dict:
+def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = None, solid_masks: bool = False) -> dict:
     """Seeded synthetic weights in Ultralytics state-dict layout (fp32, CPU).
 
     cls_bias: None -> Ultralytics' prior (Detect.bias_init: log(5 / nc / (640 / stride)^2));
-    a number -> every class bias set to it (the 'dense' regime uses +4)."""
+    a number -> every class bias set to it (the 'dense' regime uses +4).
+    solid_masks: the prototypes made constant (proto.cv3's BN scale 0: channel 0 = SiLU(3), the others SiLU(0) = 0)
+    and mask coefficient 0 fixed at +5, so every instance mask is its whole box -- one compact blob per detection,
+    as a trained model's masks are, instead of the random weights' noise (the 'dense_box' regime)."""
     sd = {}
     for idx, (prefix, kind, ci, co, k) in enumerate(arch.conv_specs()):
         g = torch.Generator().manual_seed(seed * 100003 + idx)
@@ -198,6 +201,16 @@ def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = Non
             else:
                 b = torch.randn(co, generator=g) * 0.1
             sd[f"{prefix}.bias"] = b
+    if solid_masks:
+        p = "model.22.proto.cv3"
+        sd[f"{p}.bn.weight"] = torch.zeros_like(sd[f"{p}.bn.weight"])
+        beta = torch.zeros_like(sd[f"{p}.bn.bias"])
+        beta[0] = 3.0
+        sd[f"{p}.bn.bias"] = beta
+        for lvl in range(3):
+            q = f"model.22.cv4.{lvl}.2"
+            sd[f"{q}.weight"][0].zero_()
+            sd[f"{q}.bias"][0] = 5.0
     return sd
 
 
