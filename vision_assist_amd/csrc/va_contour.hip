@@ -541,6 +541,7 @@ struct CtArgs {
     int32_t* poly_n;
     int poly_cap;
     int gate;                 // pool kernel: hold new claims while a wave waits for pages
+    int64_t pool_max;         // bytes: larger images go to the global-memory form
 };
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -778,7 +779,7 @@ __global__ __launch_bounds__(CP_THREADS) void post_contour_pool_kernel(CtArgs a)
             if (k < uni(s.ndet[b])) {
                 r = uni_region(region_of(s, b, k));
                 if (r.w <= 0) contour_empty(a, b, k, r);
-                else run_it = region_need(s, r) <= CP_POOL;  // else the global kernel's
+                else run_it = region_need(s, r) <= a.pool_max;  // else the global kernel's
             }
         }
         if (run_it) {
@@ -838,7 +839,7 @@ __global__ __launch_bounds__(CT_THREADS) void post_contour_global_kernel(CtArgs 
         const int b = item / a.max_det, k = item % a.max_det;
         if (k >= uni(s.ndet[b])) continue;
         const Region r = uni_region(region_of(s, b, k));
-        if (r.w <= 0 || region_need(s, r) <= CP_POOL) continue;
+        if (r.w <= 0 || region_need(s, r) <= a.pool_max) continue;
         contour_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, item);
         __syncthreads();  // the slot is reused by the next item
     }
@@ -1166,6 +1167,9 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     ca.poly_cap = poly_cap;
     static const int gate_env = getenv("VA_CT_GATE") ? atoi(getenv("VA_CT_GATE")) : 1;  // A/B knob
     ca.gate = gate_env;
+    // images needing more than VA_CT_POOL_PAGES pages (default all 32) run in global memory (A/B knob)
+    static const int pool_pages = getenv("VA_CT_POOL_PAGES") ? atoi(getenv("VA_CT_POOL_PAGES")) : CP_PAGES;
+    ca.pool_max = (int64_t)(pool_pages < CP_PAGES ? pool_pages : CP_PAGES) * CP_PAGE;
     const int64_t items = (int64_t)src.B * max_det;
     static DevVal<int> n_cu;  // per device: one pool block per CU
     if (n_cu() <= 0) {

@@ -7,6 +7,7 @@ reading the head buffers ``SegNet`` produced (no copies) and writing the
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -49,7 +50,7 @@ class MaskSelectArgs(ctypes.Structure):  # va_mask_select_args
 
 CSTAT_DTYPE = [("npts", "<i4"), ("ox", "<i4"), ("oy", "<i4"), ("ncont", "<i4"), ("X0", "<i4"), ("Y0", "<i4"),
                ("status", "<i4"), ("half", "<i4"), ("area", "<f8")]
-CONTOUR_SLOTS = 1024   # contour scratch slots: one wave each, 4 per CU
+CONTOUR_SLOTS = int(os.environ.get("VA_CT_SLOTS", "1024"))  # contour scratch slots: one wave each, 4 per CU
 CONTOUR_CAP = 16384    # points of the chosen contour per frame (the fill kernel's buffer)
 CONTOUR_PTS = 1024     # points kept per instance and buffer half (va_post_args.cpts_cap); longer: followed again
 
