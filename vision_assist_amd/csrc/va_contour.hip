@@ -330,17 +330,30 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
         // eight lanes per low-res pixel (its 128 bytes of proto in one coalesced run): lane q's partial sum of 4
         // channels, then the pairwise tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) by xor shuffles --
         // post-processing's 8-lane dot (same order, same result)
-        const int npx = (s1 - s0 + 1) * tw;
+        // (four pixels' loads in flight per lane before the first is used: the strip is latency-bound on them)
+        const int npx = (s1 - s0 + 1) * tw, ntot = npx * 8;
 #pragma unroll 1
-        for (int i = tid; i < npx * 8; i += nt) {  // whole 8-lane groups are active together
-            const int px = i >> 3;
-            const int y = s0 + px / tw, x = r.rx0 + px % tw;
-            const float4 v = ((const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC))[tid & 7];
-            float part = (cq.x * v.x + cq.y * v.y) + (cq.z * v.z + cq.w * v.w);
-            part += __shfl_xor(part, 1);
-            part += __shfl_xor(part, 2);
-            part += __shfl_xor(part, 4);
-            if ((tid & 7) == 0) strip[px] = part;
+        for (int i0 = tid; i0 < ntot; i0 += 4 * nt) {  // whole 8-lane groups are active together
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * nt, px = i >> 3;
+                if (i < ntot) {
+                    const int y = s0 + px / tw, x = r.rx0 + px % tw;
+                    v[u] = ((const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC))[tid & 7];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * nt;
+                if (i < ntot) {
+                    float part = (cq.x * v[u].x + cq.y * v[u].y) + (cq.z * v[u].z + cq.w * v[u].w);
+                    part += __shfl_xor(part, 1);
+                    part += __shfl_xor(part, 2);
+                    part += __shfl_xor(part, 4);
+                    if ((tid & 7) == 0) strip[i >> 3] = part;
+                }
+            }
         }
         ct_sync<WAVE>();
         // the rows whose taps inside the window all lie in s0 .. s1 (taps are non-decreasing in the row)
