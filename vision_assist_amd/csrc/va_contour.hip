@@ -366,27 +366,27 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
             if (hi > s1) break;
             ++end;
         }
-        auto val = [&](int yy, int xx) -> float {
-            if (xx < r.rx0 || xx > r.rx1 || yy < r.ry0 || yy > r.ry1) return 0.f;
-            const int li = (yy - s0) * tw + (xx - r.rx0);
-            if (!CT_OK(li >= 0 && li < CT_STRIP, 7, li, tw)) return 0.f;
-            return strip[li];
-        };
 #pragma unroll 1
         for (int i = tid; i < (end - next) * r.ww; i += nt) {
             const int yy = next + i / r.ww, x32 = 32 * (i % r.ww);
             int ya, yb;
             float wy0, wy1;
             taps(r.Y0 + yy - 1, sy, s.mh, &ya, &yb, &wy0, &wy1);
+            // val() per tap, its row tests hoisted out of the pixel loop: a tap outside the window reads 0
+            const bool oka = ya >= r.ry0 && ya <= r.ry1, okb = yb >= r.ry0 && yb <= r.ry1;
+            const int la = (ya - s0) * tw - r.rx0, lb = (yb - s0) * tw - r.rx0;
+            if (!CT_OK(!oka || (la + r.rx0 >= 0 && la + r.rx1 < CT_STRIP), 7, la, tw)) continue;
+            if (!CT_OK(!okb || (lb + r.rx0 >= 0 && lb + r.rx1 < CT_STRIP), 7, lb, tw)) continue;
+            const int j0 = max(0, 1 - x32), j1 = min(31, r.w - x32);  // pixels 1 .. w of the framed row
             uint32_t w = 0;
 #pragma unroll 4
-            for (int j = 0; j < 32; ++j) {
-                const int x = x32 + j;
-                if (x < 1 || x > r.w) continue;
+            for (int j = j0; j <= j1; ++j) {
                 int xa, xb;
                 float wx0, wx1;
-                taps(r.X0 + x - 1, sx, s.mw, &xa, &xb, &wx0, &wx1);
-                const float A = val(ya, xa), B = val(ya, xb), C = val(yb, xa), D = val(yb, xb);
+                taps(r.X0 + x32 + j - 1, sx, s.mw, &xa, &xb, &wx0, &wx1);
+                const bool ixa = xa >= r.rx0 && xa <= r.rx1, ixb = xb >= r.rx0 && xb <= r.rx1;
+                const float A = oka && ixa ? strip[la + xa] : 0.f, B = oka && ixb ? strip[la + xb] : 0.f;
+                const float C = okb && ixa ? strip[lb + xa] : 0.f, D = okb && ixb ? strip[lb + xb] : 0.f;
                 const float ha = wx0 * A + wx1 * B, hb = wx0 * C + wx1 * D;
                 if (wy0 * ha + wy1 * hb > 0.f) w |= 1u << j;
             }
