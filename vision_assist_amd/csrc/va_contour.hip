@@ -555,6 +555,7 @@ struct CtArgs {
     int poly_cap;
     int gate;                 // pool kernel: hold new claims while a wave waits for pages
     int64_t pool_max;         // bytes: larger images go to the global-memory form
+    int pages;                // pages of the pool kernel's LDS (<= CP_PAGES)
 };
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -804,7 +805,7 @@ __global__ __launch_bounds__(CP_THREADS) void post_contour_pool_kernel(CtArgs a)
             while (true) {
                 const unsigned cur = uni((int)__hip_atomic_load(&s_map, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
                 int q = -1;
-                for (int t = 0; t + np <= CP_PAGES; ++t)
+                for (int t = 0; t + np <= a.pages; ++t)
                     if (!(cur & (run << t))) {
                         q = t;
                         break;
@@ -1181,8 +1182,12 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     static const int gate_env = getenv("VA_CT_GATE") ? atoi(getenv("VA_CT_GATE")) : 1;  // A/B knob
     ca.gate = gate_env;
     // images needing more than VA_CT_POOL_PAGES pages (default all 32) run in global memory (A/B knob)
+    // the pool kernel's LDS: VA_CT_PAGES pages (default all 32 = 160 KiB; fewer leave LDS for a concurrent conv
+    // workgroup of the next batch's forward on the same CU)
+    static const int pages_env = getenv("VA_CT_PAGES") ? atoi(getenv("VA_CT_PAGES")) : CP_PAGES;
+    ca.pages = pages_env < 1 ? 1 : (pages_env > CP_PAGES ? CP_PAGES : pages_env);
     static const int pool_pages = getenv("VA_CT_POOL_PAGES") ? atoi(getenv("VA_CT_POOL_PAGES")) : CP_PAGES;
-    ca.pool_max = (int64_t)(pool_pages < CP_PAGES ? pool_pages : CP_PAGES) * CP_PAGE;
+    ca.pool_max = (int64_t)(pool_pages < ca.pages ? pool_pages : ca.pages) * CP_PAGE;
     const int64_t items = (int64_t)src.B * max_det;
     static DevVal<int> n_cu;  // per device: one pool block per CU
     if (n_cu() <= 0) {
@@ -1194,7 +1199,7 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     }
     const int pgrid = (int)(items < n_cu() ? items : n_cu());
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
-    hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), CP_POOL, st, ca);
+    hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st, ca);
     hipLaunchKernelGGL(post_contour_global_kernel, dim3(grid), dim3(CT_THREADS), 0, st, ca);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     if (!cells) return hipSuccess;
