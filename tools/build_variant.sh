@@ -7,11 +7,12 @@ SEG=$1; NAME=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CSRC=$ROOT/vision_assist_amd/csrc
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I$CSRC -I$ROOT/include"
-make -s -C "$CSRC" va_nav.o va_post.o
+OBJS="va_nav.o va_c2f.o va_stem.o va_pw.o va_post.o va_contour.o va_fp8.o va_handle.o"
+make -s -C "$CSRC" $OBJS
 SRC=$CSRC/.variant_$NAME.hip  # next to the real source: relative includes resolve
 cp "$SEG" "$SRC"
 /opt/rocm/bin/hipcc $FLAGS -c "$SRC" -o "$CSRC/.variant_$NAME.o"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/vision_assist_amd/libva355_$NAME.so" \
-    "$CSRC/va_nav.o" "$CSRC/va_post.o" "$CSRC/.variant_$NAME.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o "$ROOT/vision_assist_amd/libva355_$NAME.so" \
+    $(for o in $OBJS; do echo "$CSRC/$o"; done) "$CSRC/.variant_$NAME.o"
 rm -f "$SRC" "$CSRC/.variant_$NAME.o"
 echo "built vision_assist_amd/libva355_$NAME.so"
