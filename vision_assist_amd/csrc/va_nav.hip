@@ -607,7 +607,7 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     uint32_t* osec = (uint32_t*)(okey + N);       // per open slot: x << 24 | y << 16
     uint16_t* par = (uint16_t*)(osec + N);
     uint16_t* hd = par + N;
-    uint16_t* open = hd + N;
+    uint16_t* open = hd + N;                      // (unused slot array: the popped node comes from osec)
     uint8_t* st = (uint8_t*)(open + N);
     const double* __restrict__ pen = npen;  // global (see above)
 
@@ -630,7 +630,6 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         int sx = s % LC, sy = s / LC;
         hd[s] = 0;
         st[s] |= ST_HASG | ST_INOPEN;
-        open[0] = (uint16_t)s;
         okey[0] = (unsigned long long)__double_as_longlong((double)(VA_GRID * (abs(sx - ex) + abs(sy - ey))));
         osec[0] = ((unsigned)sx << 24) | ((unsigned)sy << 16);
     }
@@ -653,9 +652,10 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
             }
         }
         wave_argmin(fb, sec);
+        // the popped node straight from its key (osec holds x << 24 | y << 16): no dependent read of open[]
         const int slot = (int)(sec & 0xFFFFu);
-        const int cur = (int)open[slot];
-        const int cx = cur % LC, cy = cur / LC;
+        const int cx = (int)(sec >> 24), cy = (int)((sec >> 16) & 0xFFu);
+        const int cur = cy * LC + cx;
         // the neighbours (lanes 0..3) and their penalties, loaded now and consumed by the relaxation
         int nb = -1;
         if (lane < 4) {
@@ -666,7 +666,6 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         WAVE_SYNC();
         if (lane == 0) {
             const int last = open_n - 1;
-            open[slot] = open[last];
             okey[slot] = okey[last];
             osec[slot] = osec[last];
         }
@@ -746,7 +745,6 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
             unsigned long long pb = __ballot(push);
             if (push) {
                 const int pos = open_n + __popcll(pb & ((1ull << lane) - 1ull));
-                open[pos] = (uint16_t)nb;
                 okey[pos] = (unsigned long long)__double_as_longlong(fnew);
                 osec[pos] = secn;
             }
