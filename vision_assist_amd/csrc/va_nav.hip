@@ -663,6 +663,7 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
             if (nx >= 0 && nx < LC && ny >= 0 && ny < a.LR) nb = ny * LC + nx;
         }
         const double pnb = pen[nb >= 0 ? nb : cur];  // unconditional: the wait lands at the use
+        const uint8_t snb = st[nb >= 0 ? nb : cur];   // with it: closing cur below never touches a neighbour
         WAVE_SYNC();
         if (lane == 0) {
             const int last = open_n - 1;
@@ -681,11 +682,7 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         WAVE_SYNC();
         if (lane == 0) st[cur] |= ST_CLOSED;
         WAVE_SYNC();
-        bool valid = false;
-        if (nb >= 0) {
-            const uint8_t sv = st[nb];
-            valid = (sv & ST_EXISTS) && !(sv & ST_CLOSED);
-        }
+        const bool valid = nb >= 0 && (snb & ST_EXISTS) && !(snb & ST_CLOSED);
         unsigned long long vb = __ballot(valid);
         // angle penalty of the first non-closed neighbour (newest-window rule, Q3)
         double ap = 0.0;
