@@ -467,6 +467,8 @@ __device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int 
         return 1;
     }
     const int x1 = x0 + dir_dx(s), y1 = y0 + dir_dy(s);  // i1
+    // the stop test on packed (x | y << 16) positions: framed coordinates are non-negative and below 2^16
+    const int p0 = x0 | (y0 << 16), p1 = x1 | (y1 << 16);
     int x3 = x0, y3 = y0;
     int prev_s = s ^ 4, n = 0;
     unsigned nb3 = nb;
@@ -482,7 +484,7 @@ __device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int 
             ++n;
             prev_s = s;
         }
-        if (x4 == x0 && y4 == y0 && x3 == x1 && y3 == y1) break;
+        if ((((x4 | (y4 << 16)) ^ p0) | ((x3 | (y3 << 16)) ^ p1)) == 0) break;
         x3 = x4;
         y3 = y4;
         s = (s + 4) & 7;
