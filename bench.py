@@ -51,7 +51,7 @@ def f32_split_terms() -> int:
     e = os.environ.get("VA_F32_SPLIT")
     if e is None:
         return 6
-    return 9 if e.startswith("9") else 6 if e.startswith("6") else 0
+    return 9 if e.startswith("9") else 6 if e.startswith("6") or e.startswith("16") else 0
 CONV_KINDS = (1, 5, 6, 7)  # va355.h VA_OP_CONV, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM
 
 
@@ -65,9 +65,15 @@ def parse():
     p.add_argument("--batch", type=int, default=0, help="frames per step per GPU (0 = the dtype's default)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
-    p.add_argument("--regime", default="natural", choices=["natural", "mid", "dense", "dense_box"])
-    p.add_argument("--extras", default="bf16,dense,dense_box,c5",
-                   help="comma list of extra measurements in the same run: bf16 (the bf16 MFMA pipeline), "
+    p.add_argument("--regime", default="sparse", choices=["sparse", "natural", "mid", "dense", "dense_box"],
+                   help="detection regime of the synthetic weights (regime_kwargs); the headline is 'sparse': 1-5 "
+                        "compact detections per frame through decode / NMS / contours / mask choice, planted "
+                        "navigation masks only on frames without a detection")
+    p.add_argument("--extras", default="c4,c2,dropin,bf16,dense,dense_box,c5",
+                   help="comma list of extra measurements in the same run: c4 (BASELINE configs[3]: one frame per GPU "
+                        "per step, s-seg f32), c2 (configs[1]: n-seg bf16 batch-1 latency, seg-only and end to end), "
+                        "dropin (FrameProcessor.__call__ per frame from host numpy frames, answers included), "
+                        "bf16 (the bf16 MFMA pipeline), "
                         "dense (300 detections per frame, the random weights' noise masks), dense_box (300 "
                         "detections per frame with solid box masks, one contour each, as a trained model's compact "
                         "masks), c5 (YOLOv8m-seg 1280 on fp8 MFMA, batch 8); 'none' to skip")
@@ -84,6 +90,15 @@ def parse():
     p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2],
                    help="network streams of the overlapped pipeline (2: consecutive forwards run concurrently)")
     return p.parse_args()
+
+
+def regime_kwargs(regime: str, res: int) -> dict:
+    """synthetic_state_dict keywords of a detection regime: 'sparse' = one live class whose bias
+    leaves ~1-5 detections per frame with solid (compact) masks, as a trained model's frames; 'natural' =
+    Ultralytics' prior bias (no detections on noise frames: A* runs on planted masks); 'mid' = bias 0 (saturates
+    max_det on these weights); 'dense' = +4 (300 noise masks); 'dense_box' = +4 with solid box masks."""
+    return {"sparse": {"sparse": res}, "natural": {}, "mid": {"cls_bias": 0.0}, "dense": {"cls_bias": 4.0},
+            "dense_box": {"cls_bias": 4.0, "solid_masks": True}}[regime]
 
 
 def planted_pool(n: int, res: int, seed: int):
@@ -165,10 +180,8 @@ class Run:
         from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
         self.args, self.dtype, self.B, self.regime = args, dtype, B, regime
         self.scale, self.res = scale or args.scale, res or args.res
-        cls_bias = {"natural": None, "mid": 0.0, "dense": 4.0, "dense_box": 4.0}[regime]
         self.arch = Arch(self.scale)
-        self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, cls_bias=cls_bias,
-                                                       solid_masks=regime == "dense_box"))
+        self.fw = fold(self.arch, synthetic_state_dict(self.arch, seed=0, **regime_kwargs(regime, self.res)))
         H = W = self.res
         self.overlap = not args.no_overlap
         if self.overlap:
@@ -322,6 +335,118 @@ class Run:
         torch.cuda.empty_cache()
 
 
+def c4_rate(args, dev, rank, world, prof) -> dict:
+    """C4 (BASELINE.json configs[3]): YOLOv8s-seg 640x640 f32, ONE frame per GPU per step (batch 8 over 8 GPUs),
+    frames dealt round-robin, no collective; the same overlapped pipeline as the headline with batch 1 (three
+    frames in flight per GPU).  value = frames of all ranks / max-over-ranks time."""
+    steps = max(200, 10 * args.steps)
+    r = Run(args, dev, rank, "f32", 1, args.regime, scale="s", res=640)
+    m = r.measure(steps, 20, world, prof)
+    r.release()
+    e = {"value": round(m["value"], 2), "unit": "frames/s", "ms_per_step": round(m["ms_per_step"], 4), "steps": steps,
+         "dtype": "f32", "batch_per_gpu": 1, "global_batch": world, "regime": args.regime,
+         "workload": "C4 (BASELINE.json configs[3]): YOLOv8s-seg 640x640, one frame per GPU per step, network masks "
+                     "(planted only when a frame has no detection) -> contours -> grid / A*, 3 frames in flight per GPU",
+         "parity": "tests/test_gpu_c4.py (2 ranks, one frame per rank per step, vs the per-shard oracle-chain replay)"}
+    if prof:
+        rl = m["roofline"]
+        e["roofline"] = {k: rl[k] for k in ("achieved", "peak", "frac", "avg_launch_us", "traffic")}
+    return e
+
+
+def c2_latency(args, dev, iters=200) -> dict:
+    """C2 (BASELINE.json configs[1]): YOLOv8n-seg 640x640 bf16, batch 1, one frame resident in HBM, synchronised
+    after every frame; median / p90 of the seg kernels alone and of the whole path (network masks of the sparse
+    regime, a planted corridor when a frame has none).  Also the network + post-processing replayed as one HIP
+    graph on its own stream (the grid stage reads a device flag per A* round on the host, so it stays eager)."""
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_IF_NONE
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    from workloads.corridors import cells_rect, corridor_cells
+    arch = Arch("n")
+    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, **regime_kwargs(args.regime, 640))),
+                         1, 640, 640, dtype="bf16", device=dev)
+    g = corridor_cells(11, 32, 32)
+    pc = torch.tensor(g[None].astype(np.uint8), device=dev)
+    pr = torch.tensor(np.array([cells_rect(g)], dtype=np.int32), device=dev)
+    frame = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(1),
+                          dtype=torch.uint8).to(dev)
+    st = torch.cuda.Stream(device=dev)
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            pipe.load(frame, stream=st)
+            pipe.seg_post(pc, pr, PLANT_IF_NONE, stream=st)
+        st.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=st):
+            pipe.load(frame, stream=st)
+            pipe.seg_post(pc, pr, PLANT_IF_NONE, stream=st)
+    torch.cuda.synchronize()
+
+    def graph_e2e():
+        graph.replay()
+        pipe.nav_run(stream=st)
+
+    out = {"workload": "C2 (BASELINE.json configs[1]): YOLOv8n-seg 640x640 bf16, batch 1, 1 MI355X; frame resident "
+                       "in HBM, synchronised per frame", "iters": iters, "regime": args.regime}
+    for name, fn in (("seg_only", lambda: pipe.run_seg_only(stream=st)),
+                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_IF_NONE, stream=st)),
+                     ("end_to_end_graph", graph_e2e)):
+        with torch.cuda.stream(st):
+            for _ in range(20):
+                fn()
+            st.synchronize()
+            ts = []
+            for _ in range(iters):
+                t0 = time.perf_counter()
+                fn()
+                st.synchronize()
+                ts.append(time.perf_counter() - t0)
+        ts = np.array(ts) * 1e3
+        out[name] = {"median_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4)}
+    out["ndet_last_frame"] = int(pipe.post.ndet[0])
+    del graph, pipe
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
+
+
+def dropin_rate(args, dev, calls=200) -> dict:
+    """The drop-in surface's own rate: main.py:80-82 calls processor(frame) once per frame with a host numpy
+    frame.  FrameProcessor.__call__ (YOLO s-seg f32, the sparse regime's network masks) does the H2D copy, one
+    batch-1 device pipeline, the host pydantic Path construction (sections, corners) and the PathAnalyser
+    answer per call; frames cycle through 16 distinct seeded 640x640 frames."""
+    import warnings
+
+    from vision_assist_amd.FrameProcessor import FrameProcessor
+    from vision_assist_amd.yolo import YOLO
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = YOLO("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)).to(dev)
+    fp = FrameProcessor(model=model, verbose=False, debug=False)
+    fp.model = model
+    rng = np.random.default_rng(77)
+    frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
+    answers = 0
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):  # "No path found." prints, as the reference's
+        for i in range(10):
+            fp(frames[i % 16])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(calls):
+            a = fp(frames[i % 16])
+            answers += a != []
+        dt = time.perf_counter() - t0
+    return {"value": round(calls / dt, 2), "unit": "frames/s", "ms_per_call": round(1e3 * dt / calls, 4),
+            "calls": calls, "calls_with_answer": answers, "dtype": "f32", "regime": args.regime,
+            "workload": "FrameProcessor.__call__(frame) per frame (main.py:80-82): host numpy 640x640 frame -> pinned "
+                        "H2D -> YOLOv8s-seg f32 + post + grid / A* (batch 1) -> host Path sections/corners + "
+                        "PathAnalyser answer"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -362,6 +487,17 @@ def main():
 
     extras = {}
     for ex in [e for e in args.extras.split(",") if e and e != "none"]:
+        if ex == "c2":
+            if world == 1:
+                extras[ex] = c2_latency(args, dev)
+            continue
+        if ex == "dropin":
+            if world == 1:
+                extras[ex] = dropin_rate(args, dev)
+            continue
+        if ex == "c4":
+            extras[ex] = c4_rate(args, dev, rank, world, prof)
+            continue
         if ex == "bf16" and args.dtype != "bf16":
             dt_, B_, reg_ = "bf16", args.batch or DEFAULT_BATCH["bf16"], args.regime
         elif ex in ("dense", "dense_box") and args.regime != ex:

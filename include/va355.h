@@ -432,6 +432,12 @@ int va_handle_device(va_handle h, int32_t* device);
 int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
              int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds);
 
+/* Out-of-range state the kernels rejected instead of faulting (a rect no frame holds, an A* node outside the
+ * lattice, a traced pixel outside its image, candidate counts past the anchors -- csrc/va_diag.h lists the
+ * codes): out[4 i .. 4 i + 3] = {first code, v0, v1, count} for the units post, contour, nav (n >= 12); the
+ * words are zeroed when clear != 0.  Synchronises the current device.  Debug / test surface. */
+int va_diag(uint32_t* out, int32_t n, int32_t clear);
+
 /* Library version / build info string. */
 const char* va_version(void);
 

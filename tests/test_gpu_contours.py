@@ -65,3 +65,24 @@ def test_select_masks_small_frames_lds_image():
         kk, pts, rect, cells = C.select_cells(ms, (Hn, Wn))
         assert got["chosen"][b] == kk and tuple(got["rects"][b]) == rect
         assert np.array_equal(got["cells"][b], cells)
+
+
+@pytest.mark.parametrize("cap", [1024, 16384])
+def test_select_masks_contours_longer_than_the_point_buffer(cap):
+    """Noise masks whose largest external contour has 14k-45k points (more than the contour kernel's kept 1024
+    and, at p = 0.42, more than the fill kernel's 16384-point buffer): the fill kernel follows the chosen contour
+    again once per chunk of `cap` points (a capped buffer dropped the frame's grid); cells, rect and
+    chosen instance equal to the oracle's, status 0."""
+    from vision_assist_amd.post import select_masks
+    rng = np.random.default_rng(3)
+    ms = [(rng.random((640, 640)) < p).astype(np.uint8) for p in (0.42, 0.45)]
+    masks = np.stack([np.stack([ms[0], ms[1]]), np.stack([ms[1], np.zeros_like(ms[1])])])
+    n = np.array([2, 1], np.int32)
+    got = select_masks(torch.from_numpy(masks).cuda(), torch.from_numpy(n), 640, 640, cap=cap)
+    assert (got["status"] == 0).all()
+    for b in range(2):
+        kk, pts, rect, cells = C.select_cells(masks[b, :n[b]], (640, 640))
+        assert len(pts) > 14000
+        assert got["chosen"][b] == kk
+        assert tuple(got["rects"][b]) == rect, (b, tuple(got["rects"][b]), rect)
+        assert np.array_equal(got["cells"][b], cells), (b, int((got["cells"][b] != cells).sum()))

@@ -1,27 +1,16 @@
 #!/bin/bash
-# Run GPU steps in order, each under its own time limit; stop at the first step that ends in a fault, an abort,
-# a segfault or a time limit (exit status >= 124, or 134 / 139) -- an ordinary failure (status 1-123, e.g.
-# failing tests) does not stop the later steps.  Usage:
-#   tools/gpu_steps.sh <outdir> "<seconds>:<name>:<command>" ...
-OUT=$1
-shift
-mkdir -p "$OUT"
-export TMPDIR=/tmp
-worst=0
-for spec in "$@"; do
-  secs=${spec%%:*}
-  rest=${spec#*:}
-  name=${rest%%:*}
-  cmd=${rest#*:}
-  echo "[$(date +%T)] $name: $cmd"
-  timeout -k 10 "$secs" bash -c "$cmd" > "$OUT/$name.log" 2>&1
+# Runs GPU steps in order, each under its own time limit; a step that fails its checks (exit 1) lets the next
+# one run, anything else (fault, abort, signal, time limit) ends the script there.
+#   bash tools/gpu_steps.sh SECONDS LOGNAME -- cmd ... [:: SECONDS LOGNAME -- cmd ...]
+mkdir -p gpurun_out
+while [ $# -gt 0 ]; do
+  t=$1; log=$2; shift 3
+  cmd=()
+  while [ $# -gt 0 ] && [ "$1" != "::" ]; do cmd+=("$1"); shift; done
+  [ "$1" = "::" ] && shift
+  echo "== ${cmd[*]}  (limit ${t}s, log gpurun_out/$log)"
+  timeout -k 10 "$t" "${cmd[@]}" > "gpurun_out/$log" 2>&1
   rc=$?
-  echo "[$(date +%T)] $name rc=$rc"
-  tail -3 "$OUT/$name.log"
-  [ $rc -gt $worst ] && worst=$rc
-  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
-    echo "stopping after $name (rc=$rc)"
-    exit $rc
-  fi
+  echo "   rc=$rc"; tail -n 4 "gpurun_out/$log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
 done
-exit $worst

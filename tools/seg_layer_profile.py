@@ -25,8 +25,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
-    ap.add_argument("--ab", default="", help="env switch NAME: interleave rounds with NAME=0 and NAME=1 "
-                                            "(one process, cdna_hip_programming.md §5.4 rule 24)")
+    ap.add_argument("--ab", default="", help="env switch NAME (or NAME:V0:V1): interleave rounds with NAME=0 and "
+                                            "NAME=1 (or V0 / V1) (one process, cdna_hip_programming.md §5.4 rule 24)")
     ap.add_argument("--env", action="append", default=[], help="KEY=VAL set before planning")
     args = ap.parse_args()
     for kv in args.env:
@@ -58,19 +58,20 @@ def main():
         return list(ms)
 
     if args.ab:
-        tot = {"0": [0.0] * n, "1": [0.0] * n}
+        name, v0, v1 = (args.ab.split(":") + ["0", "1"])[:3] if ":" in args.ab else (args.ab, "0", "1")
+        tot = {v0: [0.0] * n, v1: [0.0] * n}
         for rnd in range(args.iters):
-            for v in ("0", "1"):
-                os.environ[args.ab] = v
+            for v in (v0, v1):
+                os.environ[name] = v
                 net.run_plan(plan)  # one untimed forward after the switch
                 t = timed(1)
                 tot[v] = [a + b for a, b in zip(tot[v], t)]
         for i, m in enumerate(plan["meta"]):
-            a0, a1 = 1000 * tot["0"][i] / args.iters, 1000 * tot["1"][i] / args.iters
-            print(json.dumps({"i": i, "name": m["name"], f"{args.ab}=0": round(a0, 2), f"{args.ab}=1": round(a1, 2),
+            a0, a1 = 1000 * tot[v0][i] / args.iters, 1000 * tot[v1][i] / args.iters
+            print(json.dumps({"i": i, "name": m["name"], f"{name}={v0}": round(a0, 2), f"{name}={v1}": round(a1, 2),
                               "ratio": round(a1 / a0, 3) if a0 else None}))
-        s0, s1 = 1000 * sum(tot["0"]) / args.iters, 1000 * sum(tot["1"]) / args.iters
-        print(json.dumps({"total_us": {f"{args.ab}=0": round(s0, 1), f"{args.ab}=1": round(s1, 1)}}))
+        s0, s1 = 1000 * sum(tot[v0]) / args.iters, 1000 * sum(tot[v1]) / args.iters
+        print(json.dumps({"total_us": {f"{name}={v0}": round(s0, 1), f"{name}={v1}": round(s1, 1)}}))
         return
     ms = timed(args.iters)
     rows = []

@@ -79,6 +79,7 @@ SIGNATURES = [
     ("va_post_polygons", I32, [P, P, P, P, I32]),
     ("va_letterbox", I32, [P, P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_abi_struct_sizes", I32, [P, I32]),
+    ("va_diag", I32, [P, I32, I32]),
     ("va_version", ctypes.c_char_p, []),
 ]
 
@@ -103,6 +104,17 @@ def load(path: str = LIB_PATH):
 def check(rc: int, what: str) -> None:
     if rc != VA_OK:
         raise VaError(f"{what} failed with status {rc}")
+
+
+DIAG_UNITS = ("post", "contour", "nav")
+
+
+def diag(clear: bool = True) -> dict:
+    """Out-of-range state the kernels rejected instead of faulting since the last clear (va_diag; codes in
+    csrc/va_diag.h): {unit: (first code, v0, v1, count)} for the units that recorded any (synchronises the device)."""
+    w = (ctypes.c_uint32 * 12)()
+    check(load().va_diag(w, 12, int(clear)), "va_diag")
+    return {u: tuple(int(v) for v in w[4 * i:4 * i + 4]) for i, u in enumerate(DIAG_UNITS) if w[4 * i + 3]}
 
 
 def nav_dims(H: int, W: int) -> VaNavDims:

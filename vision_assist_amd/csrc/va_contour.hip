@@ -39,6 +39,7 @@
 #include "../../include/va355.h"
 #include "va_contour.h"
 #include "va_dev.h"
+#include "va_diag.h"
 
 namespace {
 
@@ -84,7 +85,8 @@ __device__ unsigned long long g_ct_fill[CT_FILL_FRAMES][8];
 #define CT_PROF(...) __VA_ARGS__
 #define CT_STEPS (&nsteps)
 #else
-#define CT_OK(c, code, v0, v1) true
+// production: the same sites reject the access and record it (va_diag.h: code 20 + site)
+#define CT_OK(c, code, v0, v1) VA_DIAG_OK((c), 20 + (code), (v0), (v1))
 #define CT_PROF(...)
 #define CT_STEPS nullptr
 #endif
@@ -874,7 +876,7 @@ struct FillArgs {
     uint8_t* cells;   // [B][H0/20][W0/20]
     int32_t* rects;   // [B][4]
     int32_t* chosen;  // [B]
-    int32_t* status;  // [B] or NULL: 0 ok, 1 contour larger than the point buffer
+    int32_t* status;  // [B] or NULL: 0 ok (no failure mode left: long contours are taken in chunks)
 };
 
 constexpr int FILL_MAX_CELLS = 64 * 64;  // lattice of a 1280 x 1280 frame
@@ -920,7 +922,7 @@ __device__ bool clip_line(int W, int H, long long& x1, long long& y1, long long&
 
 __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
     extern __shared__ __align__(16) uint32_t fill_lds[];  // FILL_LDS bytes: the chosen instance's image
-    __shared__ int s_k, s_n, s_edges;
+    __shared__ int s_k, s_n, s_edges, s_px, s_py, s_lx, s_ly;
     __shared__ int s_minx, s_miny, s_maxx, s_maxy;
     __shared__ unsigned long long s_exmin, s_exmax;  // edge x extremes, biased by 2^62
     __shared__ int s_eymin, s_eymax;
@@ -971,48 +973,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
         }
         const int64_t di = (int64_t)b * a.max_det + k;
         const va_contour_stat st = a.cstats[di];
-        if (st.npts > a.sc.cap) {
-            if (tid == 0 && a.status) a.status[b] = 1;
-            if (tid < 4) a.rects[4 * b + tid] = 0;
-            __syncthreads();
-            continue;
-        }
-        // the chosen instance's best contour as int32 frame points (np.int32 of scale_coords: truncation, >= 0)
-        if (st.npts > 0 && st.npts <= a.sc.capd) {
-            const uint32_t* P = a.sc.cpts + (di * 2 + st.half) * a.sc.capd;
-            for (int i = tid; i < st.npts; i += nt) {
-                const uint32_t q = P[i];
-                float xs, ys;
-                scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
-                pts[2 * i] = (int)xs;
-                pts[2 * i + 1] = (int)ys;
-            }
-            if (tid == 0) s_n = st.npts;
-        } else if (st.npts > 0) {  // longer than the buffer: the image rebuilt (in LDS if it fits) and followed again
-            const Region r = uni_region(region_of(s, b, k));
-            MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
-            auto retrace = [&](uint32_t* img, float* strip) {
-                build_image<false>(s, b, k, r, img, strip, tid, nt, ms);
-                if (tid < 64) {
-                    int i = 0;
-                    fetch_contour(img, r.ww, st.ox, st.oy, [&](int qx, int qy) {
-                        float xs, ys;
-                        scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
-                        if (tid == 0 && i < a.sc.cap) {
-                            pts[2 * i] = (int)xs;
-                            pts[2 * i + 1] = (int)ys;
-                        }
-                        ++i;
-                    });
-                    if (tid == 0) s_n = i;
-                }
-            };
-            // two call sites, each with its own pointer (an LDS / global select would make the accesses flat)
-            if (region_need(s, r) <= FILL_LDS) retrace(fill_lds, (float*)(fill_lds + ((image_words(r) + 3) & ~3ll)));
-            else retrace((uint32_t*)(slot + a.sc.img_off), (float*)slot);
-        } else if (tid == 0) {
-            s_n = 0;
-        }
+        const int n = st.npts;
         if (tid == 0) {
             s_minx = s_miny = INT32_MAX;
             s_maxx = s_maxy = INT32_MIN;
@@ -1023,103 +984,157 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
             s_eymax = INT32_MIN;
         }
         __syncthreads();
-        const int n = s_n;
         CT_PROF(const unsigned long long f1 = __builtin_amdgcn_s_memtime(); fb = st.npts > a.sc.capd);
-        // boundingRect + the edges: lines through cell centres, span counts at the sampled rows
-        for (int i = tid; i < n; i += nt) {
-            const int x1i = pts[2 * i], y1i = pts[2 * i + 1];
-            const int j = i == 0 ? n - 1 : i - 1;  // CollectPolyEdges: pt0 = v[count - 1], then v[0], v[1], ...
-            const int x0i = pts[2 * j], y0i = pts[2 * j + 1];
-            atomicMin(&s_minx, x1i);
-            atomicMin(&s_miny, y1i);
-            atomicMax(&s_maxx, x1i);
-            atomicMax(&s_maxy, y1i);
-            // cv::Line(img, t0, t1, color, LINE_8): LineIterator(8, leftToRight) after clipLine
-            {
-                long long lx1 = x0i, ly1 = y0i, lx2 = x1i, ly2 = y1i;
-                bool ok = true;
-                if (!(lx1 >= 0 && lx1 < W0 && lx2 >= 0 && lx2 < W0 && ly1 >= 0 && ly1 < H0 && ly2 >= 0 && ly2 < H0))
-                    ok = clip_line(W0, H0, lx1, ly1, lx2, ly2);
-                if (ok) {
-                    long long dx = lx2 - lx1, dy = ly2 - ly1;
-                    long long sy = 1;
-                    if (dx < 0) {
-                        dx = -dx, dy = -dy;
-                        long long t = lx1;
-                        lx1 = lx2, lx2 = t;
-                        t = ly1;
-                        ly1 = ly2, ly2 = t;
-                    }
-                    if (dy < 0) dy = -dy, sy = -1;
-                    const bool vert = dy > dx;
-                    if (vert) {
-                        const long long t = dx;
-                        dx = dy, dy = t;
-                    }
-                    long long err = dx - (dy + dy);
-                    const long long plus = dx + dx, minus = -(dy + dy);
-                    long long x = lx1, y = ly1;
-                    for (long long st2 = 0; st2 <= dx; ++st2) {
-                        if (x % VA_GRID == VA_GRID / 2 && y % VA_GRID == VA_GRID / 2 && x >= 0 && y >= 0 && x < W0 &&
-                            y < H0 && CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
-                            hit[(y / VA_GRID) * LC + x / VA_GRID] = 1;
-                        const bool minor = err < 0;
-                        err += minus + (minor ? plus : 0);
+        // boundingRect + the edges of points pts[0, n) (int32 frame points, np.int32 of scale_coords: truncation,
+        // >= 0): lines through cell centres, span counts at the sampled rows.  Every term is order-free (min / max,
+        // hit flags, counts), so a contour longer than the point buffer is taken a chunk at a time.
+        auto edges = [&](const int n, const int px, const int py) {
+            for (int i = tid; i < n; i += nt) {
+                const int x1i = pts[2 * i], y1i = pts[2 * i + 1];
+                // CollectPolyEdges: pt0 = v[count - 1], then v[0], v[1], ...: the predecessor of the chunk's first
+                // point is (px, py) -- the contour's last point for the first chunk
+                const int x0i = i == 0 ? px : pts[2 * (i - 1)], y0i = i == 0 ? py : pts[2 * (i - 1) + 1];
+                atomicMin(&s_minx, x1i);
+                atomicMin(&s_miny, y1i);
+                atomicMax(&s_maxx, x1i);
+                atomicMax(&s_maxy, y1i);
+                // cv::Line(img, t0, t1, color, LINE_8): LineIterator(8, leftToRight) after clipLine
+                {
+                    long long lx1 = x0i, ly1 = y0i, lx2 = x1i, ly2 = y1i;
+                    bool ok = true;
+                    if (!(lx1 >= 0 && lx1 < W0 && lx2 >= 0 && lx2 < W0 && ly1 >= 0 && ly1 < H0 && ly2 >= 0 && ly2 < H0))
+                        ok = clip_line(W0, H0, lx1, ly1, lx2, ly2);
+                    if (ok) {
+                        long long dx = lx2 - lx1, dy = ly2 - ly1;
+                        long long sy = 1;
+                        if (dx < 0) {
+                            dx = -dx, dy = -dy;
+                            long long t = lx1;
+                            lx1 = lx2, lx2 = t;
+                            t = ly1;
+                            ly1 = ly2, ly2 = t;
+                        }
+                        if (dy < 0) dy = -dy, sy = -1;
+                        const bool vert = dy > dx;
                         if (vert) {
-                            y += sy;
-                            x += minor ? 1 : 0;
-                        } else {
-                            x += 1;
-                            y += minor ? sy : 0;
+                            const long long t = dx;
+                            dx = dy, dy = t;
+                        }
+                        long long err = dx - (dy + dy);
+                        const long long plus = dx + dx, minus = -(dy + dy);
+                        long long x = lx1, y = ly1;
+                        for (long long st2 = 0; st2 <= dx; ++st2) {
+                            if (x % VA_GRID == VA_GRID / 2 && y % VA_GRID == VA_GRID / 2 && x >= 0 && y >= 0 && x < W0 &&
+                                y < H0 && CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
+                                hit[(y / VA_GRID) * LC + x / VA_GRID] = 1;
+                            const bool minor = err < 0;
+                            err += minus + (minor ? plus : 0);
+                            if (vert) {
+                                y += sy;
+                                x += minor ? 1 : 0;
+                            } else {
+                                x += 1;
+                                y += minor ? sy : 0;
+                            }
                         }
                     }
                 }
-            }
-            // PolyEdge (CollectPolyEdges, shift 0, line_type < CV_AA)
-            if (y0i != y1i) {
-                long long p0x = (long long)x0i << 16, p0y = y0i, p1x = (long long)x1i << 16, p1y = y1i;
-                long long c0x = p0x, c0y = p0y, c1x = p1x, c1y = p1y;
-                if (!(x0i >= 0 && x0i < W0 && x1i >= 0 && x1i < W0 && y0i >= 0 && y0i < H0 && y1i >= 0 && y1i < H0)) {
-                    long long t0x = x0i, t0y = y0i, t1x = x1i, t1y = y1i;
-                    clip_line(W0, H0, t0x, t0y, t1x, t1y);
-                    if (t0y != t1y) {
-                        c0y = t0y, c1y = t1y;
-                        c0x = t0x << 16, c1x = t1x << 16;
+                // PolyEdge (CollectPolyEdges, shift 0, line_type < CV_AA)
+                if (y0i != y1i) {
+                    long long p0x = (long long)x0i << 16, p0y = y0i, p1x = (long long)x1i << 16, p1y = y1i;
+                    long long c0x = p0x, c0y = p0y, c1x = p1x, c1y = p1y;
+                    if (!(x0i >= 0 && x0i < W0 && x1i >= 0 && x1i < W0 && y0i >= 0 && y0i < H0 && y1i >= 0 && y1i < H0)) {
+                        long long t0x = x0i, t0y = y0i, t1x = x1i, t1y = y1i;
+                        clip_line(W0, H0, t0x, t0y, t1x, t1y);
+                        if (t0y != t1y) {
+                            c0y = t0y, c1y = t1y;
+                            c0x = t0x << 16, c1x = t1x << 16;
+                        }
+                    } else {
+                        c0x += 1 << 15;
+                        c1x += 1 << 15;
                     }
-                } else {
-                    c0x += 1 << 15;
-                    c1x += 1 << 15;
-                }
-                const long long edx = (c1x - c0x) / (c1y - c0y);  // C++ truncating division
-                int ey0, ey1;
-                long long ex;
-                if (p0y < p1y) {
-                    ey0 = (int)p0y, ey1 = (int)p1y, ex = c0x + (p0y - c0y) * edx;
-                } else {
-                    ey0 = (int)p1y, ey1 = (int)p0y, ex = c1x + (p1y - c1y) * edx;
-                }
-                atomicAdd(&s_edges, 1);
-                const long long xend = ex + (long long)(ey1 - ey0) * edx;
-                atomicMin(&s_eymin, ey0);
-                atomicMax(&s_eymax, ey1);
-                constexpr unsigned long long BIAS = 1ull << 62;
-                atomicMin(&s_exmin, (unsigned long long)min(ex, xend) + BIAS);
-                atomicMax(&s_exmax, (unsigned long long)max(ex, xend) + BIAS);
-                // sampled rows cy = 20 r + 10 with ey0 <= cy < ey1
-                int r0 = ey0 <= VA_GRID / 2 ? 0 : (ey0 - VA_GRID / 2 + VA_GRID - 1) / VA_GRID;
-                for (int rr = r0; rr < LR; ++rr) {
-                    const int cy = VA_GRID * rr + VA_GRID / 2;
-                    if (cy >= ey1) break;
-                    const long long xx = ex + (long long)(cy - ey0) * edx;
-                    const long long xi = xx >> 16;
-                    const long long qa = xi - VA_GRID / 2, qb = xi - VA_GRID / 2 - 1;
-                    const long long ca = qa < 0 ? 0 : qa / VA_GRID + 1, cb = qb < 0 ? 0 : qb / VA_GRID + 1;
-                    if (ca < LC) atomicAdd(&cnt_a[rr * (LC + 1) + ca], 1);
-                    if (cb < LC) atomicAdd(&cnt_b[rr * (LC + 1) + cb], 1);
+                    const long long edx = (c1x - c0x) / (c1y - c0y);  // C++ truncating division
+                    int ey0, ey1;
+                    long long ex;
+                    if (p0y < p1y) {
+                        ey0 = (int)p0y, ey1 = (int)p1y, ex = c0x + (p0y - c0y) * edx;
+                    } else {
+                        ey0 = (int)p1y, ey1 = (int)p0y, ex = c1x + (p1y - c1y) * edx;
+                    }
+                    atomicAdd(&s_edges, 1);
+                    const long long xend = ex + (long long)(ey1 - ey0) * edx;
+                    atomicMin(&s_eymin, ey0);
+                    atomicMax(&s_eymax, ey1);
+                    constexpr unsigned long long BIAS = 1ull << 62;
+                    atomicMin(&s_exmin, (unsigned long long)min(ex, xend) + BIAS);
+                    atomicMax(&s_exmax, (unsigned long long)max(ex, xend) + BIAS);
+                    // sampled rows cy = 20 r + 10 with ey0 <= cy < ey1
+                    int r0 = ey0 <= VA_GRID / 2 ? 0 : (ey0 - VA_GRID / 2 + VA_GRID - 1) / VA_GRID;
+                    for (int rr = r0; rr < LR; ++rr) {
+                        const int cy = VA_GRID * rr + VA_GRID / 2;
+                        if (cy >= ey1) break;
+                        const long long xx = ex + (long long)(cy - ey0) * edx;
+                        const long long xi = xx >> 16;
+                        const long long qa = xi - VA_GRID / 2, qb = xi - VA_GRID / 2 - 1;
+                        const long long ca = qa < 0 ? 0 : qa / VA_GRID + 1, cb = qb < 0 ? 0 : qb / VA_GRID + 1;
+                        if (ca < LC) atomicAdd(&cnt_a[rr * (LC + 1) + ca], 1);
+                        if (cb < LC) atomicAdd(&cnt_b[rr * (LC + 1) + cb], 1);
+                    }
                 }
             }
+            __syncthreads();
+        };
+        if (st.npts > 0 && st.npts <= a.sc.capd) {
+            // the chosen instance's best contour, kept by the contour kernel
+            const uint32_t* P = a.sc.cpts + (di * 2 + st.half) * a.sc.capd;
+            for (int i = tid; i < st.npts; i += nt) {
+                const uint32_t q = P[i];
+                float xs, ys;
+                scale_pt(a.f, (int)(q & 0xFFFFu), (int)(q >> 16), &xs, &ys);
+                pts[2 * i] = (int)xs;
+                pts[2 * i + 1] = (int)ys;
+            }
+            __syncthreads();
+            edges(st.npts, pts[2 * (st.npts - 1)], pts[2 * (st.npts - 1) + 1]);
+        } else if (st.npts > 0) {
+            // longer than the kept buffer: the image rebuilt (in LDS if it fits) and the contour followed again,
+            // once per chunk of sc.cap points (pass p stores points [p cap, (p + 1) cap), the point before the
+            // chunk and the contour's last point) -- no length limit (a capped buffer dropped the grid)
+            const Region r = uni_region(region_of(s, b, k));
+            MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+            auto retrace = [&](uint32_t* img, float* strip) {
+                build_image<false>(s, b, k, r, img, strip, tid, nt, ms);
+                for (int lo = 0;; lo += a.sc.cap) {
+                    if (tid < 64) {
+                        int i = 0;
+                        fetch_contour(img, r.ww, st.ox, st.oy, [&](int qx, int qy) {
+                            if (tid == 0) {
+                                float xs, ys;
+                                scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
+                                if (i >= lo && i < lo + a.sc.cap) {
+                                    pts[2 * (i - lo)] = (int)xs;
+                                    pts[2 * (i - lo) + 1] = (int)ys;
+                                }
+                                if (i == lo - 1) s_px = (int)xs, s_py = (int)ys;
+                                s_lx = (int)xs, s_ly = (int)ys;
+                            }
+                            ++i;
+                        });
+                        if (tid == 0) s_n = i;
+                    }
+                    __syncthreads();
+                    const int total = s_n;
+                    if (lo >= total) break;
+                    const int cnt = total - lo < a.sc.cap ? total - lo : a.sc.cap;
+                    edges(cnt, lo == 0 ? s_lx : s_px, lo == 0 ? s_ly : s_py);
+                    if (lo + cnt >= total) break;
+                }
+            };
+            // two call sites, each with its own pointer (an LDS / global select would make the accesses flat)
+            if (region_need(s, r) <= FILL_LDS) retrace(fill_lds, (float*)(fill_lds + ((image_words(r) + 3) & ~3ll)));
+            else retrace((uint32_t*)(slot + a.sc.img_off), (float*)slot);
         }
-        __syncthreads();
         CT_PROF(const unsigned long long f2 = __builtin_amdgcn_s_memtime());
         // FillEdgeCollection's early outs: fewer than 2 edges, or all edges outside the image
         constexpr unsigned long long BIAS = 1ull << 62;
@@ -1316,3 +1331,5 @@ extern "C" int va_contour_watch(void** host) {
     return VA_OK;
 }
 #endif
+
+int va_diag_contour(unsigned int* out4, int clear) { return diag_read_tu(out4, clear); }

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include "../../include/va355.h"
+#include "va_diag.h"
 
 struct va_handle_s {
     int32_t device;
@@ -65,6 +66,14 @@ int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, cons
     rc = va_post_run(stream, post);
     if (rc != VA_OK) return rc;
     return va_nav_run(stream, post->cells, post->rects, post->B, H0, W0, seen, nav_work, rounds);
+}
+
+int va_diag(uint32_t* out, int32_t n, int32_t clear) {
+    if (!out || n < 12) return VA_ERR_ARG;
+    int (*const tu[3])(unsigned int*, int) = {va_diag_post, va_diag_contour, va_diag_nav};
+    for (int i = 0; i < 3; ++i)
+        if (tu[i](out + 4 * i, clear) != 0) return VA_ERR_HIP;
+    return VA_OK;
 }
 
 }  // extern "C"

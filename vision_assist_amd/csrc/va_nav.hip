@@ -30,6 +30,7 @@
 
 #include "../../include/va355.h"
 #include "va_dev.h"
+#include "va_diag.h"
 #include "va_angle_table.h"
 
 #define VA_MAX_LAT 64          // max lattice rows / cols (1280 px)
@@ -217,6 +218,12 @@ __global__ __launch_bounds__(VA_NAV_THREADS) void nav_grid_kernel(GridArgs a) {
         int x = a.rects[4 * f + 0], y = a.rects[4 * f + 1], w = a.rects[4 * f + 2], h = a.rects[4 * f + 3];
         int status = VA_FRAME_OK;
         if (w <= 0 || h <= 0) status = VA_FRAME_NO_MASK;
+        // a boundingRect lies in the frame (points are clipped to it): anything far outside is not a rect the
+        // mask choice wrote -- rejected (no mask) before the arithmetic below could overflow
+        constexpr int LIM = 1 << 24;
+        if (status == VA_FRAME_OK &&
+            !VA_DIAG_OK(x > -LIM && x < LIM && y > -LIM && y < LIM && w < LIM && h < LIM, 31, x, w))
+            status = VA_FRAME_NO_MASK;
         // FrameProcessor.py:79-83 (only w is clamped to the frame, Q14)
         x = x - (x % VA_GRID);
         y = y - (y % VA_GRID);
@@ -594,6 +601,7 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
     va_query_hdr* qh = (va_query_hdr*)(a.qwork + (int64_t)q * a.query_bytes);
     if (s < 0 || e < 0) return;  // empty slot (status already VA_QUERY_NONE)
     const int LC = a.LC, N = a.LR * a.LC;
+    if (!VA_DIAG_OK(s < N && e < N, 32, s, e)) return;  // never written by the grid kernel: rejected
     const int fr = q / a.qpf;
     const uint8_t* nflags = (const uint8_t*)((const uint8_t*)a.node_flags + (int64_t)fr * a.node_stride);
     const double* npen = (const double*)((const uint8_t*)a.node_pen + (int64_t)fr * a.node_stride);
@@ -929,6 +937,12 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
         hipFuncSetAttribute((const void*)nav_astar_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
         return VA_ERR_HIP;
+    // the round's verdict is read through a pinned host word (one per device), copied on the launch stream
+    // behind the validation kernel and waited for on that stream -- never a pageable copy, whose staging the
+    // runtime orders on its own
+    static DevVal<int32_t*> flag;
+    if (!flag() && hipHostMalloc((void**)&flag(), 64, hipHostMallocDefault) != hipSuccess) return VA_ERR_HIP;
+    volatile int32_t* rerun_h = flag();
     int slot0 = 0, rounds = 0;
     while (true) {
         ++rounds;
@@ -939,10 +953,15 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
         hipLaunchKernelGGL(nav_validate_kernel, dim3(1), dim3(VAL_THREADS), 0, st, a.starts, a.qwork, a.query_bytes,
                            a.nslots, slot0, seen, ctrl);
         if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
-        int32_t rerun = -1;
-        if (hipMemcpyAsync(&rerun, ctrl, sizeof rerun, hipMemcpyDeviceToHost, st) != hipSuccess) return VA_ERR_HIP;
+        *rerun_h = -2;
+        if (hipMemcpyAsync((void*)rerun_h, ctrl, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
+            return VA_ERR_HIP;
         if (hipStreamSynchronize(st) != hipSuccess) return VA_ERR_HIP;
-        if (rerun < 0) break;
+        const int32_t rerun = *rerun_h;
+        if (rerun == -1) break;
+        // the first conflicting slot lies after this round's first slot; anything else (or the -2 the copy
+        // should have overwritten) means the copy did not see the validation's result: refuse, never launch on it
+        if (rerun <= slot0 || rerun >= a.nslots) return VA_ERR_RANGE;
         if (rounds > 130) return VA_ERR_RANGE;  // impossible: every round adds a key (<= 128)
         slot0 = rerun;
     }
@@ -1102,3 +1121,5 @@ int va_abi_struct_sizes(int64_t* out, int32_t n) {
 const char* va_version(void) { return "libva355 0.1 gfx950 (" __DATE__ ")"; }
 
 }  // extern "C"
+
+int va_diag_nav(unsigned int* out4, int clear) { return diag_read_tu(out4, clear); }

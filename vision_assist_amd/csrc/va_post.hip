@@ -20,6 +20,7 @@
 #include "../../include/va355.h"
 #include "va_contour.h"
 #include "va_dev.h"
+#include "va_diag.h"
 
 namespace {
 
@@ -152,7 +153,12 @@ __global__ __launch_bounds__(DEC_THREADS) void post_decode_kernel(LevelPtrs lv, 
     __syncthreads();
     if (threadIdx.x == 0) s_base = s_n ? atomicAdd(&count[b], s_n) : 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < s_n; i += DEC_THREADS) cand[(int64_t)b * A + s_base + i] = s_c[i];
+    // A frame holds at most A candidates; a count past A can only come from a second decode racing this one on
+    // the same buffers (count not reset in between) -- drop, never write past the frame's region (the NMS kernel
+    // clamps its count the same way)
+    const int lim = A - s_base < s_n ? A - s_base : s_n;
+    if (threadIdx.x == 0) (void)VA_DIAG_OK(lim == s_n, 11, s_base, s_n);
+    for (int i = threadIdx.x; i < lim; i += DEC_THREADS) cand[(int64_t)b * A + s_base + i] = s_c[i];
 }
 
 // ------------------------------------------------------------------------------------------- NMS
@@ -260,7 +266,8 @@ __global__ __launch_bounds__(NMS_THREADS) void post_nms_kernel(const va_cand* ca
                                                                int32_t* ndet, unsigned long long* gkeys) {
     extern __shared__ __align__(16) unsigned long long nms_smem[];
     const int b = blockIdx.x, tid = threadIdx.x;
-    const int n = count[b];
+    const int n = min(max(count[b], 0), A);  // clamped: see post_decode_kernel
+    if (tid == 0) (void)VA_DIAG_OK(n == count[b], 12, count[b], A);
     const va_cand* C = cand + (int64_t)b * A;
     va_det* D = dets + (int64_t)b * max_det;
     __shared__ int s_kept;
@@ -615,3 +622,5 @@ int va_post_polygons(void* stream, const va_post_args* p, float* polys, int32_t*
 }
 
 }  // extern "C"
+
+int va_diag_post(unsigned int* out4, int clear) { return diag_read_tu(out4, clear); }

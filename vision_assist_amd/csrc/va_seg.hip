@@ -26,6 +26,7 @@
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 // staging registers: a native vector type (HIP's uint4 is a union-based class whose arrays defeat
 // SROA and end up in scratch / LDS)
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
@@ -437,48 +438,13 @@ __device__ __forceinline__ void e4m3_unpack4(unsigned q, float inv, float* v) {
     v[0] = a[0] * inv, v[1] = a[1] * inv, v[2] = b[0] * inv, v[3] = b[1] * inv;
 }
 
-template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename RT = __bf16>
-__device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
-                                              int wm, int wn, int tid, int fr, int fq, RowFn orow, int m0 = 0,
-                                              int cls = 0) {
-    constexpr bool F8 = sizeof(RT) == 1;  // the fp8 mode (e4m3 activations)
+// epilogue stage 2 (Cs -> global): 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous stores
+template <int NT, int BM, int BN, typename OutT, typename RowFn, typename RT>
+__device__ __forceinline__ void conv_epilogue_store(const va_conv_args& a, unsigned char* smem, int n0, int tid,
+                                                    RowFn orow) {
+    constexpr bool F8 = sizeof(RT) == 1;
     constexpr int CW = BN + 4;
-    float* Cs = (float*)smem;
-    int brow[4];  // bias row offset per pixel fragment
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        brow[j] = n0;
-        if (a.bias4) {
-            const int m = m0 + wm * 64 + 16 * j + fr;
-            const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
-            const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
-            brow[j] = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < TNS; ++i) {
-        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float4 bv = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
-            f32x4 ac = acc[i][j];
-            if constexpr (F8) {
-                const float4 sv = *(const float4*)(a.wscale + n0 + col);
-                ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
-            }
-            float v0 = ac[0] + bv.x, v1 = ac[1] + bv.y, v2 = ac[2] + bv.z, v3 = ac[3] + bv.w;
-            if (a.act) {
-                const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
-                v0 = s01[0];
-                v1 = s01[1];
-                v2 = s23[0];
-                v3 = s23[1];
-            }
-            *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
-        }
-    }
-    __syncthreads();
-    // ---- epilogue 2: 16-byte runs of consecutive channels per pixel (+ residual), row-contiguous stores
+    const float* Cs = (const float*)smem;
     constexpr int OV = 16 / sizeof(OutT);
     constexpr int CPRO = BN / OV;
     OutT* Y = (OutT*)a.y;
@@ -542,6 +508,93 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
     }
 }
 
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename RT = __bf16>
+__device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc)[TNS][4], unsigned char* smem, int n0,
+                                              int wm, int wn, int tid, int fr, int fq, RowFn orow, int m0 = 0,
+                                              int cls = 0) {
+    constexpr bool F8 = sizeof(RT) == 1;  // the fp8 mode (e4m3 activations)
+    constexpr int CW = BN + 4;
+    float* Cs = (float*)smem;
+    int brow[4];  // bias row offset per pixel fragment
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        brow[j] = n0;
+        if (a.bias4) {
+            const int m = m0 + wm * 64 + 16 * j + fr;
+            const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
+            const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
+            brow[j] = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) {
+        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 bv = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
+            f32x4 ac = acc[i][j];
+            if constexpr (F8) {
+                const float4 sv = *(const float4*)(a.wscale + n0 + col);
+                ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
+            }
+            float v0 = ac[0] + bv.x, v1 = ac[1] + bv.y, v2 = ac[2] + bv.z, v3 = ac[3] + bv.w;
+            if (a.act) {
+                const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                v0 = s01[0];
+                v1 = s01[1];
+                v2 = s23[0];
+                v3 = s23[1];
+            }
+            *(float4*)(Cs + (wm * 64 + 16 * j + fr) * CW + col) = make_float4(v0, v1, v2, v3);
+        }
+    }
+    __syncthreads();
+    conv_epilogue_store<NT, BM, BN, OutT, RowFn, RT>(a, smem, n0, tid, orow);
+}
+
+// epilogue stage 1 of the 32x32-fragment form (conv2_kernel SPL 16): acc[ib][jb] is the 32 x 32 block of channels
+// wn 16 TNS + 32 ib .. and pixels wm 64 + 32 jb ..; lane l holds pixel l % 32, items q: channel 8 (q / 4) + 4 (l / 32)
+// + q % 4 (v_mfma_f32_32x32x16 D layout)
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn>
+__device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&acc)[TNS / 2][2], unsigned char* smem,
+                                                int n0, int wm, int wn, int tid, int lane, RowFn orow, int m0 = 0,
+                                                int cls = 0) {
+    constexpr int CW = BN + 4;
+    float* Cs = (float*)smem;
+    const int r = lane & 31, g = lane >> 5;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+        const int pl = wm * 64 + 32 * jb + r;
+        int brow = n0;
+        if (a.bias4) {
+            const int m = m0 + pl;
+            const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
+            const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
+            brow = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
+        }
+#pragma unroll
+        for (int ib = 0; ib < TNS / 2; ++ib) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int col = wn * 16 * TNS + 32 * ib + 8 * k + 4 * g;
+                const float4 bv = *(const float4*)(a.bias + brow + col);
+                float v0 = acc[ib][jb][4 * k] + bv.x, v1 = acc[ib][jb][4 * k + 1] + bv.y,
+                      v2 = acc[ib][jb][4 * k + 2] + bv.z, v3 = acc[ib][jb][4 * k + 3] + bv.w;
+                if (a.act) {
+                    const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                    v0 = s01[0];
+                    v1 = s01[1];
+                    v2 = s23[0];
+                    v3 = s23[1];
+                }
+                *(float4*)(Cs + pl * CW + col) = make_float4(v0, v1, v2, v3);
+            }
+        }
+    }
+    __syncthreads();
+    conv_epilogue_store<NT, BM, BN, OutT, RowFn, float>(a, smem, n0, tid, orow);
+}
+
 // FK (LDS-DMA form, Cin % 64 == 0): a 64-deep K-step never straddles a tap, so (ky, kx, channel base) are
 // wave-uniform scalars and each staged row keeps a precomputed base pointer: per K-step and row the B
 // address is one 64-bit add of a scalar offset plus a bounds select (the general form re-derives the
@@ -579,7 +632,9 @@ __device__ __forceinline__ void split3_bf16(const u32x4& c0, const u32x4& c1, bf
 // operands split into three exact bf16 terms (split3_bf16) and multiplied on v_mfma_f32_16x16x32_bf16 (16 cycles
 // per SIMD, 8x the K per instruction): the term products h.h, h.m, m.h, h.l, m.m, l.h (+ m.l, l.m, l.l for 9) are
 // exact in f32 and accumulated in f32; the three left out at 6 are <= 2^-23 of |a b| together, below one f32
-// rounding of the sum.
+// rounding of the sum.  SPL 16 (VA_F32_SPLIT=16, A/B only): the same six products on v_mfma_f32_32x32x16_bf16 (32 x 32
+// blocks, 32 cycles per SIMD with 24 of them free for the split's VALU, against 8 of 16 for 16x16x32) -- measured
+// 2-10 % slower on every layer of the s-seg forward (33.9 vs 32.2 ms per 128 frames, profiles/r03/ab_split_6_16.log).
 template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false,
           int SPL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
@@ -743,6 +798,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     for (int i = 0; i < TNS; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x16 acc32[SPL == 16 ? TNS / 2 : 1][2];  // SPL 16: 32 x 32 blocks (channels x pixels)
+#pragma unroll
+    for (int i = 0; i < (SPL == 16 ? TNS / 2 : 1); ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc32[i][j] = (f32x16){};
 
     const int nk = a.Kpad / KS;
     if constexpr (GLDS) {
@@ -766,6 +826,42 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         }
         const T* as_ = As(s);
         const T* bs_ = Bs(s);
+        if constexpr (SPL == 16) {
+            // the six term products on v_mfma_f32_32x32x16_bf16: lane (r, g) = (lane % 32, lane / 32) feeds row r
+            // of a 32-row block with the 8 K values of chunks 4 h + 2 g and 4 h + 2 g + 1 (K-half h of the step;
+            // the same K order for both operands).  A 32-cycle MFMA holds the SIMD's vector issue for 8 of its
+            // cycles (16x16x32: 8 of 16), so the split's VALU fits in the MFMA shadow
+            constexpr int CB = TNS / 2;
+            const int r32 = lane & 31, g32 = lane >> 5;
+            bf16x8 at[CB][2][3], bt[2][2][3];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c0 = 4 * h + 2 * g32;
+                const int s0 = GLDS ? ((c0 ^ (r32 & 7)) * VEC) : c0 * VEC;
+                const int s1 = GLDS ? (((c0 + 1) ^ (r32 & 7)) * VEC) : (c0 + 1) * VEC;
+#pragma unroll
+                for (int ib = 0; ib < CB; ++ib) {
+                    const T* rp = as_ + (wn * 16 * TNS + 32 * ib + r32) * RS;
+                    split3_bf16(*(const u32x4*)(rp + s0), *(const u32x4*)(rp + s1), at[ib][h]);
+                }
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb) {
+                    const T* rp = bs_ + (wm * 64 + 32 * jb + r32) * RS;
+                    split3_bf16(*(const u32x4*)(rp + s0), *(const u32x4*)(rp + s1), bt[jb][h]);
+                }
+            }
+            constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int ib = 0; ib < CB; ++ib)
+#pragma unroll
+                        for (int jb = 0; jb < 2; ++jb)
+                            acc32[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(at[ib][h][TA[t]], bt[jb][h][TB[t]],
+                                                                                    acc32[ib][jb], 0, 0, 0);
+        } else {
         // all fragments of the K-step first (the second half's reads overlap the first half's MFMAs)
         u32x4 af[2][TNS], bfr[2][4];
 #pragma unroll
@@ -837,6 +933,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                                                                              __uint_as_float(bfr[kh][j][e]),
                                                                              acc[i][j], 0, 0, 0);
         }
+        }  // SPL != 16
         if constexpr (GLDS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
@@ -858,7 +955,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             return;
         }
     }
-    conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
+    if constexpr (SPL == 16) {
+        static_assert(WM * 64 == BM && TNS % 2 == 0, "32 x 32 blocks: 64-pixel waves, even channel fragments");
+        conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc32, smem, n0, wm, wn, tid, lane, orow, m0, cls);
+    } else {
+        conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
+    }
 }
 
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
@@ -2401,7 +2503,7 @@ bool getenv_dn() {
 int f32_split() {
     const char* e = getenv("VA_F32_SPLIT");
     if (!e) return 6;
-    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
+    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : (e[0] == '1' && e[1] == '6') ? 16 : 0;
 }
 
 template <int SPL, typename OutT>
@@ -2474,6 +2576,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         if (a.Kpad % 32 == 0 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && (a.mode != 1 || (a.Cout / 4) % 4 == 0) &&
             getenv("VA_CONV_F32_OLD") == nullptr) {
             switch (f32_split()) {
+                case 16: return launch_conv2_f32<16, OutT>(a, st);
                 case 6: return launch_conv2_f32<6, OutT>(a, st);
                 case 9: return launch_conv2_f32<9, OutT>(a, st);
                 default: return launch_conv2_f32<0, OutT>(a, st);

@@ -59,19 +59,38 @@ class FramePipeline:
         """The device buffer (uint8 [B, Hn, Wn, 3]) the forward reads (the letterboxed frames, if any)."""
         return self.plan["frames"]
 
+    def _pinned(self, frames: torch.Tensor) -> torch.Tensor:
+        """Host frames (a camera's numpy frame, main.py:62-82) copied into a pinned staging buffer, so that the H2D
+        copy that follows is asynchronous on the launch stream (a pageable source makes it synchronous and staged
+        by the runtime).  The buffer is reused only after the previous copy out of it has completed (_pin_ev)."""
+        if getattr(self, "_pin", None) is None or self._pin.shape != frames.shape:
+            self._pin = torch.empty(frames.shape, dtype=frames.dtype, pin_memory=True)
+            self._pin_ev = None
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()
+        self._pin.copy_(frames)
+        return self._pin
+
     def load(self, frames: torch.Tensor, stream=None) -> None:
-        """Frames (uint8 BGR [B, H, W, 3] on the device) into the network's input buffer, letterboxed if needed."""
+        """Frames (uint8 BGR [B, H, W, 3], on the device or the host) into the network's input buffer, letterboxed
+        if needed, on the current stream; host frames go through a pinned staging buffer (_pinned)."""
+        staged = frames.device.type == "cpu" and not frames.is_pinned()
+        if staged:
+            frames = self._pinned(frames.contiguous())
         if self.lb is None:
             self.plan["frames"].copy_(frames, non_blocking=True)
-            return
-        if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
-            raise _lib.VaError(f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
-        frames = frames.to(self.device, non_blocking=True).contiguous()
-        Hn, Wn, top, left, newh, neww = self.lb
-        with torch.cuda.device(self.device):
-            _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream, self.device), frames.data_ptr(), self.B, self.H,
-                                             self.W, self.plan["frames"].data_ptr(), Hn, Wn, top, left, newh, neww),
-                       "va_letterbox")
+        else:
+            if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
+                raise _lib.VaError(f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
+            frames = frames.to(self.device, non_blocking=True).contiguous()
+            Hn, Wn, top, left, newh, neww = self.lb
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream, self.device), frames.data_ptr(), self.B,
+                                                 self.H, self.W, self.plan["frames"].data_ptr(), Hn, Wn, top, left,
+                                                 newh, neww), "va_letterbox")
+        if staged:
+            self._pin_ev = torch.cuda.Event()
+            self._pin_ev.record(torch.cuda.current_stream(self.device))
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:

@@ -51,7 +51,7 @@ class MaskSelectArgs(ctypes.Structure):  # va_mask_select_args
 CSTAT_DTYPE = [("npts", "<i4"), ("ox", "<i4"), ("oy", "<i4"), ("ncont", "<i4"), ("X0", "<i4"), ("Y0", "<i4"),
                ("status", "<i4"), ("half", "<i4"), ("area", "<f8")]
 CONTOUR_SLOTS = int(os.environ.get("VA_CT_SLOTS", "1024"))  # contour scratch slots: one wave each, 4 per CU
-CONTOUR_CAP = 16384    # points of the chosen contour per frame (the fill kernel's buffer)
+CONTOUR_CAP = 16384    # points of the fill kernel's buffer per pass (a longer chosen contour takes several passes)
 CONTOUR_PTS = 1024     # points kept per instance and buffer half (va_post_args.cpts_cap); longer: followed again
 
 
@@ -186,16 +186,18 @@ class PostEngine:
         return out, raw[:, 6].clone()
 
 
-def select_masks(masks: torch.Tensor, nmask: torch.Tensor, H0: int, W0: int, poly_cap: int = 4096, stream=None):
+def select_masks(masks: torch.Tensor, nmask: torch.Tensor, H0: int, W0: int, poly_cap: int = 4096, stream=None,
+                 cap: int = CONTOUR_CAP):
     """The mask -> polygon -> cells boundary (va_post_select_masks) on given binary masks uint8 [B, maxn, Hn, Wn]
-    (device) with nmask[b] masks in frame b, mapped onto an H0 x W0 frame as scale_coords does.
+    (device) with nmask[b] masks in frame b, mapped onto an H0 x W0 frame as scale_coords does.  cap: points of
+    the fill kernel's buffer per pass (a longer chosen contour is taken in several passes; >= CONTOUR_PTS).
     -> dict(cells [B, H0/20, W0/20], rects [B, 4], chosen [B], status [B], cstats [B, maxn], polys list per frame)."""
     import numpy as np
     lib = _lib.load()
     dev = masks.device
     B, maxn, Hn, Wn = masks.shape
     gain, padx, pady = scale_coords_params(Hn, Wn, H0, W0)
-    scratch = contour_scratch(Hn, Wn, device=dev)
+    scratch = contour_scratch(Hn, Wn, cap=cap, device=dev)
     cstats = torch.empty((B, maxn, ctypes.sizeof(ContourStat)), dtype=torch.uint8, device=dev)
     cells = torch.empty((B, H0 // 20, W0 // 20), dtype=torch.uint8, device=dev)
     rects = torch.empty((B, 4), dtype=torch.int32, device=dev)
@@ -208,7 +210,7 @@ def select_masks(masks: torch.Tensor, nmask: torch.Tensor, H0: int, W0: int, pol
     m = masks.contiguous()
     a = MaskSelectArgs(masks=m.data_ptr(), nmask=nm.data_ptr(), B=B, maxn=maxn, Hn=Hn, Wn=Wn, H0=H0, W0=W0,
                        gain=gain, padx=padx, pady=pady, scratch=scratch.data_ptr(), nslots=CONTOUR_SLOTS,
-                       cap=CONTOUR_CAP, cstats=cstats.data_ptr(), cells=cells.data_ptr(), rects=rects.data_ptr(),
+                       cap=cap, cstats=cstats.data_ptr(), cells=cells.data_ptr(), rects=rects.data_ptr(),
                        chosen=chosen.data_ptr(), status=status.data_ptr(), polys=polys.data_ptr(), poly_n=pn.data_ptr(),
                        cpts=cpts.data_ptr(), poly_cap=poly_cap, cpts_cap=CONTOUR_PTS)
     with torch.cuda.device(dev):

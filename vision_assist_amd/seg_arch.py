@@ -30,6 +30,16 @@ BN_EPS = 1e-3
 REG_MAX = 16
 NM = 32  # mask coefficients
 STRIDES = (8, 16, 32)
+# the 'sparse' regime (synthetic_state_dict(sparse=640 | 1280)): per (scale, network side, seed) and head level, the
+# class-0 logit (bias 0, solid masks) that one anchor per frame exceeds on average over seeded uniform-noise
+# frames (tools/sparse_calib.py, on the oracle forward); class 0's weights are scaled by SPARSE_GAIN and its
+# bias set to -SPARSE_GAIN * threshold, every other class is off, so a frame keeps ~1-5 detections
+SPARSE_GAIN = 10.0
+SPARSE_THRESHOLDS = {
+    ("s", 640, 0): (0.234166, 0.323434, 0.273133),
+    ("n", 640, 0): (0.553922, 56.835182, 18.296261),
+    ("m", 1280, 0): (287.544861, 125.099106, 66.233734),
+}
 
 
 def _make_div(x: float, d: int = 8) -> int:
@@ -165,14 +175,18 @@ def learnable_params(arch: Arch) -> int:
     return n
 
 
-def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = None, solid_masks: bool = False) -> dict:
+def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = None, solid_masks: bool = False,
+                         sparse: int | None = None) -> dict:
     """Seeded synthetic weights in Ultralytics state-dict layout (fp32, CPU).
 
     cls_bias: None -> Ultralytics' prior (Detect.bias_init: log(5 / nc / (640 / stride)^2));
     a number -> every class bias set to it (the 'dense' regime uses +4).
     solid_masks: the prototypes made constant (proto.cv3's BN scale 0: channel 0 = SiLU(3), the others SiLU(0) = 0)
     and mask coefficient 0 fixed at +5, so every instance mask is its whole box -- one compact blob per detection,
-    as a trained model's masks are, instead of the random weights' noise (the 'dense_box' regime)."""
+    as a trained model's masks are, instead of the random weights' noise (the 'dense_box' regime).
+    sparse: the network side (640 / 1280) of a 'sparse' regime -- solid masks, one live class whose per-level
+    bias leaves ~1-5 detections per noise frame (SPARSE_THRESHOLDS), the rest off: a trained model's
+    few-object frames."""
     sd = {}
     for idx, (prefix, kind, ci, co, k) in enumerate(arch.conv_specs()):
         g = torch.Generator().manual_seed(seed * 100003 + idx)
@@ -201,6 +215,17 @@ def synthetic_state_dict(arch: Arch, seed: int = 0, cls_bias: float | None = Non
             else:
                 b = torch.randn(co, generator=g) * 0.1
             sd[f"{prefix}.bias"] = b
+    if sparse is not None:
+        key = (arch.scale, int(sparse), seed)
+        if key not in SPARSE_THRESHOLDS:
+            raise KeyError(f"no sparse calibration for {key}: run tools/sparse_calib.py")
+        for lvl, t in enumerate(SPARSE_THRESHOLDS[key]):
+            q = f"model.22.cv3.{lvl}.2"
+            sd[f"{q}.weight"][0].mul_(SPARSE_GAIN)
+            sd[f"{q}.weight"][1:].zero_()
+            sd[f"{q}.bias"][0] = -SPARSE_GAIN * t
+            sd[f"{q}.bias"][1:] = -50.0
+        solid_masks = True
     if solid_masks:
         p = "model.22.proto.cv3"
         sd[f"{p}.bn.weight"] = torch.zeros_like(sd[f"{p}.bn.weight"])

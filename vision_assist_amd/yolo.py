@@ -44,7 +44,9 @@ class Results:
 
 class YOLO:
     def __init__(self, model: str = "yolov8s-seg.pt", task: str | None = None, *, dtype: str = "f32", nc: int = 80,
-                 seed: int = 0, cls_bias: float | None = None):
+                 seed: int = 0, cls_bias: float | None = None, sparse: int | None = None, solid_masks: bool = False):
+        """model: a .safetensors state dict with Ultralytics key names, or a yolov8{n,s,m}-seg name (seeded
+        synthetic weights; cls_bias / sparse / solid_masks select the synthetic regime, seg_arch.synthetic_state_dict)."""
         name = os.path.basename(str(model))
         if str(model).endswith(".safetensors") and os.path.exists(model):
             from safetensors.torch import load_file
@@ -60,7 +62,7 @@ class YOLO:
             self.arch = Arch(m.group(1), nc)
             warnings.warn(f"{model}: no local weights, using seeded synthetic yolov8{m.group(1)}-seg weights "
                           "(nothing is downloaded)")
-            sd = synthetic_state_dict(self.arch, seed=seed, cls_bias=cls_bias)
+            sd = synthetic_state_dict(self.arch, seed=seed, cls_bias=cls_bias, sparse=sparse, solid_masks=solid_masks)
         self.folded = fold(self.arch, sd)
         self.dtype = dtype
         self.device = None
@@ -94,7 +96,7 @@ class YOLO:
             t = torch.as_tensor(fr) if not isinstance(fr, torch.Tensor) else fr
             H, W = int(t.shape[0]), int(t.shape[1])
             pipe = self.pipeline(H, W, conf, iou, max_det, imgsz=imgsz)
-            pipe.load(t.reshape(1, H, W, 3).to(pipe.device))  # letterboxed to the network input if needed
+            pipe.load(t.reshape(1, H, W, 3))  # pinned-staged H2D, letterboxed to the network input if needed
             pipe.seg.run_plan(pipe.plan)
             o = pipe.plan["out"]
             pipe.post.run(o.levels, o.proto, select=True)
