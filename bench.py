@@ -357,8 +357,8 @@ def c4_rate(args, dev, rank, world, prof) -> dict:
 def c2_latency(args, dev, iters=200) -> dict:
     """C2 (BASELINE.json configs[1]): YOLOv8n-seg 640x640 bf16, batch 1, one frame resident in HBM, synchronised
     after every frame; median / p90 of the seg kernels alone and of the whole path (network masks of the sparse
-    regime, a planted corridor when a frame has none).  Also the network + post-processing replayed as one HIP
-    graph on its own stream (the grid stage reads a device flag per A* round on the host, so it stays eager)."""
+    regime, a planted corridor when a frame has none), eager launches on a stream of the run's own (the
+    graph-replayed form is tools/latency.py --graph: it measured within 1 % of eager)."""
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_IF_NONE
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
@@ -373,26 +373,11 @@ def c2_latency(args, dev, iters=200) -> dict:
                           dtype=torch.uint8).to(dev)
     st = torch.cuda.Stream(device=dev)
     st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        for _ in range(3):
-            pipe.load(frame, stream=st)
-            pipe.seg_post(pc, pr, PLANT_IF_NONE, stream=st)
-        st.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=st):
-            pipe.load(frame, stream=st)
-            pipe.seg_post(pc, pr, PLANT_IF_NONE, stream=st)
-    torch.cuda.synchronize()
-
-    def graph_e2e():
-        graph.replay()
-        pipe.nav_run(stream=st)
 
     out = {"workload": "C2 (BASELINE.json configs[1]): YOLOv8n-seg 640x640 bf16, batch 1, 1 MI355X; frame resident "
                        "in HBM, synchronised per frame", "iters": iters, "regime": args.regime}
     for name, fn in (("seg_only", lambda: pipe.run_seg_only(stream=st)),
-                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_IF_NONE, stream=st)),
-                     ("end_to_end_graph", graph_e2e)):
+                     ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_IF_NONE, stream=st))):
         with torch.cuda.stream(st):
             for _ in range(20):
                 fn()
@@ -406,7 +391,7 @@ def c2_latency(args, dev, iters=200) -> dict:
         ts = np.array(ts) * 1e3
         out[name] = {"median_ms": round(float(np.median(ts)), 4), "p90_ms": round(float(np.percentile(ts, 90)), 4)}
     out["ndet_last_frame"] = int(pipe.post.ndet[0])
-    del graph, pipe
+    del pipe
     gc.collect()
     torch.cuda.empty_cache()
     return out

@@ -76,20 +76,28 @@ def build_grids(mask_img: np.ndarray, rect: tuple[int, int, int, int], H: int, W
     w = w + (GRID - w % GRID) if w % GRID != 0 else w
     w = W if w > W else w
     h = h + (GRID - h % GRID) if h % GRID != 0 else h
-    j_vals = list(range(x, x + w, GRID))  # :88-89
-    i_vals = list(range(y, y + h, GRID))
+    # the reference's own structure from here (:85-97): the filled frame-size mask image, numpy coordinate
+    # vectors, the centre grid and one numpy lookup per centre (timed as the CPU baseline)
+    mask = np.zeros((H, W), dtype=np.uint8)
+    mask[:] = mask_img
+    j_np = np.arange(x, x + w, GRID)  # :88-89
+    i_np = np.arange(y, y + h, GRID)
     half = GRID // 2
-    in_mask = [[mask_img[i + half, j + half] > 0 for j in j_vals] for i in i_vals]  # :94-97
-    if not any(any(r) for r in in_mask):  # :99-101
+    J, I = np.meshgrid(j_np + half, i_np + half)
+    centers = np.stack((J, I), axis=-1).reshape(-1, 2)
+    in_np = np.array([mask[pt[1], pt[0]] > 0 for pt in centers]).reshape(len(i_np), len(j_np))  # :94-97
+    if not np.any(in_np):  # :99-101
         return st
-    for r, i in enumerate(i_vals):  # :104-124
+    for r, i in enumerate(i_np):  # :104-124 (numpy coordinates, as the reference iterates them)
         row = []
-        for c, j in enumerate(j_vals):
-            cell = Cell(coords=Coordinate(x=j, y=i), centre=Coordinate(x=j + half, y=i + half),
-                        penalty=None, row=r, col=c, empty=not in_mask[r][c], artificial=False)
+        for c, j in enumerate(j_np):
+            centre = Coordinate(x=(j + half), y=(i + half))
+            cell = Cell(coords=Coordinate(x=j, y=i), centre=centre, penalty=None, row=r, col=c,
+                        empty=not in_np[r, c], artificial=False)
             row.append(cell)
-            st.lookup[(j, i)] = cell
+            st.lookup[(int(j), int(i))] = cell
         st.grids.append(row)
+    j_vals = [int(v) for v in j_np]
     start_y = int(H * 0.875)  # :126-127
     start_y = start_y + (GRID - start_y % GRID) % GRID
     for i in range(start_y, H, GRID):  # :130-165
@@ -138,12 +146,13 @@ def _segment_penalty(cell: Cell, lookup, easy, direction: str) -> float:
     key = cell.row if direction == "row" else cell.col  # Q11: attribute, not list index
     if key in easy:
         left, right = easy[key]
-    else:
+    else:  # the walks build a Coordinate per step, as the reference does (:76-97)
         while True:
             nxt = (x - GRID, y) if direction == "row" else (x, y - GRID)
             if nxt not in lookup or lookup[nxt].empty:
                 left = Coordinate(x=x, y=y)
                 break
+            left = Coordinate(x=nxt[0], y=nxt[1])
             x, y = nxt
         x, y = s.x, s.y
         while True:
@@ -151,6 +160,7 @@ def _segment_penalty(cell: Cell, lookup, easy, direction: str) -> float:
             if nxt not in lookup or lookup[nxt].empty:
                 right = Coordinate(x=x, y=y)
                 break
+            right = Coordinate(x=nxt[0], y=nxt[1])
             x, y = nxt
     den = right.x - left.x if direction == "row" else right.y - left.y
     if den == 0:
@@ -204,19 +214,36 @@ def create_graph(st: GridState):
 
 
 # ----------------------------------------------------------------------------- protrusions
+class Peak(BaseModel):  # models.py:38-42
+    centre: Coordinate
+    left: Coordinate | None = None
+    right: Coordinate | None = None
+    orientation: str
+
+
+def _fill_square(binary: np.ndarray, corners: np.ndarray) -> None:
+    """cv2.fillPoly(binary, [corners], 255) for the 4 corners of an axis-aligned square (inclusive edges,
+    clipped to the image) -- what the reference's per-cell fillPoly produces (:53)."""
+    x0, y0 = corners.min(0)
+    x1, y1 = corners.max(0)
+    binary[max(0, y0):y1 + 1, max(0, x0):x1 + 1] = 255
+
+
 def protrusion_peaks(st: GridState) -> list[tuple[int, int]]:
-    """ProtrusionDetector.__call__ live path (ProtrusionDetector.py:419-439,535):
-    raster the non-empty cells as inclusive 21x21 squares (cv2.fillPoly of the
-    4 corners, :41-55, clipped to the frame), take the top-most pixel row, split
-    its sorted xs at gaps > grid_size//4 and return each group's middle x
-    (:77-99,151-156)."""
+    """ProtrusionDetector.__call__ live path (ProtrusionDetector.py:419-439,535) with the reference's structure:
+    _create_binary_image (:38-57: per non-empty cell a 4-corner int32 array and a fill of that square, then the
+    binary threshold over the frame), _find_peak on the whole frame (:59-158: np.where of the binary image, the
+    top-most row's sorted xs split at gaps > grid_size//4, per group its middle x, the vertical slice below it,
+    height / width / upward test and orientation, a Peak object), the global peaks' centres returned (:535)."""
     binary = np.zeros((st.H, st.W), dtype=np.uint8)
     for row in st.grids:
         for cell in row:
             if cell.empty:
                 continue
             x, y = cell.coords.x, cell.coords.y
-            binary[max(0, y):y + GRID + 1, max(0, x):x + GRID + 1] = 255
+            corners = np.array([[x, y], [x + GRID, y], [x + GRID, y + GRID], [x, y + GRID]], np.int32)
+            _fill_square(binary, corners)
+    binary = np.where(binary > 127, 255, 0).astype(np.uint8)  # cv2.threshold(binary, 127, 255, THRESH_BINARY)
     ys, xs = np.where(binary == 255)
     if not ys.size:
         return []
@@ -224,7 +251,20 @@ def protrusion_peaks(st: GridState) -> list[tuple[int, int]]:
     px = np.sort(xs[ys == min_y])
     gaps = np.diff(px)
     groups = np.split(px, np.where(gaps > (GRID // 4))[0] + 1)
-    return [(int(g[len(g) // 2]), int(min_y)) for g in groups]
+    peaks = []
+    for g in groups:
+        cx = int(g[len(g) // 2])
+        sel = (xs >= cx - GRID // 2) & (xs <= cx + GRID // 2)
+        vy = ys[sel]
+        if len(vy) == 0:
+            continue
+        height = np.max(vy) - min_y
+        width = np.max(xs) - np.min(xs)
+        upward = height > width * 0.5 and len(vy) > height * 0.5
+        orientation = "up" if upward else "right" if cx > np.mean(xs) else "left"
+        peaks.append(Peak(centre=Coordinate(x=cx, y=int(min_y)), left=Coordinate(x=int(g[0]), y=int(min_y)),
+                          right=Coordinate(x=int(g[-1]), y=int(min_y)), orientation=orientation))
+    return [(p.centre.x, p.centre.y) for p in peaks]
 
 
 # ----------------------------------------------------------------------------- start / end
