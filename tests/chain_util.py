@@ -142,9 +142,47 @@ def load_fixture(name: str) -> list[dict]:
         det = np.frombuffer(base64.b64decode(r["det"]), np.float32).reshape(r["ndet"], 6).copy()
         cells = None
         if r["cells"] is not None:
-            cells = np.frombuffer(base64.b64decode(r["cells"]), np.uint8).reshape(32, 32).copy()
+            shape = tuple(r.get("cells_shape") or (32, 32))
+            cells = np.frombuffer(base64.b64decode(r["cells"]), np.uint8).reshape(shape).copy()
         out.append({"det": torch.from_numpy(det), "chosen": r["chosen"],
                     "rect": tuple(r["rect"]) if r["rect"] is not None else None, "cells": cells,
                     "paths": [[tuple(p) for p in q] for q in r["paths"]] if r["paths"] is not None else None,
                     "costs": r["costs"]})
     return out
+
+
+FRAMES_DIR = __file__.rsplit("/", 1)[0] + "/golden/frames"
+
+
+def real_frames(n: int = 8) -> np.ndarray:
+    """The reference's own validation frames (model/valid/images, 640 x 640 camera frames of paths; copied as data
+    into tests/golden/frames) as uint8 BGR [n, 640, 640, 3] -- the channel order cv2 delivers (main.py:62-70)."""
+    from PIL import Image
+    out = []
+    for i in range(n):
+        rgb = np.asarray(Image.open(f"{FRAMES_DIR}/valid_{i}.jpg").convert("RGB"))
+        out.append(rgb[..., ::-1])
+    return np.ascontiguousarray(np.stack(out))
+
+
+def mosaic_1280(frames: np.ndarray) -> np.ndarray:
+    """2 x 2 mosaics of consecutive 640 x 640 frames: real content at C5's 1280 x 1280 network size."""
+    n = frames.shape[0] // 4
+    out = np.zeros((n, 1280, 1280, 3), np.uint8)
+    for k in range(n):
+        f = frames[4 * k:4 * k + 4]
+        out[k, :640, :640], out[k, :640, 640:], out[k, 640:, :640], out[k, 640:, 640:] = f
+    return out
+
+
+def label_polygons(i: int, H: int = 640, W: int = 640) -> list[np.ndarray]:
+    """The segmentation labels of validation frame i (YOLO-seg txt: class x1 y1 x2 y2 ..., normalised) as int32
+    pixel polygons -- real path shapes as annotated for the reference's model (model/valid/labels)."""
+    polys = []
+    with open(f"{FRAMES_DIR}/valid_{i}.txt") as f:
+        for line in f:
+            v = [float(t) for t in line.split()[1:]]
+            if len(v) >= 6:
+                p = np.array(v, np.float64).reshape(-1, 2) * (W, H)
+                polys.append(np.clip(np.round(p), 0, [W - 1, H - 1]).astype(np.int32))
+    return polys

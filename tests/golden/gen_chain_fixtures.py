@@ -10,6 +10,8 @@ Sets:
                   sparse / dense / dense_box (s-seg 640);
   c4/<regime>:    frames frame_batch(7000 + i, 1), i < 8, dealt round-robin to 2 ranks; one PathFinder state
                   per shard, frames in shard order (SURVEY.md §8e per-shard replay); regimes sparse / dense_box.
+  c5/<regime>:    YOLOv8m-seg at 1280 x 1280 (BASELINE configs[4]), frames frame_batch(8000, 4, 1280), one
+                  PathFinder state; regimes sparse / dense_box (the fp8 chain test's reference).
 
 Per frame: det float32 [k, 6] (x1 y1 x2 y2 score cls, base64), chosen index, rect, cells uint8 [32, 32]
 (base64), A* paths and float64 costs (hex).  Re-run:  python tests/golden/gen_chain_fixtures.py  (~5 min, 8 CPUs)
@@ -29,15 +31,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "chain_oracle.json.gz")
-CHAIN_FRAMES, C4_FRAMES, C4_WORLD = 16, 8, 2
+CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 16, 8, 2, 4
 
 
 def _enc(rec: dict) -> dict:
+    """One oracle record; cells travel as raw bytes with their shape."""
     det = rec["det"].numpy().astype(np.float32)
     out = {"det": base64.b64encode(det.tobytes()).decode(), "ndet": int(det.shape[0]), "chosen": int(rec["chosen"]),
            "rect": list(rec["rect"]) if rec["rect"] is not None else None, "paths": rec["paths"], "costs": rec["costs"]}
     out["cells"] = base64.b64encode(np.ascontiguousarray(rec["cells"], np.uint8).tobytes()).decode() \
         if rec["cells"] is not None else None
+    out["cells_shape"] = list(rec["cells"].shape) if rec["cells"] is not None else None
     return out
 
 
@@ -51,6 +55,10 @@ def _job(args):
     arch, fw = weights(regime)
     if kind == "chain":
         return f"chain/{regime}", [_enc(r) for r in oracle_sequence(arch, fw, frame_batch(21, CHAIN_FRAMES))]
+    if kind == "c5":
+        arch, fw = weights(regime, scale="m")
+        torch.set_num_threads(4)
+        return f"c5/{regime}", [_enc(r) for r in oracle_sequence(arch, fw, frame_batch(8000, C5_FRAMES, 1280))]
     recs = [None] * C4_FRAMES
     for r in range(C4_WORLD):
         pf = onav.PathFinderOracle()
@@ -60,9 +68,16 @@ def _job(args):
 
 
 def main():
-    jobs = [("chain", r) for r in ("sparse", "dense", "dense_box")] + [("c4", r) for r in ("sparse", "dense_box")]
+    only = sys.argv[1:]  # optional set names to (re)generate, the rest kept from the existing file
+    jobs = [("chain", r) for r in ("sparse", "dense", "dense_box")] + [("c4", r) for r in ("sparse", "dense_box")] + \
+        [("c5", r) for r in ("sparse", "dense_box")]
+    old = {}
+    if only and os.path.exists(OUT):
+        with gzip.open(OUT, "rt") as f:
+            old = json.load(f)
+        jobs = [j for j in jobs if f"{j[0]}/{j[1]}" in only]
     with ProcessPoolExecutor(max_workers=len(jobs)) as ex:
-        out = dict(ex.map(_job, jobs))
+        out = {**old, **dict(ex.map(_job, jobs))}
     with gzip.open(OUT, "wt") as f:
         json.dump(out, f)
     print("wrote", OUT, {k: [r["ndet"] for r in v] for k, v in out.items()})

@@ -24,7 +24,7 @@ from .seg import SegNet
 class FramePipeline:
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", conf: float = 0.5,
                  iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None,
-                 seg: SegNet | None = None, tag: int = 0, imgsz: int | None = None):
+                 seg: SegNet | None = None, tag: int = 0, imgsz: int | None = None, fp8_calib=None):
         """H x W: the frame size.  ``imgsz`` = YOLO.predict's imgsz: frames are letterboxed to it on the device
         (va_letterbox; LetterBox(imgsz, auto=True, scaleup=True)) whenever that changes them -- the 640
         default of the reference's model.predict call -- and the mask choice maps back to frame coordinates,
@@ -48,6 +48,8 @@ class FramePipeline:
             frame = (H, W, gain, pad_x, pad_y)
         self.Hn, self.Wn = Hn, Wn
         self.seg = seg if seg is not None else SegNet(arch, folded, dtype=dtype, device=self.device)
+        if fp8_calib is not None:  # fp8: representative frames (uint8 [n, Hn, Wn, 3]) for the activation scales
+            self.seg.fp8_calib_frames = torch.as_tensor(fp8_calib)
         self.plan = self.seg.plan(B, Hn, Wn, tag)
         self.post = PostEngine(B, Hn, Wn, arch.nc, conf, iou, max_det, device=self.device, frame=frame)
         self.nav = NavEngine(H, W, max_batch=B, device=self.device)

@@ -26,6 +26,7 @@ from .seg_arch import NM, REG_MAX, Arch
 VA_DTYPE_BF16, VA_DTYPE_F32, VA_DTYPE_FP8 = 1, 2, 3
 F8_KS = 128        # K-step of the fp8 kernel (va_fp8.hip): fp8 weights are padded to it
 F8_MAX = 448.0     # largest OCP e4m3 value
+FP8_HEADROOM = 2.0  # calibration amax x this maps to [224, 448] (SegNet.calibrate_fp8)
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -155,6 +156,11 @@ class SegNet:
         self.w8 = {}
         self.xscale = None   # per fp8 conv: its input's scale (calibrate_fp8)
         self.bscale = None   # per activation buffer of the plan, in creation order (calibrate_fp8)
+        # fp8 calibration: frames to calibrate on (uint8 [n, H, W, 3]; None = 2 seeded noise frames) and the
+        # headroom factor above the calibration amax (real frames on trained weights can exceed the
+        # calibration frames' amax; 2 keeps amax in [112, 224], one binade below e4m3's 448)
+        self.fp8_calib_frames = None
+        self.fp8_headroom = FP8_HEADROOM
         if dtype == "fp8":
             for prefix, p in self.w.items():
                 if p.cin % 16 == 0:
@@ -172,15 +178,23 @@ class SegNet:
         q = w8.to(torch.float8_e4m3fn).view(torch.uint8)
         return q.to(self.device).contiguous(), sw.to(self.device).contiguous(), Kp
 
-    def calibrate_fp8(self, H: int, W: int, frames_u8: torch.Tensor | None = None, seed: int = 0) -> dict:
+    def calibrate_fp8(self, H: int, W: int, frames_u8: torch.Tensor | None = None, seed: int = 0,
+                      headroom: float | None = None) -> dict:
         """Static scales of the fp8 mode: one forward of this network in bf16 (same weights, the same buffers in
-        the same order) on `frames_u8` (default: 2 seeded uniform uint8 frames, the bench's input distribution).
-        Every activation buffer gets the power of two s with amax * s in [224, 448], amax the largest |x| it held
-        there; buffers an upsample copies between share one scale (the copy moves bytes).  Values are stored as
-        sat(x * s) in e4m3.  -> {conv prefix: its input's scale}."""
+        the same order) on `frames_u8` (default: self.fp8_calib_frames, else 2 seeded uniform uint8 frames, the
+        bench's input distribution).  Every activation buffer gets the power of two s with amax * headroom * s in
+        [224, 448] (headroom default self.fp8_headroom), amax the largest |x| it held there; buffers an upsample
+        copies between share one scale (the copy moves bytes).  Values are stored as sat(x * s) in e4m3, so the
+        accuracy depends on how well the calibration frames cover the deployment's activations: pass
+        representative frames (FramePipeline / YOLO fp8_calib).  -> {conv prefix: its input's scale}."""
+        hr = float(self.fp8_headroom if headroom is None else headroom)
+        if frames_u8 is None:
+            frames_u8 = self.fp8_calib_frames
         if frames_u8 is None:
             g = torch.Generator().manual_seed(seed)
             frames_u8 = torch.randint(0, 256, (2, H, W, 3), generator=g, dtype=torch.uint8)
+        if tuple(frames_u8.shape[1:]) != (H, W, 3):
+            raise _lib.VaError(f"fp8 calibration frames {tuple(frames_u8.shape)} for a {H}x{W} network")
         B = frames_u8.shape[0]
         p = self.plan(B, H, W, tag=-1, _calib=True)
         p["frames"].copy_(frames_u8.to(self.device), non_blocking=True)
@@ -203,7 +217,7 @@ class SegNet:
             r = find(i)
             gmax[r] = max(gmax.get(r, 0.0), m)
         # a power of two (exact in the kernels' conversions): amax lands in [224, 448]
-        self.bscale = [2.0 ** math.floor(math.log2(F8_MAX / gmax[find(i)])) if gmax[find(i)] > 0 else 1.0
+        self.bscale = [2.0 ** math.floor(math.log2(F8_MAX / (hr * gmax[find(i)]))) if gmax[find(i)] > 0 else 1.0
                        for i in range(len(bufs))]
         index = {t.data_ptr(): i for i, t in enumerate(bufs)}
         self.xscale = {m["prefix"]: self.bscale[index[m["src"].buf.data_ptr()]] for m in p["meta"]

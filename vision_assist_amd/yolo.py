@@ -65,6 +65,7 @@ class YOLO:
             sd = synthetic_state_dict(self.arch, seed=seed, cls_bias=cls_bias, sparse=sparse, solid_masks=solid_masks)
         self.folded = fold(self.arch, sd)
         self.dtype = dtype
+        self.fp8_calib = None  # fp8: representative frames for the activation scales (SegNet.calibrate_fp8)
         self.device = None
         self._pipes = {}
 
@@ -85,7 +86,8 @@ class YOLO:
             if self.device is None:
                 self.to("cuda")
             self._pipes[key] = FramePipeline(self.arch, self.folded, 1, H, W, dtype=self.dtype, conf=conf, iou=iou,
-                                             max_det=max_det, device=self.device, seen=seen, imgsz=imgsz)
+                                             max_det=max_det, device=self.device, seen=seen, imgsz=imgsz,
+                                             fp8_calib=self.fp8_calib)
         return self._pipes[key]
 
     def predict(self, source, conf: float = 0.5, verbose: bool = False, iou: float = 0.7, max_det: int = 300,
