@@ -215,6 +215,11 @@ typedef struct va_conv_args {
     int32_t x8;
     float yscale;
     float rscale;
+    /* VA_DTYPE_F32 only: the weights pre-split into their three exact bf16 terms h, m, l (x = h + m + l, each the
+     * round-to-nearest bf16 of what remains), [Npad][Kpad / 8][3][8] -- per 8-channel K group the 8 h, then the
+     * 8 m, then the 8 l.  When set (and Cin % 16 == 0, Npad % 128 == 0, K == Kpad, mode 0 or 2) the conv runs on
+     * the three-plane kernel (va_seg.hip conv3t_kernel); NULL keeps conv2's in-loop split. */
+    const void* w3;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

@@ -54,3 +54,21 @@ def test_term_products_exact_and_dropped_terms_small():
     nz = ab != 0
     rel = np.abs(six - ab)[nz] / np.abs(ab)[nz]
     assert rel.max() < 2.0 ** -22
+
+
+def test_host_split_of_the_weights_matches_the_device_split():
+    """seg.split3_bf16 (the pre-split weights of va_conv_args.w3, conv3t_kernel) gives the same three terms as the
+    device's split (restated above) and h + m + l == x exactly, in the [K/8][3][8] layout."""
+    import torch
+
+    from vision_assist_amd.seg import split3_bf16
+    x = _samples(20_000)
+    x = x[: (len(x) // 64) * 64].reshape(-1, 64)
+    t = split3_bf16(torch.from_numpy(x)).float().numpy()  # [rows, 8, 3, 8]
+    h, m, _, lb = split3(x)
+    g = x.shape[:-1] + (8, 8)
+    assert np.array_equal(t[..., 0, :], h.reshape(g))
+    assert np.array_equal(t[..., 1, :], m.reshape(g))
+    assert np.array_equal(t[..., 2, :], lb.reshape(g))
+    s = (t[..., 0, :].astype(np.float64) + t[..., 1, :] + t[..., 2, :]).reshape(x.shape)
+    assert np.array_equal(s, x.astype(np.float64))

@@ -17,6 +17,7 @@
 //   sppf_pool_kernel<T>     SPPF's three chained MaxPool2d(5,1,2) as one pass: 5x5, 9x9, 13x13 maxima
 //   upsample2x_kernel<T>    nearest x2 into a concat slice
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -297,7 +298,13 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 //     covers 16 distinct slots of the 256-byte bank row (conflict-free).  Out-of-image / K-tail
 //     chunks are fetched from a zeroed device page.
 constexpr int BK2 = 64;
-__device__ __attribute__((aligned(16))) unsigned int g_zero_page[4];
+__device__ __attribute__((aligned(16))) unsigned int g_zero_page[8];  // 32 zero bytes (conv3t reads two 16-byte words)
+// diagnosis builds only (tools/build_variant.sh ... -DCONV2_ABL=N; wrong results): ablations of conv2's three-term
+// K-loop -- 1 = no DMA after the first K-step (compute on stale stages), 2 = one MFMA per K-step instead of 96,
+// 3 = no split (the raw f32 words reinterpreted as the three bf16 terms); 0 (the library) = none
+#ifndef CONV2_ABL
+#define CONV2_ABL 0
+#endif
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -526,15 +533,25 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
             brow[j] = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
         }
     }
+    // bias (and fp8 weight scales) loaded up front: under the a.act branch below each load would otherwise be
+    // waited for on its own (vmcnt(0) per fragment)
+    float4 bvs[TNS][4], svs[TNS];
+#pragma unroll
+    for (int i = 0; i < TNS; ++i) {
+        const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+        if constexpr (F8) svs[i] = *(const float4*)(a.wscale + n0 + col);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bvs[i][j] = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
+    }
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
         const int col = wn * 16 * TNS + 16 * i + 4 * fq;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float4 bv = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
+            const float4 bv = bvs[i][j];
             f32x4 ac = acc[i][j];
             if constexpr (F8) {
-                const float4 sv = *(const float4*)(a.wscale + n0 + col);
+                const float4 sv = svs[i];
                 ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
             }
             float v0 = ac[0] + bv.x, v1 = ac[1] + bv.y, v2 = ac[2] + bv.z, v3 = ac[3] + bv.w;
@@ -562,6 +579,7 @@ __device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
     const int r = lane & 31, g = lane >> 5;
+    float4 bvs[2][TNS / 2][4];  // loaded up front (see conv_epilogue)
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
         const int pl = wm * 64 + 32 * jb + r;
@@ -573,11 +591,20 @@ __device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&
             brow = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
         }
 #pragma unroll
+        for (int ib = 0; ib < TNS / 2; ++ib)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bvs[jb][ib][k] = *(const float4*)(a.bias + brow + wn * 16 * TNS + 32 * ib + 8 * k + 4 * g);
+    }
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+        const int pl = wm * 64 + 32 * jb + r;
+#pragma unroll
         for (int ib = 0; ib < TNS / 2; ++ib) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int col = wn * 16 * TNS + 32 * ib + 8 * k + 4 * g;
-                const float4 bv = *(const float4*)(a.bias + brow + col);
+                const float4 bv = bvs[jb][ib][k];
                 float v0 = acc[ib][jb][4 * k] + bv.x, v1 = acc[ib][jb][4 * k + 1] + bv.y,
                       v2 = acc[ib][jb][4 * k + 2] + bv.z, v3 = acc[ib][jb][4 * k + 3] + bv.w;
                 if (a.act) {
@@ -818,7 +845,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int s = kt & 1;
         const bool more = kt + 1 < nk;
         if constexpr (GLDS) {
-            if (more) {
+            if (more && !(SPL > 0 && SPL != 16 && CONV2_ABL == 1)) {
                 CONV2_DMA((kt + 1) * KS, s ^ 1);
             }
         } else {
@@ -903,11 +930,27 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             // the lane's 8 f32 of a row (chunks fq and 4 + fq) as one 8-deep bf16 operand per term: a 32-deep
             // K-step is one 16x16x32 MFMA per term pair
             bf16x8 at[TNS][3], bt[4][3];
+            if constexpr (CONV2_ABL == 3) {  // diagnosis: no split
 #pragma unroll
-            for (int i = 0; i < TNS; ++i) split3_bf16(af[0][i], af[1][i], at[i]);
+                for (int i = 0; i < TNS; ++i)
+                    at[i][0] = at[i][1] = at[i][2] = __builtin_bit_cast(bf16x8, af[kt & 1][i]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) split3_bf16(bfr[0][j], bfr[1][j], bt[j]);
+                for (int j = 0; j < 4; ++j) bt[j][0] = bt[j][1] = bt[j][2] = __builtin_bit_cast(bf16x8, bfr[kt & 1][j]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < TNS; ++i) split3_bf16(af[0][i], af[1][i], at[i]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) split3_bf16(bfr[0][j], bfr[1][j], bt[j]);
+            }
             constexpr int TA[9] = {0, 0, 1, 0, 1, 2, 1, 2, 2}, TB[9] = {0, 1, 0, 2, 1, 0, 2, 1, 2};
+            if constexpr (CONV2_ABL == 2) {  // diagnosis: one MFMA per K-step (the operands still consumed)
+                bf16x8 sa = at[0][0], sb = bt[0][0];
+#pragma unroll
+                for (int i = 1; i < TNS; ++i) sa = sa + at[i][1] + at[i][2];
+#pragma unroll
+                for (int j = 1; j < 4; ++j) sb = sb + bt[j][1] + bt[j][2];
+                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, sb, acc[0][0], 0, 0, 0);
+            } else {
 #pragma unroll
             for (int t = 0; t < SPL; ++t)
 #pragma unroll
@@ -916,6 +959,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                     for (int j = 0; j < 4; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i][TA[t]], bt[j][TB[t]], acc[i][j], 0,
                                                                             0, 0);
+            }
         } else {
             // f32: element e of lane (fr, fq)'s chunk 4 kh + fq is K index 16 kh + 4 fq + e of the stage -- MFMA
             // (kh, e) sums over fq, so the four MFMAs of a chunk cover its 16 K values (the same permutation of
@@ -961,6 +1005,203 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     } else {
         conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
     }
+}
+
+// ------------------------------------------------------------------------ conv3t (f32 mode, three-plane K-loop)
+// The f32 conv as six exact bf16 term products (conv2's SPL 6) without the per-wave split in the K-loop: the
+// weights arrive pre-split (va_conv_args.w3: [Npad][Kpad/8][3][8] bf16, h / m / l per 8-channel group) and each
+// f32 activation is split ONCE per workgroup, while it is staged: a thread loads the 8 channels of one (pixel,
+// group) of K-step k + 2 into registers, and splits and stores the three bf16 planes of K-step k + 1 into LDS
+// while the MFMAs of step k run.  256-pixel x 128-channel tiles, 8 waves (4 x 2, 64 x 64 each), K-step 16
+// channels, three LDS stages (A by LDS-DMA two steps ahead), one workgroup per CU.  The MFMA is
+// v_mfma_f32_32x32x16_bf16: lane (r, g) = (lane % 32, lane / 32) feeds row r of a 32-row block with channels
+// 8 g .. 8 g + 7 of the step, plane p of a row is one 16-byte read; per 32 x 32 block pair the six products
+// h.h, h.m, m.h, h.l, m.m, l.h are six MFMAs (24 per wave per K-step).
+// LDS row: 128 bytes = 8 slots of 16 B; chunk c = 3 g + p (c < 6) sits in slot c ^ (r & 7) ^ ((r >> 4) & 1) -- the
+// 32-row fragment reads are conflict-free, slots 6-7 of a chunk are DMA'd from the zero page.
+constexpr int T3_BN = 128, T3_KS = 16, T3_ROW = 128;
+template <int WM, int NSTAGE>
+struct T3Cfg {
+    static constexpr int BM = 64 * WM, NT = 128 * WM, STAGE = (BM + T3_BN) * T3_ROW;
+    static constexpr int EPI = BM * (T3_BN + 4) * 4;
+    static constexpr int LDS = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
+    static constexpr int NA = 16 / (2 * WM);  // A-DMA instructions per wave per K-step (16 KiB of A rows)
+    static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+__device__ __forceinline__ int t3_slot(int c, int r) { return c ^ (r & 7) ^ ((r >> 4) & 1); }
+// 16-byte buffer_load ... lds of w3 (base, bytes: the descriptor's range; out-of-range offsets load zeros).  A
+// plain __device__ function: the host pass of a kernel template whose body names the LDS-DMA buffer builtin drops
+// the kernel's stub without a diagnostic (an undefined symbol at load time).
+__device__ __forceinline__ void t3_dma16(const void* base, int bytes, void* lds, int voff, int soff) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lvoid_t*)lds, 16, voff, soff, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void t3_waitvm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// WM = 4, NSTAGE = 3: 256-pixel tiles, 8 waves, one workgroup per CU, A DMA'd two K-steps ahead;
+// WM = 2, NSTAGE = 2: 128-pixel tiles, 4 waves, two workgroups per CU, A one K-step ahead.  B registers always
+// two K-steps ahead.
+template <int WM, int NSTAGE, typename OutT>
+__global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int ntn, int ntiles) {
+    using Cfg = T3Cfg<WM, NSTAGE>;
+    extern __shared__ __align__(16) unsigned char smt[];
+    constexpr int BM = Cfg::BM, BN = T3_BN, NT = Cfg::NT, WN = 2, TNS = 4, NA = Cfg::NA;
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    auto stA = [&](int s) { return smt + s * Cfg::STAGE; };
+    auto stB = [&](int s) { return smt + s * Cfg::STAGE + BN * T3_ROW; };
+
+    // ---- B staging unit of this thread: row br (pixel m0 + br), 8-channel group bg of each K-step; lanes 0-7 of
+    // a wave take 8 consecutive rows of one group (conflict-free 16-byte plane stores)
+    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
+    int b_hi, b_wi;
+    int64_t b_base;
+    {
+        const int m = m0 + br;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi = ho * a.stride - pad_y;
+            b_wi = wo * a.stride - pad_x;
+            b_base = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
+        }
+    }
+    // ---- A DMA: instructions i = wid + 2 WM j (rows 8 i .. 8 i + 7 of the stage); lane l: row 8 i + (l >> 3),
+    // slot l & 7 -> chunk (slot ^ swizzle), whose 16 bytes are bf16 elements 8 chunk .. of the row's K-step run.
+    // buffer_load ... lds, not global_load_lds: the compiler's wait pass takes a pending FLAT-encoded LDS DMA as
+    // "VM and LGKM out of order" and answers the next register dependency with vmcnt(0), draining the B loads two
+    // steps ahead.  Chunks 6-7 (and K-steps past the last) use an offset past the descriptor's range: zeros.
+    const void* zpage = (const void*)g_zero_page;
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int T3_OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int row = 8 * (wid + 2 * WM * j) + (lane >> 3);
+        const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
+        aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
+    }
+    auto dmaA = [&](int k, int s, bool live) {  // K-step k (channels 16 k ..) into stage s; !live: zeros
+        unsigned char* base = stA(s);
+        const int soff = live ? k * 96 : T3_OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+            t3_dma16(W3, w3_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
+    };
+    // K-step -> (tap, channel) of the im2col row, advanced per load (uniform)
+    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    u32x4 rb[2][2];  // B registers of two K-steps in flight
+    // unconditional: out-of-range taps and the loads past the last K-step read the zero page, so the loop body
+    // has no branches and the compiler's own waits on rb see one straight-line load / use pattern
+    auto loadB = [&](int slot, bool live) {
+        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
+        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
+        rb[slot][0] = *(const u32x4*)p;
+        rb[slot][1] = *(const u32x4*)(p + 4);
+        ld_c += T3_KS;
+        if (ld_c == a.Cin) {
+            ld_c = 0;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                ++ld_ky;
+            }
+        }
+    };
+    auto storeB = [&](int slot, int s) {  // split the 8 f32 once, three plane chunks into stage s
+        bf16x8 t[3];
+        split3_bf16(rb[slot][0], rb[slot][1], t);
+        unsigned char* rowp = stB(s) + br * T3_ROW;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3_slot(3 * bg + p, br)) = t[p];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nk = a.Kpad / T3_KS;
+    // prologue: A of steps 0 .. NSTAGE - 2 in their stages, B of steps 0 and 1 in registers; step 0 staged
+#pragma unroll
+    for (int k = 0; k < NSTAGE - 1; ++k) dmaA(k, k, k < nk);
+    loadB(0, true);
+    loadB(1, nk > 1);
+    t3_waitvm<2>();  // everything but step 1's two B loads
+    storeB(0, 0);
+    __syncthreads();
+    const int r32 = lane & 31, g32 = lane >> 5;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    // one K-step; LS = the register slot of step k (step k + 2 loads into it, step k + 1 is in 1 - LS): compile-time,
+    // so the compiler's own waits on the B registers stay where their data is consumed (a runtime slot index made
+    // it wait for every load at once).  Every step issues the same NA DMAs + 2 loads (zero-page sources past the
+    // last K-step) and stores the next step's B, so the counted waits are constants and the body has no branch.
+    // The step ends in a raw s_barrier (__syncthreads() would add vmcnt(0) and drain the loads two steps ahead).
+    auto step = [&](const int k, auto LSc) {
+        constexpr int LS = decltype(LSc)::value;
+        const int s = k % NSTAGE;
+        dmaA(k + NSTAGE - 1, (k + NSTAGE - 1) % NSTAGE, k + NSTAGE - 1 < nk);  // stage last read at step k - 1
+        loadB(LS, k + 2 < nk);  // step k's registers were stored at step k - 1
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(s);
+        const unsigned char* bs_ = stB(s);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = wn * 64 + 32 * ib + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int row = wm * 64 + 32 * jb + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(bs_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
+                                                                          0, 0);
+        // step k + 1's A (DMA'd NSTAGE - 1 steps ago: this step when NSTAGE = 2) and B (loaded one step ago)
+        // complete; this step's two B loads stay in flight, and with NSTAGE = 3 this step's DMA too
+        t3_waitvm<NSTAGE == 2 ? 2 : NA + 2>();
+        storeB(1 - LS, (k + 1) % NSTAGE);  // past the last step: a harmless store into a stage nobody reads
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stores visible, stage reads retired
+    };
+    int k = 0;
+    for (; k + 1 < nk; k += 2) {
+        step(k, std::integral_constant<int, 0>{});
+        step(k + 1, std::integral_constant<int, 1>{});
+    }
+    if (k < nk) step(k, std::integral_constant<int, 0>{});
+    t3_waitvm<0>();  // the zero-page DMAs past the last step land before the epilogue reuses the LDS
+    __syncthreads();
+
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? conv_out_row(a, m, cls) : -1;
+    };
+    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smt, n0, wm, wn, tid, lane, orow, m0, cls);
 }
 
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
@@ -2506,8 +2747,43 @@ int f32_split() {
     return e[0] == '9' ? 9 : e[0] == '6' ? 6 : (e[0] == '1' && e[1] == '6') ? 16 : 0;
 }
 
+// VA_CONV3T: 1 = 256-pixel tiles (8 waves, 3 stages), 2 = 128-pixel tiles (4 waves, 2 stages, 2 per CU), 0 = off
+int conv3t_form() {
+    const char* e = getenv("VA_CONV3T");
+    return e ? e[0] - '0' : 2;
+}
+
+// conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
+bool use_conv3t(const va_conv_args& a) {
+    if (!a.w3 || conv3t_form() == 0) return false;
+    return (a.mode == 0 || a.mode == 2) && a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K &&
+           a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
+}
+
+template <int WM, int NSTAGE, typename OutT>
+hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3Cfg<WM, NSTAGE>;
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Cfg::LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
+    return conv3t_form() == 1 ? launch_conv3t_v<4, 3, OutT>(a, st) : launch_conv3t_v<2, 2, OutT>(a, st);
+}
+
 template <int SPL, typename OutT>
 hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
+    if (SPL == 6 && use_conv3t(a)) return launch_conv3t<OutT>(a, st);
     if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
     if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float, SPL>(a, st);
     if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float, SPL>(a, st);

@@ -49,6 +49,7 @@ class ConvArgs(ctypes.Structure):
         ("xu", ctypes.c_void_p), ("ldu", ctypes.c_int32), ("cu", ctypes.c_int32),
         ("wscale", ctypes.c_void_p), ("xscale", ctypes.c_float), ("x8", ctypes.c_int32),
         ("yscale", ctypes.c_float), ("rscale", ctypes.c_float),
+        ("w3", ctypes.c_void_p),
     ]
 
 
@@ -71,6 +72,20 @@ class Packed:
     Kpad: int
     Npad: int
     deconv: bool = False
+    w3: torch.Tensor | None = None  # f32 mode: the weights as three exact bf16 terms (split3_bf16, va_conv_args.w3)
+
+
+def split3_bf16(w: torch.Tensor) -> torch.Tensor:
+    """f32 [..., K] (K % 8 == 0) -> bf16 [..., K / 8, 3, 8]: per 8-element group the round-to-nearest bf16 h of each
+    value, then m = bf16(x - h), then l = bf16(x - h - m) -- x == h + m + l exactly (both subtractions are exact in
+    f32, l has at most 8 significant bits; tests/test_split_cpu.py), the layout conv3t_kernel stages."""
+    w = w.float()
+    h = w.to(torch.bfloat16)
+    r = w - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    g = w.shape[:-1] + (w.shape[-1] // 8, 8)
+    return torch.stack([h.reshape(g), m.reshape(g), lo.reshape(g)], -2).contiguous()
 
 
 class Slice:
@@ -311,8 +326,11 @@ class SegNet:
                                 continue
                             acc += wb[c, :, fy, fx]
                     bt[c, rf, cf, :o] = acc
-        return Packed(wm.to(self.device, self.tdtype).contiguous(),
-                      bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
+        p = Packed(wm.to(self.device, self.tdtype).contiguous(),
+                   bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
+        if self.store == "f32" and ci % 16 == 0 and K == Kpad:
+            p.w3 = split3_bf16(p.w)
+        return p
 
     @property
     def store(self) -> str:
@@ -346,8 +364,11 @@ class SegNet:
         wm[:cout, :K] = wp.reshape(cout, K)
         bm = torch.zeros(Npad, dtype=torch.float32)
         bm[:cout] = b
-        return Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
-                      Kpad, Npad)
+        p = Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
+                   Kpad, Npad)
+        if self.store == "f32" and cin_p % 16 == 0 and K == Kpad:
+            p.w3 = split3_bf16(p.w)
+        return p
 
     # ------------------------------------------------------------------ planning
     def _buf(self, B, h, w, c, dtype=None):
@@ -420,6 +441,8 @@ class SegNet:
                 args.rscale = scale[res.buf.data_ptr()] if res is not None and res.e4m3 else 0.0
             if up is not None:
                 args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
+            if p.w3 is not None and self.store == "f32" and tail is None and up is None:
+                args.w3 = p.w3.data_ptr()  # the three-plane kernel takes the layers it fits (va_seg.hip use_conv3t)
             cout = p.cout
             if p2 is not None:
                 if p2.cin != p.cout or p2.k != 1:
@@ -577,7 +600,8 @@ class SegNet:
             ops.append(SegOp(kind=VA_OP_CONV, a=ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
-                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1)))
+                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1,
+                w3=pf.w3.data_ptr() if pf.w3 is not None else None)))
             meta.append({"name": "model.22.proto.upsample+cv2 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
