@@ -220,6 +220,18 @@ typedef struct va_conv_args {
      * 8 m, then the 8 l.  When set (and Cin % 16 == 0, Npad % 128 == 0, K == Kpad, mode 0 or 2) the conv runs on
      * the three-plane kernel (va_seg.hip conv3t_kernel); NULL keeps conv2's in-loop split. */
     const void* w3;
+    /* Optional split-K workspace (any dtype; conv2's LDS-DMA form, mode 0 / 2): when ws != NULL and the layer has
+     * too few output tiles to fill the chip (a batch-1 forward's 40 x 40 and 20 x 20 layers), the dispatcher may
+     * split the K loop of each tile over up to 16 workgroups.  Each writes its f32 partial tile to ws, the last
+     * to arrive (per-tile arrival counter in wcnt, agent-scope release / acquire) sums them and runs the usual
+     * epilogue -- same operands, same per-split f32 accumulation, then one f32 sum of the partials.  The
+     * dispatcher only splits when tiles * splits * 64 KiB <= ws_bytes and tiles <= ncnt.  wcnt must be zero
+     * before the first call; every split launch leaves it zero again.  A plan's ops run in order on one
+     * stream, so one workspace serves them all; two streams need two. */
+    void* ws;
+    int64_t ws_bytes;
+    int32_t* wcnt;
+    int32_t ncnt;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

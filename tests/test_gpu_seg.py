@@ -23,11 +23,11 @@ def _net(dtype, scale="s", nc=80, seed=0, cls_bias=None):
     return arch, fw, SegNet(arch, fw, dtype=dtype)
 
 
-def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, act=True):
+def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, act=True, ws=None,
+                     B=2):
     from vision_assist_amd import seg as S
     from vision_assist_amd.seg_arch import Arch
     g = torch.Generator().manual_seed(cin * 1000 + cout + k)
-    B = 2
     if deconv:
         w = torch.randn(cin, cout, 2, 2, generator=g) * 0.2
     else:
@@ -66,6 +66,8 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
                       y=y.data_ptr() + 8 * y.element_size(), ldy=ld_out,
                       res=res.data_ptr() if res is not None else None, ldr=cout, act=1 if act else 0,
                       mode=1 if deconv else 0, M=B * Ho * Wo, dtype=net.va_dtype, out_f32=0)
+    if ws is not None:  # split-K workspace (va_conv_args.ws): (slabs uint8, counters int32)
+        args.ws, args.ws_bytes, args.wcnt, args.ncnt = ws[0].data_ptr(), ws[0].numel(), ws[1].data_ptr(), ws[1].numel()
     _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), __import__("ctypes").byref(args)), "va_seg_conv")
     torch.cuda.synchronize()
     got = y[..., 8:8 + cout].float().cpu().permute(0, 3, 1, 2)
@@ -106,6 +108,44 @@ def test_conv_op(dtype, cin, cout, k, stride, H, W, residual, deconv, slice_in):
     else:
         err = (got - ref).abs().max() / ref.abs().max()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,slice_in", [
+    (256, 256, 3, 1, 20, 20, False, 0),   # 4 tiles x 16 slices
+    (128, 256, 3, 2, 40, 40, True, 8),    # stride 2, residual, channel slice
+    (512, 192, 1, 1, 17, 23, False, 0),   # 1x1, ragged last tile
+    (96, 160, 3, 1, 11, 9, False, 0),     # bf16: per-lane im2col (Cin % 64 != 0), ragged channel tile
+    (40, 136, 3, 1, 12, 10, False, 0),    # both dtypes per-lane im2col, K padded past 9 Cin
+])
+def test_conv_split_k(dtype, cin, cout, k, stride, H, W, residual, slice_in):
+    """Split-K (va_conv_args.ws, batch-1 shapes): against torch at the unsplit tolerances, bit-identical on a
+    second run (the slices are summed in slice order, not arrival order), and the arrival counters back at zero."""
+    ws = (torch.empty(32 << 20, dtype=torch.uint8, device="cuda"), torch.zeros(128, dtype=torch.int32, device="cuda"))
+    got, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1)
+    again, _ = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1)
+    assert int(ws[1].abs().sum()) == 0
+    assert torch.equal(got, again)
+    if dtype == "f32":
+        assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+    else:
+        err = (got - ref).abs().max() / ref.abs().max()
+        assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_forward_batch1_split_k_matches_unsplit(dtype, monkeypatch):
+    """The batch-1 n-seg forward with split-K (the C2 shape) against the same forward with VA_SPLITK=0: f32 to
+    f32 rounding of the reordered sums, bf16 to bf16 rounding of the stored activations."""
+    arch, fw, net = _net(dtype, "n", seed=5)
+    frames = _frames(1, seed=8)
+    monkeypatch.setenv("VA_SPLITK", "1")
+    a = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_SPLITK", "0")
+    b = _gpu_heads(net, frames)
+    for name, x, y in zip(("box", "cls", "coef", "proto"), a, b):
+        err = ((x - y).abs().max() / y.abs().max()).item()
+        assert err < (1e-5 if dtype == "f32" else 3e-2), f"{name}: {err}"
 
 
 def _ref_heads(arch, fw, frames):

@@ -662,9 +662,19 @@ __device__ __forceinline__ void split3_bf16(const u32x4& c0, const u32x4& c1, bf
 // rounding of the sum.  SPL 16 (VA_F32_SPLIT=16, A/B only): the same six products on v_mfma_f32_32x32x16_bf16 (32 x 32
 // blocks, 32 cycles per SIMD with 24 of them free for the split's VALU, against 8 of 16 for 16x16x32) -- measured
 // 2-10 % slower on every layer of the s-seg forward (33.9 vs 32.2 ms per 128 frames, profiles/r03/ab_split_6_16.log).
+// 16-byte write-through (sc1) store of a split-K slab (conv2_kernel's combine): base / bytes = the workspace.  A
+// plain __device__ function: the host pass of a kernel template whose body names a buffer builtin can drop the
+// kernel's stub (see t3_dma16)
+__device__ __forceinline__ void sk_store16(void* base, int64_t bytes, int off, f32x4 v) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+
 template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false,
           int SPL = 0>
-__global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles) {
+__global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles, int ksplit,
+                                                           int kper) {
     using Cfg = Conv2Cfg<T, WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
     constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, RS = Cfg::RS;
@@ -678,6 +688,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
+    // split K (ksplit > 1): the ksplit slices of one tile are consecutive virtual blocks (one XCD: the reducer
+    // reads its partners' slabs from its own L2); slice sk runs K-steps [sk kper, min(nk, (sk + 1) kper))
+    const int sk = bid % ksplit;
+    bid /= ksplit;
+    const int vt = bid;  // virtual tile (with the sub-pixel class): the arrival counter's index
     // mode 2: the 4 sub-pixel classes of one tile are consecutive virtual tiles (same input, same XCD)
     const int cls = a.mode == 2 ? (bid & 3) : 0;
     if (a.mode == 2) bid >>= 2;
@@ -685,6 +700,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
+    const int nk_all = a.Kpad / KS;
+    const int kt0 = sk * kper, kt1 = min(nk_all, kt0 + kper);
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ Wt = (const T*)a.w + (int64_t)cls * a.Npad * a.Kpad;
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
@@ -713,19 +730,24 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             b_base[i] = 0;
         }
     }
-    int ci = VEC * g, ky = 0, kx = 0;
-    while (ci >= a.Cin) {
-        ci -= a.Cin;
-        if (++kx == a.kw) {
-            kx = 0;
-            ++ky;
-        }
+    // im2col position (tap ky, kx; channel ci) of this thread's 8-element group of K-step kt0
+    int kcur = kt0 * KS + VEC * g, ci, ky, kx;
+    {
+        const int tap = kcur / a.Cin;
+        ci = kcur - tap * a.Cin;
+        ky = tap / a.kw;
+        kx = tap - ky * a.kw;
     }
-    int kcur = VEC * g;
     // FK state: per-row base pointers (pixel at tap (0, 0), this lane's 8-channel group) and weight rows
     const T* rowp[B_CH];
     const T* wrow[A_CH];
-    int fk_ky = 0, fk_kx = 0, fk_c = 0;  // tap and 64-channel chunk of the next K-step (wave-uniform)
+    int fk_ky, fk_kx, fk_c;  // tap and 64-channel chunk of the next K-step (wave-uniform)
+    {
+        const int tap = kt0 * KS / a.Cin;
+        fk_c = kt0 * KS - tap * a.Cin;
+        fk_ky = tap / a.kw;
+        fk_kx = tap - fk_ky * a.kw;
+    }
     const void* zpage = (const void*)g_zero_page;  // hoisted: the asm waits' memory clobbers force a reload
     if constexpr (FK) {
 #pragma unroll
@@ -831,19 +853,18 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc32[i][j] = (f32x16){};
 
-    const int nk = a.Kpad / KS;
     if constexpr (GLDS) {
-        CONV2_DMA(0, 0);
+        CONV2_DMA(kt0 * KS, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-        CONV2_LOAD(0);
+        CONV2_LOAD(kt0 * KS);
         CONV2_STORE(0);
     }
     __syncthreads();
     const int fr = lane & 15, fq = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        const int s = kt & 1;
-        const bool more = kt + 1 < nk;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const int s = (kt - kt0) & 1;
+        const bool more = kt + 1 < kt1;
         if constexpr (GLDS) {
             if (more && !(SPL > 0 && SPL != 16 && CONV2_ABL == 1)) {
                 CONV2_DMA((kt + 1) * KS, s ^ 1);
@@ -988,6 +1009,45 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_LOAD
 #undef CONV2_STORE
 #undef CONV2_DMA
+
+    if constexpr (SPL != 16) {
+        if (ksplit > 1) {
+            // split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction", §6 Guideline 16, its sc1
+            // form): every slice stores its f32 partial tile write-through (slab [vt][sk][fragment q][thread], 1 KiB
+            // per wave-store), drains, and takes an arrival ticket; the slice that draws ksplit - 1 acquires, sums
+            // the slabs in slice order (its own read back: the result does not depend on arrival order) and runs the
+            // epilogue (a second slab in flight under the adds would cost 64 VGPRs: past 256, one wave per SIMD)
+            constexpr int NQ = TNS * 4;
+            const int64_t sbase = (int64_t)vt * ksplit * NQ * NT;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            int* last_s = (int*)smem;  // the stage buffers are free: the K-loop ended on a barrier
+            if (tid == 0) {
+                const int prev = __hip_atomic_fetch_add(a.wcnt + vt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int last = prev == ksplit - 1;
+                if (last) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(a.wcnt + vt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+                }
+                last_s[0] = last;
+            }
+            __syncthreads();
+            const bool last = last_s[0] != 0;
+            __syncthreads();  // the flag is read before the epilogue reuses the LDS
+            if (!last) return;
+            const f32x4* sl = (const f32x4*)a.ws + sbase + tid;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[q / 4][q % 4] = sl[q * NT];
+            for (int o = 1; o < ksplit; ++o) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q / 4][q % 4] += sl[((int64_t)o * NQ + q) * NT];
+            }
+        }
+    }
 
     auto orow = [&](int pl) -> int64_t {
         const int m = m0 + pl;
@@ -2548,6 +2608,32 @@ bool getenv_glds() {
     return v == 1;
 }
 
+// Split-K policy (va_conv_args.ws): a launch of fewer than 128 tiles leaves most of the 256 CUs idle while each
+// tile walks its whole K loop, one LDS-DMA round trip + barrier per K-step -- the batch-1 forward's cost.  Cost
+// model per tile (us, measured at batch 1, profiles/r03/splitk/): ts per K-step (f32 three-term 1.4, bf16 0.6);
+// splitting into ks slices costs a slab write + ticket (1.0) and ~1.5 per slice of the combine (one workgroup reads
+// ks x 64 KiB).  Pick the ks <= 16
+// with tiles x ks <= 256 that minimises ceil(nk / ks) ts + 1.0 + 1.5 ks, if it beats the unsplit nk ts by 15 %.
+// VA_SPLITK=0 disables it (A/B timing; read per launch).  Returns the slice count (1 = no split); *kper = K-steps
+// per slice (every slice non-empty).
+int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* kper) {
+    *kper = nk;
+    const char* e = getenv("VA_SPLITK");
+    if ((e && e[0] == '0') || !a.ws || !a.wcnt || tiles >= 128 || nk < 4 || tiles > a.ncnt) return 1;
+    const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f, tw = 1.0f, tc = 1.5f;
+    int best = 1;
+    float bt = nk * ts;
+    for (int ks = 2; ks <= 16 && ks <= nk / 2 && tiles * ks <= 256; ++ks) {
+        if ((int64_t)tiles * ks * bm * bn * 4 > a.ws_bytes) break;
+        const float t = ((nk + ks - 1) / ks) * ts + tw + tc * ks;
+        if (t < bt) bt = t, best = ks;
+    }
+    if (best == 1 || bt > 0.85f * nk * ts) return 1;
+    const int per = (nk + best - 1) / best;
+    *kper = per;
+    return (nk + per - 1) / per;
+}
+
 template <int WM, int WN, int TNS, typename OutT, typename T = __bf16, int SPL = 0>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     using Cfg = Conv2Cfg<T, WM, WN, TNS>;
@@ -2556,21 +2642,25 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
     const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
+    int kper = a.Kpad / KS, ks = 1;
+    if (SPL != 16 && a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
+    const int nb = ntiles * ks;
     if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st,
-                           a, ntn, ntiles);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL>), dim3(nb), dim3(Cfg::NT), 0, st,
+                           a, ntn, nb, ks, kper);
         return hipGetLastError();
     }
     if (getenv_glds() && a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st,
-                               a, ntn, ntiles);
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL>), dim3(nb), dim3(Cfg::NT), 0,
+                               st, a, ntn, nb, ks, kper);
         else
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn,
-                               ntiles);
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL>), dim3(nb), dim3(Cfg::NT), 0,
+                               st, a, ntn, nb, ks, kper);
     }
     else
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL>), dim3(ntiles), dim3(Cfg::NT), 0, st, a, ntn, ntiles);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL>), dim3(nb), dim3(Cfg::NT), 0, st,
+                           a, ntn, nb, ks, kper);
     return hipGetLastError();
 }
 
@@ -2756,6 +2846,9 @@ int conv3t_form() {
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
 bool use_conv3t(const va_conv_args& a) {
     if (!a.w3 || conv3t_form() == 0) return false;
+    int kper;  // a layer conv2 would split over K (batch-1 shapes) stays on conv2
+    const int t2 = ((a.M + 127) / 128) * ((a.Cout + 127) / 128) * (a.mode == 2 ? 4 : 1);
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper) > 1) return false;
     return (a.mode == 0 || a.mode == 2) && a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K &&
            a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }

@@ -28,6 +28,7 @@ F8_KS = 128        # K-step of the fp8 kernel (va_fp8.hip): fp8 weights are padd
 F8_MAX = 448.0     # largest OCP e4m3 value
 FP8_HEADROOM = 2.0  # calibration amax x this maps to [224, 448] (SegNet.calibrate_fp8)
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
+SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
 
@@ -50,6 +51,10 @@ class ConvArgs(ctypes.Structure):
         ("wscale", ctypes.c_void_p), ("xscale", ctypes.c_float), ("x8", ctypes.c_int32),
         ("yscale", ctypes.c_float), ("rscale", ctypes.c_float),
         ("w3", ctypes.c_void_p),
+        ("ws", ctypes.c_void_p),
+        ("ws_bytes", ctypes.c_int64),
+        ("wcnt", ctypes.c_void_p),
+        ("ncnt", ctypes.c_int32),
     ]
 
 
@@ -393,6 +398,14 @@ class SegNet:
         bufs = []  # activation buffers in creation order (fp8: one scale each, calibrate_fp8)
         links = []  # (i, j): buffers an upsample copies between (one scale)
         scale = {}  # fp8: buffer data_ptr -> its scale
+        # split-K workspace of this plan (va355.h va_conv_args.ws; its ops run in order on one stream)
+        ws = torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=self.device)
+        wcnt = torch.zeros(SPLITK_NCNT, dtype=torch.int32, device=self.device)
+        keep += [ws, wcnt]
+
+        def with_ws(args: ConvArgs) -> ConvArgs:
+            args.ws, args.ws_bytes, args.wcnt, args.ncnt = ws.data_ptr(), ws.numel(), wcnt.data_ptr(), wcnt.numel()
+            return args
 
         def new(h, w, c, dtype=None):
             # fp8: activations as e4m3 bytes, except the float outputs and the bf16 map model.0 writes
@@ -419,12 +432,12 @@ class SegNet:
             ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
             if src.c != p.cin and not (src.c < p.cin and src.ld >= p.cin):
                 raise _lib.VaError(f"{prefix}: input has {src.c} channels, packed for {p.cin}")
-            args = ConvArgs(
+            args = with_ws(ConvArgs(
                 x=src.ptr, N=B, H=h, W=w, Cin=p.cin, ldx=src.ld, kh=k, kw=k, stride=stride, pad=pad, Ho=ho, Wo=wo,
                 w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=p.cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
                 y=dst.ptr, ldy=dst.ld, res=res.ptr if res is not None else None, ldr=res.ld if res is not None else 0,
                 act=1 if act else 0, mode=1 if p.deconv else 0, M=B * ho * wo, dtype=self.va_dtype,
-                out_f32=1 if (out_f32 and self.store == "bf16") else 0)
+                out_f32=1 if (out_f32 and self.store == "bf16") else 0))
             on_fp8 = fp8 and prefix in self.w8 and tail is None and up is None and self._fp8_fits(p, src, dst, res,
                                                                                                   out_f32)
             if fp8 and not on_fp8:
@@ -597,11 +610,11 @@ class SegNet:
             pr1 = new(h3, w3, a.npr)
             conv("model.22.proto.cv1", o3, pr1, h3, w3)
             pr3 = new(h2, w2, a.npr)
-            ops.append(SegOp(kind=VA_OP_CONV, a=ConvArgs(
+            ops.append(SegOp(kind=VA_OP_CONV, a=with_ws(ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
                 y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1,
-                w3=pf.w3.data_ptr() if pf.w3 is not None else None)))
+                w3=pf.w3.data_ptr() if pf.w3 is not None else None))))
             meta.append({"name": "model.22.proto.upsample+cv2 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
@@ -622,11 +635,11 @@ class SegNet:
             p3 = self.w["model.22.proto.cv3"]
             w3c = p3.w[:, :pf.cout].contiguous()
             keep.append(w3c)
-            ops.append(SegOp(kind=VA_OP_CONV, a=ConvArgs(
+            ops.append(SegOp(kind=VA_OP_CONV, a=with_ws(ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
                 y=proto.ptr, ldy=proto.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, out_f32=1, bias4=1,
-                w2=w3c.data_ptr(), b2=p3.b.data_ptr(), c2=p3.cout, act2=1)))
+                w2=w3c.data_ptr(), b2=p3.b.data_ptr(), c2=p3.cout, act2=1))))
             meta.append({"name": "model.22.proto.upsample+cv2+cv3 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * (pf.K + p3.cout),
