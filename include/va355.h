@@ -376,7 +376,7 @@ typedef struct va_post_args {
     void* cscratch;
     int32_t cslots, ccap;
     va_contour_stat* cstats;    /* out [B][max_det] */
-    int32_t* cstatus;           /* out [B] or NULL: 1 = the chosen contour exceeded ccap points (cells left 0) */
+    int32_t* cstatus;           /* out [B] or NULL: 0 (a chosen contour longer than cpts_cap is filled in chunks) */
     /* per instance two buffers of cpts_cap contour points (network pixel x | y << 16): the contour being
      * followed and the longest so far; a longer contour is followed again from the image instead */
     uint32_t* cpts;             /* scratch [B][max_det][2][cpts_cap] */
@@ -397,6 +397,7 @@ int va_letterbox(void* stream, const uint8_t* src, int32_t B, int32_t H, int32_t
 
 /* Number of anchors A for an H x W input (strides 8, 16, 32), or < 0. */
 int va_post_anchors(int32_t H, int32_t W);
+/* cells == NULL and cstats == NULL: decode + NMS only (the contour pass and its buffers are not touched). */
 int va_post_run(void* stream, const va_post_args* p);
 
 /* Bytes of one contour scratch slot for an H x W network input with point capacity cap, and the offsets of its
@@ -455,7 +456,8 @@ int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, cons
  * words are zeroed when clear != 0.  Synchronises the current device.  Debug / test surface. */
 int va_diag(uint32_t* out, int32_t n, int32_t clear);
 
-/* Library version / build info string. */
+/* Library version / build info string; "abi 3": va_post_args as above (sc_* floats, cpts / cpts_cap / max_nms;
+ * round 2 changed its layout from round 1's int pad_x / pad_y) -- check va_abi_struct_sizes as well. */
 const char* va_version(void);
 
 #ifdef __cplusplus

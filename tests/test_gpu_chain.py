@@ -186,3 +186,44 @@ def test_predict_720x1280_letterboxed_matches_oracle():
         assert C.bounding_rect(r.masks.xy[k].astype(np.int32)) == tuple(r.masks.rect)
         checked += 1
     assert checked >= 1
+
+
+@pytest.mark.parametrize("H0,W0,bias", [(640, 640, 4.0), (720, 1280, 0.0)])
+def test_masks_xy_from_point_buffers_equals_retrace(H0, W0, bias):
+    """Results.masks.xy is read from the point buffers va_post_run filled (no second contour pass): every
+    detection's polygon equals the one va_post_polygons traces again from the image, bit for bit."""
+    import ctypes
+    import warnings
+    from vision_assist_amd import _lib
+    from vision_assist_amd.yolo import YOLO
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = YOLO("yolov8n-seg.pt", cls_bias=bias, dtype="bf16").to("cuda")
+    rng = np.random.default_rng(11)
+    checked = 0
+    for _ in range(2):
+        frame = rng.integers(0, 256, (H0, W0, 3), dtype=np.uint8)
+        r = model.predict(frame)[0]
+        pipe = model.pipeline(H0, W0, 0.5, 0.7, 300)
+        post = pipe.post
+        fast = post._points_polygons(0)
+        n = int(post.ndet[0])
+        if n == 0:
+            continue
+        assert fast is not None and len(fast) == n
+        a = post._last[0]
+        cap = 4096
+        polys = torch.empty((post.B, post.max_det, cap, 2), dtype=torch.float32, device="cuda")
+        pn = torch.zeros((post.B, post.max_det), dtype=torch.int32, device="cuda")
+        _lib.check(post.lib.va_post_polygons(_lib.stream_ptr(None, post.device), ctypes.byref(a), polys.data_ptr(),
+                                             pn.data_ptr(), cap), "va_post_polygons")
+        cnt = pn[0, :n].cpu().numpy()
+        assert (cnt <= cap).all()
+        full = polys[0, :n].cpu().numpy()
+        for k in range(n):
+            assert fast[k].shape == (cnt[k], 2)
+            assert np.array_equal(fast[k].view(np.uint32), full[k, :cnt[k]].view(np.uint32)), k
+        if r.masks is not None:
+            assert len(r.masks.xy) == n
+        checked += n
+    assert checked > 0

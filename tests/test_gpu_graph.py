@@ -55,9 +55,9 @@ def test_graph_replay_equals_eager(scale, dtype, B, regime):
 
 
 def test_graph_replay_then_nav_equals_eager():
-    """The batch-1 latency form (tools/latency.py --graph): frame copy + network + post-processing replayed from
-    a graph, then the grid / A* stage eagerly on the replayed cells -- the same paths, costs and angle-cache keys
-    as the eager pipeline, over several replays."""
+    """The batch-1 latency form (tools/latency.py --graph, pipeline.SegPostGraph): frame copy + network +
+    post-processing replayed from a graph, then the grid / A* stage eagerly on the replayed cells -- the same paths,
+    costs and angle-cache keys as the eager pipeline, over several replays, issued from the default stream."""
     import numpy as np
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_ALWAYS
@@ -84,31 +84,17 @@ def test_graph_replay_then_nav_equals_eager():
         res = pipe.run(frame, c, r, PLANT_ALWAYS)
         want.append((summary(res), sorted(pipe.seen.keys())))
     pipe.seen.clear()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        for _ in range(2):
-            pipe.load(frame)
-            pipe.seg_post(pc, pr, PLANT_ALWAYS)
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        pipe.load(frame)
-        pipe.seg_post(pc, pr, PLANT_ALWAYS)
-    torch.cuda.synchronize()
-    # replay and the eager stage on a stream of their own: on the legacy default stream (handle 0) the replayed
-    # graph was observed not to be ordered before the following launches (illegal address in the nav stage,
-    # gone with AMD_SERIALIZE_KERNEL=3), so graphs are never launched on it here
+    from vision_assist_amd.pipeline import SegPostGraph
+    g = SegPostGraph(pipe, frame, pc, pr, PLANT_ALWAYS)
+    # from the caller's current stream -- the legacy default stream here, where a direct hipGraphLaunch followed
+    # by the grid stage faulted (profiles/r03/graph_fault/): the replay runs on the graph's own stream, ordered by
+    # events before and after, and the grid stage follows on the default stream
+    assert torch.cuda.current_stream().cuda_stream == 0
     got = []
-    st = torch.cuda.Stream()
-    st.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(st):
-        for c, r in runs:
-            pc.copy_(c)
-            pr.copy_(r)
-            g.replay()
-            res = pipe.nav_run()
-            got.append((summary(res), sorted(pipe.seen.keys())))
-    torch.cuda.current_stream().wait_stream(st)
+    for c, r in runs:
+        pc.copy_(c)
+        pr.copy_(r)
+        g.replay()
+        res = pipe.nav_run()
+        got.append((summary(res), sorted(pipe.seen.keys())))
     assert got == want

@@ -8,6 +8,7 @@ while [ $# -gt 0 ]; do
   cmd=()
   while [ $# -gt 0 ] && [ "$1" != "::" ]; do cmd+=("$1"); shift; done
   [ "$1" = "::" ] && shift
+  mkdir -p "$(dirname "gpurun_out/$log")"
   echo "== ${cmd[*]}  (limit ${t}s, log gpurun_out/$log)"
   timeout -k 10 "$t" "${cmd[@]}" > "gpurun_out/$log" 2>&1
   rc=$?

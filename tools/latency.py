@@ -38,25 +38,14 @@ def main():
     out = {"config": f"C2 shape: YOLOv8{args.scale}-seg {H}x{W} {args.dtype}, batch 1, 1 MI355X", "iters": args.iters}
     variants = [("seg_only", lambda: pipe.run_seg_only()),
                 ("end_to_end", lambda: pipe.run(frame, pc, pr, PLANT_ALWAYS))]
-    # every variant runs on a stream of its own: a graph replayed on the legacy default stream was observed not to
-    # be ordered before the following launches there (tests/test_gpu_graph.py)
+    # every variant runs on a stream of its own (graph replays are on SegPostGraph's private stream, ordered after
+    # and before this one by events)
     run_stream = torch.cuda.Stream()
     if args.graph:
         # the frame copy + network + post-processing captured once as a HIP graph (the nav stage reads a device
         # flag on the host per speculative A* round, so it stays eager)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(3):
-                pipe.load(frame)
-                pipe.seg_post(pc, pr, PLANT_ALWAYS)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            pipe.load(frame)
-            pipe.seg_post(pc, pr, PLANT_ALWAYS)
-        torch.cuda.synchronize()
+        from vision_assist_amd.pipeline import SegPostGraph
+        graph = SegPostGraph(pipe, frame, pc, pr, PLANT_ALWAYS, warmup=3)
 
         def graph_e2e():
             graph.replay()

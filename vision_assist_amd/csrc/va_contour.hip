@@ -765,9 +765,10 @@ __device__ __forceinline__ void contour_empty(const CtArgs& a, int b, int k, con
 
 // The LDS form.  Block g takes detections g, g + G, ...; its 16 waves claim them one at a time from an LDS counter
 // and each runs its own detection in a page run of the pool (first fit on the page map, CAS).  A wave that finds
-// no free run raises the gate, and no wave claims a new detection while the gate is up, so the pool drains towards
-// the waiting wave (which holds no pages: no deadlock); it lowers the gate once it has its run.  Detections
-// needing more than the pool are left to post_contour_global_kernel.
+// no free run counts itself into the gate, and no wave claims a new detection while any wave waits, so the pool
+// drains towards the waiting waves (which hold no pages: no deadlock); each leaves the count once it has its run
+// (a count, not a flag: the first of two waiting waves to get pages does not reopen claims for the other, ADVICE
+// r2).  Detections needing more than the pool are left to post_contour_global_kernel.
 __global__ __launch_bounds__(CP_THREADS) void post_contour_pool_kernel(CtArgs a) {
     extern __shared__ __align__(16) uint32_t cp_pool[];
     __shared__ unsigned s_map;
@@ -821,15 +822,15 @@ __global__ __launch_bounds__(CP_THREADS) void post_contour_pool_kernel(CtArgs a)
                         break;
                     }
                 } else {
-                    if (!gated && a.gate) {
-                        __hip_atomic_store(&s_gate, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (!gated && a.gate) {  // one more waiting wave (lane 0 adds, the others add 0)
+                        atomicAdd(&s_gate, lane == 0 ? 1 : 0);
                         gated = true;
                     }
                     ++spins;
                     __builtin_amdgcn_s_sleep(4);
                 }
             }
-            if (gated) __hip_atomic_store(&s_gate, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (gated) atomicAdd(&s_gate, lane == 0 ? -1 : 0);  // claims resume when no wave waits
             CT_WATCH(1, 3);
             CT_WATCH(2, page);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

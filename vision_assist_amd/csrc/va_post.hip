@@ -613,6 +613,9 @@ int va_post_run(void* stream, const va_post_args* p) {
     hipLaunchKernelGGL(post_nms_kernel, dim3(B), dim3(NMS_THREADS), NMS_LDS, st, p->cand, p->cand_count, A, p->iou,
                        p->max_det, max_nms, p->dets, p->ndet, p->keys);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
+    // detections only (no mask choice, no per-detection contour stats asked for): the contour pass is skipped,
+    // and so are its buffer checks
+    if (!p->cells && !p->cstats) return VA_OK;
     return contours(st, p, nullptr, nullptr, 0, p->cells != nullptr);
 }
 

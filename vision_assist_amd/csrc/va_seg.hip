@@ -305,6 +305,11 @@ __device__ __attribute__((aligned(16))) unsigned int g_zero_page[8];  // 32 zero
 #ifndef CONV2_ABL
 #define CONV2_ABL 0
 #endif
+// the same for conv3t_kernel (-DCONV3T_ABL=N): 1 = no A DMA after the prologue, 2 = one MFMA per K-step instead of
+// 24 (the operands still read and consumed), 3 = no B loads / split / plane stores after the prologue
+#ifndef CONV3T_ABL
+#define CONV3T_ABL 0
+#endif
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -1217,8 +1222,9 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     auto step = [&](const int k, auto LSc) {
         constexpr int LS = decltype(LSc)::value;
         const int s = k % NSTAGE;
-        dmaA(k + NSTAGE - 1, (k + NSTAGE - 1) % NSTAGE, k + NSTAGE - 1 < nk);  // stage last read at step k - 1
-        loadB(LS, k + 2 < nk);  // step k's registers were stored at step k - 1
+        if constexpr (CONV3T_ABL != 1)
+            dmaA(k + NSTAGE - 1, (k + NSTAGE - 1) % NSTAGE, k + NSTAGE - 1 < nk);  // stage last read at step k - 1
+        if constexpr (CONV3T_ABL != 3) loadB(LS, k + 2 < nk);  // step k's registers were stored at step k - 1
         bf16x8 ap[2][3], bp[2][3];
         const unsigned char* as_ = stA(s);
         const unsigned char* bs_ = stB(s);
@@ -1234,6 +1240,11 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
 #pragma unroll
             for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(bs_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
         }
+        if constexpr (CONV3T_ABL == 2) {  // diagnosis: one MFMA per K-step
+            bf16x8 sa = ap[0][0] + ap[0][1] + ap[0][2] + ap[1][0] + ap[1][1] + ap[1][2];
+            bf16x8 sb = bp[0][0] + bp[0][1] + bp[0][2] + bp[1][0] + bp[1][1] + bp[1][2];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, sb, acc[0][0], 0, 0, 0);
+        } else {
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -1242,10 +1253,15 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
                 for (int jb = 0; jb < 2; ++jb)
                     acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
                                                                           0, 0);
+        }
         // step k + 1's A (DMA'd NSTAGE - 1 steps ago: this step when NSTAGE = 2) and B (loaded one step ago)
         // complete; this step's two B loads stay in flight, and with NSTAGE = 3 this step's DMA too
-        t3_waitvm<NSTAGE == 2 ? 2 : NA + 2>();
-        storeB(1 - LS, (k + 1) % NSTAGE);  // past the last step: a harmless store into a stage nobody reads
+        if constexpr (CONV3T_ABL == 3) {
+            t3_waitvm<0>();
+        } else {
+            t3_waitvm<NSTAGE == 2 ? 2 : NA + 2>();
+            storeB(1 - LS, (k + 1) % NSTAGE);  // past the last step: a harmless store into a stage nobody reads
+        }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stores visible, stage reads retired
     };
     int k = 0;

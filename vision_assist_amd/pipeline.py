@@ -178,3 +178,47 @@ class OverlappedPipelines:
 
 
 __all__ = ["FramePipeline", "OverlappedPipelines", "PLANT_IF_NONE", "PLANT_NEVER"]
+
+
+class SegPostGraph:
+    """The frame copy + network + post-processing of a FramePipeline (``load`` + ``seg_post``) captured once as a
+    HIP graph, for the batch-1 latency form (tools/latency.py --graph).
+
+    hipGraphLaunch is only ever issued on a private stream of this object: ``replay(stream)`` makes the private
+    stream wait for ``stream``'s prior work (an event), launches the graph there and makes ``stream`` wait for the
+    graph's end (another event), so work the caller queues next on ``stream`` -- the grid stage, a copy out --
+    is ordered after the graph by an explicit dependency, whatever ``stream`` is.  A graph launched directly on
+    the legacy default stream (handle 0) and followed there by the grid stage faulted the GPU (round 2 and
+    profiles/r03/graph_fault/: the same sequence on a private stream, and eagerly on the default stream, runs
+    clean), so the legacy stream never sees a graph launch."""
+
+    def __init__(self, pipe: FramePipeline, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
+                 plant_mode: int = PLANT_NEVER, warmup: int = 2):
+        self.pipe = pipe
+        dev = pipe.device
+        self.stream = torch.cuda.Stream(device=dev)
+        s = self.stream
+        cur = torch.cuda.current_stream(dev)
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            for _ in range(warmup):  # plans, attributes, lazily allocated buffers: before the capture
+                if frames is not None:
+                    pipe.load(frames, stream=s)
+                pipe.seg_post(plant_cells, plant_rects, plant_mode, stream=s)
+        s.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            if frames is not None:
+                pipe.load(frames, stream=s)
+            pipe.seg_post(plant_cells, plant_rects, plant_mode, stream=s)
+        s.synchronize()
+
+    def replay(self, stream=None) -> None:
+        """One replay, ordered after ``stream``'s (default: the current stream's) queued work and before
+        anything queued on it afterwards."""
+        dev = self.pipe.device
+        cur = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.graph.replay()
+        cur.wait_stream(self.stream)

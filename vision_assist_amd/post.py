@@ -160,6 +160,9 @@ class PostEngine:
         coordinates (float32 [k, 2], masks2segments 'largest' + scale_coords)."""
         import numpy as np
         a, _levels, _proto = self._last
+        pts = self._points_polygons(b)
+        if pts is not None:
+            return pts
         polys = torch.empty((self.B, self.max_det, cap, 2), dtype=torch.float32, device=self.device)
         pn = torch.zeros((self.B, self.max_det), dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
@@ -171,6 +174,36 @@ class PostEngine:
             return self.polygons(b, cap=int(cnt.max()), stream=stream)
         pts = polys[b, :n].cpu().numpy()
         return [np.ascontiguousarray(pts[k, :cnt[k]]) for k in range(n)]
+
+    def _points_polygons(self, b: int):
+        """masks.xy from the point buffers the last va_post_run already holds (polygons() used to repeat
+        the whole contour pass): each detection's longest contour sits in half cstats.half of its cpts slot as
+        network pixels x | y << 16, mapped by the float32 scale_coords the kernel applies (scale_pt: (p - pad) /
+        gain, clipped -- IEEE float32 subtract / divide / min / max, the same bits on the host).  None when a contour
+        was longer than the buffer (then only a trace from the image has it)."""
+        import numpy as np
+        n = int(self.ndet[b])
+        if n == 0:
+            return []
+        cs = self.contour_stats(b)
+        npts = cs["npts"].astype(np.int64)
+        if (npts > CONTOUR_PTS).any():
+            return None
+        raw = self.cpts[b, :n].cpu().numpy().view(np.uint32)  # [n, 2, CONTOUR_PTS]
+        if self.frame:
+            g, px, py = (np.float32(v) for v in scale_coords_params(self.H, self.W, self.H0, self.W0))
+            W0, H0 = np.float32(self.W0), np.float32(self.H0)
+        else:
+            g, px, py, W0, H0 = np.float32(1), np.float32(0), np.float32(0), np.float32(self.W), np.float32(self.H)
+        out = []
+        for k in range(n):
+            q = raw[k, int(cs["half"][k]), :int(npts[k])]
+            x = (q & 0xFFFF).astype(np.float32)
+            y = (q >> 16).astype(np.float32)
+            xs = np.minimum(np.maximum((x - px) / g, np.float32(0)), W0)
+            ys = np.minimum(np.maximum((y - py) / g, np.float32(0)), H0)
+            out.append(np.ascontiguousarray(np.stack([xs, ys], 1).astype(np.float32)))
+        return out
 
     def contour_stats(self, b: int):
         import numpy as np
