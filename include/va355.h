@@ -281,6 +281,14 @@ int va_seg_conv0_e4m3(void* stream, const uint8_t* frames, int32_t N, int32_t H,
 int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const float* w,
                      const float* bias, int32_t Cout, float* y, int32_t ldy);
 
+/* The f32 layer on the MFMA: the [Cout][32] (K-padded) weights as three exact bf16 terms w3 = bf16 [Cout][4][3][8]
+ * (per 8-element group h, m, l with h + m + l == w exactly), the frame bytes as exact bf16 operands, three term
+ * products accumulated in f32 per fragment pair, then * (1/255) + bias and SiLU (exp2 / rcp form of the f32 convs)
+ * -> f32 NHWC as va_seg_conv0_f32 (max |diff| against it at f32 rounding level: tests/test_gpu_seg.py).  The
+ * VA_OP_CONV0 op takes this form when a.w3 is set.  W * 3 % 16 == 0 (the 16-byte patch loads). */
+int va_seg_conv0_f32m(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w3,
+                      const float* bias, int32_t Cout, float* y, int32_t ldy);
+
 /* SPPF (block.py SPPF): slice 0 (c channels) of an NHWC buffer of channel stride ld >= 4c -> slices 1..3
  * = MaxPool2d(5, 1, 2) applied once, twice, three times (dtype F32 / BF16 / FP8: e4m3 bytes, ordered as the
  * values they encode). */
@@ -297,8 +305,8 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_UPSAMPLE 3    /* upsample2x: a.x/a.ldx -> a.y/a.ldy, a.N/H/W (source size), a.Cin = c, a.dtype */
 #define VA_OP_PREPROCESS 4  /* preprocess: a.x = uint8 frames, a.y = out, a.N/H/W, a.dtype */
 #define VA_OP_CONV0 5       /* preprocess fused into model.0: a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
-                               a.Cout, a.y, a.ldy, a.dtype (FP8: e4m3 output with a.yscale) -- see va_seg_conv0 /
-                               va_seg_conv0_f32 / va_seg_conv0_e4m3 */
+                               a.Cout, a.y, a.ldy, a.dtype (FP8: e4m3 output with a.yscale; F32 with a.w3: the
+                               MFMA form) -- see va_seg_conv0 / va_seg_conv0_f32(m) / va_seg_conv0_e4m3 */
 #define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
 #define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: see va_seg_stem */
 typedef struct va_seg_op {

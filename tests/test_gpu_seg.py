@@ -295,6 +295,44 @@ def test_conv0_fused_preprocess(cout, H, W):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("cout,H,W", [(32, 64, 64), (48, 34, 48), (64, 40, 80), (16, 16, 16), (32, 640, 640)])
+def test_conv0_f32_mfma_matches_fp32(cout, H, W):
+    """va_seg_conv0_f32m (three exact bf16 weight terms x the raw frame bytes on the MFMA, the sum scaled by 1/255)
+    against torch fp32 (x / 255 then conv2d, bias, SiLU) and against the VALU kernel va_seg_conv0_f32: f32-level
+    agreement (odd fragment count at 48, ragged edges at H = 34, a full 640 frame)."""
+    import ctypes
+    from vision_assist_amd import _lib
+    from vision_assist_amd.seg import split3_bf16
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(cout + H + W + 7)
+    B = 2
+    frames = torch.randint(0, 256, (B, H, W, 3), generator=g, dtype=torch.uint8)
+    w = torch.randn(cout, 3, 3, 3, generator=g) * 0.3
+    b = torch.randn(cout, generator=g) * 0.1
+    wp = torch.zeros(cout, 32)
+    wp[:, :27] = w.permute(0, 2, 3, 1).reshape(cout, 27)
+    w3 = split3_bf16(wp).cuda()
+    w27 = wp[:, :27].contiguous().cuda()
+    bd = b.float().cuda()
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    fd = frames.cuda()
+    ym = torch.full((B, Ho, Wo, cout), float("nan"), device="cuda")
+    yv = torch.full((B, Ho, Wo, cout), float("nan"), device="cuda")
+    _lib.check(lib.va_seg_conv0_f32m(_lib.stream_ptr(), ctypes.c_void_p(fd.data_ptr()), B, H, W,
+                                     ctypes.c_void_p(w3.data_ptr()), ctypes.c_void_p(bd.data_ptr()), cout,
+                                     ctypes.c_void_p(ym.data_ptr()), cout), "va_seg_conv0_f32m")
+    _lib.check(lib.va_seg_conv0_f32(_lib.stream_ptr(), ctypes.c_void_p(fd.data_ptr()), B, H, W,
+                                    ctypes.c_void_p(w27.data_ptr()), ctypes.c_void_p(bd.data_ptr()), cout,
+                                    ctypes.c_void_p(yv.data_ptr()), cout), "va_seg_conv0_f32")
+    torch.cuda.synchronize()
+    x = (frames.flip(-1).float() / 255.0).permute(0, 3, 1, 2)
+    ref = F.silu(F.conv2d(x.double(), w.double(), b.double(), 2, 1)).float()
+    got = ym.cpu().permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() < 2e-6 * max(1.0, ref.abs().max().item())
+    assert (got - yv.cpu().permute(0, 3, 1, 2)).abs().max().item() < 4e-6 * max(1.0, ref.abs().max().item())
+
+
 def test_conv3_matches_conv2(monkeypatch):
     """The 256 x 128-tile kernel (conv3: three LDS-DMA stages, two K-tiles in flight) forced onto every wide
     layer of a bf16 forward -- stride 2, residual C2f bottlenecks, Cout 224 (a ragged channel tile), the fused
@@ -302,6 +340,7 @@ def test_conv3_matches_conv2(monkeypatch):
     same outputs as the 128 x 128 conv2 kernel: same fragments, same MFMA order, so bit-identical."""
     arch, fw, net = _net("bf16", "s", seed=4)
     frames = _frames(2, seed=7)
+    monkeypatch.setenv("VA_SPLITK", "0")  # conv2 slicing the P5 layers' K loops would sum in another order
     monkeypatch.delenv("VA_CONV3", raising=False)
     ref = _gpu_heads(net, frames)
     monkeypatch.setenv("VA_CONV3", "1")
@@ -309,6 +348,28 @@ def test_conv3_matches_conv2(monkeypatch):
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: conv3 vs conv2 max diff {(g - r).abs().max().item()}"
+
+
+@pytest.mark.parametrize("B,form", [(2, "3"), (3, "3"), (2, "4"), (3, "4")])
+def test_conv3u_matches_conv3t(B, form, monkeypatch):
+    """conv3u (96-byte stage rows, three A stages, B registers three K-steps ahead) and conv3v (its B loads a K-step
+    pair at a time, whole 128-byte lines) against conv3t's 128-pixel form
+    on the f32 forward's wide layers (P3 3x3 / 1x1 layers, Cout 224 ragged channel tile, the proto sub-pixel fold
+    in mode 2, ragged pixel tiles at B = 3): the same operands, the same six MFMAs per block pair in the same order,
+    so bit-identical; and within the f32 bar of the torch fp32 reference."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(B, seed=11)
+    monkeypatch.setenv("VA_CONV3T", "2")
+    ref = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_CONV3T", form)  # 3: conv3u, 4: conv3v (paired whole-line B loads)
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.equal(g, r), f"{name}: conv3t form {form} vs 2 max diff {(g - r).abs().max().item()}"
+    if B == 2:
+        torch.set_num_threads(8)
+        want = _ref_heads(arch, fw, frames)
+        for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+            assert (g - r).abs().max().item() <= 1e-3, name
 
 
 def test_patch_conv_matches_dn(monkeypatch):
@@ -369,6 +430,7 @@ def test_conv4_matches_conv2(monkeypatch):
     same 32-deep MFMA k-sequence per output, so bit-identical."""
     arch, fw, net = _net("bf16", "s", seed=12)
     frames = _frames(2, seed=13)
+    monkeypatch.setenv("VA_SPLITK", "0")  # conv2 slicing the P5 layers' K loops would sum in another order
     monkeypatch.setenv("VA_CONV4", "0")
     ref = _gpu_heads(net, frames)
     monkeypatch.setenv("VA_CONV4", "1")

@@ -60,6 +60,7 @@ SIGNATURES = [
     ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
     ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_conv0_f32", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
+    ("va_seg_conv0_f32m", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),
     ("va_seg_conv0_e4m3", I32, [P, P, I32, I32, I32, P, P, I32, P, I32, ctypes.c_float]),
     ("va_create", I32, [I32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     ("va_destroy", I32, [P]),

@@ -1280,6 +1280,352 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smt, n0, wm, wn, tid, lane, orow, m0, cls);
 }
 
+// ------------------------------------------------------------------------ conv3u (conv3t with a deeper pipeline)
+// conv3t's 128-pixel form measured staging-bound, not MFMA-bound (profiles/r03/conv3t_abl: one MFMA per K-step
+// instead of 24 left the forward as slow; no in-loop A DMA saved 19 %, no B loads / split / plane stores 27 %): a
+// K-step of 24 MFMAs per wave (768 MFMA cycles) is shorter than the DMA round trip, and the A stage was waited for
+// one step after its DMA.  conv3u keeps conv3t's operands and MFMAs but (1) packs a stage row into 96 bytes (the
+// six 16-byte plane chunks, no zero-page slots: a stage is 12 KiB per operand), which leaves LDS for (2) THREE A
+// stages, so A(k + 2) is DMA'd at step k and waited for at the end of step k + 1, and (3) B registers three steps
+// ahead; B planes keep two stages (stored at the end of step k for step k + 1).  Per step, in issue order: DMA A(k +
+// 2), load B(k + 3); at the end of step k the counted wait leaves this step's ops and step k - 1's B(k + 2) in
+// flight.  Row swizzle: chunk c of row r sits in slot (c + (r >> 3)) % 6 -- rows r and r + 8 differ in slot parity,
+// so a 16-lane group of 16-byte reads down 16 rows covers 64 distinct banks (96-byte rows: 8 rows span the bank
+// groups 8 m).  The A DMA is linear in LDS per instruction (lane l -> bytes 16 l of a 1 KiB piece): each lane's
+// row / slot / source chunk are per-lane constants.  128-pixel x 128-channel tiles, 4 waves, two workgroups per CU.
+constexpr int T3U_ROW = 96, T3U_BM = 128, T3U_NT = 256;
+constexpr int T3U_ASTAGE = T3_BN * T3U_ROW, T3U_BSTAGE = T3U_BM * T3U_ROW;  // 12 KiB each
+constexpr int T3U_NSA = 3, T3U_NSB = 2;
+constexpr int T3U_EPI = T3U_BM * (T3_BN + 4) * 4;
+constexpr int T3U_LDS = (T3U_NSA * T3U_ASTAGE + T3U_NSB * T3U_BSTAGE) > T3U_EPI ? (T3U_NSA * T3U_ASTAGE + T3U_NSB * T3U_BSTAGE)
+                                                                              : T3U_EPI;
+constexpr int T3U_NA = T3U_ASTAGE / 1024 / (T3U_NT / 64);  // A-DMA instructions per wave per K-step (3)
+static_assert(T3U_ASTAGE % 1024 == 0 && T3U_NA * 1024 * (T3U_NT / 64) == T3U_ASTAGE, "A stage in 1 KiB pieces");
+static_assert(2 * T3U_LDS <= 160 * 1024, "two workgroups per CU");
+__device__ __forceinline__ int t3u_slot(int c, int r) {
+    const int s = c + ((r >> 3) & 1);
+    return s >= 6 ? s - 6 : s;
+}
+
+template <typename OutT>
+__global__ __launch_bounds__(T3U_NT) void conv3u_kernel(va_conv_args a, int ntn, int ntiles) {
+    extern __shared__ __align__(16) unsigned char smu[];
+    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, TNS = 4, NA = T3U_NA;
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    auto stA = [&](int s) { return smu + s * T3U_ASTAGE; };
+    auto stB = [&](int s) { return smu + T3U_NSA * T3U_ASTAGE + s * T3U_BSTAGE; };
+
+    // ---- B staging unit (as conv3t): row br, 8-channel group bg
+    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
+    int b_hi, b_wi;
+    int64_t b_base;
+    {
+        const int m = m0 + br;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi = ho * a.stride - pad_y;
+            b_wi = wo * a.stride - pad_x;
+            b_base = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
+        }
+    }
+    // ---- A DMA: piece j of this wave = LDS bytes 1024 (wid + 4 j) .. of the stage; lane l -> byte 16 l of it
+    const void* zpage = (const void*)g_zero_page;
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int T3_OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
+        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
+        int c = slot - ((row >> 3) & 1);
+        if (c < 0) c += 6;
+        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+    }
+    auto dmaA = [&](int k, int s, bool live) {
+        unsigned char* base = stA(s);
+        const int soff = live ? k * 96 : T3_OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
+    };
+    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    u32x4 rb[3][2];  // B registers of three K-steps in flight
+    auto loadB = [&](int slot, bool live) {
+        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
+        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
+        rb[slot][0] = *(const u32x4*)p;
+        rb[slot][1] = *(const u32x4*)(p + 4);
+        ld_c += T3_KS;
+        if (ld_c == a.Cin) {
+            ld_c = 0;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                ++ld_ky;
+            }
+        }
+    };
+    auto storeB = [&](int slot, int s) {
+        bf16x8 t[3];
+        split3_bf16(rb[slot][0], rb[slot][1], t);
+        unsigned char* rowp = stB(s) + br * T3U_ROW;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nk = a.Kpad / T3_KS;
+    // prologue, in issue order: A(0), B(0), A(1), B(1), B(2); then A(0) and B(0) complete, B(0)'s planes stored
+    dmaA(0, 0, true);
+    loadB(0, true);
+    dmaA(1, 1, nk > 1);
+    loadB(1, nk > 1);
+    loadB(2, nk > 2);
+    t3_waitvm<NA + 4>();
+    storeB(0, 0);
+    __syncthreads();
+    const int r32 = lane & 31, g32 = lane >> 5;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    auto step = [&](const int k, auto LSc) {
+        constexpr int LS = decltype(LSc)::value;  // = k % 3: B(k) was in slot LS (stored at step k - 1)
+        dmaA(k + 2, (k + 2) % T3U_NSA, k + 2 < nk);  // the stage read at step k - 1
+        loadB(LS, k + 3 < nk);
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(k % T3U_NSA);
+        const unsigned char* bs_ = stB(k & 1);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = wn * 64 + 32 * ib + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int row = wm * 64 + 32 * jb + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
+                                                                          0, 0);
+        // A(k + 1) (DMA'd at step k - 1) and B(k + 1) (loaded at step k - 2) complete; step k - 1's B(k + 2) and
+        // this step's A(k + 2) / B(k + 3) stay in flight
+        t3_waitvm<NA + 4>();
+        storeB((LS + 1) % 3, (k + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    int k = 0;
+    for (; k + 2 < nk; k += 3) {
+        step(k, std::integral_constant<int, 0>{});
+        step(k + 1, std::integral_constant<int, 1>{});
+        step(k + 2, std::integral_constant<int, 2>{});
+    }
+    if (k < nk) step(k, std::integral_constant<int, 0>{});
+    if (k + 1 < nk) step(k + 1, std::integral_constant<int, 1>{});
+    t3_waitvm<0>();
+    __syncthreads();
+
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? conv_out_row(a, m, cls) : -1;
+    };
+    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smu, n0, wm, wn, tid, lane, orow, m0, cls);
+}
+
+// conv3v: conv3u with the B loads taken a K-step PAIR at a time (Cin % 32 == 0: a pair never straddles a tap).  A
+// thread's four 16-byte loads -- channels 8 bg .. of step 2j and 16 + 8 bg .. of step 2j + 1 -- and its partner's
+// (bg ^ 1) cover a pixel's whole 128-byte line in one burst, where conv3u's per-step loads touch each line twice, a
+// K-step apart (half a line each time: the line is fetched from L2 again once the CU's 32 KiB L1 has turned over).
+// Pair j + 2 is loaded at step 2 j (three pair slots in registers); per step one A DMA as conv3u, so every step
+// ends in the same counted wait (this step's ops and, after an even step, nothing older than A(k + 1) pending).
+template <typename OutT>
+__global__ __launch_bounds__(T3U_NT) void conv3v_kernel(va_conv_args a, int ntn, int ntiles) {
+    extern __shared__ __align__(16) unsigned char smv[];
+    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, TNS = 4, NA = T3U_NA;
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    auto stA = [&](int s) { return smv + s * T3U_ASTAGE; };
+    auto stB = [&](int s) { return smv + T3U_NSA * T3U_ASTAGE + s * T3U_BSTAGE; };
+    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
+    int b_hi, b_wi;
+    int64_t b_base;
+    {
+        const int m = m0 + br;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi = ho * a.stride - pad_y;
+            b_wi = wo * a.stride - pad_x;
+            b_base = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
+        }
+    }
+    const void* zpage = (const void*)g_zero_page;
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int T3_OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
+        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
+        int c = slot - ((row >> 3) & 1);
+        if (c < 0) c += 6;
+        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+    }
+    auto dmaA = [&](int k, int s, bool live) {
+        unsigned char* base = stA(s);
+        const int soff = live ? k * 96 : T3_OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
+    };
+    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    u32x4 rb[3][4];  // three K-step pairs: [0..1] = step 2j (channels 8 bg ..), [2..3] = step 2j + 1
+    auto loadPair = [&](int slot, bool live) {
+        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
+        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
+        const int s1 = ok ? 16 : 0;  // the zero page holds 8 floats
+        rb[slot][0] = *(const u32x4*)p;
+        rb[slot][1] = *(const u32x4*)(p + 4);
+        rb[slot][2] = *(const u32x4*)(p + s1);
+        rb[slot][3] = *(const u32x4*)(p + s1 + 4);
+        ld_c += 2 * T3_KS;
+        if (ld_c == a.Cin) {
+            ld_c = 0;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                ++ld_ky;
+            }
+        }
+    };
+    auto storeB = [&](int slot, int half, int s) {
+        bf16x8 t[3];
+        split3_bf16(rb[slot][2 * half], rb[slot][2 * half + 1], t);
+        unsigned char* rowp = stB(s) + br * T3U_ROW;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nk = a.Kpad / T3_KS;  // even (Cin % 32 == 0)
+    // prologue, in issue order: A(0), pair 0, A(1), pair 1; then A(0) and pair 0 complete, B(0)'s planes stored
+    dmaA(0, 0, true);
+    loadPair(0, true);
+    dmaA(1, 1, nk > 1);
+    loadPair(1, nk > 2);
+    t3_waitvm<NA + 4>();
+    storeB(0, 0, 0);
+    __syncthreads();
+    const int r32 = lane & 31, g32 = lane >> 5;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    // step k = 2 j + H; PS = j % 3 (the pair slot of B(k)); an even step loads pair j + 2 into slot (j + 2) % 3
+    auto step = [&](const int k, auto PSc, auto Hc) {
+        constexpr int PS = decltype(PSc)::value, H = decltype(Hc)::value;
+        dmaA(k + 2, (k + 2) % T3U_NSA, k + 2 < nk);
+        if constexpr (H == 0) loadPair((PS + 2) % 3, k + 4 < nk);
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(k % T3U_NSA);
+        const unsigned char* bs_ = stB(k & 1);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = wn * 64 + 32 * ib + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int row = wm * 64 + 32 * jb + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
+                                                                          0, 0);
+        // A(k + 1) complete (and every B load older than it: B(k + 1) is in pair (k + 1) / 2, loaded two steps
+        // or more before)
+        t3_waitvm<NA + 4>();
+        if constexpr (H == 0) storeB(PS, 1, (k + 1) & 1);           // B(k + 1) = second half of this pair
+        else storeB((PS + 1) % 3, 0, (k + 1) & 1);                  // first half of the next pair
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    int k = 0;
+    for (; k + 5 < nk; k += 6) {
+        step(k, I0{}, I0{});
+        step(k + 1, I0{}, I1{});
+        step(k + 2, I1{}, I0{});
+        step(k + 3, I1{}, I1{});
+        step(k + 4, I2{}, I0{});
+        step(k + 5, I2{}, I1{});
+    }
+    if (k < nk) {  // 2 or 4 steps left
+        step(k, I0{}, I0{});
+        step(k + 1, I0{}, I1{});
+        if (k + 2 < nk) {
+            step(k + 2, I1{}, I0{});
+            step(k + 3, I1{}, I1{});
+        }
+    }
+    t3_waitvm<0>();
+    __syncthreads();
+
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? conv_out_row(a, m, cls) : -1;
+    };
+    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smv, n0, wm, wn, tid, lane, orow, m0, cls);
+}
+
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
 // 256-pixel x 128-channel tiles for the large layers: 8 waves (4 x 2, each 64 pixels x 64 channels as in
 // conv2), BK = 64, THREE LDS stages filled by LDS-DMA with two K-tiles in flight.  Per K-step: a counted
@@ -2488,6 +2834,91 @@ __global__ __launch_bounds__(256) void conv0_kernel(const uint8_t* __restrict__ 
     }
 }
 
+// f32 model.0 on the MFMA (va_conv_args.w3 set on the VA_OP_CONV0 op): conv0_kernel's tiling and LDS patch, with
+// the weights as three exact bf16 terms h + m + l ([Cout][4][3][8], split3_bf16 of the [Cout][32] K-padded rows) and
+// the B operand the raw frame bytes (0..255: exact in bf16), so each fragment pair is three exact term products
+// accumulated in f32 (l first) -- sum_k w_k p_k to f32 accuracy -- and the /255 is applied to the sum: the same
+// value as the reference's conv of x / 255 up to f32 rounding.  Epilogue: bias, SiLU (the f32 convs' silu2), f32
+// NHWC out, 8 consecutive channels (two 16-byte stores) per lane and fragment pair.  Replaces conv0_f32_kernel's
+// 27 v_fma per channel and pixel (VALU-bound).
+template <int NCO>
+__global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
+                                                         const __bf16* __restrict__ w3, const float* __restrict__ bias,
+                                                         float* __restrict__ y, int ldy) {
+    __shared__ __align__(16) uint8_t patch[C0_PR * C0_PP];
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    const int tx = blockIdx.x, ty = blockIdx.y, n = blockIdx.z;
+    const int ox0 = tx * C0_TW, oy0 = ty * C0_TH;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint8_t* img = frames + (int64_t)n * H * W * 3;
+    const int iy0 = 2 * oy0 - 1, rb0 = 6 * ox0 - 16;
+    for (int i = tid; i < C0_PR * (C0_PP / 16); i += 256) {
+        const int r = i / (C0_PP / 16), c = i - r * (C0_PP / 16);
+        const int iy = iy0 + r, rb = rb0 + 16 * c;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if ((unsigned)iy < (unsigned)H && rb >= 0 && rb < 3 * W) v = *(const u32x4*)(img + (int64_t)iy * W * 3 + rb);
+        *(u32x4*)(patch + r * C0_PP + 16 * c) = v;
+    }
+    const int fr = lane & 15, fq = lane >> 4;
+    // fragment i, row r -> channel 32 (i / 2) + 8 (r / 4) + 4 (i % 2) + r % 4 (conv0_kernel's permutation)
+    bf16x8 af[NCO][3];
+#pragma unroll
+    for (int i = 0; i < NCO; ++i) {
+        const int co = (NCO % 2 == 0 || i < NCO - 1) ? 32 * (i / 2) + 8 * (fr / 4) + 4 * (i % 2) + fr % 4 : 16 * i + fr;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[i][p] = *(const bf16x8*)(w3 + ((co * 4 + fq) * 3 + p) * 8);
+    }
+    int koff[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * fq + e;
+        if (k < 27) {
+            const int tap = k / 3, c = k % 3;  // c: 0 = R, 1 = G, 2 = B; the frame is BGR
+            koff[e] = (tap / 3) * C0_PP + (tap % 3) * 3 + (2 - c);
+        } else {
+            koff[e] = -1;
+        }
+    }
+    __syncthreads();
+    constexpr float inv255 = 1.0f / 255.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int rl = 2 * wid + (j >> 2), cl = (j & 3) * 16 + fr;
+        const int base = (2 * rl) * C0_PP + C0_OFF + 6 * cl;
+        bf16x8 bfr;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bfr[e] = koff[e] >= 0 ? (__bf16)(float)patch[base + koff[e]] : (__bf16)0.0f;
+        const int oy = oy0 + rl, ox = ox0 + cl;
+        f32x4 acc[NCO];
+#pragma unroll
+        for (int i = 0; i < NCO; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bfr, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr, acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr, acc[i], 0, 0, 0);
+        }
+        if (oy >= Ho || ox >= Wo) continue;
+        float* yp = y + (((int64_t)n * Ho + oy) * Wo + ox) * ldy;
+#pragma unroll
+        for (int p = 0; p < NCO / 2; ++p) {
+            const int co = 32 * p + 8 * fq;
+            const float4 b0 = *(const float4*)(bias + co), b1 = *(const float4*)(bias + co + 4);
+            const f32x4 lo = fz::act((f32x4){acc[2 * p][0] * inv255 + b0.x, acc[2 * p][1] * inv255 + b0.y,
+                                             acc[2 * p][2] * inv255 + b0.z, acc[2 * p][3] * inv255 + b0.w});
+            const f32x4 hi = fz::act((f32x4){acc[2 * p + 1][0] * inv255 + b1.x, acc[2 * p + 1][1] * inv255 + b1.y,
+                                             acc[2 * p + 1][2] * inv255 + b1.z, acc[2 * p + 1][3] * inv255 + b1.w});
+            *(f32x4*)(yp + co) = lo;
+            *(f32x4*)(yp + co + 4) = hi;
+        }
+        if constexpr (NCO % 2) {
+            const int co = 16 * (NCO - 1) + 4 * fq;
+            const float4 bv = *(const float4*)(bias + co);
+            const f32x4 t = acc[NCO - 1];
+            *(f32x4*)(yp + co) =
+                fz::act((f32x4){t[0] * inv255 + bv.x, t[1] * inv255 + bv.y, t[2] * inv255 + bv.z, t[3] * inv255 + bv.w});
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------------------- SPPF pool
 // in: slice 0 of buf (c channels), writes slices 1..3 = MaxPool2d(5,1,2) applied 1, 2, 3 times (-inf padding).
 // With -inf padding and stride 1, k chained 5x5 pools equal one (4k+1)x(4k+1) pool clipped to the
@@ -2853,7 +3284,9 @@ int f32_split() {
     return e[0] == '9' ? 9 : e[0] == '6' ? 6 : (e[0] == '1' && e[1] == '6') ? 16 : 0;
 }
 
-// VA_CONV3T: 1 = 256-pixel tiles (8 waves, 3 stages), 2 = 128-pixel tiles (4 waves, 2 stages, 2 per CU), 0 = off
+// VA_CONV3T: 1 = 256-pixel tiles (8 waves, 3 stages), 2 = 128-pixel tiles (4 waves, 2 stages, 2 per CU), 3 = conv3u
+// (128-pixel tiles, 96-byte rows, three A stages, B three steps ahead), 4 = conv3v (conv3u with whole-line B loads a
+// K-step pair at a time; conv3u where Cin % 32 != 0), 0 = off
 int conv3t_form() {
     const char* e = getenv("VA_CONV3T");
     return e ? e[0] - '0' : 2;
@@ -2886,8 +3319,41 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
 }
 
 template <typename OutT>
+hipError_t launch_conv3u(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3u_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                T3U_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3u_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3U_LDS, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t launch_conv3v(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3v_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                T3U_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3v_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3U_LDS, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
+template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
-    return conv3t_form() == 1 ? launch_conv3t_v<4, 3, OutT>(a, st) : launch_conv3t_v<2, 2, OutT>(a, st);
+    const int f = conv3t_form();
+    if (f == 4 && a.Cin % (2 * T3_KS) == 0) return launch_conv3v<OutT>(a, st);
+    if (f == 3 || f == 4) return launch_conv3u<OutT>(a, st);
+    return f == 1 ? launch_conv3t_v<4, 3, OutT>(a, st) : launch_conv3t_v<2, 2, OutT>(a, st);
 }
 
 template <int SPL, typename OutT>
@@ -3210,6 +3676,24 @@ int va_seg_conv0_f32(void* stream, const uint8_t* frames, int32_t N, int32_t H, 
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+int va_seg_conv0_f32m(void* stream, const uint8_t* frames, int32_t N, int32_t H, int32_t W, const void* w3,
+                      const float* bias, int32_t Cout, float* y, int32_t ldy) {
+    if (!frames || !w3 || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Cout % 16 || Cout > 64 || ldy % 4 ||
+        ldy < Cout || ((uintptr_t)y & 15) || (W * 3) % 16 || N > 65535)
+        return VA_ERR_ARG;
+    const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+    dim3 grid((Wo + C0_TW - 1) / C0_TW, (Ho + C0_TH - 1) / C0_TH, N);
+    hipStream_t st = (hipStream_t)stream;
+    const __bf16* wp = (const __bf16*)w3;
+    switch (Cout / 16) {
+        case 1: hipLaunchKernelGGL(conv0_f32m_kernel<1>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy); break;
+        case 2: hipLaunchKernelGGL(conv0_f32m_kernel<2>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy); break;
+        case 3: hipLaunchKernelGGL(conv0_f32m_kernel<3>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy); break;
+        default: hipLaunchKernelGGL(conv0_f32m_kernel<4>, grid, dim3(256), 0, st, frames, N, H, W, wp, bias, y, ldy);
+    }
+    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
     if (!ops || n < 0) return VA_ERR_ARG;
     for (int i = 0; i < n; ++i) {
@@ -3232,8 +3716,10 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                 break;
             case VA_OP_CONV0:
                 rc = a.dtype == VA_DTYPE_F32
-                         ? va_seg_conv0_f32(stream, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w, a.bias,
-                                            a.Cout, (float*)a.y, a.ldy)
+                         ? (a.w3 ? va_seg_conv0_f32m(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w3, a.bias, a.Cout,
+                                                     (float*)a.y, a.ldy)
+                                 : va_seg_conv0_f32(stream, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w,
+                                                    a.bias, a.Cout, (float*)a.y, a.ldy))
                      : a.dtype == VA_DTYPE_FP8
                          ? va_seg_conv0_e4m3(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout,
                                              (uint8_t*)a.y, a.ldy, a.yscale)

@@ -151,9 +151,13 @@ class SegNet:
         w0p[:, :27] = w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27)
         self.w0 = (w0p.to(self.device, self.tdtype).contiguous(), b0.float().to(self.device).contiguous())
         self.fuse_first = w0.shape[0] % 16 == 0 and w0.shape[0] <= 64 and os.environ.get("VA_CONV0", "1") != "0"
+        self.w0_3 = None
         if dtype == "f32":  # va_seg_conv0_f32: [Cout][27], k = (ky*3 + kx)*3 + c (RGB)
             self.w0 = (w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27).float().to(self.device).contiguous(),
                        b0.float().to(self.device).contiguous())
+            # va_seg_conv0_f32m: the K-padded rows as three exact bf16 terms (VA_CONV0_F32M=0: the VALU form, A/B)
+            if os.environ.get("VA_CONV0_F32M", "1") != "0":
+                self.w0_3 = split3_bf16(w0p).to(self.device).contiguous()
         # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
         fold_ok = arch.npr == 128 if dtype == "bf16" else (arch.npr >= 128 and dtype == "f32")
         self.proto_fold = self._fold_proto(folded) if (fold_ok and os.environ.get("VA_FOLD_PROTO", "1") != "0") \
@@ -528,6 +532,8 @@ class SegNet:
             if self.fuse_first:
                 c0 = ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, w=self.w0[0].data_ptr(), bias=self.w0[1].data_ptr(),
                               Cout=a.c1, y=a0.ptr, ldy=a0.ld, dtype=self.va_dtype)
+                if self.w0_3 is not None and (W * 3) % 16 == 0:
+                    c0.w3 = self.w0_3.data_ptr()
                 if a0.e4m3:
                     c0.dtype, c0.yscale = VA_DTYPE_FP8, scale[a0.buf.data_ptr()]
                 ops.append(SegOp(kind=VA_OP_CONV0, a=c0))
