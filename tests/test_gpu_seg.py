@@ -350,7 +350,8 @@ def test_conv3_matches_conv2(monkeypatch):
         assert torch.equal(g, r), f"{name}: conv3 vs conv2 max diff {(g - r).abs().max().item()}"
 
 
-@pytest.mark.parametrize("B,form", [(2, "3"), (3, "3"), (2, "4"), (3, "4"), (2, "5"), (3, "5"), (3, "6")])
+@pytest.mark.parametrize("B,form", [(2, "3"), (3, "3"), (2, "4"), (3, "4"), (2, "5"), (3, "5"), (3, "6"), (2, "7"),
+                                    (3, "7")])
 def test_conv3u_matches_conv3t(B, form, monkeypatch):
     """conv3u (96-byte stage rows, three A stages, B registers three K-steps ahead) and conv3v (its B loads a K-step
     pair at a time, whole 128-byte lines) against conv3t's 128-pixel form
@@ -361,7 +362,7 @@ def test_conv3u_matches_conv3t(B, form, monkeypatch):
     frames = _frames(B, seed=11)
     monkeypatch.setenv("VA_CONV3T", "2")
     ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV3T", form)  # 3: conv3u, 4: conv3v (paired whole-line B loads), 5 / 6: conv3w
+    monkeypatch.setenv("VA_CONV3T", form)  # 3: conv3u, 4: conv3v (paired whole-line B loads), 5 / 6: conv3w, 7: conv3x
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: conv3t form {form} vs 2 max diff {(g - r).abs().max().item()}"

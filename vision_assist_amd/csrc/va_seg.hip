@@ -1798,6 +1798,188 @@ __global__ __launch_bounds__(T3U_NT) void conv3w_kernel(va_conv_args a, int ntn,
     conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smw, n0, wm, wn, tid, lane, orow, m0, cls);
 }
 
+// conv3x: conv3t's 128-pixel schedule (A DMA one K-step ahead, B registers two steps ahead, the B planes stored
+// after the MFMAs, one barrier per step) with 96-byte rows (conv3u) and the epilogue staged in two halves of 64
+// pixels, so a workgroup needs 48 KiB of LDS and THREE fit a CU (12 waves, three per SIMD, register budget 168):
+// more workgroups to overlap one another's staging and barriers, the one lever the ablations leave (staging-bound,
+// conv3t_abl; deeper prefetch, whole-line loads and overlapping the B work with the MFMAs were all neutral).
+constexpr int T3X_LDS = 2 * T3U_ASTAGE + 2 * T3U_BSTAGE;  // 48 KiB
+static_assert(64 * (T3_BN + 4) * 4 <= T3X_LDS && 3 * T3X_LDS <= 160 * 1024, "three workgroups per CU");
+template <typename OutT>
+__global__ __launch_bounds__(T3U_NT, 3) void conv3x_kernel(va_conv_args a, int ntn, int ntiles) {
+    extern __shared__ __align__(16) unsigned char smx[];
+    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, NA = T3U_NA;
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    auto stA = [&](int s) { return smx + s * T3U_ASTAGE; };
+    auto stB = [&](int s) { return smx + 2 * T3U_ASTAGE + s * T3U_BSTAGE; };
+    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
+    int b_hi, b_wi;
+    int64_t b_base;
+    {
+        const int m = m0 + br;
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi = ho * a.stride - pad_y;
+            b_wi = wo * a.stride - pad_x;
+            b_base = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
+        }
+    }
+    const void* zpage = (const void*)g_zero_page;
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int T3_OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
+        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
+        int c = slot - ((row >> 3) & 1);
+        if (c < 0) c += 6;
+        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+    }
+    auto dmaA = [&](int k, int s, bool live) {
+        unsigned char* base = stA(s);
+        const int soff = live ? k * 96 : T3_OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
+    };
+    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    u32x4 rb[2][2];
+    auto loadB = [&](int slot, bool live) {
+        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
+        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
+        rb[slot][0] = *(const u32x4*)p;
+        rb[slot][1] = *(const u32x4*)(p + 4);
+        ld_c += T3_KS;
+        if (ld_c == a.Cin) {
+            ld_c = 0;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                ++ld_ky;
+            }
+        }
+    };
+    auto storeB = [&](int slot, int s) {
+        bf16x8 t[3];
+        split3_bf16(rb[slot][0], rb[slot][1], t);
+        unsigned char* rowp = stB(s) + br * T3U_ROW;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nk = a.Kpad / T3_KS;
+    dmaA(0, 0, true);
+    loadB(0, true);
+    loadB(1, nk > 1);
+    t3_waitvm<2>();
+    storeB(0, 0);
+    __syncthreads();
+    const int r32 = lane & 31, g32 = lane >> 5;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    auto step = [&](const int k, auto LSc) {
+        constexpr int LS = decltype(LSc)::value;
+        const int s = k & 1;
+        dmaA(k + 1, (k + 1) & 1, k + 1 < nk);
+        loadB(LS, k + 2 < nk);
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(s);
+        const unsigned char* bs_ = stB(s);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = wn * 64 + 32 * ib + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int row = wm * 64 + 32 * jb + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
+                                                                          0, 0);
+        t3_waitvm<2>();
+        storeB(1 - LS, (k + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    int k = 0;
+    for (; k + 1 < nk; k += 2) {
+        step(k, std::integral_constant<int, 0>{});
+        step(k + 1, std::integral_constant<int, 1>{});
+    }
+    if (k < nk) step(k, std::integral_constant<int, 0>{});
+    t3_waitvm<0>();
+    __syncthreads();
+    // epilogue in two halves of 64 pixels (rows wm * 64 ..): conv_epilogue32's math, a 64-row staging tile
+    constexpr int CW = BN + 4;
+    float* Cs = (float*)smx;
+    const int r = lane & 31, g = lane >> 5;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        if (wm == half) {
+#pragma unroll
+            for (int jb = 0; jb < 2; ++jb) {
+                const int pl = 32 * jb + r;
+                int brow = n0;
+                if (a.bias4) {
+                    const int m = m0 + half * 64 + pl;
+                    const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
+                    const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
+                    brow = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
+                }
+#pragma unroll
+                for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int col = wn * 64 + 32 * ib + 8 * q + 4 * g;
+                        const float4 bv = *(const float4*)(a.bias + brow + col);
+                        float v0 = acc[ib][jb][4 * q] + bv.x, v1 = acc[ib][jb][4 * q + 1] + bv.y,
+                              v2 = acc[ib][jb][4 * q + 2] + bv.z, v3 = acc[ib][jb][4 * q + 3] + bv.w;
+                        if (a.act) {
+                            const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                            v0 = s01[0], v1 = s01[1], v2 = s23[0], v3 = s23[1];
+                        }
+                        *(float4*)(Cs + pl * CW + col) = make_float4(v0, v1, v2, v3);
+                    }
+            }
+        }
+        __syncthreads();
+        auto orow = [&](int pl) -> int64_t {
+            const int m = m0 + half * 64 + pl;
+            return m < a.M ? conv_out_row(a, m, cls) : -1;
+        };
+        conv_epilogue_store<NT, 64, BN, OutT, decltype(orow), float>(a, smx, n0, tid, orow);
+        __syncthreads();
+    }
+}
+
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
 // 256-pixel x 128-channel tiles for the large layers: 8 waves (4 x 2, each 64 pixels x 64 channels as in
 // conv2), BK = 64, THREE LDS stages filled by LDS-DMA with two K-tiles in flight.  Per K-step: a counted
@@ -3459,7 +3641,7 @@ int f32_split() {
 // VA_CONV3T: 1 = 256-pixel tiles (8 waves, 3 stages), 2 = 128-pixel tiles (4 waves, 2 stages, 2 per CU), 3 = conv3u
 // (128-pixel tiles, 96-byte rows, three A stages, B three steps ahead), 4 = conv3v (conv3u with whole-line B loads a
 // K-step pair at a time; conv3u where Cin % 32 != 0), 5 / 6 = conv3w (B split + stores beside the MFMAs; 6 with an
-// explicit MFMA / VALU / DS interleave), 0 = off
+// explicit MFMA / VALU / DS interleave), 7 = conv3x (three workgroups per CU), 0 = off
 int conv3t_form() {
     const char* e = getenv("VA_CONV3T");
     return e ? e[0] - '0' : 2;
@@ -3537,8 +3719,24 @@ hipError_t launch_conv3w(const va_conv_args& a, hipStream_t st) {
 }
 
 template <typename OutT>
+hipError_t launch_conv3x(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3x_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                T3X_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3x_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3X_LDS, st, a, ntn, ntiles);
+    return hipGetLastError();
+}
+
+template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
     const int f = conv3t_form();
+    if (f == 7) return launch_conv3x<OutT>(a, st);
     if (f == 5) return launch_conv3w<OutT, 0>(a, st);
     if (f == 6) return launch_conv3w<OutT, 1>(a, st);
     if (f == 4 && a.Cin % (2 * T3_KS) == 0) return launch_conv3v<OutT>(a, st);
