@@ -289,7 +289,8 @@ class Run:
         f32eq = None
         if terms:
             # the MFMA the f32 convs execute is bf16 (terms products per f32 product): price the executed bf16
-            # MFMA work against the bf16 peak; model.0 (VALU, no MFMA) is counted once
+            # MFMA work against the bf16 peak; model.0 is counted once at K = 27 (it runs three term products on
+            # the MFMA at K = 32, conv0_f32m, or on the VALU: counting it once under-states, never over-states)
             fl_c0 = sum(2.0 * m["M"] * m["N"] * m["K"] for m in pipe.plan["meta"] if m["name"] == "model.0") / launches
             f32eq = {"achieved": round(achieved, 2), "peak": PEAK_TFLOPS["f32"],
                      "frac": round(achieved / PEAK_TFLOPS["f32"], 5),
@@ -300,7 +301,7 @@ class Run:
         rl = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
               "frac": round(achieved / peak, 5), "traffic": None,
               "kernel": f"the {launches:.0f} conv-family launches of one YOLOv8{self.scale}-seg forward "
-                        + (f"(f32 convs on conv2_kernel's bf16 three-term form; model.0 on conv0_f32)" if terms else
+                        + (f"(f32 convs on conv3t_kernel's / conv2_kernel's bf16 three-term forms; model.0 on conv0_f32m)" if terms else
                            f"({self.dtype} MFMA GEMM kernels: conv/conv2/conv4/conv_dn/conv_patch/pw/c2f/stem)"),
               "flops_per_launch": round(fl_exec), "flops_per_launch_def": "executed GEMM FLOPs of the plan / launch",
               "avg_launch_us": round(avg_s * 1e6, 3),

@@ -2,7 +2,7 @@
 """Summarise rocprofv3 output of a bench.py run for profiles/.
 
   stats  <kernel_stats.csv> <out.json>
-      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/2/3/4/_dn/_patch/_wp, c2f, stem, pw
+      per-family sums of the --kernel-trace --stats summary; the conv family (conv0/0_f32/0_f32m/2/3/3t/3u-3x/4/_dn/_patch/_wp, c2f, stem, pw
       kernels: every launch of the YOLOv8-seg forward's GEMMs) gives the average launch duration that
       bench.py's roofline.avg_launch_us must agree with.
   agree  <kernel_trace.csv> <bench_under_rocprof.json> <out.json> [launches_per_forward]
@@ -23,7 +23,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"(conv(0|2|3|4|_dn|_patch|_wp|0_f32)?|c2f|stem|pw)_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|3t|3u|3v|3w|3x|_dn|_patch|_wp|0_f32|0_f32m)?|c2f|stem|pw)_kernel")
 
 
 def family(name: str) -> str:
