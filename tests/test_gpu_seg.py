@@ -373,6 +373,28 @@ def test_conv3u_matches_conv3t(B, form, monkeypatch):
             assert (g - r).abs().max().item() <= 1e-3, name
 
 
+@pytest.mark.parametrize("B", [2, 3])
+def test_conv3n_narrow_layers_f32(B, monkeypatch):
+    """conv3n (three-plane 256 x 64 tiles) on the narrow f32 layers -- 1x1 and 3x3, stride 2 (model.1), residual
+    C2f bottlenecks, channel slices, ragged pixel tiles at B = 3 -- against conv2's three-term form
+    (VA_CONV3N=0): the same six exact term products per f32 product summed in another order, so f32-rounding
+    close; and within the f32 bar of the torch fp32 reference."""
+    arch, fw, net = _net("f32", "s", seed=6)
+    frames = _frames(B, seed=12)
+    monkeypatch.setenv("VA_CONV3N", "0")  # the default
+    ref = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_CONV3N", "1")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3n vs conv2 max diff {d}"
+    if B == 2:
+        torch.set_num_threads(8)
+        want = _ref_heads(arch, fw, frames)
+        for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+            assert (g - r).abs().max().item() <= 1e-3, name
+
+
 def test_patch_conv_matches_dn(monkeypatch):
     """The patch-staged narrow 3x3 kernel (input patch in LDS once per 16 x 16 tile) against the im2col
     narrow-layer kernel on a whole bf16 forward (P2/P3 bottlenecks with residuals, the fused head tails).

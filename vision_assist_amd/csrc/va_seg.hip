@@ -1980,6 +1980,163 @@ __global__ __launch_bounds__(T3U_NT, 3) void conv3x_kernel(va_conv_args a, int n
     }
 }
 
+// conv3n: conv3t for the narrow f32 layers (33..64 output channels): 256-pixel x 64-channel tiles, 4 waves each
+// 64 pixels x all 64 channels (the same 2 x 2 blocks of 32 x 32 and 24 MFMAs per K-step as conv3t), so the
+// operand split happens once per workgroup and staged pixel instead of once per wave and fragment (conv2's
+// three-term form on these layers: 90-145 TF f32-equivalent against 170-185 for conv3t's).  A = weight planes
+// (conv3t's 128-byte rows and DMA map, 64 rows: 2 DMA pieces per wave), B = activation planes in 96-byte rows
+// (conv3u's swizzle), each thread staging two (pixel, 8-channel group) units per K-step.  Two stages, two
+// workgroups per CU.  Same products and order as conv3t per output (bit-identical to the forms above where
+// both apply).
+constexpr int T3N_BM = 256, T3N_BN = 64, T3N_NT = 256;
+constexpr int T3N_ASTAGE = T3N_BN * T3_ROW, T3N_BSTAGE = T3N_BM * T3U_ROW;  // 8 + 24 KiB
+constexpr int T3N_EPI = T3N_BM * (T3N_BN + 4) * 4;
+constexpr int T3N_LDS = 2 * (T3N_ASTAGE + T3N_BSTAGE) > T3N_EPI ? 2 * (T3N_ASTAGE + T3N_BSTAGE) : T3N_EPI;
+static_assert(2 * T3N_LDS <= 160 * 1024, "two workgroups per CU");
+template <typename OutT>
+__global__ __launch_bounds__(T3N_NT) void conv3n_kernel(va_conv_args a, int ntiles) {
+    extern __shared__ __align__(16) unsigned char smn[];
+    constexpr int BM = T3N_BM, NT = T3N_NT, TNS = 4, NA = T3N_BN / 8 / (T3N_NT / 64);  // 2
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int tm = bid;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid, wn = 0;
+    const int m0 = tm * BM, n0 = 0;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3;
+    auto stA = [&](int s) { return smn + s * (T3N_ASTAGE + T3N_BSTAGE); };
+    auto stB = [&](int s) { return smn + s * (T3N_ASTAGE + T3N_BSTAGE) + T3N_ASTAGE; };
+    // two B units per thread: unit u = tid + 256 i -> row (u & 7) | ((u >> 4) << 3), group (u >> 3) & 1
+    int brr[2], bgg[2], b_hi[2], b_wi[2];
+    int64_t b_base[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int u = tid + 256 * i;
+        brr[i] = (u & 7) | ((u >> 4) << 3);
+        bgg[i] = (u >> 3) & 1;
+        const int m = m0 + brr[i];
+        if (m < a.M) {
+            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
+            b_hi[i] = ho * a.stride - a.pad;
+            b_wi[i] = wo * a.stride - a.pad;
+            b_base[i] = (int64_t)n * a.H * a.W;
+        } else {
+            b_hi[i] = -(1 << 28), b_wi[i] = 0, b_base[i] = 0;
+        }
+    }
+    const void* zpage = (const void*)g_zero_page;
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int T3_OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int row = 8 * (wid + 4 * j) + (lane >> 3);
+        const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
+        aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
+    }
+    auto dmaA = [&](int k, int s, bool live) {
+        unsigned char* base = stA(s);
+        const int soff = live ? k * 96 : T3_OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + 4 * j) * 1024, aoff[j], soff);
+    };
+    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    u32x4 rb[2][2][2];  // [slot][unit][half]
+    auto loadB = [&](int slot, bool live) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int hi = b_hi[i] + ld_ky, wi = b_wi[i] + ld_kx;
+            const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const float* p =
+                ok ? X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bgg[i] : (const float*)zpage;
+            rb[slot][i][0] = *(const u32x4*)p;
+            rb[slot][i][1] = *(const u32x4*)(p + 4);
+        }
+        ld_c += T3_KS;
+        if (ld_c == a.Cin) {
+            ld_c = 0;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                ++ld_ky;
+            }
+        }
+    };
+    auto storeB = [&](int slot, int s) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            bf16x8 t[3];
+            split3_bf16(rb[slot][i][0], rb[slot][i][1], t);
+            unsigned char* rowp = stB(s) + brr[i] * T3U_ROW;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bgg[i] + p, brr[i])) = t[p];
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nk = a.Kpad / T3_KS;
+    dmaA(0, 0, true);
+    loadB(0, true);
+    loadB(1, nk > 1);
+    t3_waitvm<4>();  // all but step 1's four B loads
+    storeB(0, 0);
+    __syncthreads();
+    const int r32 = lane & 31, g32 = lane >> 5;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    auto step = [&](const int k, auto LSc) {
+        constexpr int LS = decltype(LSc)::value;
+        const int s = k & 1;
+        dmaA(k + 1, (k + 1) & 1, k + 1 < nk);
+        loadB(LS, k + 2 < nk);
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(s);
+        const unsigned char* bs_ = stB(s);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = 32 * ib + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int row = wm * 64 + 32 * jb + r32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
+        }
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
+                                                                          0, 0);
+        t3_waitvm<4>();  // A(k + 1) and B(k + 1) landed; this step's four B loads stay in flight
+        storeB(1 - LS, (k + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    int k = 0;
+    for (; k + 1 < nk; k += 2) {
+        step(k, std::integral_constant<int, 0>{});
+        step(k + 1, std::integral_constant<int, 1>{});
+    }
+    if (k < nk) step(k, std::integral_constant<int, 0>{});
+    t3_waitvm<0>();
+    __syncthreads();
+    auto orow = [&](int pl) -> int64_t {
+        const int m = m0 + pl;
+        return m < a.M ? conv_out_row(a, m, 0) : -1;
+    };
+    conv_epilogue32<NT, BM, T3N_BN, TNS, OutT, decltype(orow)>(a, acc, smn, n0, wm, wn, tid, lane, orow, m0, 0);
+}
+
 // ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
 // 256-pixel x 128-channel tiles for the large layers: 8 waves (4 x 2, each 64 pixels x 64 channels as in
 // conv2), BK = 64, THREE LDS stages filled by LDS-DMA with two K-tiles in flight.  Per K-step: a counted
@@ -3744,9 +3901,37 @@ hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
     return f == 1 ? launch_conv3t_v<4, 3, OutT>(a, st) : launch_conv3t_v<2, 2, OutT>(a, st);
 }
 
+// conv3n (three-plane kernel, 64-channel tiles) for the narrow f32 layers: 33..64 output channels, the conv3t
+// conditions otherwise.  Off by default: measured neutral against conv2's three-term form (29.73 vs 29.54 ms per
+// 128-frame forward, profiles/r03/conv3n/); VA_CONV3N=1 selects it (A/B; read per launch)
+bool use_conv3n(const va_conv_args& a) {
+    const char* e = getenv("VA_CONV3N");
+    if (!(e && e[0] == '1') || !a.w3 || a.mode != 0 || a.Cout <= 32 || a.Cout > T3N_BN) return false;
+    int kper;
+    const int t2 = ((a.M + 255) / 256) * ((a.Cout + 63) / 64);
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 256, 64, &kper) > 1) return false;
+    return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.ldx % 4 == 0 &&
+           ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2 && a.Cout % 4 == 0 && a.ldy % 4 == 0;
+}
+
+template <typename OutT>
+hipError_t launch_conv3n(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3n_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                T3N_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int ntiles = (a.M + T3N_BM - 1) / T3N_BM;
+    hipLaunchKernelGGL((conv3n_kernel<OutT>), dim3(ntiles), dim3(T3N_NT), T3N_LDS, st, a, ntiles);
+    return hipGetLastError();
+}
+
 template <int SPL, typename OutT>
 hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
     if (SPL == 6 && use_conv3t(a)) return launch_conv3t<OutT>(a, st);
+    if (SPL == 6 && use_conv3n(a)) return launch_conv3n<OutT>(a, st);
     if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
     if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float, SPL>(a, st);
     if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float, SPL>(a, st);
