@@ -3970,7 +3970,10 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         if constexpr (sizeof(OutT) == 2) {
             // narrow layers: weights in LDS, activations straight into MFMA fragments
             if (use_patch(a)) return launch_conv_patch<false, __bf16>(a, st);
-            if (a.mode == 0 && a.Cout <= 64 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 &&
+            // (a launch of under 4096 pixels goes to conv2 instead: conv_dn stages the whole weight matrix per
+            // workgroup, which a handful of tiles cannot amortise -- batch-1 model.16, 23.6 -> 16.7 us,
+            // profiles/r03/batch1/)
+            if (a.mode == 0 && a.Cout <= 64 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 && a.M >= 4096 &&
                 (size_t)16 * ((a.Cout + 15) / 16) * (a.Kpad + 8) * 2 <= 120 * 1024 && getenv_dn()) {
                 switch ((a.Cout + 15) / 16) {
                     case 1: return launch_conv_dn<1>(a, st);
@@ -4095,8 +4098,8 @@ int va_seg_sppf_pool(void* stream, void* buf, int32_t N, int32_t H, int32_t W, i
     if (!buf || N <= 0 || c <= 0 || ld < 4 * c || c % cg || ld % cg || H * W > SPPF_MAXPIX || ((uintptr_t)buf & 15))
         return VA_ERR_ARG;
     // 2 channel groups per workgroup while the four planes fit 52 KiB of LDS (20 x 20 maps: three
-    // workgroups per CU), else one
-    const int cgw = ((c / cg) % 2 == 0 && (size_t)4 * H * W * 16 * 2 <= 52 * 1024) ? 2 : 1;
+    // workgroups per CU) and the launch still fills the CUs, else one (batch 1: 8 -> 16 workgroups for n-seg)
+    const int cgw = ((c / cg) % 2 == 0 && (size_t)4 * H * W * 16 * 2 <= 52 * 1024 && N * (c / cg) >= 512) ? 2 : 1;
     const int blocks = N * (c / cg / cgw);
     const size_t lds = (size_t)4 * H * W * 16 * cgw;
     hipStream_t st = (hipStream_t)stream;
