@@ -284,7 +284,7 @@ __device__ __forceinline__ void ct_sync() {
     }
 }
 
-template <bool WAVE>
+template <bool WAVE, int MEMCLASS = 0>  // MEMCLASS: a distinct instantiation per image memory class (see below)
 __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Region& r, uint32_t* img, float* strip,
                                             int tid, int nt, MaskStat& ms) {
     auto account = [&](uint32_t w, int x32, int yy) {
@@ -582,18 +582,17 @@ __device__ __forceinline__ int wave_max(int v) {
 // scratch slot) and, for a head-source mask, the low-res strip at strip.  LDS = the image is in LDS (the
 // compiler sees the pointer's address space through the inlining).
 template <bool LDS>
+__device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, const Region& r, uint32_t* img, int item
+                                             CT_PROF(, unsigned long long t0, unsigned long long t1));
+
+template <bool LDS>
 __device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, const Region& r, uint32_t* img,
                                              float* strip, int item) {
     const int lane = threadIdx.x & 63;
     const Src& s = a.s;
-    va_contour_stat st{};
-    st.ox = st.oy = -1;
-    st.X0 = r.X0, st.Y0 = r.Y0;
     const int64_t di = (int64_t)b * a.max_det + k;
-    float* poly = a.polys ? a.polys + di * a.poly_cap * 2 : nullptr;
     MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
-    CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime(); unsigned long long nrows = 0, npos = 0;
-            int nsteps = 0; unsigned long long ttr = 0);
+    CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime());
     CT_WATCH(1, 10);
     build_image<true>(s, b, k, r, img, strip, lane, 64, ms);
     CT_WATCH(1, 11);
@@ -605,6 +604,21 @@ __device__ __forceinline__ void contour_item(const CtArgs& a, int b, int k, cons
         if (lane == 0) s.stats[di] = va_mask_stat{cnt, x0, y0, x1, y1, {0, 0, 0}};
     }
     if constexpr (!LDS) __threadfence();  // the image before the coherent reads of the scan
+    contour_scan<LDS>(a, b, k, r, img, item CT_PROF(, t0, t1));
+}
+
+// cvFindNextContour's raster scan (RETR_EXTERNAL) over a built image, the largest contour's area and the
+// detection's va_contour_stat -- by one wave (the calling wave)
+template <bool LDS>
+__device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, const Region& r, uint32_t* img, int item
+                                             CT_PROF(, unsigned long long t0, unsigned long long t1)) {
+    const int lane = threadIdx.x & 63;
+    va_contour_stat st{};
+    st.ox = st.oy = -1;
+    st.X0 = r.X0, st.Y0 = r.Y0;
+    const int64_t di = (int64_t)b * a.max_det + k;
+    float* poly = a.polys ? a.polys + di * a.poly_cap * 2 : nullptr;
+    CT_PROF(unsigned long long nrows = 0, npos = 0; int nsteps = 0; unsigned long long ttr = 0);
     // cvFindNextContour's raster scan (RETR_EXTERNAL); the contour with the most points stays in its half of
     // the instance's point buffer
     uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
@@ -861,6 +875,67 @@ __global__ __launch_bounds__(CT_THREADS) void post_contour_global_kernel(CtArgs 
         if (r.w <= 0 || region_need(s, r) <= a.pool_max) continue;
         contour_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, item);
         __syncthreads();  // the slot is reused by the next item
+    }
+}
+
+// Small batches (every detection of the launch has its own scratch slot: B x max_det <= slots): ONE WORKGROUP per
+// detection, the image built by all its waves in the detection's global slot (build_image with the block's
+// threads), then the scan / trace by wave 0 as in the other forms.  The pool kernel builds an image with one
+// wave, which a few large compact masks (batch 1: 1-5 detections, the whole GPU otherwise idle) leave as the
+// network-to-answer path's longest serial stage.
+constexpr int CT_WG_THREADS = 512;
+constexpr int CT_WG_LDS = CP_POOL;  // the image (+ strip) of a region up to the pool's size lives in LDS
+template <bool LDS>
+__device__ __forceinline__ void contour_wg_item(const CtArgs& a, int b, int k, const Region& r, uint32_t* img,
+                                                float* strip, int item, int* s_ms) {
+    const Src& s = a.s;
+    MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+    CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime());
+    // its own build instantiation per memory class: one body serving an LDS and a global image through one pointer
+    // faulted on gfx950 (an aperture violation, §4.2 of DESIGN.md)
+    build_image<false, LDS ? 1 : 2>(s, b, k, r, img, strip, threadIdx.x, CT_WG_THREADS, ms);
+    CT_PROF(const unsigned long long t1 = __builtin_amdgcn_s_memtime());
+    const int lane = threadIdx.x & 63;
+    if (s.stats) {  // pixel count and bbox: per wave, then across the block
+        const int cnt = wave_sum(ms.cnt);
+        const int x0 = wave_min(ms.x1 >= 0 ? ms.x0 : s.Wn), x1 = wave_max(ms.x1);
+        const int y0 = wave_min(ms.x1 >= 0 ? ms.y0 : s.Hn), y1 = wave_max(ms.x1 >= 0 ? ms.y1 : -1);
+        if (lane == 0) {
+            atomicAdd(&s_ms[0], cnt);
+            atomicMin(&s_ms[1], x0);
+            atomicMax(&s_ms[2], x1);
+            atomicMin(&s_ms[3], y0);
+            atomicMax(&s_ms[4], y1);
+        }
+    }
+    if constexpr (!LDS) __threadfence();  // every wave's image words before wave 0's scan reads them
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    if (s.stats && lane == 0)
+        s.stats[(int64_t)b * a.max_det + k] = va_mask_stat{s_ms[0], s_ms[1], s_ms[3], s_ms[2], s_ms[4], {0, 0, 0}};
+    contour_scan<LDS>(a, b, k, r, img, item CT_PROF(, t0, t1));
+}
+
+__global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wg_kernel(CtArgs a) {
+    extern __shared__ __align__(16) uint32_t wg_img[];
+    const Src& s = a.s;
+    const int item = blockIdx.x;
+    const int b = item / a.max_det, k = item % a.max_det;
+    if (k >= s.ndet[b]) return;  // block-uniform
+    const Region r = region_of(s, b, k);
+    if (r.w <= 0) {
+        contour_empty(a, b, k, r);
+        return;
+    }
+    __shared__ int s_ms[5];
+    if (threadIdx.x == 0) s_ms[0] = 0, s_ms[1] = INT32_MAX, s_ms[2] = -1, s_ms[3] = INT32_MAX, s_ms[4] = -1;
+    __syncthreads();
+    if (region_need(s, r) <= CT_WG_LDS) {  // block-uniform: the image and the strip in LDS, the trace on LDS
+        float* strip = (float*)(wg_img + ((image_words(r) + 3) & ~3ll));
+        contour_wg_item<true>(a, b, k, r, wg_img, strip, item, s_ms);
+    } else {  // a larger region: the detection's global slot
+        unsigned char* slot = a.sc.base + (int64_t)item * a.sc.slot_bytes;
+        contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, item, s_ms);
     }
 }
 
@@ -1182,6 +1257,8 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     if (!pool_attr()) {
         if (hipFuncSetAttribute((const void*)post_contour_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 CP_POOL) != hipSuccess ||
+            hipFuncSetAttribute((const void*)post_contour_wg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                CT_WG_LDS) != hipSuccess ||
             hipFuncSetAttribute((const void*)post_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 FILL_LDS) != hipSuccess)
             return hipErrorInvalidValue;
@@ -1217,8 +1294,15 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     }
     const int pgrid = (int)(items < n_cu() ? items : n_cu());
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
-    hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st, ca);
-    hipLaunchKernelGGL(post_contour_global_kernel, dim3(grid), dim3(CT_THREADS), 0, st, ca);
+    // a slot per detection (small batches): the workgroup-per-detection form; VA_CT_WG=0 keeps the pool form (A/B)
+    static const bool wg_env = !(getenv("VA_CT_WG") && getenv("VA_CT_WG")[0] == '0');
+    if (wg_env && items <= sc.nslots) {
+        hipLaunchKernelGGL(post_contour_wg_kernel, dim3((int)items), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca);
+    } else {
+        hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st,
+                           ca);
+        hipLaunchKernelGGL(post_contour_global_kernel, dim3(grid), dim3(CT_THREADS), 0, st, ca);
+    }
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
     if (!cells) return hipSuccess;
     FillArgs fa;
