@@ -22,10 +22,14 @@ def main():
     from vision_assist_amd.post import PLANT_NEVER
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
     arch = Arch(sys.argv[1] if len(sys.argv) > 1 else "n")
-    bias = float(sys.argv[2]) if len(sys.argv) > 2 else None  # e.g. 4.0: the bench's dense regime
-    solid = len(sys.argv) > 3 and sys.argv[3] == "box"         # the dense_box regime's solid box masks
-    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, cls_bias=bias, solid_masks=solid)), 1,
-                         640, 640, dtype="bf16")
+    if len(sys.argv) > 2 and sys.argv[2] == "sparse":  # the bench's headline regime (bench.regime_kwargs)
+        from bench import regime_kwargs
+        kw = regime_kwargs("sparse", 640)
+    else:
+        bias = float(sys.argv[2]) if len(sys.argv) > 2 else None  # e.g. 4.0: the bench's dense regime
+        solid = len(sys.argv) > 3 and sys.argv[3] == "box"         # the dense_box regime's solid box masks
+        kw = dict(cls_bias=bias, solid_masks=solid)
+    pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, **kw)), 1, 640, 640, dtype="bf16")
     frame = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(1), dtype=torch.uint8)
     pipe.load(frame.cuda())
     for _ in range(2):

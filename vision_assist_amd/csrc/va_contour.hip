@@ -264,6 +264,29 @@ __device__ __forceinline__ bool row_has_start(const uint32_t* img, int ww, int y
     return __ballot(any) != 0ull;
 }
 
+// The first row in [y, yend) that row_has_start would accept, or yend: the rows' words taken 64 at a time across
+// rows (one ballot per 64 words instead of one per row).  Exact as a look-ahead: marks only grow and NZ never
+// changes, so a row without an unmarked start keeps having none; the scan calls this again after each trace.
+template <bool LDS>
+__device__ __forceinline__ int next_start_row(const uint32_t* img, int ww, int y, int yend) {
+    const int lane = threadIdx.x & 63;
+    const int total = (yend - y) * ww;
+    for (int i0 = 0; i0 < total; i0 += 64) {
+        const int i = i0 + lane;
+        bool hit = false;
+        if (i < total) {
+            const int dy = i / ww, wi = i - dy * ww;
+            const uint32_t* nzr = plane(img, ww, y + dy, 0);
+            const uint32_t nz = nzr[wi], pnz = wi >= 1 ? nzr[wi - 1] : 0u;
+            const uint32_t mk = ldm<LDS>(plane(img, ww, y + dy, 1) + wi) | ldm<LDS>(plane(img, ww, y + dy, 2) + wi);
+            hit = (nz & ~mk & ~((nz << 1) | (pnz >> 31))) != 0u;
+        }
+        const unsigned long long bal = __ballot(hit);
+        if (bal) return y + (i0 + __builtin_ctzll(bal)) / ww;
+    }
+    return yend;
+}
+
 // ------------------------------------------------------------------------------------------ building
 struct MaskStat {
     int cnt, x0, x1, y0, y1;
@@ -624,8 +647,9 @@ __device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, cons
     uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
     int best_n = 0, best_half = 0, bx = -1, by = -1, ncont = 0, alt = 0;
     for (int y = 1; y < r.rH - 1; ++y) {
+        y = next_start_row<LDS>(img, r.ww, y, r.rH - 1);  // skips the rows row_has_start would reject
+        if (y >= r.rH - 1) break;
         CT_WATCH(2, y);
-        if (!row_has_start<LDS>(img, r.ww, y)) continue;
         CT_PROF(++nrows);
         // OpenCV's skip loop, evaluated a 2048-pixel chunk at a time instead of position by position (the scan's
         // prev is always the value at x - 1, so its stops are the change positions of the current image).  Between
