@@ -245,27 +245,9 @@ __device__ __forceinline__ void code_planes(uint32_t nz, uint32_t n, uint32_t r,
     lo = r | (nz & ~n);
 }
 
-// Whether row y holds a non-zero, unmarked pixel right of a zero pixel: the only rows where cvFindNextContour can
-// start an outer border (traces only mark, so the answer at the row's start holds through the row).  Wave-wide.
-template <bool LDS>
-__device__ __forceinline__ bool row_has_start(const uint32_t* img, int ww, int y) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t* nzr = plane(img, ww, y, 0);
-    bool any = false;
-    for (int w0 = 0; w0 < ww; w0 += 64) {
-        const int wi = w0 + lane;
-        if (wi < ww) {
-            const uint32_t nz = nzr[wi], pnz = wi >= 1 ? nzr[wi - 1] : 0u;
-            const uint32_t mk = ldm<LDS>(plane(img, ww, y, 1) + wi) | ldm<LDS>(plane(img, ww, y, 2) + wi);
-            const uint32_t left0 = ~((nz << 1) | (pnz >> 31));
-            any |= (nz & ~mk & left0) != 0u;
-        }
-    }
-    return __ballot(any) != 0ull;
-}
-
-// The first row in [y, yend) that row_has_start would accept, or yend: the rows' words taken 64 at a time across
-// rows (one ballot per 64 words instead of one per row).  Exact as a look-ahead: marks only grow and NZ never
+// The first row in [y, yend) holding a non-zero, unmarked pixel right of a zero pixel -- the only rows where
+// cvFindNextContour can start an outer border (traces only mark, so the answer at the row's start holds through
+// the row) -- or yend: the rows' words taken 64 at a time across rows (one ballot per 64 words, not one per row).  Exact as a look-ahead: marks only grow and NZ never
 // changes, so a row without an unmarked start keeps having none; the scan calls this again after each trace.
 template <bool LDS>
 __device__ __forceinline__ int next_start_row(const uint32_t* img, int ww, int y, int yend) {
@@ -647,7 +629,7 @@ __device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, cons
     uint32_t* cp = a.sc.cpts + di * 2 * a.sc.capd;
     int best_n = 0, best_half = 0, bx = -1, by = -1, ncont = 0, alt = 0;
     for (int y = 1; y < r.rH - 1; ++y) {
-        y = next_start_row<LDS>(img, r.ww, y, r.rH - 1);  // skips the rows row_has_start would reject
+        y = next_start_row<LDS>(img, r.ww, y, r.rH - 1);  // skips the rows no outer border can start in
         if (y >= r.rH - 1) break;
         CT_WATCH(2, y);
         CT_PROF(++nrows);
