@@ -299,7 +299,8 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
                       int32_t W, int32_t c, int32_t dtype);
 
 /* A whole forward as a list of ops executed back-to-back on one stream by ONE call (no per-layer
- * host round trip; the list is built once per (batch, frame size) by the host planner). */
+ * host round trip; the list is built once per (batch, frame size) by the host planner), optionally with
+ * independent branches on lanes (VA_OP_FORK). */
 #define VA_OP_CONV 1        /* conv: all fields of .a */
 #define VA_OP_SPPF 2        /* sppf pool: a.y = buffer, a.N/H/W, a.Cin = c, a.ldy = ld, a.dtype */
 #define VA_OP_UPSAMPLE 3    /* upsample2x: a.x/a.ldx -> a.y/a.ldy, a.N/H/W (source size), a.Cin = c, a.dtype */
@@ -309,9 +310,20 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
                                MFMA form) -- see va_seg_conv0 / va_seg_conv0_f32(m) / va_seg_conv0_e4m3 */
 #define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
 #define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: see va_seg_stem */
+/* Branch-parallel lists (small batches, where one layer does not fill the 256 CUs): an op with lane L > 0
+ * is issued on auxiliary stream L of the calling stream (VA_LANES - 1 of them, created on first use per
+ * (device, calling stream) and kept for the process).  FORK (a.N = L): lane L waits for everything issued
+ * so far on the calling stream; JOIN (a.N = L): the calling stream waits for everything issued so far on
+ * lane L.  An op on lane L needs an earlier FORK of L in the same list; lanes still open at the end of the
+ * list are joined by the call, so the calling stream covers the whole list when it returns (and a graph
+ * captured on it holds the lanes as parallel branches).  While va_prof_* recording is on, lanes are
+ * ignored (every op on the calling stream, in list order -- a valid serial order of any laned list). */
+#define VA_OP_FORK 8
+#define VA_OP_JOIN 9
+#define VA_LANES 4
 typedef struct va_seg_op {
     int32_t kind;
-    int32_t pad_;
+    int32_t lane; /* 0 = the calling stream; 1 .. VA_LANES - 1 (see VA_OP_FORK) */
     va_conv_args a;
 } va_seg_op;
 

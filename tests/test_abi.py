@@ -79,3 +79,25 @@ def test_struct_layouts_match_python_mirrors():
     assert np.dtype(CSTAT_DTYPE).itemsize == ctypes.sizeof(ContourStat)
     assert list(out) == want
     del np
+
+
+def test_seg_run_rejects_bad_lanes():
+    """va_seg_run's lane checks (va355.h VA_OP_FORK) fail before any launch: a lane out of range, a join or an
+    op on a lane never forked, a fork of lane 0.  The failing op's index is encoded as rc - 1000 * (i + 1)."""
+    from vision_assist_amd import _lib
+    from vision_assist_amd.seg import VA_OP_CONV, VA_OP_FORK, VA_OP_JOIN, ConvArgs, SegOp
+    lib = _lib.load()
+
+    def run(*ops):
+        arr = (SegOp * len(ops))(*ops)
+        return lib.va_seg_run(None, arr, len(ops))
+
+    err = -1  # VA_ERR_ARG
+    assert run(SegOp(kind=VA_OP_CONV, lane=4)) == err - 1000
+    assert run(SegOp(kind=VA_OP_CONV, lane=-1)) == err - 1000
+    assert run(SegOp(kind=VA_OP_JOIN, a=ConvArgs(N=1))) == err - 1000
+    assert run(SegOp(kind=VA_OP_FORK, a=ConvArgs(N=0))) == err - 1000
+    assert run(SegOp(kind=VA_OP_FORK, a=ConvArgs(N=4))) == err - 1000
+    assert run(SegOp(kind=VA_OP_FORK, lane=1, a=ConvArgs(N=2))) == err - 1000
+    assert run(SegOp(kind=VA_OP_CONV, lane=2)) == err - 1000
+    assert lib.va_seg_run(None, (SegOp * 1)(), 0) == 0

@@ -715,6 +715,28 @@ def test_forward_deterministic():
             assert torch.equal(g_, r), f"{name}: run-to-run max diff {(g_ - r).abs().max().item()}"
 
 
+@pytest.mark.parametrize("dtype,scale,B", [("bf16", "s", 1), ("f32", "s", 1), ("bf16", "n", 3), ("f32", "n", 2),
+                                            ("fp8", "s", 1)])
+def test_lanes_match_serial(dtype, scale, B):
+    """The small-batch laned list (head levels 0 / 1 and proto on lanes 1 / 2 beside the neck, each lane with its
+    own split-K workspace -- va355.h VA_OP_FORK) gives bit-identical outputs to the same plan run serially,
+    run after run."""
+    arch, fw, net = _net(dtype, scale)
+    frames = _frames(B, seed=31)
+    p = net.plan(B, 640, 640)
+    kinds = [m["kind"] for m in p["meta"]]
+    assert kinds.count("sync") == 4 and {op.lane for op in p["ops"]} == {0, 1, 2}
+    laned = [_gpu_heads(net, frames) for _ in range(3)]
+    net.lanes = False
+    net._plans.clear()
+    assert "sync" not in [m["kind"] for m in net.plan(B, 640, 640)["meta"]]
+    serial = _gpu_heads(net, frames)
+    for run in laned:
+        for name, g_, r in zip(("box", "cls", "coef", "proto"), run, serial):
+            assert torch.isfinite(g_).all(), name
+            assert torch.equal(g_, r), f"{name}: laned vs serial max diff {(g_ - r).abs().max().item()}"
+
+
 # ---- BASELINE.json configs[4] shape (C5): YOLOv8m-seg at 1280 x 1280 (bf16 here; fp8 weights are not built)
 _M1280 = {}
 

@@ -17,6 +17,7 @@
 //   sppf_pool_kernel<T>     SPPF's three chained MaxPool2d(5,1,2) as one pass: 5x5, 9x9, 13x13 maxima
 //   upsample2x_kernel<T>    nearest x2 into a concat slice
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
@@ -4270,42 +4271,113 @@ int va_seg_conv0_f32m(void* stream, const uint8_t* frames, int32_t N, int32_t H,
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+}  // extern "C"
+
+// ---- lanes of a laned op list (va355.h VA_OP_FORK) ----
+// One set of VA_LANES - 1 non-blocking streams + fork / join events per (device, calling stream): two
+// pipelines with forwards in flight on two streams never share a lane (no false ordering between them).
+// Every wait a list issues points at work already submitted (a fork waits on the calling stream's past, a
+// join on the lane's past), so lanes sharing a hardware queue cannot deadlock.
+namespace {
+struct LaneSet {
+    int dev;
+    hipStream_t owner;
+    hipStream_t s[VA_LANES];
+    hipEvent_t fork[VA_LANES], join[VA_LANES];
+};
+constexpr int VA_LANE_SETS = 32;
+LaneSet g_lane_sets[VA_LANE_SETS];
+int g_nlane_sets = 0;
+std::mutex g_lane_mu;
+
+// -> the calling stream's lane set (created on first use), or nullptr (table full / HIP error: the list then
+// runs serially on the calling stream, in list order)
+LaneSet* lane_set(hipStream_t owner) {
+    const int dev = va_cur_dev();
+    std::lock_guard<std::mutex> lk(g_lane_mu);
+    for (int i = 0; i < g_nlane_sets; ++i)
+        if (g_lane_sets[i].dev == dev && g_lane_sets[i].owner == owner) return &g_lane_sets[i];
+    if (g_nlane_sets == VA_LANE_SETS) return nullptr;
+    LaneSet& ls = g_lane_sets[g_nlane_sets];
+    ls.dev = dev;
+    ls.owner = owner;
+    for (int l = 1; l < VA_LANES; ++l)
+        if (hipStreamCreateWithFlags(&ls.s[l], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ls.fork[l], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ls.join[l], hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+    ++g_nlane_sets;
+    return &ls;
+}
+}  // namespace
+
+extern "C" {
+
 int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
     if (!ops || n < 0) return VA_ERR_ARG;
+    LaneSet* ls = nullptr;          // resolved at the first fork
+    bool serial = g_prof_on;        // live timing brackets every op on the calling stream
+    unsigned forked = 0, open = 0;  // lanes forked in this list / with work not yet joined
     for (int i = 0; i < n; ++i) {
         const va_conv_args& a = ops[i].a;
+        const int kind = ops[i].kind, lane = ops[i].lane;
+        if (lane < 0 || lane >= VA_LANES) return VA_ERR_ARG - 1000 * (i + 1);
+        if (kind == VA_OP_FORK || kind == VA_OP_JOIN) {
+            const int l = a.N;
+            if (l < 1 || l >= VA_LANES || lane != 0 || (kind == VA_OP_JOIN && !(forked >> l & 1)))
+                return VA_ERR_ARG - 1000 * (i + 1);
+            forked |= 1u << l;
+            if (serial) continue;
+            if (!ls && !(ls = lane_set((hipStream_t)stream))) {
+                serial = true;
+                continue;
+            }
+            const bool fk = kind == VA_OP_FORK;
+            hipStream_t from = fk ? (hipStream_t)stream : ls->s[l], to = fk ? ls->s[l] : (hipStream_t)stream;
+            hipEvent_t ev = fk ? ls->fork[l] : ls->join[l];
+            if (hipEventRecord(ev, from) != hipSuccess || hipStreamWaitEvent(to, ev, 0) != hipSuccess)
+                return VA_ERR_HIP - 1000 * (i + 1);
+            open = fk ? (open | 1u << l) : (open & ~(1u << l));
+            continue;
+        }
+        if (lane && !(forked >> lane & 1)) return VA_ERR_ARG - 1000 * (i + 1);
+        void* st = stream;
+        if (lane && !serial) {
+            st = ls->s[lane];
+            open |= 1u << lane;
+        }
         int rc;
         const bool prof = g_prof_on && g_ev_used < g_ev_cap;
         if (prof && hipEventRecord(g_ev[2 * g_ev_used], (hipStream_t)stream) != hipSuccess) return VA_ERR_HIP;
-        switch (ops[i].kind) {
+        switch (kind) {
             case VA_OP_CONV:
-                rc = va_seg_conv(stream, &a);
+                rc = va_seg_conv(st, &a);
                 break;
             case VA_OP_SPPF:
-                rc = va_seg_sppf_pool(stream, a.y, a.N, a.H, a.W, a.Cin, a.ldy, a.dtype);
+                rc = va_seg_sppf_pool(st, a.y, a.N, a.H, a.W, a.Cin, a.ldy, a.dtype);
                 break;
             case VA_OP_UPSAMPLE:
-                rc = va_seg_upsample2x(stream, a.x, a.ldx, a.y, a.ldy, a.N, a.H, a.W, a.Cin, a.dtype);
+                rc = va_seg_upsample2x(st, a.x, a.ldx, a.y, a.ldy, a.N, a.H, a.W, a.Cin, a.dtype);
                 break;
             case VA_OP_PREPROCESS:
-                rc = va_seg_preprocess(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.dtype, a.y);
+                rc = va_seg_preprocess(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.dtype, a.y);
                 break;
             case VA_OP_CONV0:
                 rc = a.dtype == VA_DTYPE_F32
-                         ? (a.w3 ? va_seg_conv0_f32m(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w3, a.bias, a.Cout,
+                         ? (a.w3 ? va_seg_conv0_f32m(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.w3, a.bias, a.Cout,
                                                      (float*)a.y, a.ldy)
-                                 : va_seg_conv0_f32(stream, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w,
+                                 : va_seg_conv0_f32(st, (const uint8_t*)a.x, a.N, a.H, a.W, (const float*)a.w,
                                                     a.bias, a.Cout, (float*)a.y, a.ldy))
                      : a.dtype == VA_DTYPE_FP8
-                         ? va_seg_conv0_e4m3(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout,
+                         ? va_seg_conv0_e4m3(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout,
                                              (uint8_t*)a.y, a.ldy, a.yscale)
-                         : va_seg_conv0(stream, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
+                         : va_seg_conv0(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             case VA_OP_C2F:
-                rc = va_seg_c2f(stream, &a);
+                rc = va_seg_c2f(st, &a);
                 break;
             case VA_OP_STEM:
-                rc = va_seg_stem(stream, &a);
+                rc = va_seg_stem(st, &a);
                 break;
             default:
                 rc = VA_ERR_ARG;
@@ -4314,9 +4386,14 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
         if (prof) {
             if (hipEventRecord(g_ev[2 * g_ev_used + 1], (hipStream_t)stream) != hipSuccess) return VA_ERR_HIP;
             g_ev_op[g_ev_used] = i;
-            g_ev_kind[g_ev_used++] = ops[i].kind;
+            g_ev_kind[g_ev_used++] = kind;
         }
     }
+    for (int l = 1; l < VA_LANES; ++l)  // lanes the list left open
+        if (open >> l & 1)
+            if (hipEventRecord(ls->join[l], ls->s[l]) != hipSuccess ||
+                hipStreamWaitEvent((hipStream_t)stream, ls->join[l], 0) != hipSuccess)
+                return VA_ERR_HIP;
     return VA_OK;
 }
 

@@ -24,13 +24,15 @@ from .seg import SegNet
 class FramePipeline:
     def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "bf16", conf: float = 0.5,
                  iou: float = 0.7, max_det: int = 300, device=None, seen: AngleSeen | None = None,
-                 seg: SegNet | None = None, tag: int = 0, imgsz: int | None = None, fp8_calib=None):
+                 seg: SegNet | None = None, tag: int = 0, imgsz: int | None = None, fp8_calib=None,
+                 lanes: bool | None = None):
         """H x W: the frame size.  ``imgsz`` = YOLO.predict's imgsz: frames are letterboxed to it on the device
         (va_letterbox; LetterBox(imgsz, auto=True, scaleup=True)) whenever that changes them -- the 640
         default of the reference's model.predict call -- and the mask choice maps back to frame coordinates,
         so cells / rects / the nav stage stay at H x W.  ``imgsz=None``: the network runs at the frame's own
         size when its sides are multiples of 32 (the C5 shape, m-seg at 1280x1280, BASELINE.json configs[4];
-        640x640 is the same either way), else at the 640 letterbox."""
+        640x640 is the same either way), else at the 640 letterbox.  ``lanes``: SegNet.plan's branch-parallel
+        list (default: on for small batches)."""
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.B, self.H, self.W = B, H, W
         self.lb = None
@@ -50,7 +52,7 @@ class FramePipeline:
         self.seg = seg if seg is not None else SegNet(arch, folded, dtype=dtype, device=self.device)
         if fp8_calib is not None:  # fp8: representative frames (uint8 [n, Hn, Wn, 3]) for the activation scales
             self.seg.fp8_calib_frames = torch.as_tensor(fp8_calib)
-        self.plan = self.seg.plan(B, Hn, Wn, tag)
+        self.plan = self.seg.plan(B, Hn, Wn, tag, lanes=lanes)
         self.post = PostEngine(B, Hn, Wn, arch.nc, conf, iou, max_det, device=self.device, frame=frame)
         self.nav = NavEngine(H, W, max_batch=B, device=self.device)
         self.seen = seen if seen is not None else AngleSeen(self.device)
@@ -141,6 +143,9 @@ class OverlappedPipelines:
                  seg_streams: int = 2, depth: int = 2, **kw):
         if depth < 2:
             raise ValueError("depth >= 2")
+        # whole forwards already overlap here: the laned list's extra streams would only contend with them for
+        # the hardware queues (C4 shape: 904 -> 506 frames/s with lanes)
+        kw.setdefault("lanes", False)
         first = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, tag=0, **kw)
         self.pipes = [first] + [FramePipeline(arch, folded, B, H, W, dtype=dtype, device=first.device,
                                               seen=first.seen, seg=first.seg, tag=i, **kw) for i in range(1, depth)]

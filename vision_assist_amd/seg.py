@@ -28,6 +28,7 @@ F8_KS = 128        # K-step of the fp8 kernel (va_fp8.hip): fp8 weights are padd
 F8_MAX = 448.0     # largest OCP e4m3 value
 FP8_HEADROOM = 2.0  # calibration amax x this maps to [224, 448] (SegNet.calibrate_fp8)
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
+VA_OP_FORK, VA_OP_JOIN = 8, 9  # lanes of a branch-parallel list (va355.h)
 SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -59,7 +60,7 @@ class ConvArgs(ctypes.Structure):
 
 
 class SegOp(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_int32), ("pad_", ctypes.c_int32), ("a", ConvArgs)]
+    _fields_ = [("kind", ctypes.c_int32), ("lane", ctypes.c_int32), ("a", ConvArgs)]
 
 
 def _ceil(a, b):
@@ -152,6 +153,9 @@ class SegNet:
         self.w0 = (w0p.to(self.device, self.tdtype).contiguous(), b0.float().to(self.device).contiguous())
         self.fuse_first = w0.shape[0] % 16 == 0 and w0.shape[0] <= 64 and os.environ.get("VA_CONV0", "1") != "0"
         self.w0_3 = None
+        # small batches: head levels + proto on lanes beside the neck (plan() laned; VA_LANES=0 off, A/B)
+        self.lanes = os.environ.get("VA_LANES", "1") != "0"
+        self.lanes_max_b = int(os.environ.get("VA_LANES_MAX_B", "8"))
         if dtype == "f32":  # va_seg_conv0_f32: [Cout][27], k = (ky*3 + kx)*3 + c (RGB)
             self.w0 = (w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27).float().to(self.device).contiguous(),
                        b0.float().to(self.device).contiguous())
@@ -246,7 +250,7 @@ class SegNet:
         index = {t.data_ptr(): i for i, t in enumerate(bufs)}
         self.xscale = {m["prefix"]: self.bscale[index[m["src"].buf.data_ptr()]] for m in p["meta"]
                        if m.get("src") is not None and m["prefix"] in self.w8}
-        del self._plans[(B, H, W, -1, True)]
+        self._plans = {k: v for k, v in self._plans.items() if k[3:5] != (-1, True)}
         return self.xscale
 
     def _pack_stem(self, w0p: torch.Tensor, b0: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor):
@@ -383,11 +387,14 @@ class SegNet:
     def _buf(self, B, h, w, c, dtype=None):
         return torch.empty((B, h, w, c), dtype=dtype or self.tdtype, device=self.device)
 
-    def plan(self, B: int, H: int, W: int, tag: int = 0, _calib: bool = False):
+    def plan(self, B: int, H: int, W: int, tag: int = 0, _calib: bool = False, lanes: bool | None = None):
         """Op list + buffers for B frames of H x W (``tag`` gives independent buffer sets, e.g. for
         double-buffered batches that overlap on two streams).  fp8: calibrated on first use (calibrate_fp8);
-        _calib = the bf16 plan that calibration runs."""
-        key = (B, H, W, tag, _calib)
+        _calib = the bf16 plan that calibration runs.  ``lanes``: the branch-parallel list (laned(); default
+        self.lanes for B <= self.lanes_max_b) -- off for callers that already overlap whole forwards."""
+        if lanes is None:
+            lanes = self.lanes and B <= self.lanes_max_b
+        key = (B, H, W, tag, _calib, lanes)
         if key in self._plans:
             return self._plans[key]
         fp8 = self.dtype == "fp8" and not _calib
@@ -510,6 +517,60 @@ class SegNet:
                                                               dtype=VA_DTYPE_FP8 if src.e4m3 else self.va_dtype)))
             meta.append({"name": "upsample", "kind": "upsample"})
 
+        def finish(proto: Slice):
+            nonlocal ops, meta
+            marks["P"] = len(ops)
+            if lanes:
+                ops, meta = laned(ops, meta)
+            assert len(meta) == len(ops)
+            plan = {"ops": (SegOp * len(ops))(*ops), "n": len(ops), "meta": meta, "keep": keep, "frames": frames,
+                    "bufs": bufs, "links": links, "out": SegOutputs(levels=levels, proto=proto.buf)}
+            self._plans[key] = plan
+            return plan
+
+        def laned(ops, meta):
+            """Small batches: the head's levels and proto overlap the rest of the neck (va355.h VA_OP_FORK).
+            Lane 1 runs head level 0 then proto once model.15 (o3) is out, lane 2 head level 1 once model.18
+            (o4) is, the calling stream model.16 .. model.21 then head level 2: the critical path drops from
+            the whole list to backbone + neck + one head level.  Each lane gets its own split-K workspace
+            (the kernels' slabs and arrival counters must not be shared by launches that can overlap)."""
+            m = marks
+            rng = {"A": (0, m["A"]), "B": (m["A"], m["B"]), "C": (m["B"], m["C"]), "H0": (m["C"], m["H0"]),
+                   "H1": (m["H0"], m["H1"]), "H2": (m["H1"], m["H2"]), "P": (m["H2"], m["P"])}
+            out_ops, out_meta = [], []
+
+            def take(part, lane):
+                for i in range(*rng[part]):
+                    op = ops[i]
+                    op.lane = lane
+                    if lane and op.kind == VA_OP_CONV and op.a.ws:
+                        lws, lcnt = lane_ws[lane]
+                        op.a.ws, op.a.wcnt = lws.data_ptr(), lcnt.data_ptr()
+                    out_ops.append(op)
+                    out_meta.append(meta[i])
+
+            def sync(kind, lane):
+                out_ops.append(SegOp(kind=kind, a=ConvArgs(N=lane)))
+                out_meta.append({"name": f"{'fork' if kind == VA_OP_FORK else 'join'} lane {lane}", "kind": "sync"})
+
+            lane_ws = {}
+            for lane in (1, 2):
+                lane_ws[lane] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=self.device),
+                                 torch.zeros(SPLITK_NCNT, dtype=torch.int32, device=self.device))
+                keep.extend(lane_ws[lane])
+            take("A", 0)
+            sync(VA_OP_FORK, 1)
+            take("H0", 1)
+            take("P", 1)
+            take("B", 0)
+            sync(VA_OP_FORK, 2)
+            take("H1", 2)
+            take("C", 0)
+            take("H2", 0)
+            sync(VA_OP_JOIN, 1)
+            sync(VA_OP_JOIN, 2)
+            return out_ops, out_meta
+
         frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
         h1, w1 = H // 2, W // 2
         h2, w2 = H // 4, W // 4
@@ -585,12 +646,15 @@ class SegNet:
             upsample(h12, cat14.sub(0, a.c4), h4, w4)
         o3 = new(h3, w3, a.c3)
         c2f(15, cat14, o3, h3, w3, up=h12 if fuse_up else None)
+        marks = {"A": len(ops)}  # op index ranges of the branches finish() may put on lanes
         conv("model.16", o3, cat17.sub(0, a.c3), h3, w3, stride=2)
         o4 = new(h4, w4, a.c4)
         c2f(18, cat17, o4, h4, w4)
+        marks["B"] = len(ops)
         conv("model.19", o4, cat20.sub(0, a.c4), h4, w4, stride=2)
         o5 = new(h5, w5, a.c5)
         c2f(21, cat20, o5, h5, w5)
+        marks["C"] = len(ops)
         # Segment head: per level [box 64 | cls nc | coef 32] float32
         cb, cc, cm = a.head_c2, a.head_c3, a.head_c4
         no = 4 * REG_MAX + a.nc + NM
@@ -609,6 +673,7 @@ class SegNet:
                     continue
                 conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
                 conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False, out_f32=True)
+            marks[f"H{l}"] = len(ops)
         # Proto
         if self.proto_fold is not None and self.dtype == "f32":
             # the sub-pixel fold (mode 2, border bias table) into the 4x map, then cv3 as its own 1x1 GEMM
@@ -627,12 +692,7 @@ class SegNet:
                          "bytes": 4 * B * h3 * w3 * pf.cin + 4 * pf.w.numel() + 4 * B * h2 * w2 * pf.cout})
             proto = new(h2, w2, NM, torch.float32)
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
-            op_arr = (SegOp * len(ops))(*ops)
-            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
-                    "links": links,
-                    "out": SegOutputs(levels=levels, proto=proto.buf)}
-            self._plans[key] = plan
-            return plan
+            return finish(proto)
         if self.proto_fold is not None:
             pf = self.proto_fold
             pr1 = new(h3, w3, a.npr)
@@ -650,12 +710,7 @@ class SegNet:
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * (pf.K + p3.cout),
                          "bytes": 2 * B * h3 * w3 * pf.cin + 2 * pf.w.numel() + 4 * B * h2 * w2 * NM})
-            op_arr = (SegOp * len(ops))(*ops)
-            plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
-                    "links": links,
-                    "out": SegOutputs(levels=levels, proto=proto.buf)}
-            self._plans[key] = plan
-            return plan
+            return finish(proto)
         pr1 = new(h3, w3, a.npr)
         conv("model.22.proto.cv1", o3, pr1, h3, w3)
         pr2 = new(h2, w2, a.npr)
@@ -667,13 +722,7 @@ class SegNet:
             pr3 = new(h2, w2, a.npr)
             conv("model.22.proto.cv2", pr2, pr3, h2, w2)
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
-        op_arr = (SegOp * len(ops))(*ops)
-        assert len(meta) == len(ops)
-        plan = {"ops": op_arr, "n": len(ops), "meta": meta, "keep": keep, "frames": frames, "bufs": bufs,
-                    "links": links,
-                "out": SegOutputs(levels=levels, proto=proto.buf)}
-        self._plans[key] = plan
-        return plan
+        return finish(proto)
 
     @staticmethod
     def _fp8_fits(p: Packed, src: Slice, dst: Slice, res, out_f32: bool) -> bool:
