@@ -718,14 +718,18 @@ def test_forward_deterministic():
 @pytest.mark.parametrize("dtype,scale,B", [("bf16", "s", 1), ("f32", "s", 1), ("bf16", "n", 3), ("f32", "n", 2),
                                             ("fp8", "s", 1)])
 def test_lanes_match_serial(dtype, scale, B):
-    """The small-batch laned list (head levels 0 / 1 and proto on lanes 1 / 2 beside the neck, each lane with its
-    own split-K workspace -- va355.h VA_OP_FORK) gives bit-identical outputs to the same plan run serially,
+    """The small-batch laned list (head levels 0 / 1 and proto on lanes 1 / 2 beside the neck, head level 2's
+    branches on three streams, each lane with its own split-K workspace -- va355.h VA_OP_FORK) gives bit-identical outputs to the same plan run serially,
     run after run."""
     arch, fw, net = _net(dtype, scale)
     frames = _frames(B, seed=31)
     p = net.plan(B, 640, 640)
     kinds = [m["kind"] for m in p["meta"]]
-    assert kinds.count("sync") == 4 and {op.lane for op in p["ops"]} == {0, 1, 2}
+    split = dtype == "f32"  # head level 2's branches on lanes too
+    assert kinds.count("sync") == (7 if split else 4)
+    assert {op.lane for op in p["ops"]} == ({0, 1, 2, 3} if split else {0, 1, 2})
+    assert sorted(m["name"] for m in p["meta"] if m["kind"] != "sync") == \
+        sorted(m["name"] for m in net.plan(B, 640, 640, lanes=False)["meta"])
     laned = [_gpu_heads(net, frames) for _ in range(3)]
     net.lanes = False
     net._plans.clear()

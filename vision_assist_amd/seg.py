@@ -531,12 +531,20 @@ class SegNet:
         def laned(ops, meta):
             """Small batches: the head's levels and proto overlap the rest of the neck (va355.h VA_OP_FORK).
             Lane 1 runs head level 0 then proto once model.15 (o3) is out, lane 2 head level 1 once model.18
-            (o4) is, the calling stream model.16 .. model.21 then head level 2: the critical path drops from
-            the whole list to backbone + neck + one head level.  Each lane gets its own split-K workspace
-            (the kernels' slabs and arrival counters must not be shared by launches that can overlap)."""
+            (o4) is, the calling stream model.16 .. model.21 then head.2.0, whose three branches (box / cls /
+            coef, independent 3x3 + 1x1 pairs) then run on the calling stream, lane 3 and lane 2 (f32): the
+            critical path drops from the whole list to backbone + neck + head.2.0 + one branch.  Each lane gets its own
+            split-K workspace (the kernels' slabs and arrival counters must not be shared by launches that can
+            overlap)."""
             m = marks
             rng = {"A": (0, m["A"]), "B": (m["A"], m["B"]), "C": (m["B"], m["C"]), "H0": (m["C"], m["H0"]),
-                   "H1": (m["H0"], m["H1"]), "H2": (m["H1"], m["H2"]), "P": (m["H2"], m["P"])}
+                   "H1": (m["H0"], m["H1"]), "H2.0": (m["H1"], m["H2.0"]), "H2.cv2": (m["H2.0"], m["H2.cv2"]),
+                   "H2.cv3": (m["H2.cv2"], m["H2.cv3"]), "H2.cv4": (m["H2.cv3"], m["H2.cv4"]),
+                   "P": (m["H2"], m["P"])}
+            assert m["H2.cv4"] == m["H2"]
+            # a fork + join costs a few us of cross-queue signalling: worth it for the f32 branches (~40 us each,
+            # f32 s batch 1: 1302 -> 1282 us), not for the bf16 ones (~15 us: 714 -> 728 us)
+            split_h2 = self.store == "f32"
             out_ops, out_meta = [], []
 
             def take(part, lane):
@@ -554,7 +562,7 @@ class SegNet:
                 out_meta.append({"name": f"{'fork' if kind == VA_OP_FORK else 'join'} lane {lane}", "kind": "sync"})
 
             lane_ws = {}
-            for lane in (1, 2):
+            for lane in (1, 2, 3) if split_h2 else (1, 2):
                 lane_ws[lane] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=self.device),
                                  torch.zeros(SPLITK_NCNT, dtype=torch.int32, device=self.device))
                 keep.extend(lane_ws[lane])
@@ -566,9 +574,18 @@ class SegNet:
             sync(VA_OP_FORK, 2)
             take("H1", 2)
             take("C", 0)
-            take("H2", 0)
-            sync(VA_OP_JOIN, 1)
-            sync(VA_OP_JOIN, 2)
+            take("H2.0", 0)
+            if split_h2:
+                sync(VA_OP_FORK, 3)
+                take("H2.cv3", 3)
+                sync(VA_OP_FORK, 2)  # lane 2 is through head level 1 by now (model.19 .. head.2.0 ran meanwhile)
+                take("H2.cv4", 2)
+                take("H2.cv2", 0)
+            else:
+                for br in ("cv2", "cv3", "cv4"):
+                    take(f"H2.{br}", 0)
+            for lane in (1, 2, 3) if split_h2 else (1, 2):
+                sync(VA_OP_JOIN, lane)
             return out_ops, out_meta
 
         frames = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
@@ -662,6 +679,7 @@ class SegNet:
         for l, (src, hh, ww) in enumerate(((o3, h3, w3), (o4, h4, w4), (o5, h5, w5))):
             hb = new(hh, ww, cb + cc + cm)
             conv(f"head.{l}.0", src, hb, hh, ww)
+            marks[f"H{l}.0"] = len(ops)
             hb2 = new(hh, ww, cb + cc + cm)
             out = new(hh, ww, no, torch.float32)
             levels.append(out.buf)
@@ -670,9 +688,11 @@ class SegNet:
                 if self._can_fuse_tail(f"model.22.{br}.{l}.1", f"model.22.{br}.{l}.2"):
                     conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), out.sub(ooff, oc), hh, ww, out_f32=True,
                          tail=f"model.22.{br}.{l}.2", act2=False)
-                    continue
-                conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
-                conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False, out_f32=True)
+                else:
+                    conv(f"model.22.{br}.{l}.1", hb.sub(off, cw), hb2.sub(off, cw), hh, ww)
+                    conv(f"model.22.{br}.{l}.2", hb2.sub(off, cw), out.sub(ooff, oc), hh, ww, act=False,
+                         out_f32=True)
+                marks[f"H{l}.{br}"] = len(ops)
             marks[f"H{l}"] = len(ops)
         # Proto
         if self.proto_fold is not None and self.dtype == "f32":
