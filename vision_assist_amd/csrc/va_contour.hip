@@ -454,12 +454,35 @@ __device__ __forceinline__ void mark_at(uint32_t* img, int ww, int x, int y, boo
     atomicOr(plane(img, ww, y, right ? 2 : 1) + (x >> 5), 1u << (x & 31));
 }
 
-// icvFetchContour (CHAIN_APPROX_SIMPLE) from the outer-border start (x0, y0) of the framed image, executed by the
-// whole wave in lock step (every lane the same pixel, scalar state).  mark(x, y, right) gets every visit's mark,
-// emit(x, y) every kept point in order.  Returns the number of points.
-template <typename Mark, typename Emit>
-__device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int y0, Mark mark, Emit emit,
-                                             int* steps = nullptr) {
+// A straight run of the border: with the follow at P_0 = (x, y) having arrived in direction D (s_end = D + 4), the
+// number k of consecutive pixels P_j = P_0 + j D (j < 63) at which it leaves in direction D again, i.e. the
+// counter-clockwise search from s_end + 1 meets zeros at D + 5, D + 6, D + 7 and a non-zero at D: no point is kept
+// there (the direction does not change) and P_j + D = P_(j + 1) is the next position.  Lane j tests P_j (four bits
+// of the NZ plane, which no trace changes); k = the ballot's trailing ones.  Lanes whose neighbourhood leaves the
+// framed image test false (the border is zero, so a run never reaches it).
+__device__ __forceinline__ int border_run(const uint32_t* img, int ww, int rh, int x, int y, int D) {
+    const int j = threadIdx.x & 63;
+    const int px = x + j * dir_dx(D), py = y + j * dir_dy(D);
+    bool run = false;
+    if (j < 63 && px >= 1 && py >= 1 && py < rh - 1 && px + 1 < 32 * ww) {
+        auto nz = [&](int d) {
+            const int qx = px + dir_dx(d & 7), qy = py + dir_dy(d & 7);
+            return (plane(img, ww, qy, 0)[qx >> 5] >> (qx & 31)) & 1u;
+        };
+        run = nz(D) && !(nz(D + 5) | nz(D + 6) | nz(D + 7));
+    }
+    return __builtin_ctzll(~__ballot(run));
+}
+
+// icvFetchContour (CHAIN_APPROX_SIMPLE) from the outer-border start (x0, y0) of the framed image (rh rows), executed
+// by the whole wave in lock step (every lane the same pixel, scalar state).  mark(x, y, right) gets a visit's mark,
+// mark_run(x, y, D, k, right) the marks of k visits P_0 + j D (j < k) at once, emit(x, y) every kept point in order.
+// Where the follow continues in the direction it came (no point kept), the straight run ahead is measured by
+// border_run and crossed in one move: a box-like mask's border is a handful of runs instead of one serial step
+// (≈ 560 cycles of dependent scalar work) per pixel.  Returns the number of points.
+template <typename Mark, typename MarkRun, typename Emit>
+__device__ __forceinline__ int follow_border(uint32_t* img, int ww, int rh, bool runs, int x0, int y0, Mark mark,
+                                             MarkRun mark_run, Emit emit, int* steps = nullptr) {
     TraceWin w{0ull, 0ull, 0ull, -1, -1};
     win_at(img, ww, x0, y0, w);
     const unsigned nb = win_nbrs(w, x0);
@@ -478,12 +501,38 @@ __device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int 
     const int p0 = x0 | (y0 << 16), p1 = x1 | (y1 << 16);
     int x3 = x0, y3 = y0;
     int prev_s = s ^ 4, n = 0;
+    bool cont1 = false;  // the previous step continued in its direction
     unsigned nb3 = nb;
     while (true) {
         const int s_end = s;
         // counter-clockwise from s_end + 1 to the first non-zero neighbour (one exists: i1 at the latest)
         const unsigned rot = ((nb3 | (nb3 << 8)) >> ((s_end + 1) & 7)) & 0xFFu;
         s = (s_end + 1 + __builtin_ctz(rot)) & 7;
+        // s_end = prev_s + 4 always: s == prev_s is a run from (x3, y3) on, k >= 1 (x3 itself continues; the
+        // k > 0 test only keeps a broken invariant from stalling the loop).  Measured from the run's second pixel
+        // on: noise-like masks' runs are mostly one pixel, where the probe would cost more than the step.
+        const bool cont = s == prev_s;
+        const int k = runs && cont && cont1 ? border_run(img, ww, rh, x3, y3, s) : 0;
+        cont1 = cont;
+        if (k > 0) {
+            const int dx = dir_dx(s), dy = dir_dy(s);
+            const bool right = (unsigned)(s - 1) < (unsigned)s_end;
+            // the stop (x3 = i1 and the next position = i0) inside the run: i1 = P_j, j < k, with i1 + D = i0
+            const int j1 = dx ? (x1 - x3) * dx : (y1 - y3) * dy;
+            if (j1 >= 0 && j1 < k && x3 + j1 * dx == x1 && y3 + j1 * dy == y1 && x1 + dx == x0 && y1 + dy == y0) {
+                mark_run(x3, y3, s, j1 + 1, right);
+                CT_PROF(if (steps) *steps += j1 + 1);
+                break;
+            }
+            mark_run(x3, y3, s, k, right);
+            CT_PROF(if (steps) *steps += k);
+            x3 += k * dx;
+            y3 += k * dy;
+            s = (s + 4) & 7;
+            win_at(img, ww, x3, y3, w);
+            nb3 = win_nbrs(w, x3);
+            continue;
+        }
         const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
         mark(x3, y3, (unsigned)(s - 1) < (unsigned)s_end);
         if (s != prev_s) {
@@ -504,8 +553,8 @@ __device__ __forceinline__ int follow_border(uint32_t* img, int ww, int x0, int 
 
 // the unmarked form (a contour followed again for its points)
 template <typename Emit>
-__device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int y0, Emit emit) {
-    return follow_border(img, ww, x0, y0, [](int, int, bool) {}, emit);
+__device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int rh, bool runs, int x0, int y0, Emit emit) {
+    return follow_border(img, ww, rh, runs, x0, y0, [](int, int, bool) {}, [](int, int, int, int, bool) {}, emit);
 }
 
 // The scan's form: marks and points are collected one per lane in registers (lane i takes record i)
@@ -514,8 +563,8 @@ __device__ __forceinline__ int fetch_contour(uint32_t* img, int ww, int x0, int 
 // only the mask plane, never the marks, so deferring them changes nothing it sees).  Points go to dst[0, capd)
 // as network pixels X | Y << 16.  Returns the number of points.
 template <bool LDS>
-__device__ __forceinline__ int trace_marked(uint32_t* img, int ww, int x0, int y0, uint32_t* dst, int capd, int X0,
-                                            int Y0, int* steps = nullptr) {
+__device__ __forceinline__ int trace_marked(uint32_t* img, int ww, int rh, bool runs, int x0, int y0, uint32_t* dst,
+                                            int capd, int X0, int Y0, int* steps = nullptr) {
     const int lane = threadIdx.x & 63;
     int mrec = 0, nm = 0;   // lane i: pending mark i (x | y << 16 | right << 31)
     int prec = 0, np = 0;   // lane i: pending point i
@@ -530,10 +579,17 @@ __device__ __forceinline__ int trace_marked(uint32_t* img, int ww, int x0, int y
         if (lane < cnt && base + lane < capd) dst[base + lane] = (uint32_t)prec;
     };
     const int n = follow_border(
-        img, ww, x0, y0,
+        img, ww, rh, runs, x0, y0,
         [&](int x, int y, bool right) {
             if (lane == (nm & 63)) mrec = x | (y << 16) | (right ? (int)0x80000000 : 0);
             if ((++nm & 63) == 0) flush_marks(64);
+        },
+        [&](int x, int y, int D, int k, bool right) {  // a run's marks: lane j ORs visit j's bit, now
+            if (lane < k) {
+                const int px = x + lane * dir_dx(D), py = y + lane * dir_dy(D);
+                if (CT_OK(px >= 0 && py >= 0 && (px >> 5) < ww, 3, px, py))
+                    atomicOr(plane(img, ww, py, right ? 2 : 1) + (px >> 5), 1u << (px & 31));
+            }
         },
         [&](int x, int y) {
             if (lane == (np & 63)) prec = (X0 + x - 1) | ((Y0 + y - 1) << 16);
@@ -563,6 +619,7 @@ struct CtArgs {
     int32_t* poly_n;
     int poly_cap;
     int gate;                 // pool kernel: hold new claims while a wave waits for pages
+    int runs;                 // border following crosses straight runs in one move (border_run; 0: step by step)
     int64_t pool_max;         // bytes: larger images go to the global-memory form
     int pages;                // pages of the pool kernel's LDS (<= CP_PAGES)
 };
@@ -693,8 +750,8 @@ __device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, cons
                 const int l = __builtin_ctzll(okb);
                 const int x = 32 * (w0 + l) + __builtin_amdgcn_readlane(okbit, l);
                 CT_PROF(const unsigned long long ta = __builtin_amdgcn_s_memtime());
-                const int n = trace_marked<LDS>(img, r.ww, x, y, cp + alt * a.sc.capd, a.sc.capd, r.X0, r.Y0,
-                                                CT_STEPS);
+                const int n = trace_marked<LDS>(img, r.ww, r.rH, a.runs, x, y, cp + alt * a.sc.capd, a.sc.capd,
+                                                r.X0, r.Y0, CT_STEPS);
                 CT_PROF(ttr += __builtin_amdgcn_s_memtime() - ta);
                 ++ncont;
                 CT_WATCH(3, ncont);
@@ -740,11 +797,11 @@ __device__ __forceinline__ void contour_scan(const CtArgs& a, int b, int k, cons
             }
         } else {  // longer than the buffer: followed again from the image (marks off)
             int lx = 0, ly = 0;
-            fetch_contour(img, r.ww, bx, by, [&](int px, int py) { lx = px, ly = py; });
+            fetch_contour(img, r.ww, r.rH, a.runs, bx, by, [&](int px, int py) { lx = px, ly = py; });
             float pxs, pys;
             scale_pt(a.f, r.X0 + lx - 1, r.Y0 + ly - 1, &pxs, &pys);
             int i = 0;
-            fetch_contour(img, r.ww, bx, by, [&](int qx, int qy) {
+            fetch_contour(img, r.ww, r.rH, a.runs, bx, by, [&](int qx, int qy) {
                 float xs, ys;
                 scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
                 acc += (double)pxs * (double)ys - (double)pys * (double)xs;
@@ -959,6 +1016,7 @@ struct FillArgs {
     int32_t* rects;   // [B][4]
     int32_t* chosen;  // [B]
     int32_t* status;  // [B] or NULL: 0 ok (no failure mode left: long contours are taken in chunks)
+    int runs;         // as CtArgs::runs
 };
 
 constexpr int FILL_MAX_CELLS = 64 * 64;  // lattice of a 1280 x 1280 frame
@@ -1190,7 +1248,7 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                 for (int lo = 0;; lo += a.sc.cap) {
                     if (tid < 64) {
                         int i = 0;
-                        fetch_contour(img, r.ww, st.ox, st.oy, [&](int qx, int qy) {
+                        fetch_contour(img, r.ww, r.rH, a.runs, st.ox, st.oy, [&](int qx, int qy) {
                             if (tid == 0) {
                                 float xs, ys;
                                 scale_pt(a.f, r.X0 + qx - 1, r.Y0 + qy - 1, &xs, &ys);
@@ -1282,6 +1340,8 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     ca.poly_cap = poly_cap;
     static const int gate_env = getenv("VA_CT_GATE") ? atoi(getenv("VA_CT_GATE")) : 1;  // A/B knob
     ca.gate = gate_env;
+    static const int runs_env = getenv("VA_CT_RUNS") ? atoi(getenv("VA_CT_RUNS")) : 1;  // A/B knob
+    ca.runs = runs_env;
     // images needing more than VA_CT_POOL_PAGES pages (default all 32) run in global memory (A/B knob)
     // the pool kernel's LDS: VA_CT_PAGES pages (default all 32 = 160 KiB; fewer leave LDS for a concurrent conv
     // workgroup of the next batch's forward on the same CU)
@@ -1324,6 +1384,7 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     fa.rects = rects;
     fa.chosen = chosen;
     fa.status = status;
+    fa.runs = ca.runs;
     const int fgrid = src.B < sc.nslots ? src.B : sc.nslots;
     hipLaunchKernelGGL(post_fill_kernel, dim3(fgrid), dim3(FILL_THREADS), FILL_LDS, st, fa);
     return hipGetLastError();
