@@ -1144,38 +1144,35 @@ __global__ __launch_bounds__(FILL_THREADS) void post_fill_kernel(FillArgs a) {
                     bool ok = true;
                     if (!(lx1 >= 0 && lx1 < W0 && lx2 >= 0 && lx2 < W0 && ly1 >= 0 && ly1 < H0 && ly2 >= 0 && ly2 < H0))
                         ok = clip_line(W0, H0, lx1, ly1, lx2, ly2);
-                    if (ok) {
-                        long long dx = lx2 - lx1, dy = ly2 - ly1;
-                        long long sy = 1;
+                    if (ok) {  // inside the frame now: int arithmetic
+                        int x1 = (int)lx1, y1 = (int)ly1, x2 = (int)lx2, y2 = (int)ly2;
+                        int dx = x2 - x1, dy = y2 - y1, sy = 1;
                         if (dx < 0) {
                             dx = -dx, dy = -dy;
-                            long long t = lx1;
-                            lx1 = lx2, lx2 = t;
-                            t = ly1;
-                            ly1 = ly2, ly2 = t;
+                            int t = x1;
+                            x1 = x2, x2 = t;
+                            t = y1;
+                            y1 = y2, y2 = t;
                         }
                         if (dy < 0) dy = -dy, sy = -1;
                         const bool vert = dy > dx;
                         if (vert) {
-                            const long long t = dx;
+                            const int t = dx;
                             dx = dy, dy = t;
                         }
-                        long long err = dx - (dy + dy);
-                        const long long plus = dx + dx, minus = -(dy + dy);
-                        long long x = lx1, y = ly1;
-                        for (long long st2 = 0; st2 <= dx; ++st2) {
-                            if (x % VA_GRID == VA_GRID / 2 && y % VA_GRID == VA_GRID / 2 && x >= 0 && y >= 0 && x < W0 &&
-                                y < H0 && CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
+                        // The walk (err = dx - 2 dy; per step err -= 2 dy, += 2 dx on a minor step when err < 0)
+                        // has taken m_t = (2 dy t + dx - 1) / (2 dx) minor steps after t major ones (exact, checked
+                        // against the step-by-step walk for every dy <= dx < 300); only positions on a cell centre
+                        // (x = y = 10 mod 20) are kept, so only the major-axis steps landing on 10 mod 20 are
+                        // evaluated: dx / 20 of them instead of dx serial 64-bit steps per edge.
+                        constexpr int h = VA_GRID / 2;
+                        const int m0 = vert ? sy * (h - y1) : h - x1;
+                        for (int t = (m0 % VA_GRID + VA_GRID) % VA_GRID; t <= dx; t += VA_GRID) {
+                            const int m = dx ? (2 * dy * t + dx - 1) / (2 * dx) : 0;
+                            const int x = vert ? x1 + m : x1 + t, y = vert ? y1 + sy * t : y1 + sy * m;
+                            if (x >= 0 && y >= 0 && x < W0 && y < H0 && (vert ? x : y) % VA_GRID == h &&
+                                CT_OK((y / VA_GRID) * LC + x / VA_GRID < FILL_MAX_CELLS, 10, x, y))
                                 hit[(y / VA_GRID) * LC + x / VA_GRID] = 1;
-                            const bool minor = err < 0;
-                            err += minus + (minor ? plus : 0);
-                            if (vert) {
-                                y += sy;
-                                x += minor ? 1 : 0;
-                            } else {
-                                x += 1;
-                                y += minor ? sy : 0;
-                            }
                         }
                     }
                 }
