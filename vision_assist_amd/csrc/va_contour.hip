@@ -289,9 +289,44 @@ __device__ __forceinline__ void ct_sync() {
     }
 }
 
+// Low-res rows s0 .. s1 of the detection's crop window, coef . proto per pixel, into strip[(y - s0) tw + x - rx0]:
+// eight lanes per low-res pixel (its 128 bytes of proto in one coalesced run): lane q's partial sum of 4 channels,
+// then the pairwise tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) by xor shuffles -- post-processing's
+// 8-lane dot (same order, same result).  U pixels' loads in flight per lane before the first is used (the phase is
+// latency-bound on them; the block-wide forms have the registers for 8).
+template <int U>
+__device__ __forceinline__ void strip_dots(const Src& s, int b, const float4& cq, const Region& r, int s0, int s1,
+                                           int tw, float* strip, int tid, int nt) {
+    const int npx = (s1 - s0 + 1) * tw, ntot = npx * 8;
+#pragma unroll 1
+    for (int i0 = tid; i0 < ntot; i0 += U * nt) {  // whole 8-lane groups are active together
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * nt, px = i >> 3;
+            if (i < ntot) {
+                const int y = s0 + px / tw, x = r.rx0 + px % tw;
+                v[u] = ((const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC))[tid & 7];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * nt;
+            if (i < ntot) {
+                float part = (cq.x * v[u].x + cq.y * v[u].y) + (cq.z * v[u].z + cq.w * v[u].w);
+                part += __shfl_xor(part, 1);
+                part += __shfl_xor(part, 2);
+                part += __shfl_xor(part, 4);
+                if ((tid & 7) == 0) strip[i >> 3] = part;
+            }
+        }
+    }
+}
+
 template <bool WAVE, int MEMCLASS = 0>  // MEMCLASS: a distinct instantiation per image memory class (see below)
 __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Region& r, uint32_t* img, float* strip,
-                                            int tid, int nt, MaskStat& ms) {
+                                            int tid, int nt, MaskStat& ms, int strip_cap = CT_STRIP,
+                                            int sep_cap = 0) {
     auto account = [&](uint32_t w, int x32, int yy) {
         if (!w) return;
         ms.cnt += __builtin_popcount(w);
@@ -329,39 +364,54 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
     const float4* coef4 = (const float4*)coef_row(s, b, anchor);
     const float4 cq = coef4[tid & 7];  // this lane's 4 of the 32 coefficients (nt is a multiple of 8)
     const int tw = r.rx1 - r.rx0 + 1;
-    const int S = CT_STRIP / tw;  // >= 2: tw <= mw <= CT_STRIP / 2 (va_contour_launch)
+    const int S = strip_cap / tw;  // >= 2: tw <= mw <= CT_STRIP / 2 <= strip_cap / 2 (va_contour_launch)
     const float sx = (float)s.mw / (float)s.Wn, sy = (float)s.mh / (float)s.Hn;
+    const int nly = r.ry1 - r.ry0 + 1;
+    if (!WAVE && (int64_t)nly * (tw + r.w) <= sep_cap) {  // block-uniform
+        // Separable form (the workgroup-per-detection kernel, when the whole window and its rows interpolated to
+        // the region's columns fit in LDS): every low-res row's horizontal pass hrow[ly][c] = wx0 A + wx1 B is
+        // computed once per column instead of once per full-res pixel, then a pixel is wy0 ha + wy1 hb > 0 of two
+        // hrow reads -- the same products and sums in the same order as the per-pixel form, so the same bits.
+        float* hrow = strip + nly * tw;
+        strip_dots<8>(s, b, cq, r, r.ry0, r.ry1, tw, strip, tid, nt);
+        ct_sync<WAVE>();
+#pragma unroll 1
+        for (int i = tid; i < nly * r.w; i += nt) {
+            const int ly = i / r.w, c = i - ly * r.w;
+            int xa, xb;
+            float wx0, wx1;
+            taps(r.X0 + c, sx, s.mw, &xa, &xb, &wx0, &wx1);
+            const bool ixa = xa >= r.rx0 && xa <= r.rx1, ixb = xb >= r.rx0 && xb <= r.rx1;
+            const float A = ixa ? strip[ly * tw + xa - r.rx0] : 0.f, B = ixb ? strip[ly * tw + xb - r.rx0] : 0.f;
+            hrow[i] = wx0 * A + wx1 * B;
+        }
+        ct_sync<WAVE>();
+#pragma unroll 1
+        for (int i = tid; i < r.h * r.ww; i += nt) {
+            const int yy = 1 + i / r.ww, x32 = 32 * (i % r.ww);
+            int ya, yb;
+            float wy0, wy1;
+            taps(r.Y0 + yy - 1, sy, s.mh, &ya, &yb, &wy0, &wy1);
+            const bool oka = ya >= r.ry0 && ya <= r.ry1, okb = yb >= r.ry0 && yb <= r.ry1;
+            const int ra = (oka ? ya - r.ry0 : 0) * r.w - 1, rb = (okb ? yb - r.ry0 : 0) * r.w - 1;  // by framed x
+            const int j0 = max(0, 1 - x32), j1 = min(31, r.w - x32);  // pixels 1 .. w of the framed row
+            uint32_t w = 0;
+#pragma unroll 4
+            for (int j = j0; j <= j1; ++j) {
+                const int x = x32 + j;
+                const float ha = oka ? hrow[ra + x] : 0.f, hb = okb ? hrow[rb + x] : 0.f;
+                if (wy0 * ha + wy1 * hb > 0.f) w |= 1u << j;
+            }
+            account(w, x32, yy);
+            plane(img, r.ww, yy, 0)[x32 >> 5] = w;
+        }
+        ct_sync<WAVE>();
+        return;
+    }
     int next = 1, s0 = r.ry0;     // next framed row to produce; first low-res row of the strip
     while (next <= r.h) {         // block-uniform
         const int s1 = min(s0 + S - 1, r.ry1);
-        // eight lanes per low-res pixel (its 128 bytes of proto in one coalesced run): lane q's partial sum of 4
-        // channels, then the pairwise tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) by xor shuffles --
-        // post-processing's 8-lane dot (same order, same result)
-        // (four pixels' loads in flight per lane before the first is used: the strip is latency-bound on them)
-        const int npx = (s1 - s0 + 1) * tw, ntot = npx * 8;
-#pragma unroll 1
-        for (int i0 = tid; i0 < ntot; i0 += 4 * nt) {  // whole 8-lane groups are active together
-            float4 v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + u * nt, px = i >> 3;
-                if (i < ntot) {
-                    const int y = s0 + px / tw, x = r.rx0 + px % tw;
-                    v[u] = ((const float4*)(s.proto + (((int64_t)b * s.mh + y) * s.mw + x) * NMC))[tid & 7];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int i = i0 + u * nt;
-                if (i < ntot) {
-                    float part = (cq.x * v[u].x + cq.y * v[u].y) + (cq.z * v[u].z + cq.w * v[u].w);
-                    part += __shfl_xor(part, 1);
-                    part += __shfl_xor(part, 2);
-                    part += __shfl_xor(part, 4);
-                    if ((tid & 7) == 0) strip[i >> 3] = part;
-                }
-            }
-        }
+        strip_dots<WAVE ? 4 : 8>(s, b, cq, r, s0, s1, tw, strip, tid, nt);
         ct_sync<WAVE>();
         // the rows whose taps inside the window all lie in s0 .. s1 (taps are non-decreasing in the row)
         int end = next;
@@ -382,8 +432,8 @@ __device__ __forceinline__ void build_image(const Src& s, int b, int k, const Re
             // val() per tap, its row tests hoisted out of the pixel loop: a tap outside the window reads 0
             const bool oka = ya >= r.ry0 && ya <= r.ry1, okb = yb >= r.ry0 && yb <= r.ry1;
             const int la = (ya - s0) * tw - r.rx0, lb = (yb - s0) * tw - r.rx0;
-            if (!CT_OK(!oka || (la + r.rx0 >= 0 && la + r.rx1 < CT_STRIP), 7, la, tw)) continue;
-            if (!CT_OK(!okb || (lb + r.rx0 >= 0 && lb + r.rx1 < CT_STRIP), 7, lb, tw)) continue;
+            if (!CT_OK(!oka || (la + r.rx0 >= 0 && la + r.rx1 < strip_cap), 7, la, tw)) continue;
+            if (!CT_OK(!okb || (lb + r.rx0 >= 0 && lb + r.rx1 < strip_cap), 7, lb, tw)) continue;
             const int j0 = max(0, 1 - x32), j1 = min(31, r.w - x32);  // pixels 1 .. w of the framed row
             uint32_t w = 0;
 #pragma unroll 4
@@ -950,13 +1000,14 @@ constexpr int CT_WG_THREADS = 512;
 constexpr int CT_WG_LDS = CP_POOL;  // the image (+ strip) of a region up to the pool's size lives in LDS
 template <bool LDS>
 __device__ __forceinline__ void contour_wg_item(const CtArgs& a, int b, int k, const Region& r, uint32_t* img,
-                                                float* strip, int item, int* s_ms) {
+                                                float* strip, int strip_cap, int item, int* s_ms) {
     const Src& s = a.s;
     MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
     CT_PROF(const unsigned long long t0 = __builtin_amdgcn_s_memtime());
     // its own build instantiation per memory class: one body serving an LDS and a global image through one pointer
     // faulted on gfx950 (an aperture violation, §4.2 of DESIGN.md)
-    build_image<false, LDS ? 1 : 2>(s, b, k, r, img, strip, threadIdx.x, CT_WG_THREADS, ms);
+    build_image<false, LDS ? 1 : 2>(s, b, k, r, img, strip, threadIdx.x, CT_WG_THREADS, ms, strip_cap,
+                                    LDS ? strip_cap : 0);
     CT_PROF(const unsigned long long t1 = __builtin_amdgcn_s_memtime());
     const int lane = threadIdx.x & 63;
     if (s.stats) {  // pixel count and bbox: per wave, then across the block
@@ -994,11 +1045,14 @@ __global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wg_kernel(CtArgs a
     if (threadIdx.x == 0) s_ms[0] = 0, s_ms[1] = INT32_MAX, s_ms[2] = -1, s_ms[3] = INT32_MAX, s_ms[4] = -1;
     __syncthreads();
     if (region_need(s, r) <= CT_WG_LDS) {  // block-uniform: the image and the strip in LDS, the trace on LDS
-        float* strip = (float*)(wg_img + ((image_words(r) + 3) & ~3ll));
-        contour_wg_item<true>(a, b, k, r, wg_img, strip, item, s_ms);
+        // the strip takes the rest of the LDS: the whole low-res window of a typical detection in one strip (one
+        // round of proto loads and one barrier instead of one per CT_STRIP floats)
+        const int64_t img4 = (image_words(r) + 3) & ~3ll;
+        float* strip = (float*)(wg_img + img4);
+        contour_wg_item<true>(a, b, k, r, wg_img, strip, (int)(CT_WG_LDS / 4 - img4), item, s_ms);
     } else {  // a larger region: the detection's global slot
         unsigned char* slot = a.sc.base + (int64_t)item * a.sc.slot_bytes;
-        contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, item, s_ms);
+        contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, item, s_ms);
     }
 }
 
