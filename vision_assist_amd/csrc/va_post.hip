@@ -66,18 +66,18 @@ struct LevelPtrs {
 // list order is free.
 constexpr int DEC_GROUP = 16;
 constexpr int DEC_THREADS = 256;
-constexpr int DEC_APB = 256;  // anchors per workgroup
+constexpr int DEC_APB = 256;  // anchors per workgroup (at most; small batches take fewer, see va_post_run)
 
 __global__ __launch_bounds__(DEC_THREADS) void post_decode_kernel(LevelPtrs lv, int B, int H, int W, int nc, int A,
-                                                                  float conf, va_cand* cand, int32_t* count) {
+                                                                  float conf, va_cand* cand, int32_t* count, int apb) {
     const int no = 4 * REG_MAX + nc + NMC;
-    const int b = blockIdx.y, a_base = blockIdx.x * DEC_APB;
+    const int b = blockIdx.y, a_base = blockIdx.x * apb;
     const int grp = threadIdx.x / DEC_GROUP, gl = threadIdx.x % DEC_GROUP;
     __shared__ va_cand s_c[DEC_APB];
     __shared__ int s_n, s_base;
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    for (int ai = grp; ai < DEC_APB; ai += DEC_THREADS / DEC_GROUP) {
+    for (int ai = grp; ai < apb; ai += DEC_THREADS / DEC_GROUP) {
         const int a = a_base + ai;
         if (a >= A) break;  // whole group
         int local;
@@ -599,8 +599,12 @@ int va_post_run(void* stream, const va_post_args* p) {
     if (hipMemsetAsync(p->cand_count, 0, sizeof(int32_t) * B, st) != hipSuccess) return VA_ERR_HIP;
     LevelPtrs lv{{p->levels[0], p->levels[1], p->levels[2]}};
     if (B > 65535) return VA_ERR_ARG;
-    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, DEC_APB), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
-                       p->nc, A, p->conf, p->cand, p->cand_count);
+    // anchors per workgroup: 256, halved (down to one per 16-lane group) while the launch has under 2048
+    // workgroups -- at batch 1 a group's 16 anchors in a row were 16 dependent loads (23 us for the n-seg frame)
+    int apb = DEC_APB;
+    while (apb > DEC_THREADS / DEC_GROUP && (int64_t)B * grid1(A, apb) < 2048) apb /= 2;
+    hipLaunchKernelGGL(post_decode_kernel, dim3(grid1(A, apb), B), dim3(DEC_THREADS), 0, st, lv, B, p->H, p->W,
+                       p->nc, A, p->conf, p->cand, p->cand_count, apb);
     if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
     static DevFlag nms_attr;  // post_nms_kernel's 150 KiB of dynamic LDS (set explicitly: graph kernel nodes too)
     if (!nms_attr()) {
