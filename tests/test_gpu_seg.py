@@ -741,6 +741,37 @@ def test_lanes_match_serial(dtype, scale, B):
             assert torch.equal(g_, r), f"{name}: laned vs serial max diff {(g_ - r).abs().max().item()}"
 
 
+def test_lanes_two_streams_concurrently():
+    """Two laned batch-1 plans (own buffers, tags 0 / 1) enqueued alternately on two streams, so both forwards and
+    their lanes are in flight together: each calling stream gets its own lane set (va_seg.hip lane_set) and each
+    plan its own split-K workspaces, so the outputs equal a serial run of the same frames, round after round."""
+    arch, fw, net = _net("f32", "n")
+    fa, fb = _frames(1, seed=41).cuda(), _frames(1, seed=42).cuda()
+    pa, pb = net.plan(1, 640, 640, tag=0), net.plan(1, 640, 640, tag=1)
+    assert {op.lane for op in pa["ops"]} >= {1, 2}
+    ser = net.plan(1, 640, 640, tag=2, lanes=False)
+
+    def serial(frames):
+        ser["frames"].copy_(frames)
+        net.run_plan(ser)
+        torch.cuda.synchronize()
+        return [t.clone() for t in ser["out"].levels] + [ser["out"].proto.clone()]
+
+    want_a, want_b = serial(fa), serial(fb)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(4):
+        for p, f, st in ((pa, fa, sa), (pb, fb, sb)):
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                p["frames"].copy_(f, non_blocking=True)
+                net.run_plan(p, st)
+        torch.cuda.synchronize()
+        for p, want in ((pa, want_a), (pb, want_b)):
+            got = list(p["out"].levels) + [p["out"].proto]
+            for g_, w_ in zip(got, want):
+                assert torch.equal(g_, w_)
+
+
 # ---- BASELINE.json configs[4] shape (C5): YOLOv8m-seg at 1280 x 1280 (bf16 here; fp8 weights are not built)
 _M1280 = {}
 
