@@ -1024,10 +1024,11 @@ __device__ __forceinline__ void contour_wg_item(const CtArgs& a, int b, int k, c
     }
     if constexpr (!LDS) __threadfence();  // every wave's image words before wave 0's scan reads them
     __syncthreads();
-    if (threadIdx.x >= 64) return;
-    if (s.stats && lane == 0)
-        s.stats[(int64_t)b * a.max_det + k] = va_mask_stat{s_ms[0], s_ms[1], s_ms[3], s_ms[2], s_ms[4], {0, 0, 0}};
-    contour_scan<LDS>(a, b, k, r, img, item CT_PROF(, t0, t1));
+    if (threadIdx.x < 64) {
+        if (s.stats && lane == 0)
+            s.stats[(int64_t)b * a.max_det + k] = va_mask_stat{s_ms[0], s_ms[1], s_ms[3], s_ms[2], s_ms[4], {0, 0, 0}};
+        contour_scan<LDS>(a, b, k, r, img, item CT_PROF(, t0, t1));
+    }
 }
 
 __global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wg_kernel(CtArgs a) {
@@ -1053,6 +1054,76 @@ __global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wg_kernel(CtArgs a
     } else {  // a larger region: the detection's global slot
         unsigned char* slot = a.sc.base + (int64_t)item * a.sc.slot_bytes;
         contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, item, s_ms);
+    }
+}
+
+// Batches past the per-detection launch (B x max_det > the scratch slots: the headline's B = 256): the same
+// workgroup form, persistent -- one 160 KiB workgroup per CU claims the batch's detections one at a time from a
+// counter (ct_prefix_kernel's exclusive prefix of ndet over the frames maps a claim to its (frame, detection)), so
+// each detection gets the block-wide separable build instead of one wave's per-pixel build in the pool form.
+// buf (the last scratch slot): [0] claim counter, [1 .. B] prefix, [B + 1] total.  A region past the LDS uses the
+// workgroup's own slot (blockIdx.x < nslots - 1).
+__global__ __launch_bounds__(1024) void ct_prefix_kernel(const int32_t* __restrict__ ndet, int B, int max_det,
+                                                          int32_t* __restrict__ buf) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, per = (B + 1023) / 1024, b0 = tid * per, b1 = min(B, b0 + per);
+    auto nd = [&](int b) { return min(max(ndet[b], 0), max_det); };
+    int sum = 0;
+    for (int b = b0; b < b1; ++b) sum += nd(b);
+    part[tid] = sum;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int i = 0; i < 1024; ++i) {
+            const int v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        buf[0] = 0;
+        buf[1 + B] = acc;
+    }
+    __syncthreads();
+    int acc = part[tid];
+    for (int b = b0; b < b1; ++b) {
+        buf[1 + b] = acc;
+        acc += nd(b);
+    }
+}
+
+__global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wgp_kernel(CtArgs a, int32_t* buf) {
+    extern __shared__ __align__(16) uint32_t wg_img[];
+    __shared__ int s_ms[5], s_j;
+    const Src& s = a.s;
+    const int B = s.B, total = buf[1 + B];
+    const int32_t* pre = buf + 1;
+    unsigned char* slot = a.sc.base + (int64_t)blockIdx.x * a.sc.slot_bytes;
+    while (true) {
+        if (threadIdx.x == 0) s_j = atomicAdd(&buf[0], 1);
+        __syncthreads();
+        const int j = s_j;
+        if (j >= total) break;  // block-uniform
+        int lo = 0, hi = B - 1;  // the frame: the last b with pre[b] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        const int b = lo, k = j - pre[lo];
+        const Region r = region_of(s, b, k);
+        if (r.w <= 0) {
+            if (threadIdx.x < 64) contour_empty(a, b, k, r);
+        } else {
+            if (threadIdx.x == 0) s_ms[0] = 0, s_ms[1] = INT32_MAX, s_ms[2] = -1, s_ms[3] = INT32_MAX, s_ms[4] = -1;
+            __syncthreads();
+            if (region_need(s, r) <= CT_WG_LDS) {
+                const int64_t img4 = (image_words(r) + 3) & ~3ll;
+                contour_wg_item<true>(a, b, k, r, wg_img, (float*)(wg_img + img4), (int)(CT_WG_LDS / 4 - img4), j,
+                                      s_ms);
+            } else {
+                contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, j, s_ms);
+            }
+        }
+        __syncthreads();  // the item's LDS and s_j free for the next claim
     }
 }
 
@@ -1374,6 +1445,8 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
                                 CP_POOL) != hipSuccess ||
             hipFuncSetAttribute((const void*)post_contour_wg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 CT_WG_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)post_contour_wgp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                CT_WG_LDS) != hipSuccess ||
             hipFuncSetAttribute((const void*)post_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 FILL_LDS) != hipSuccess)
             return hipErrorInvalidValue;
@@ -1413,8 +1486,16 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
     // a slot per detection (small batches): the workgroup-per-detection form; VA_CT_WG=0 keeps the pool form (A/B)
     static const bool wg_env = !(getenv("VA_CT_WG") && getenv("VA_CT_WG")[0] == '0');
+    // larger batches: the persistent workgroup form (VA_CT_WGP=0 keeps the pool form, A/B); its claim counter and
+    // frame prefix live in the last scratch slot
+    static const bool wgp_env = !(getenv("VA_CT_WGP") && getenv("VA_CT_WGP")[0] == '0');
+    int32_t* cbuf = (int32_t*)(sc.base + (int64_t)(sc.nslots - 1) * sc.slot_bytes);
     if (wg_env && items <= sc.nslots) {
         hipLaunchKernelGGL(post_contour_wg_kernel, dim3((int)items), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca);
+    } else if (wg_env && wgp_env && sc.nslots >= 2 && (int64_t)(src.B + 2) * 4 <= sc.slot_bytes) {
+        hipLaunchKernelGGL(ct_prefix_kernel, dim3(1), dim3(1024), 0, st, src.ndet, src.B, max_det, cbuf);
+        const int g = n_cu() < sc.nslots - 1 ? n_cu() : sc.nslots - 1;
+        hipLaunchKernelGGL(post_contour_wgp_kernel, dim3(g), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca, cbuf);
     } else {
         hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st,
                            ca);
