@@ -1090,7 +1090,7 @@ __global__ __launch_bounds__(1024) void ct_prefix_kernel(const int32_t* __restri
     }
 }
 
-__global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wgp_kernel(CtArgs a, int32_t* buf) {
+__global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wgp_kernel(CtArgs a, int32_t* buf, int lds_bytes) {
     extern __shared__ __align__(16) uint32_t wg_img[];
     __shared__ int s_ms[5], s_j;
     const Src& s = a.s;
@@ -1115,9 +1115,9 @@ __global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wgp_kernel(CtArgs 
         } else {
             if (threadIdx.x == 0) s_ms[0] = 0, s_ms[1] = INT32_MAX, s_ms[2] = -1, s_ms[3] = INT32_MAX, s_ms[4] = -1;
             __syncthreads();
-            if (region_need(s, r) <= CT_WG_LDS) {
+            if (region_need(s, r) <= lds_bytes) {
                 const int64_t img4 = (image_words(r) + 3) & ~3ll;
-                contour_wg_item<true>(a, b, k, r, wg_img, (float*)(wg_img + img4), (int)(CT_WG_LDS / 4 - img4), j,
+                contour_wg_item<true>(a, b, k, r, wg_img, (float*)(wg_img + img4), (int)(lds_bytes / 4 - img4), j,
                                       s_ms);
             } else {
                 contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, j, s_ms);
@@ -1494,8 +1494,13 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
         hipLaunchKernelGGL(post_contour_wg_kernel, dim3((int)items), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca);
     } else if (wg_env && wgp_env && sc.nslots >= 2 && (int64_t)(src.B + 2) * 4 <= sc.slot_bytes) {
         hipLaunchKernelGGL(ct_prefix_kernel, dim3(1), dim3(1024), 0, st, src.ndet, src.B, max_det, cbuf);
-        const int g = n_cu() < sc.nslots - 1 ? n_cu() : sc.nslots - 1;
-        hipLaunchKernelGGL(post_contour_wgp_kernel, dim3(g), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca, cbuf);
+        // VA_CT_WGP_KB: LDS per workgroup (default 160 = one per CU; 80 = two, the rest of a region past it in the
+        // workgroup's slot) -- A/B knob
+        static const int wgp_kb = getenv("VA_CT_WGP_KB") ? atoi(getenv("VA_CT_WGP_KB")) : CT_WG_LDS / 1024;
+        const int lds = (wgp_kb < 16 ? 16 : wgp_kb > CT_WG_LDS / 1024 ? CT_WG_LDS / 1024 : wgp_kb) * 1024;
+        const int per_cu = CT_WG_LDS / lds;
+        const int g = n_cu() * per_cu < sc.nslots - 1 ? n_cu() * per_cu : sc.nslots - 1;
+        hipLaunchKernelGGL(post_contour_wgp_kernel, dim3(g), dim3(CT_WG_THREADS), lds, st, ca, cbuf, lds);
     } else {
         hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st,
                            ca);
