@@ -1627,6 +1627,9 @@ __global__ __launch_bounds__(T3U_NT) void conv3v_kernel(va_conv_args a, int ntn,
     conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smv, n0, wm, wn, tid, lane, orow, m0, cls);
 }
 
+// DIAGNOSIS ONLY (VA_CONV3T=5 / 6): with other kernels running beside it (the laned small-batch list) conv3w gave 2
+// mismatching forwards in 12 (tools/form_race.py) -- a stage-reuse race the single-stream tests never exposed;
+// conv3t (the default) and forms 3, 4, 7 stayed bit-identical in 40 laned runs each.
 // conv3w: the staging moved off each wave's serial path.  In conv3t a wave's K-step is [DMA + B-load issue, fragment
 // reads, 24 MFMAs, wait, split + plane stores of the next step's B, barrier]: the split and the stores run after
 // the wave's MFMAs and before the barrier, in series with them (conv3t_abl: without the B path the forward is 27 %
