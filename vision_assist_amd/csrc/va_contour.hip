@@ -1494,10 +1494,10 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
         hipLaunchKernelGGL(post_contour_wg_kernel, dim3((int)items), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca);
     } else if (wg_env && wgp_env && sc.nslots >= 2 && (int64_t)(src.B + 2) * 4 <= sc.slot_bytes) {
         hipLaunchKernelGGL(ct_prefix_kernel, dim3(1), dim3(1024), 0, st, src.ndet, src.B, max_det, cbuf);
-        // VA_CT_WGP_KB: LDS per workgroup (default 160 = one per CU; 80 = two, the rest of a region past it in the
-        // workgroup's slot) -- A/B knob
-        static const int wgp_kb = getenv("VA_CT_WGP_KB") ? atoi(getenv("VA_CT_WGP_KB")) : CT_WG_LDS / 1024;
-        const int lds = (wgp_kb < 16 ? 16 : wgp_kb > CT_WG_LDS / 1024 ? CT_WG_LDS / 1024 : wgp_kb) * 1024;
+        // VA_CT_WGP_KB: LDS per workgroup in KiB (default: the whole pool, one per CU; 80 = two, a region past it in
+        // the workgroup's slot) -- A/B knob
+        static const int wgp_kb = getenv("VA_CT_WGP_KB") ? atoi(getenv("VA_CT_WGP_KB")) : 0;
+        const int lds = wgp_kb <= 0 ? CT_WG_LDS : (wgp_kb < 16 ? 16 : wgp_kb > CT_WG_LDS / 1024 ? CT_WG_LDS / 1024 : wgp_kb) * 1024;
         const int per_cu = CT_WG_LDS / lds;
         const int g = n_cu() * per_cu < sc.nslots - 1 ? n_cu() * per_cu : sc.nslots - 1;
         hipLaunchKernelGGL(post_contour_wgp_kernel, dim3(g), dim3(CT_WG_THREADS), lds, st, ca, cbuf, lds);
