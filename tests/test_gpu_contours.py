@@ -86,3 +86,33 @@ def test_select_masks_contours_longer_than_the_point_buffer(cap):
         assert got["chosen"][b] == kk
         assert tuple(got["rects"][b]) == rect, (b, tuple(got["rects"][b]), rect)
         assert np.array_equal(got["cells"][b], cells), (b, int((got["cells"][b] != cells).sum()))
+
+
+def test_select_masks_many_items_persistent_form():
+    """12 frames x 88 masks (1056 detections > the 1024 scratch slots): the persistent workgroup form
+    (post_contour_wgp_kernel -- claims mapped through the frame prefix of the mask counts, ragged counts and an
+    empty frame included) gives the oracle's contours, choice, rect and cells."""
+    from tests.contour_cases import blob
+    from vision_assist_amd.post import select_masks
+    rng = np.random.default_rng(23)
+    Hn, Wn, B, maxn = 80, 160, 12, 88
+    masks = np.zeros((B, maxn, Hn, Wn), np.uint8)
+    n = np.array([88, 3, 0, 88, 17, 88, 1, 60, 88, 88, 5, 88], np.int32)
+    for b in range(B):
+        for k in range(n[b]):
+            masks[b, k] = blob(rng, Hn, Wn, sigma=float(rng.uniform(2, 4)), thr=0.52)
+    got = select_masks(torch.from_numpy(masks).cuda(), torch.from_numpy(n), Hn, Wn)
+    assert (got["status"] == 0).all()
+    for b in range(B):
+        ms = masks[b, :n[b]]
+        xy = C.masks_xy(ms, (Hn, Wn)) if n[b] else []
+        for k in range(n[b]):
+            st = got["cstats"][b, k]
+            assert st["area"] == C.contour_area(xy[k]), (b, k)
+            assert np.array_equal(got["polys"][b][k], xy[k]), (b, k)
+        if n[b] == 0:
+            assert got["chosen"][b] < 0
+            continue
+        kk, pts, rect, cells = C.select_cells(ms, (Hn, Wn))
+        assert got["chosen"][b] == kk and tuple(got["rects"][b]) == rect
+        assert np.array_equal(got["cells"][b], cells)
