@@ -1090,40 +1090,93 @@ __global__ __launch_bounds__(1024) void ct_prefix_kernel(const int32_t* __restri
     }
 }
 
+// A round takes up to eight claimed detections whose images fit the LDS side by side: each is built by the whole
+// block in turn (its strip / separable rows in the LDS past the images), then wave w scans / traces detection w --
+// eight independent scans at once, as the pool form's waves run them, instead of one wave scanning while seven
+// wait.  A detection whose image cannot share the LDS runs alone (in the workgroup's slot if it exceeds the LDS).
+constexpr int WGP_D = CT_WG_THREADS / 64;
+
 __global__ __launch_bounds__(CT_WG_THREADS) void post_contour_wgp_kernel(CtArgs a, int32_t* buf, int lds_bytes) {
     extern __shared__ __align__(16) uint32_t wg_img[];
-    __shared__ int s_ms[5], s_j;
+    __shared__ int s_ms[WGP_D][5], s_j, s_b[WGP_D], s_k[WGP_D], s_off[WGP_D], s_item[WGP_D];
     const Src& s = a.s;
     const int B = s.B, total = buf[1 + B];
     const int32_t* pre = buf + 1;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     unsigned char* slot = a.sc.base + (int64_t)blockIdx.x * a.sc.slot_bytes;
+    int qn = 0, qe = 0;  // claimed, not yet taken: [qn, qe) (block-uniform)
     while (true) {
-        if (threadIdx.x == 0) s_j = atomicAdd(&buf[0], 1);
-        __syncthreads();
-        const int j = s_j;
-        if (j >= total) break;  // block-uniform
-        int lo = 0, hi = B - 1;  // the frame: the last b with pre[b] <= j
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pre[mid] <= j) lo = mid;
-            else hi = mid - 1;
-        }
-        const int b = lo, k = j - pre[lo];
-        const Region r = region_of(s, b, k);
-        if (r.w <= 0) {
-            if (threadIdx.x < 64) contour_empty(a, b, k, r);
-        } else {
-            if (threadIdx.x == 0) s_ms[0] = 0, s_ms[1] = INT32_MAX, s_ms[2] = -1, s_ms[3] = INT32_MAX, s_ms[4] = -1;
+        if (qn == qe) {
+            if (tid == 0) s_j = atomicAdd(&buf[0], WGP_D);
             __syncthreads();
-            if (region_need(s, r) <= lds_bytes) {
-                const int64_t img4 = (image_words(r) + 3) & ~3ll;
-                contour_wg_item<true>(a, b, k, r, wg_img, (float*)(wg_img + img4), (int)(lds_bytes / 4 - img4), j,
-                                      s_ms);
-            } else {
-                contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, j, s_ms);
-            }
+            qn = s_j;
+            qe = min(qn + WGP_D, total);
+            __syncthreads();  // s_j read by every thread before the next claim writes it
+            if (qn >= total) break;  // block-uniform
         }
-        __syncthreads();  // the item's LDS and s_j free for the next claim
+        int nd = 0;
+        int64_t used = 0;  // LDS words held by this round's images
+        while (qn < qe && nd < WGP_D) {
+            const int j = qn;
+            int lo = 0, hi = B - 1;  // the frame: the last b with pre[b] <= j
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (pre[mid] <= j) lo = mid;
+                else hi = mid - 1;
+            }
+            const int b = lo, k = j - pre[lo];
+            const Region r = region_of(s, b, k);
+            if (r.w <= 0) {
+                if (tid < 64) contour_empty(a, b, k, r);
+                ++qn;
+                continue;
+            }
+            const int64_t img4 = (image_words(r) + 3) & ~3ll;
+            if ((used + img4) * 4 + CT_STRIP * 4 > lds_bytes) {  // block-uniform
+                if (nd > 0) break;  // scan this round's detections first
+                // alone and still too large for the LDS: the workgroup's slot, wave 0's scan
+                if (tid == 0) s_ms[0][0] = 0, s_ms[0][1] = INT32_MAX, s_ms[0][2] = -1, s_ms[0][3] = INT32_MAX, s_ms[0][4] = -1;
+                __syncthreads();
+                contour_wg_item<false>(a, b, k, r, (uint32_t*)(slot + a.sc.img_off), (float*)slot, CT_STRIP, j,
+                                       s_ms[0]);
+                __syncthreads();
+                ++qn;
+                continue;
+            }
+            if (tid == 0) {
+                s_ms[nd][0] = 0, s_ms[nd][1] = INT32_MAX, s_ms[nd][2] = -1, s_ms[nd][3] = INT32_MAX, s_ms[nd][4] = -1;
+                s_b[nd] = b, s_k[nd] = k, s_off[nd] = (int)used, s_item[nd] = j;
+            }
+            uint32_t* img = wg_img + used;
+            const int cap = (int)(lds_bytes / 4 - used - img4);
+            MaskStat ms{0, INT32_MAX, -1, INT32_MAX, -1};
+            build_image<false, 1>(s, b, k, r, img, (float*)(img + img4), tid, CT_WG_THREADS, ms, cap, cap);
+            if (s.stats) {
+                const int cnt = wave_sum(ms.cnt);
+                const int x0 = wave_min(ms.x1 >= 0 ? ms.x0 : s.Wn), x1 = wave_max(ms.x1);
+                const int y0 = wave_min(ms.x1 >= 0 ? ms.y0 : s.Hn), y1 = wave_max(ms.x1 >= 0 ? ms.y1 : -1);
+                if (lane == 0) {
+                    atomicAdd(&s_ms[nd][0], cnt);
+                    atomicMin(&s_ms[nd][1], x0);
+                    atomicMax(&s_ms[nd][2], x1);
+                    atomicMin(&s_ms[nd][3], y0);
+                    atomicMax(&s_ms[nd][4], y1);
+                }
+            }
+            __syncthreads();  // the image complete (and its scratch free for the next build)
+            used += img4;
+            ++nd;
+            ++qn;
+        }
+        if (wid < nd) {  // wave w: detection w of the round
+            const int b = s_b[wid], k = s_k[wid];
+            const Region r = uni_region(region_of(s, b, k));
+            if (s.stats && lane == 0)
+                s.stats[(int64_t)b * a.max_det + k] =
+                    va_mask_stat{s_ms[wid][0], s_ms[wid][1], s_ms[wid][3], s_ms[wid][2], s_ms[wid][4], {0, 0, 0}};
+            contour_scan<true>(a, b, k, r, wg_img + s_off[wid], s_item[wid] CT_PROF(, 0ull, 0ull));
+        }
+        __syncthreads();  // the round's images and records free
     }
 }
 
