@@ -154,26 +154,58 @@ def decode(box: torch.Tensor, cls: torch.Tensor, H: int, W: int):
     return torch.cat((dbox, cls.sigmoid()), 1)
 
 
-def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: float = 0.7, max_det: int = 300,
-              max_nms: int = 30000):
-    """non_max_suppression for one image (ops.py:214-363): pred [4+nc, A], coef [32, A]
-    -> [k, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) in decreasing score order.
-    max_nms (ops.py:332-333): longer candidate lists keep their max_nms highest scores first (torch's
-    argsort is not stable; ties are kept lowest anchor first here, the order the device kernel uses)."""
+def nms_candidates(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, max_nms: int = 30000):
+    """non_max_suppression for one image up to its torchvision.ops.nms call (ops.py:288-343): pred [4+nc, A],
+    coef [32, A] -> det [n, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) -- the conf filter (xc, :288 and
+    :322), xywh2xyxy (:463-480), best class only (:319-321), the max_nms cut (:332-333: the max_nms highest
+    scores; torch's argsort is not stable, ties are kept lowest anchor first here, the order the device kernel
+    uses) -- and the nms inputs: boxes offset by class * max_wh (:336-342) and the scores.  Pinned to the
+    reference's own ops.py by tests/golden/ops_goldens.npz (tests/test_ops_pinned_cpu.py)."""
     nc = pred.shape[0] - 4
     x = torch.cat((pred, coef), 0).T  # [A, 4+nc+32]
     xc = x[:, 4:4 + nc].amax(1) > conf
     x = x[xc]
     if not x.shape[0]:
-        return torch.zeros((0, 6 + coef.shape[0]))
-    xy, wh = x[:, :2], x[:, 2:4]
-    boxes = torch.cat((xy - wh / 2, xy + wh / 2), 1)
+        z = torch.zeros((0, 6 + coef.shape[0]))
+        return z, z[:, :4], z[:, 4]
+    xy, wh = x[:, :2], x[:, 2:4] / 2
+    boxes = torch.cat((xy - wh, xy + wh), 1)
     score, j = x[:, 4:4 + nc].max(1, keepdim=True)
     det = torch.cat((boxes, score, j.float(), x[:, 4 + nc:]), 1)[score.view(-1) > conf]
     if det.shape[0] > max_nms:
         det = det[torch.sort(det[:, 4], descending=True, stable=True).indices[:max_nms]]
-    keep = greedy_nms(det[:, :4] + det[:, 5:6] * MAX_WH, det[:, 4], iou)[:max_det]
+    return det, det[:, :4] + det[:, 5:6] * MAX_WH, det[:, 4]
+
+
+def nms_image(pred: torch.Tensor, coef: torch.Tensor, conf: float = 0.5, iou: float = 0.7, max_det: int = 300,
+              max_nms: int = 30000):
+    """non_max_suppression for one image (ops.py:214-363): pred [4+nc, A], coef [32, A]
+    -> [k, 6 + 32] rows (x1, y1, x2, y2, conf, cls, coef...) in decreasing score order: nms_candidates, then
+    the greedy NMS torchvision.ops.nms runs (greedy_nms; torchvision is absent: unpinned) and the max_det cut."""
+    det, boxes, scores = nms_candidates(pred, coef, conf, max_nms)
+    if not det.shape[0]:
+        return det
+    keep = greedy_nms(boxes, scores, iou)[:max_det]
     return det[keep]
+
+
+def scale_boxes(net_hw: tuple[int, int], boxes: torch.Tensor, frame_hw: tuple[int, int]) -> torch.Tensor:
+    """ops.scale_boxes(img1_shape=net, boxes xyxy, img0_shape=frame) (ops.py:139-170, then clip_boxes): gain in
+    double, integer pads round(. - 0.1), float32 tensor arithmetic, clamp to the frame."""
+    gain = min(net_hw[0] / frame_hw[0], net_hw[1] / frame_hw[1])
+    px = round((net_hw[1] - frame_hw[1] * gain) / 2 - 0.1)
+    py = round((net_hw[0] - frame_hw[0] * gain) / 2 - 0.1)
+    b = boxes.clone()
+    b[..., 0] -= px
+    b[..., 1] -= py
+    b[..., 2] -= px
+    b[..., 3] -= py
+    b[..., :4] /= gain
+    b[..., 0] = b[..., 0].clamp(0, frame_hw[1])
+    b[..., 1] = b[..., 1].clamp(0, frame_hw[0])
+    b[..., 2] = b[..., 2].clamp(0, frame_hw[1])
+    b[..., 3] = b[..., 3].clamp(0, frame_hw[0])
+    return b
 
 
 def greedy_nms(boxes: torch.Tensor, scores: torch.Tensor, thr: float) -> torch.Tensor:

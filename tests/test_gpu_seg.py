@@ -333,62 +333,21 @@ def test_conv0_f32_mfma_matches_fp32(cout, H, W):
     assert (got - yv.cpu().permute(0, 3, 1, 2)).abs().max().item() < 4e-6 * max(1.0, ref.abs().max().item())
 
 
-def test_conv3_matches_conv2(monkeypatch):
-    """The 256 x 128-tile kernel (conv3: three LDS-DMA stages, two K-tiles in flight) forced onto every wide
-    layer of a bf16 forward -- stride 2, residual C2f bottlenecks, Cout 224 (a ragged channel tile), the fused
-    1x1 tails, the proto sub-pixel fold (mode 2), ragged pixel tiles (M = 2 x 400 at P5) -- gives the
-    same outputs as the 128 x 128 conv2 kernel: same fragments, same MFMA order, so bit-identical."""
-    arch, fw, net = _net("bf16", "s", seed=4)
-    frames = _frames(2, seed=7)
-    monkeypatch.setenv("VA_SPLITK", "0")  # conv2 slicing the P5 layers' K loops would sum in another order
-    monkeypatch.delenv("VA_CONV3", raising=False)
-    ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV3", "1")
-    monkeypatch.setenv("VA_CONV3_MIN", "1")
-    got = _gpu_heads(net, frames)
-    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
-        assert torch.equal(g, r), f"{name}: conv3 vs conv2 max diff {(g - r).abs().max().item()}"
-
-
-# (forms 5 / 6, conv3w, are diagnosis-only: concurrent launches -- the laned small-batch list -- expose a race in
-# their stage reuse, 2 mismatching forwards in 12 with lanes, tools/form_race.py, profiles/r03/form_race/)
-@pytest.mark.parametrize("B,form", [(2, "3"), (3, "3"), (2, "4"), (3, "4"), (2, "7"), (3, "7")])
-def test_conv3u_matches_conv3t(B, form, monkeypatch):
-    """conv3u (96-byte stage rows, three A stages, B registers three K-steps ahead) and conv3v (its B loads a K-step
-    pair at a time, whole 128-byte lines) against conv3t's 128-pixel form
-    on the f32 forward's wide layers (P3 3x3 / 1x1 layers, Cout 224 ragged channel tile, the proto sub-pixel fold
-    in mode 2, ragged pixel tiles at B = 3): the same operands, the same six MFMAs per block pair in the same order,
-    so bit-identical; and within the f32 bar of the torch fp32 reference."""
+@pytest.mark.parametrize("B", [2, 3])
+def test_conv3t_matches_conv2_f32(B, monkeypatch):
+    """conv3t (pre-split weight planes by LDS-DMA, activations split once per workgroup, 32 x 32 blocks) against
+    conv2's three-term form (VA_CONV3T=0) on the f32 forward's wide layers -- 3x3 and 1x1, stride 2, Cout 224 (a
+    ragged channel tile), the proto sub-pixel fold (mode 2), ragged pixel tiles at B = 3: the same six exact term
+    products per f32 product summed in another order, so f32-rounding close; and within the f32 bar of torch."""
     arch, fw, net = _net("f32", "s", seed=5)
     frames = _frames(B, seed=11)
-    monkeypatch.setenv("VA_CONV3T", "2")
+    monkeypatch.setenv("VA_CONV3T", "0")
     ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV3T", form)  # 3: conv3u, 4: conv3v (paired whole-line B loads), 5 / 6: conv3w, 7: conv3x
-    got = _gpu_heads(net, frames)
-    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
-        assert torch.equal(g, r), f"{name}: conv3t form {form} vs 2 max diff {(g - r).abs().max().item()}"
-    if B == 2:
-        torch.set_num_threads(8)
-        want = _ref_heads(arch, fw, frames)
-        for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
-            assert (g - r).abs().max().item() <= 1e-3, name
-
-
-@pytest.mark.parametrize("B", [2, 3])
-def test_conv3n_narrow_layers_f32(B, monkeypatch):
-    """conv3n (three-plane 256 x 64 tiles) on the narrow f32 layers -- 1x1 and 3x3, stride 2 (model.1), residual
-    C2f bottlenecks, channel slices, ragged pixel tiles at B = 3 -- against conv2's three-term form
-    (VA_CONV3N=0): the same six exact term products per f32 product summed in another order, so f32-rounding
-    close; and within the f32 bar of the torch fp32 reference."""
-    arch, fw, net = _net("f32", "s", seed=6)
-    frames = _frames(B, seed=12)
-    monkeypatch.setenv("VA_CONV3N", "0")  # the default
-    ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV3N", "1")
+    monkeypatch.delenv("VA_CONV3T")
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         d = (g - r).abs().max().item()
-        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3n vs conv2 max diff {d}"
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3t vs conv2 max diff {d}"
     if B == 2:
         torch.set_num_threads(8)
         want = _ref_heads(arch, fw, frames)
@@ -414,24 +373,6 @@ def test_patch_conv_matches_dn(monkeypatch):
         else:
             err = ((g - r).abs().max() / r.abs().max()).item()
             assert err < 1e-5, f"{name}: patch vs dn rel diff {err}"
-
-
-def test_wide_patch_conv_matches_conv2(monkeypatch):
-    """The wide patch kernel (off by default, VA_CONV_WP=1; 16 x 16 output tile, 18 x 18 patch per 64-channel chunk, weights streamed per
-    tap) against the im2col conv2 kernel on a whole bf16 forward: its K order is chunk-major / tap-minor
-    instead of tap-major, so the two agree to accumulation-order rounding, amplified through ~60 layers of
-    bf16 storage; both must be equally close to the fp32 torch reference."""
-    arch, fw, net = _net("bf16", "s", seed=10)
-    frames = _frames(2, seed=11)
-    f32 = _ref_heads(arch, fw, frames)
-    monkeypatch.delenv("VA_CONV_WP", raising=False)
-    ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV_WP", "1")
-    got = _gpu_heads(net, frames)
-    rel = lambda g, r: ((g - r).norm() / r.norm()).item()
-    for name, g, r, t in zip(("box", "cls", "coef", "proto"), got, ref, f32):
-        assert rel(g, r) < 1e-2, f"{name}: wide patch vs conv2 relative L2 {rel(g, r)}"
-        assert rel(g, t) < 1.25 * rel(r, t) + 1e-3, f"{name}: vs fp32 {rel(g, t)} (conv2 {rel(r, t)})"
 
 
 @pytest.mark.parametrize("cin,cout,k,stride,H,W,residual", [

@@ -25,6 +25,8 @@
 //     there with the corrected set.  Every round adds >= 1 key, so a process needs
 //     at most 128 re-run rounds in its whole lifetime.
 #include <hip/hip_runtime.h>
+#include <map>
+#include <mutex>
 #include <stdint.h>
 #include <string.h>
 
@@ -928,6 +930,19 @@ hipError_t ensure_tables() {
     return hipSuccess;
 }
 
+// pinned verdict word of (current device, stream); allocated once, kept for the process
+volatile int32_t* verdict_word(hipStream_t st) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, int32_t*> words;
+    std::lock_guard<std::mutex> lock(mu);
+    int32_t*& w = words[{va_cur_dev(), st}];
+    if (!w && hipHostMalloc((void**)&w, 64, hipHostMallocDefault) != hipSuccess) {
+        w = nullptr;
+        return nullptr;
+    }
+    return w;
+}
+
 size_t astar_lds(int nodes) { return ASTAR_TABLES + (size_t)nodes * (8 + 8 + 4 + 2 + 2 + 2 + 1) + 16; }
 
 // speculative rounds over `nslots` query slots
@@ -937,12 +952,12 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
         hipFuncSetAttribute((const void*)nav_astar_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
             hipSuccess)
         return VA_ERR_HIP;
-    // the round's verdict is read through a pinned host word (one per device), copied on the launch stream
-    // behind the validation kernel and waited for on that stream -- never a pageable copy, whose staging the
-    // runtime orders on its own
-    static DevVal<int32_t*> flag;
-    if (!flag() && hipHostMalloc((void**)&flag(), 64, hipHostMallocDefault) != hipSuccess) return VA_ERR_HIP;
-    volatile int32_t* rerun_h = flag();
+    // the round's verdict is read through a pinned host word, copied on the launch stream behind the validation
+    // kernel and waited for on that stream -- never a pageable copy, whose staging the runtime orders on its own.
+    // One word per (device, stream), handed out under a mutex: two host threads running va_nav_run on different
+    // streams never share one (a shared word let one caller's verdict end another's rounds early)
+    volatile int32_t* rerun_h = verdict_word(st);
+    if (!rerun_h) return VA_ERR_HIP;
     int slot0 = 0, rounds = 0;
     while (true) {
         ++rounds;

@@ -300,17 +300,6 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 //     chunks are fetched from a zeroed device page.
 constexpr int BK2 = 64;
 __device__ __attribute__((aligned(16))) unsigned int g_zero_page[8];  // 32 zero bytes (conv3t reads two 16-byte words)
-// diagnosis builds only (tools/build_variant.sh ... -DCONV2_ABL=N; wrong results): ablations of conv2's three-term
-// K-loop -- 1 = no DMA after the first K-step (compute on stale stages), 2 = one MFMA per K-step instead of 96,
-// 3 = no split (the raw f32 words reinterpreted as the three bf16 terms); 0 (the library) = none
-#ifndef CONV2_ABL
-#define CONV2_ABL 0
-#endif
-// the same for conv3t_kernel (-DCONV3T_ABL=N): 1 = no A DMA after the prologue, 2 = one MFMA per K-step instead of
-// 24 (the operands still read and consumed), 3 = no B loads / split / plane stores after the prologue
-#ifndef CONV3T_ABL
-#define CONV3T_ABL 0
-#endif
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -665,9 +654,8 @@ __device__ __forceinline__ void split3_bf16(const u32x4& c0, const u32x4& c1, bf
 // operands split into three exact bf16 terms (split3_bf16) and multiplied on v_mfma_f32_16x16x32_bf16 (16 cycles
 // per SIMD, 8x the K per instruction): the term products h.h, h.m, m.h, h.l, m.m, l.h (+ m.l, l.m, l.l for 9) are
 // exact in f32 and accumulated in f32; the three left out at 6 are <= 2^-23 of |a b| together, below one f32
-// rounding of the sum.  SPL 16 (VA_F32_SPLIT=16, A/B only): the same six products on v_mfma_f32_32x32x16_bf16 (32 x 32
-// blocks, 32 cycles per SIMD with 24 of them free for the split's VALU, against 8 of 16 for 16x16x32) -- measured
-// 2-10 % slower on every layer of the s-seg forward (33.9 vs 32.2 ms per 128 frames, profiles/r03/ab_split_6_16.log).
+// rounding of the sum.  (The same six products on v_mfma_f32_32x32x16_bf16 measured 2-10 % slower on every layer
+// of the s-seg forward, profiles/r03/ab_split_6_16.log.)
 // 16-byte write-through (sc1) store of a split-K slab (conv2_kernel's combine): base / bytes = the workspace.  A
 // plain __device__ function: the host pass of a kernel template whose body names a buffer builtin can drop the
 // kernel's stub (see t3_dma16)
@@ -853,11 +841,6 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     for (int i = 0; i < TNS; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    f32x16 acc32[SPL == 16 ? TNS / 2 : 1][2];  // SPL 16: 32 x 32 blocks (channels x pixels)
-#pragma unroll
-    for (int i = 0; i < (SPL == 16 ? TNS / 2 : 1); ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc32[i][j] = (f32x16){};
 
     if constexpr (GLDS) {
         CONV2_DMA(kt0 * KS, 0);
@@ -872,7 +855,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         const int s = (kt - kt0) & 1;
         const bool more = kt + 1 < kt1;
         if constexpr (GLDS) {
-            if (more && !(SPL > 0 && SPL != 16 && CONV2_ABL == 1)) {
+            if (more) {
                 CONV2_DMA((kt + 1) * KS, s ^ 1);
             }
         } else {
@@ -880,42 +863,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         }
         const T* as_ = As(s);
         const T* bs_ = Bs(s);
-        if constexpr (SPL == 16) {
-            // the six term products on v_mfma_f32_32x32x16_bf16: lane (r, g) = (lane % 32, lane / 32) feeds row r
-            // of a 32-row block with the 8 K values of chunks 4 h + 2 g and 4 h + 2 g + 1 (K-half h of the step;
-            // the same K order for both operands).  A 32-cycle MFMA holds the SIMD's vector issue for 8 of its
-            // cycles (16x16x32: 8 of 16), so the split's VALU fits in the MFMA shadow
-            constexpr int CB = TNS / 2;
-            const int r32 = lane & 31, g32 = lane >> 5;
-            bf16x8 at[CB][2][3], bt[2][2][3];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c0 = 4 * h + 2 * g32;
-                const int s0 = GLDS ? ((c0 ^ (r32 & 7)) * VEC) : c0 * VEC;
-                const int s1 = GLDS ? (((c0 + 1) ^ (r32 & 7)) * VEC) : (c0 + 1) * VEC;
-#pragma unroll
-                for (int ib = 0; ib < CB; ++ib) {
-                    const T* rp = as_ + (wn * 16 * TNS + 32 * ib + r32) * RS;
-                    split3_bf16(*(const u32x4*)(rp + s0), *(const u32x4*)(rp + s1), at[ib][h]);
-                }
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb) {
-                    const T* rp = bs_ + (wm * 64 + 32 * jb + r32) * RS;
-                    split3_bf16(*(const u32x4*)(rp + s0), *(const u32x4*)(rp + s1), bt[jb][h]);
-                }
-            }
-            constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-#pragma unroll
-            for (int t = 0; t < 6; ++t)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-#pragma unroll
-                    for (int ib = 0; ib < CB; ++ib)
-#pragma unroll
-                        for (int jb = 0; jb < 2; ++jb)
-                            acc32[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(at[ib][h][TA[t]], bt[jb][h][TB[t]],
-                                                                                    acc32[ib][jb], 0, 0, 0);
-        } else {
+        {
         // all fragments of the K-step first (the second half's reads overlap the first half's MFMAs)
         u32x4 af[2][TNS], bfr[2][4];
 #pragma unroll
@@ -957,27 +905,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             // the lane's 8 f32 of a row (chunks fq and 4 + fq) as one 8-deep bf16 operand per term: a 32-deep
             // K-step is one 16x16x32 MFMA per term pair
             bf16x8 at[TNS][3], bt[4][3];
-            if constexpr (CONV2_ABL == 3) {  // diagnosis: no split
 #pragma unroll
-                for (int i = 0; i < TNS; ++i)
-                    at[i][0] = at[i][1] = at[i][2] = __builtin_bit_cast(bf16x8, af[kt & 1][i]);
+            for (int i = 0; i < TNS; ++i) split3_bf16(af[0][i], af[1][i], at[i]);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) bt[j][0] = bt[j][1] = bt[j][2] = __builtin_bit_cast(bf16x8, bfr[kt & 1][j]);
-            } else {
-#pragma unroll
-                for (int i = 0; i < TNS; ++i) split3_bf16(af[0][i], af[1][i], at[i]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) split3_bf16(bfr[0][j], bfr[1][j], bt[j]);
-            }
+            for (int j = 0; j < 4; ++j) split3_bf16(bfr[0][j], bfr[1][j], bt[j]);
             constexpr int TA[9] = {0, 0, 1, 0, 1, 2, 1, 2, 2}, TB[9] = {0, 1, 0, 2, 1, 0, 2, 1, 2};
-            if constexpr (CONV2_ABL == 2) {  // diagnosis: one MFMA per K-step (the operands still consumed)
-                bf16x8 sa = at[0][0], sb = bt[0][0];
-#pragma unroll
-                for (int i = 1; i < TNS; ++i) sa = sa + at[i][1] + at[i][2];
-#pragma unroll
-                for (int j = 1; j < 4; ++j) sb = sb + bt[j][1] + bt[j][2];
-                acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, sb, acc[0][0], 0, 0, 0);
-            } else {
 #pragma unroll
             for (int t = 0; t < SPL; ++t)
 #pragma unroll
@@ -986,7 +918,6 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                     for (int j = 0; j < 4; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i][TA[t]], bt[j][TB[t]], acc[i][j], 0,
                                                                             0, 0);
-            }
         } else {
             // f32: element e of lane (fr, fq)'s chunk 4 kh + fq is K index 16 kh + 4 fq + e of the stage -- MFMA
             // (kh, e) sums over fq, so the four MFMAs of a chunk cover its 16 K values (the same permutation of
@@ -1004,7 +935,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
                                                                              __uint_as_float(bfr[kh][j][e]),
                                                                              acc[i][j], 0, 0, 0);
         }
-        }  // SPL != 16
+        }
         if constexpr (GLDS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
@@ -1016,7 +947,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_STORE
 #undef CONV2_DMA
 
-    if constexpr (SPL != 16) {
+    {
         if (ksplit > 1) {
             // split-K combine (cdna_hip_programming.md §5 "In-launch split-K reduction", §6 Guideline 16, its sc1
             // form): every slice stores its f32 partial tile write-through (slab [vt][sk][fragment q][thread], 1 KiB
@@ -1065,12 +996,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             return;
         }
     }
-    if constexpr (SPL == 16) {
-        static_assert(WM * 64 == BM && TNS % 2 == 0, "32 x 32 blocks: 64-pixel waves, even channel fragments");
-        conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc32, smem, n0, wm, wn, tid, lane, orow, m0, cls);
-    } else {
-        conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
-    }
+    conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
 }
 
 // ------------------------------------------------------------------------ conv3t (f32 mode, three-plane K-loop)
@@ -1208,8 +1134,10 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     // prologue: A of steps 0 .. NSTAGE - 2 in their stages, B of steps 0 and 1 in registers; step 0 staged
 #pragma unroll
     for (int k = 0; k < NSTAGE - 1; ++k) dmaA(k, k, k < nk);
+    __builtin_amdgcn_sched_barrier(0);  // the DMAs issue before the loads (the count below assumes it)
     loadB(0, true);
     loadB(1, nk > 1);
+    __builtin_amdgcn_sched_barrier(0);
     t3_waitvm<2>();  // everything but step 1's two B loads
     storeB(0, 0);
     __syncthreads();
@@ -1223,9 +1151,12 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     auto step = [&](const int k, auto LSc) {
         constexpr int LS = decltype(LSc)::value;
         const int s = k % NSTAGE;
-        if constexpr (CONV3T_ABL != 1)
-            dmaA(k + NSTAGE - 1, (k + NSTAGE - 1) % NSTAGE, k + NSTAGE - 1 < nk);  // stage last read at step k - 1
-        if constexpr (CONV3T_ABL != 3) loadB(LS, k + 2 < nk);  // step k's registers were stored at step k - 1
+        dmaA(k + NSTAGE - 1, (k + NSTAGE - 1) % NSTAGE, k + NSTAGE - 1 < nk);  // stage last read at step k - 1
+        // the counted waits below assume this step's NA DMAs issue BEFORE its two B loads: pinned, not left to the
+        // scheduler (an early B load would let vmcnt(2) retire the loads with a DMA still in flight)
+        __builtin_amdgcn_sched_barrier(0);
+        loadB(LS, k + 2 < nk);  // step k's registers were stored at step k - 1
+        __builtin_amdgcn_sched_barrier(0);
         bf16x8 ap[2][3], bp[2][3];
         const unsigned char* as_ = stA(s);
         const unsigned char* bs_ = stB(s);
@@ -1241,11 +1172,6 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
 #pragma unroll
             for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(bs_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
         }
-        if constexpr (CONV3T_ABL == 2) {  // diagnosis: one MFMA per K-step
-            bf16x8 sa = ap[0][0] + ap[0][1] + ap[0][2] + ap[1][0] + ap[1][1] + ap[1][2];
-            bf16x8 sb = bp[0][0] + bp[0][1] + bp[0][2] + bp[1][0] + bp[1][1] + bp[1][2];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, sb, acc[0][0], 0, 0, 0);
-        } else {
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -1254,15 +1180,10 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
                 for (int jb = 0; jb < 2; ++jb)
                     acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
                                                                           0, 0);
-        }
         // step k + 1's A (DMA'd NSTAGE - 1 steps ago: this step when NSTAGE = 2) and B (loaded one step ago)
         // complete; this step's two B loads stay in flight, and with NSTAGE = 3 this step's DMA too
-        if constexpr (CONV3T_ABL == 3) {
-            t3_waitvm<0>();
-        } else {
-            t3_waitvm<NSTAGE == 2 ? 2 : NA + 2>();
-            storeB(1 - LS, (k + 1) % NSTAGE);  // past the last step: a harmless store into a stage nobody reads
-        }
+        t3_waitvm<NSTAGE == 2 ? 2 : NA + 2>();
+        storeB(1 - LS, (k + 1) % NSTAGE);  // past the last step: a harmless store into a stage nobody reads
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // stores visible, stage reads retired
     };
     int k = 0;
@@ -1279,1015 +1200,6 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         return m < a.M ? conv_out_row(a, m, cls) : -1;
     };
     conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smt, n0, wm, wn, tid, lane, orow, m0, cls);
-}
-
-// ------------------------------------------------------------------------ conv3u (conv3t with a deeper pipeline)
-// conv3t's 128-pixel form measured staging-bound, not MFMA-bound (profiles/r03/conv3t_abl: one MFMA per K-step
-// instead of 24 left the forward as slow; no in-loop A DMA saved 19 %, no B loads / split / plane stores 27 %): a
-// K-step of 24 MFMAs per wave (768 MFMA cycles) is shorter than the DMA round trip, and the A stage was waited for
-// one step after its DMA.  conv3u keeps conv3t's operands and MFMAs but (1) packs a stage row into 96 bytes (the
-// six 16-byte plane chunks, no zero-page slots: a stage is 12 KiB per operand), which leaves LDS for (2) THREE A
-// stages, so A(k + 2) is DMA'd at step k and waited for at the end of step k + 1, and (3) B registers three steps
-// ahead; B planes keep two stages (stored at the end of step k for step k + 1).  Per step, in issue order: DMA A(k +
-// 2), load B(k + 3); at the end of step k the counted wait leaves this step's ops and step k - 1's B(k + 2) in
-// flight.  Row swizzle: chunk c of row r sits in slot (c + (r >> 3)) % 6 -- rows r and r + 8 differ in slot parity,
-// so a 16-lane group of 16-byte reads down 16 rows covers 64 distinct banks (96-byte rows: 8 rows span the bank
-// groups 8 m).  The A DMA is linear in LDS per instruction (lane l -> bytes 16 l of a 1 KiB piece): each lane's
-// row / slot / source chunk are per-lane constants.  128-pixel x 128-channel tiles, 4 waves, two workgroups per CU.
-constexpr int T3U_ROW = 96, T3U_BM = 128, T3U_NT = 256;
-constexpr int T3U_ASTAGE = T3_BN * T3U_ROW, T3U_BSTAGE = T3U_BM * T3U_ROW;  // 12 KiB each
-constexpr int T3U_NSA = 3, T3U_NSB = 2;
-constexpr int T3U_EPI = T3U_BM * (T3_BN + 4) * 4;
-constexpr int T3U_LDS = (T3U_NSA * T3U_ASTAGE + T3U_NSB * T3U_BSTAGE) > T3U_EPI ? (T3U_NSA * T3U_ASTAGE + T3U_NSB * T3U_BSTAGE)
-                                                                              : T3U_EPI;
-constexpr int T3U_NA = T3U_ASTAGE / 1024 / (T3U_NT / 64);  // A-DMA instructions per wave per K-step (3)
-static_assert(T3U_ASTAGE % 1024 == 0 && T3U_NA * 1024 * (T3U_NT / 64) == T3U_ASTAGE, "A stage in 1 KiB pieces");
-static_assert(2 * T3U_LDS <= 160 * 1024, "two workgroups per CU");
-__device__ __forceinline__ int t3u_slot(int c, int r) {
-    const int s = c + ((r >> 3) & 1);
-    return s >= 6 ? s - 6 : s;
-}
-
-template <typename OutT>
-__global__ __launch_bounds__(T3U_NT) void conv3u_kernel(va_conv_args a, int ntn, int ntiles) {
-    extern __shared__ __align__(16) unsigned char smu[];
-    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, TNS = 4, NA = T3U_NA;
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int cls = a.mode == 2 ? (bid & 3) : 0;
-    if (a.mode == 2) bid >>= 2;
-    const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid / WN, wn = wid % WN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
-    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
-    auto stA = [&](int s) { return smu + s * T3U_ASTAGE; };
-    auto stB = [&](int s) { return smu + T3U_NSA * T3U_ASTAGE + s * T3U_BSTAGE; };
-
-    // ---- B staging unit (as conv3t): row br, 8-channel group bg
-    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
-    int b_hi, b_wi;
-    int64_t b_base;
-    {
-        const int m = m0 + br;
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi = ho * a.stride - pad_y;
-            b_wi = wo * a.stride - pad_x;
-            b_base = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
-        }
-    }
-    // ---- A DMA: piece j of this wave = LDS bytes 1024 (wid + 4 j) .. of the stage; lane l -> byte 16 l of it
-    const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
-    constexpr int T3_OOR = 0x7ff00000;
-    int aoff[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
-        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
-        int c = slot - ((row >> 3) & 1);
-        if (c < 0) c += 6;
-        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
-    }
-    auto dmaA = [&](int k, int s, bool live) {
-        unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
-    };
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
-    u32x4 rb[3][2];  // B registers of three K-steps in flight
-    auto loadB = [&](int slot, bool live) {
-        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
-        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
-        rb[slot][0] = *(const u32x4*)p;
-        rb[slot][1] = *(const u32x4*)(p + 4);
-        ld_c += T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
-            }
-        }
-    };
-    auto storeB = [&](int slot, int s) {
-        bf16x8 t[3];
-        split3_bf16(rb[slot][0], rb[slot][1], t);
-        unsigned char* rowp = stB(s) + br * T3U_ROW;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
-    };
-
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;
-    // prologue, in issue order: A(0), B(0), A(1), B(1), B(2); then A(0) and B(0) complete, B(0)'s planes stored
-    dmaA(0, 0, true);
-    loadB(0, true);
-    dmaA(1, 1, nk > 1);
-    loadB(1, nk > 1);
-    loadB(2, nk > 2);
-    t3_waitvm<NA + 4>();
-    storeB(0, 0);
-    __syncthreads();
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-    auto step = [&](const int k, auto LSc) {
-        constexpr int LS = decltype(LSc)::value;  // = k % 3: B(k) was in slot LS (stored at step k - 1)
-        dmaA(k + 2, (k + 2) % T3U_NSA, k + 2 < nk);  // the stage read at step k - 1
-        loadB(LS, k + 3 < nk);
-        bf16x8 ap[2][3], bp[2][3];
-        const unsigned char* as_ = stA(k % T3U_NSA);
-        const unsigned char* bs_ = stB(k & 1);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = wn * 64 + 32 * ib + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int row = wm * 64 + 32 * jb + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
-                                                                          0, 0);
-        // A(k + 1) (DMA'd at step k - 1) and B(k + 1) (loaded at step k - 2) complete; step k - 1's B(k + 2) and
-        // this step's A(k + 2) / B(k + 3) stay in flight
-        t3_waitvm<NA + 4>();
-        storeB((LS + 1) % 3, (k + 1) & 1);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    int k = 0;
-    for (; k + 2 < nk; k += 3) {
-        step(k, std::integral_constant<int, 0>{});
-        step(k + 1, std::integral_constant<int, 1>{});
-        step(k + 2, std::integral_constant<int, 2>{});
-    }
-    if (k < nk) step(k, std::integral_constant<int, 0>{});
-    if (k + 1 < nk) step(k + 1, std::integral_constant<int, 1>{});
-    t3_waitvm<0>();
-    __syncthreads();
-
-    auto orow = [&](int pl) -> int64_t {
-        const int m = m0 + pl;
-        return m < a.M ? conv_out_row(a, m, cls) : -1;
-    };
-    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smu, n0, wm, wn, tid, lane, orow, m0, cls);
-}
-
-// conv3v: conv3u with the B loads taken a K-step PAIR at a time (Cin % 32 == 0: a pair never straddles a tap).  A
-// thread's four 16-byte loads -- channels 8 bg .. of step 2j and 16 + 8 bg .. of step 2j + 1 -- and its partner's
-// (bg ^ 1) cover a pixel's whole 128-byte line in one burst, where conv3u's per-step loads touch each line twice, a
-// K-step apart (half a line each time: the line is fetched from L2 again once the CU's 32 KiB L1 has turned over).
-// Pair j + 2 is loaded at step 2 j (three pair slots in registers); per step one A DMA as conv3u, so every step
-// ends in the same counted wait (this step's ops and, after an even step, nothing older than A(k + 1) pending).
-template <typename OutT>
-__global__ __launch_bounds__(T3U_NT) void conv3v_kernel(va_conv_args a, int ntn, int ntiles) {
-    extern __shared__ __align__(16) unsigned char smv[];
-    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, TNS = 4, NA = T3U_NA;
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int cls = a.mode == 2 ? (bid & 3) : 0;
-    if (a.mode == 2) bid >>= 2;
-    const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid / WN, wn = wid % WN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
-    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
-    auto stA = [&](int s) { return smv + s * T3U_ASTAGE; };
-    auto stB = [&](int s) { return smv + T3U_NSA * T3U_ASTAGE + s * T3U_BSTAGE; };
-    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
-    int b_hi, b_wi;
-    int64_t b_base;
-    {
-        const int m = m0 + br;
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi = ho * a.stride - pad_y;
-            b_wi = wo * a.stride - pad_x;
-            b_base = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
-        }
-    }
-    const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
-    constexpr int T3_OOR = 0x7ff00000;
-    int aoff[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
-        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
-        int c = slot - ((row >> 3) & 1);
-        if (c < 0) c += 6;
-        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
-    }
-    auto dmaA = [&](int k, int s, bool live) {
-        unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
-    };
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
-    u32x4 rb[3][4];  // three K-step pairs: [0..1] = step 2j (channels 8 bg ..), [2..3] = step 2j + 1
-    auto loadPair = [&](int slot, bool live) {
-        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
-        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
-        const int s1 = ok ? 16 : 0;  // the zero page holds 8 floats
-        rb[slot][0] = *(const u32x4*)p;
-        rb[slot][1] = *(const u32x4*)(p + 4);
-        rb[slot][2] = *(const u32x4*)(p + s1);
-        rb[slot][3] = *(const u32x4*)(p + s1 + 4);
-        ld_c += 2 * T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
-            }
-        }
-    };
-    auto storeB = [&](int slot, int half, int s) {
-        bf16x8 t[3];
-        split3_bf16(rb[slot][2 * half], rb[slot][2 * half + 1], t);
-        unsigned char* rowp = stB(s) + br * T3U_ROW;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
-    };
-
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;  // even (Cin % 32 == 0)
-    // prologue, in issue order: A(0), pair 0, A(1), pair 1; then A(0) and pair 0 complete, B(0)'s planes stored
-    dmaA(0, 0, true);
-    loadPair(0, true);
-    dmaA(1, 1, nk > 1);
-    loadPair(1, nk > 2);
-    t3_waitvm<NA + 4>();
-    storeB(0, 0, 0);
-    __syncthreads();
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-    // step k = 2 j + H; PS = j % 3 (the pair slot of B(k)); an even step loads pair j + 2 into slot (j + 2) % 3
-    auto step = [&](const int k, auto PSc, auto Hc) {
-        constexpr int PS = decltype(PSc)::value, H = decltype(Hc)::value;
-        dmaA(k + 2, (k + 2) % T3U_NSA, k + 2 < nk);
-        if constexpr (H == 0) loadPair((PS + 2) % 3, k + 4 < nk);
-        bf16x8 ap[2][3], bp[2][3];
-        const unsigned char* as_ = stA(k % T3U_NSA);
-        const unsigned char* bs_ = stB(k & 1);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = wn * 64 + 32 * ib + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int row = wm * 64 + 32 * jb + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
-                                                                          0, 0);
-        // A(k + 1) complete (and every B load older than it: B(k + 1) is in pair (k + 1) / 2, loaded two steps
-        // or more before)
-        t3_waitvm<NA + 4>();
-        if constexpr (H == 0) storeB(PS, 1, (k + 1) & 1);           // B(k + 1) = second half of this pair
-        else storeB((PS + 1) % 3, 0, (k + 1) & 1);                  // first half of the next pair
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    int k = 0;
-    for (; k + 5 < nk; k += 6) {
-        step(k, I0{}, I0{});
-        step(k + 1, I0{}, I1{});
-        step(k + 2, I1{}, I0{});
-        step(k + 3, I1{}, I1{});
-        step(k + 4, I2{}, I0{});
-        step(k + 5, I2{}, I1{});
-    }
-    if (k < nk) {  // 2 or 4 steps left
-        step(k, I0{}, I0{});
-        step(k + 1, I0{}, I1{});
-        if (k + 2 < nk) {
-            step(k + 2, I1{}, I0{});
-            step(k + 3, I1{}, I1{});
-        }
-    }
-    t3_waitvm<0>();
-    __syncthreads();
-
-    auto orow = [&](int pl) -> int64_t {
-        const int m = m0 + pl;
-        return m < a.M ? conv_out_row(a, m, cls) : -1;
-    };
-    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smv, n0, wm, wn, tid, lane, orow, m0, cls);
-}
-
-// DIAGNOSIS ONLY (VA_CONV3T=5 / 6): with other kernels running beside it (the laned small-batch list) conv3w gave 2
-// mismatching forwards in 12 (tools/form_race.py) -- a stage-reuse race the single-stream tests never exposed;
-// conv3t (the default) and forms 3, 4, 7 stayed bit-identical in 40 laned runs each.
-// conv3w: the staging moved off each wave's serial path.  In conv3t a wave's K-step is [DMA + B-load issue, fragment
-// reads, 24 MFMAs, wait, split + plane stores of the next step's B, barrier]: the split and the stores run after
-// the wave's MFMAs and before the barrier, in series with them (conv3t_abl: without the B path the forward is 27 %
-// faster, without MFMAs no faster).  conv3w splits and stores B(k + 1) DURING step k's MFMAs -- the planes go to the
-// other B stage, which nobody reads in step k, and their registers were loaded two steps before -- with the
-// scheduler told to interleave them (sched_group_barrier: one MFMA, then a VALU pair / a plane store).  One barrier
-// per step, at its start, after the wave's own A DMA and B loads of that step have landed: it publishes A(k) and
-// the B(k) planes of every wave and retires every read of the stages step k + 1 will overwrite.  96-byte rows
-// (conv3u), two A and two B stages, B registers three slots (loaded three steps ahead).  Bit-identical to conv3t.
-template <typename OutT, int SCHED>
-__global__ __launch_bounds__(T3U_NT) void conv3w_kernel(va_conv_args a, int ntn, int ntiles) {
-    extern __shared__ __align__(16) unsigned char smw[];
-    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, TNS = 4, NA = T3U_NA;
-    constexpr int NSA = 2;
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int cls = a.mode == 2 ? (bid & 3) : 0;
-    if (a.mode == 2) bid >>= 2;
-    const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid / WN, wn = wid % WN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
-    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
-    auto stA = [&](int s) { return smw + s * T3U_ASTAGE; };
-    auto stB = [&](int s) { return smw + NSA * T3U_ASTAGE + s * T3U_BSTAGE; };
-    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
-    int b_hi, b_wi;
-    int64_t b_base;
-    {
-        const int m = m0 + br;
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi = ho * a.stride - pad_y;
-            b_wi = wo * a.stride - pad_x;
-            b_base = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
-        }
-    }
-    const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
-    constexpr int T3_OOR = 0x7ff00000;
-    int aoff[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
-        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
-        int c = slot - ((row >> 3) & 1);
-        if (c < 0) c += 6;
-        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
-    }
-    auto dmaA = [&](int k, int s, bool live) {
-        unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
-    };
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
-    u32x4 rb[3][2];
-    auto loadB = [&](int slot, bool live) {
-        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
-        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
-        rb[slot][0] = *(const u32x4*)p;
-        rb[slot][1] = *(const u32x4*)(p + 4);
-        ld_c += T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
-            }
-        }
-    };
-    auto storeB = [&](int slot, int s) {
-        bf16x8 t[3];
-        split3_bf16(rb[slot][0], rb[slot][1], t);
-        unsigned char* rowp = stB(s) + br * T3U_ROW;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
-    };
-
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;
-    // prologue, in issue order: B(0), B(1), A(0), B(2); B(0)'s planes stored once B(0) has landed
-    loadB(0, true);
-    loadB(1, nk > 1);
-    dmaA(0, 0, true);
-    loadB(2, nk > 2);
-    t3_waitvm<NA + 4>();
-    storeB(0, 0);
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-    auto step = [&](const int k, auto LSc) {
-        constexpr int LS = decltype(LSc)::value;  // = k % 3: B(k + 1) is in slot (LS + 1) % 3
-        // A(k) and B(k + 1) landed (B(k + 2), issued after A(k), may still fly); the barrier publishes A(k) and
-        // the B(k) planes and retires every read of stages (k + 1) % 2
-        t3_waitvm<2>();
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        dmaA(k + 1, (k + 1) % NSA, k + 1 < nk);
-        loadB(LS, k + 3 < nk);  // slot LS held B(k), stored during step k - 1
-        bf16x8 ap[2][3], bp[2][3];
-        const unsigned char* as_ = stA(k % NSA);
-        const unsigned char* bs_ = stB(k & 1);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = wn * 64 + 32 * ib + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int row = wm * 64 + 32 * jb + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
-                                                                          0, 0);
-        storeB((LS + 1) % 3, (k + 1) & 1);  // B(k + 1) into the other B stage, beside the MFMAs
-        if constexpr (SCHED == 1) {
-            // 12 fragment reads first, then per MFMA up to two VALU of the split or one plane store
-#pragma unroll
-            for (int i = 0; i < 4; ++i) __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);  // DS read
-#pragma unroll
-            for (int i = 0; i < 4; ++i) __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // MFMA
-#pragma unroll
-            for (int i = 0; i < 17; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x0002, 2, 0);  // VALU
-            }
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x0200, 1, 0);  // DS write
-            }
-        }
-    };
-    int k = 0;
-    for (; k + 2 < nk; k += 3) {
-        step(k, std::integral_constant<int, 0>{});
-        step(k + 1, std::integral_constant<int, 1>{});
-        step(k + 2, std::integral_constant<int, 2>{});
-    }
-    if (k < nk) step(k, std::integral_constant<int, 0>{});
-    if (k + 1 < nk) step(k + 1, std::integral_constant<int, 1>{});
-    t3_waitvm<0>();
-    __syncthreads();
-
-    auto orow = [&](int pl) -> int64_t {
-        const int m = m0 + pl;
-        return m < a.M ? conv_out_row(a, m, cls) : -1;
-    };
-    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smw, n0, wm, wn, tid, lane, orow, m0, cls);
-}
-
-// conv3x: conv3t's 128-pixel schedule (A DMA one K-step ahead, B registers two steps ahead, the B planes stored
-// after the MFMAs, one barrier per step) with 96-byte rows (conv3u) and the epilogue staged in two halves of 64
-// pixels, so a workgroup needs 48 KiB of LDS and THREE fit a CU (12 waves, three per SIMD, register budget 168):
-// more workgroups to overlap one another's staging and barriers, the one lever the ablations leave (staging-bound,
-// conv3t_abl; deeper prefetch, whole-line loads and overlapping the B work with the MFMAs were all neutral).
-constexpr int T3X_LDS = 2 * T3U_ASTAGE + 2 * T3U_BSTAGE;  // 48 KiB
-static_assert(64 * (T3_BN + 4) * 4 <= T3X_LDS && 3 * T3X_LDS <= 160 * 1024, "three workgroups per CU");
-template <typename OutT>
-__global__ __launch_bounds__(T3U_NT, 3) void conv3x_kernel(va_conv_args a, int ntn, int ntiles) {
-    extern __shared__ __align__(16) unsigned char smx[];
-    constexpr int BM = T3U_BM, BN = T3_BN, NT = T3U_NT, WN = 2, NA = T3U_NA;
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int cls = a.mode == 2 ? (bid & 3) : 0;
-    if (a.mode == 2) bid >>= 2;
-    const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid / WN, wn = wid % WN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
-    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
-    auto stA = [&](int s) { return smx + s * T3U_ASTAGE; };
-    auto stB = [&](int s) { return smx + 2 * T3U_ASTAGE + s * T3U_BSTAGE; };
-    const int br = (tid & 7) | ((tid >> 4) << 3), bg = (tid >> 3) & 1;
-    int b_hi, b_wi;
-    int64_t b_base;
-    {
-        const int m = m0 + br;
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi = ho * a.stride - pad_y;
-            b_wi = wo * a.stride - pad_x;
-            b_base = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi = -(1 << 28), b_wi = 0, b_base = 0;
-        }
-    }
-    const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
-    constexpr int T3_OOR = 0x7ff00000;
-    int aoff[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
-        const int row = o / T3U_ROW, slot = (o - row * T3U_ROW) / 16;
-        int c = slot - ((row >> 3) & 1);
-        if (c < 0) c += 6;
-        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
-    }
-    auto dmaA = [&](int k, int s, bool live) {
-        unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
-    };
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
-    u32x4 rb[2][2];
-    auto loadB = [&](int slot, bool live) {
-        const int hi = b_hi + ld_ky, wi = b_wi + ld_kx;
-        const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
-        rb[slot][0] = *(const u32x4*)p;
-        rb[slot][1] = *(const u32x4*)(p + 4);
-        ld_c += T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
-            }
-        }
-    };
-    auto storeB = [&](int slot, int s) {
-        bf16x8 t[3];
-        split3_bf16(rb[slot][0], rb[slot][1], t);
-        unsigned char* rowp = stB(s) + br * T3U_ROW;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bg + p, br)) = t[p];
-    };
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;
-    dmaA(0, 0, true);
-    loadB(0, true);
-    loadB(1, nk > 1);
-    t3_waitvm<2>();
-    storeB(0, 0);
-    __syncthreads();
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-    auto step = [&](const int k, auto LSc) {
-        constexpr int LS = decltype(LSc)::value;
-        const int s = k & 1;
-        dmaA(k + 1, (k + 1) & 1, k + 1 < nk);
-        loadB(LS, k + 2 < nk);
-        bf16x8 ap[2][3], bp[2][3];
-        const unsigned char* as_ = stA(s);
-        const unsigned char* bs_ = stB(s);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = wn * 64 + 32 * ib + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                ap[ib][p] = *(const bf16x8*)(as_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int row = wm * 64 + 32 * jb + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
-                                                                          0, 0);
-        t3_waitvm<2>();
-        storeB(1 - LS, (k + 1) & 1);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    int k = 0;
-    for (; k + 1 < nk; k += 2) {
-        step(k, std::integral_constant<int, 0>{});
-        step(k + 1, std::integral_constant<int, 1>{});
-    }
-    if (k < nk) step(k, std::integral_constant<int, 0>{});
-    t3_waitvm<0>();
-    __syncthreads();
-    // epilogue in two halves of 64 pixels (rows wm * 64 ..): conv_epilogue32's math, a 64-row staging tile
-    constexpr int CW = BN + 4;
-    float* Cs = (float*)smx;
-    const int r = lane & 31, g = lane >> 5;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        if (wm == half) {
-#pragma unroll
-            for (int jb = 0; jb < 2; ++jb) {
-                const int pl = 32 * jb + r;
-                int brow = n0;
-                if (a.bias4) {
-                    const int m = m0 + half * 64 + pl;
-                    const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
-                    const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
-                    brow = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
-                }
-#pragma unroll
-                for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int col = wn * 64 + 32 * ib + 8 * q + 4 * g;
-                        const float4 bv = *(const float4*)(a.bias + brow + col);
-                        float v0 = acc[ib][jb][4 * q] + bv.x, v1 = acc[ib][jb][4 * q + 1] + bv.y,
-                              v2 = acc[ib][jb][4 * q + 2] + bv.z, v3 = acc[ib][jb][4 * q + 3] + bv.w;
-                        if (a.act) {
-                            const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
-                            v0 = s01[0], v1 = s01[1], v2 = s23[0], v3 = s23[1];
-                        }
-                        *(float4*)(Cs + pl * CW + col) = make_float4(v0, v1, v2, v3);
-                    }
-            }
-        }
-        __syncthreads();
-        auto orow = [&](int pl) -> int64_t {
-            const int m = m0 + half * 64 + pl;
-            return m < a.M ? conv_out_row(a, m, cls) : -1;
-        };
-        conv_epilogue_store<NT, 64, BN, OutT, decltype(orow), float>(a, smx, n0, tid, orow);
-        __syncthreads();
-    }
-}
-
-// conv3n: conv3t for the narrow f32 layers (33..64 output channels): 256-pixel x 64-channel tiles, 4 waves each
-// 64 pixels x all 64 channels (the same 2 x 2 blocks of 32 x 32 and 24 MFMAs per K-step as conv3t), so the
-// operand split happens once per workgroup and staged pixel instead of once per wave and fragment (conv2's
-// three-term form on these layers: 90-145 TF f32-equivalent against 170-185 for conv3t's).  A = weight planes
-// (conv3t's 128-byte rows and DMA map, 64 rows: 2 DMA pieces per wave), B = activation planes in 96-byte rows
-// (conv3u's swizzle), each thread staging two (pixel, 8-channel group) units per K-step.  Two stages, two
-// workgroups per CU.  Same products and order as conv3t per output (bit-identical to the forms above where
-// both apply).
-constexpr int T3N_BM = 256, T3N_BN = 64, T3N_NT = 256;
-constexpr int T3N_ASTAGE = T3N_BN * T3_ROW, T3N_BSTAGE = T3N_BM * T3U_ROW;  // 8 + 24 KiB
-constexpr int T3N_EPI = T3N_BM * (T3N_BN + 4) * 4;
-constexpr int T3N_LDS = 2 * (T3N_ASTAGE + T3N_BSTAGE) > T3N_EPI ? 2 * (T3N_ASTAGE + T3N_BSTAGE) : T3N_EPI;
-static_assert(2 * T3N_LDS <= 160 * 1024, "two workgroups per CU");
-template <typename OutT>
-__global__ __launch_bounds__(T3N_NT) void conv3n_kernel(va_conv_args a, int ntiles) {
-    extern __shared__ __align__(16) unsigned char smn[];
-    constexpr int BM = T3N_BM, NT = T3N_NT, TNS = 4, NA = T3N_BN / 8 / (T3N_NT / 64);  // 2
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int tm = bid;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wid, wn = 0;
-    const int m0 = tm * BM, n0 = 0;
-    const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3;
-    auto stA = [&](int s) { return smn + s * (T3N_ASTAGE + T3N_BSTAGE); };
-    auto stB = [&](int s) { return smn + s * (T3N_ASTAGE + T3N_BSTAGE) + T3N_ASTAGE; };
-    // two B units per thread: unit u = tid + 256 i -> row (u & 7) | ((u >> 4) << 3), group (u >> 3) & 1
-    int brr[2], bgg[2], b_hi[2], b_wi[2];
-    int64_t b_base[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int u = tid + 256 * i;
-        brr[i] = (u & 7) | ((u >> 4) << 3);
-        bgg[i] = (u >> 3) & 1;
-        const int m = m0 + brr[i];
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi[i] = ho * a.stride - a.pad;
-            b_wi[i] = wo * a.stride - a.pad;
-            b_base[i] = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi[i] = -(1 << 28), b_wi[i] = 0, b_base[i] = 0;
-        }
-    }
-    const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
-    constexpr int T3_OOR = 0x7ff00000;
-    int aoff[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-        const int row = 8 * (wid + 4 * j) + (lane >> 3);
-        const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
-        aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
-    }
-    auto dmaA = [&](int k, int s, bool live) {
-        unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + 4 * j) * 1024, aoff[j], soff);
-    };
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
-    u32x4 rb[2][2][2];  // [slot][unit][half]
-    auto loadB = [&](int slot, bool live) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int hi = b_hi[i] + ld_ky, wi = b_wi[i] + ld_kx;
-            const bool ok = live && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-            const float* p =
-                ok ? X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bgg[i] : (const float*)zpage;
-            rb[slot][i][0] = *(const u32x4*)p;
-            rb[slot][i][1] = *(const u32x4*)(p + 4);
-        }
-        ld_c += T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
-            }
-        }
-    };
-    auto storeB = [&](int slot, int s) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            bf16x8 t[3];
-            split3_bf16(rb[slot][i][0], rb[slot][i][1], t);
-            unsigned char* rowp = stB(s) + brr[i] * T3U_ROW;
-#pragma unroll
-            for (int p = 0; p < 3; ++p) *(bf16x8*)(rowp + 16 * t3u_slot(3 * bgg[i] + p, brr[i])) = t[p];
-        }
-    };
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;
-    dmaA(0, 0, true);
-    loadB(0, true);
-    loadB(1, nk > 1);
-    t3_waitvm<4>();  // all but step 1's four B loads
-    storeB(0, 0);
-    __syncthreads();
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-    auto step = [&](const int k, auto LSc) {
-        constexpr int LS = decltype(LSc)::value;
-        const int s = k & 1;
-        dmaA(k + 1, (k + 1) & 1, k + 1 < nk);
-        loadB(LS, k + 2 < nk);
-        bf16x8 ap[2][3], bp[2][3];
-        const unsigned char* as_ = stA(s);
-        const unsigned char* bs_ = stB(s);
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = 32 * ib + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int row = wm * 64 + 32 * jb + r32;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                bp[jb][p] = *(const bf16x8*)(bs_ + row * T3U_ROW + 16 * t3u_slot(3 * g32 + p, row));
-        }
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[t]], bp[jb][TB[t]], acc[ib][jb], 0,
-                                                                          0, 0);
-        t3_waitvm<4>();  // A(k + 1) and B(k + 1) landed; this step's four B loads stay in flight
-        storeB(1 - LS, (k + 1) & 1);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    int k = 0;
-    for (; k + 1 < nk; k += 2) {
-        step(k, std::integral_constant<int, 0>{});
-        step(k + 1, std::integral_constant<int, 1>{});
-    }
-    if (k < nk) step(k, std::integral_constant<int, 0>{});
-    t3_waitvm<0>();
-    __syncthreads();
-    auto orow = [&](int pl) -> int64_t {
-        const int m = m0 + pl;
-        return m < a.M ? conv_out_row(a, m, 0) : -1;
-    };
-    conv_epilogue32<NT, BM, T3N_BN, TNS, OutT, decltype(orow)>(a, acc, smn, n0, wm, wn, tid, lane, orow, m0, 0);
-}
-
-// ----------------------------------------------------------------------------------------- conv v3 (bf16, wide layers)
-// 256-pixel x 128-channel tiles for the large layers: 8 waves (4 x 2, each 64 pixels x 64 channels as in
-// conv2), BK = 64, THREE LDS stages filled by LDS-DMA with two K-tiles in flight.  Per K-step: a counted
-// vmcnt that retires only this wave's DMAs of tile kt (2 weight + 4 pixel instructions per tile), a raw
-// s_barrier (a __syncthreads() would add vmcnt(0) and drain the prefetch: cdna_hip_programming.md §5
-// "Pipelining across barriers"), the DMA of tile kt + 2 into the stage every wave finished reading at step
-// kt - 1, then the MFMAs of tile kt.  The XOR swizzle, incremental im2col, epilogue and fused 1x1 tail are
-// conv2's (GLDS form); one 512-thread workgroup per CU (144 KiB of LDS).
-constexpr int C3_BM = 256, C3_BN = 128, C3_NT = 512;
-constexpr int C3_STAGE = (C3_BM + C3_BN) * BK2 * 2;  // 48 KiB
-constexpr int C3_LDS = 3 * C3_STAGE;                 // 144 KiB
-static_assert(C3_BM * (C3_BN + 4) * 4 <= C3_LDS, "epilogue tile must fit the stage buffers");
-
-template <typename OutT, int ABL = 0>  // ABL (diagnosis only): 1 = no in-loop DMA, 2 = no MFMA
-__global__ __launch_bounds__(C3_NT) void conv3_kernel(va_conv_args a, int ntn, int ntiles) {
-    constexpr int NT = C3_NT, BM = C3_BM, BN = C3_BN, TNS = 4, WN = 2;
-    constexpr int A_CH = BN * 8 / NT, B_CH = BM * 8 / NT, RSTEP = NT / 8;  // 2, 4, 64
-    static_assert(A_CH + B_CH == 6, "vmcnt(6) below counts one tile of DMAs per wave");
-    extern __shared__ __align__(16) unsigned char smem3[];
-
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int cls = a.mode == 2 ? (bid & 3) : 0;
-    if (a.mode == 2) bid >>= 2;
-    const int tm = bid / ntn, tn = bid % ntn;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const __bf16* __restrict__ X = (const __bf16*)a.x;
-    const __bf16* __restrict__ Wt = (const __bf16*)a.w + (int64_t)cls * a.Npad * a.Kpad;
-    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
-    // DMA instruction i of wave w writes rows RSTEP i + 8 w .. +7 (lane l: row l >> 3, slot l & 7, which
-    // holds chunk (l & 7) ^ (l >> 3) of that row)
-    const int g = (lane & 7) ^ (lane >> 3);
-    const int row0 = 8 * wid + (lane >> 3);
-    int b_hi[B_CH], b_wi[B_CH];
-    int64_t b_base[B_CH];
-#pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-        const int m = m0 + row0 + RSTEP * i;
-        if (m < a.M) {
-            const int wo = m % a.Wo, t = m / a.Wo, ho = t % a.Ho, n = t / a.Ho;
-            b_hi[i] = ho * a.stride - pad_y;
-            b_wi[i] = wo * a.stride - pad_x;
-            b_base[i] = (int64_t)n * a.H * a.W;
-        } else {
-            b_hi[i] = -(1 << 28);
-            b_wi[i] = 0;
-            b_base[i] = 0;
-        }
-    }
-    int ci = 8 * g, ky = 0, kx = 0;
-    while (ci >= a.Cin) {
-        ci -= a.Cin;
-        if (++kx == a.kw) {
-            kx = 0;
-            ++ky;
-        }
-    }
-    int kcur = 8 * g;  // this lane's k of the next tile to stage (weights and pixels alike)
-
-#define CONV3_DMA(s)                                                                                               \
-    {                                                                                                              \
-        __bf16* as_ = (__bf16*)(smem3 + (s) * C3_STAGE);                                                           \
-        __bf16* bs_ = as_ + BN * BK2;                                                                              \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
-            const __bf16* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + kcur;                             \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
-                                             0);                                                                   \
-        }                                                                                                          \
-        const bool kin = kcur < a.K;                                                                               \
-        _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
-            const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
-            const bool ok = kin && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;                   \
-            const void* src = ok ? (const void*)(X + (b_base[i] + (int64_t)hi * a.W + wi) * a.ldx + ci)            \
-                                 : (const void*)g_zero_page;                                                       \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(bs_ + (RSTEP * i + 8 * wid) * BK2), 16, 0,  \
-                                             0);                                                                   \
-        }                                                                                                          \
-        kcur += BK2;                                                                                               \
-        ci += BK2;                                                                                                 \
-        while (ci >= a.Cin) {                                                                                      \
-            ci -= a.Cin;                                                                                           \
-            if (++kx == a.kw) {                                                                                    \
-                kx = 0;                                                                                            \
-                ++ky;                                                                                              \
-            }                                                                                                      \
-        }                                                                                                          \
-    }
-
-    f32x4 acc[TNS][4];
-#pragma unroll
-    for (int i = 0; i < TNS; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    const int nk = a.Kpad / BK2;
-    CONV3_DMA(0);
-    if (nk > 1) CONV3_DMA(1);
-    const int fr = lane & 15, fq = lane >> 4;
-    for (int kt = 0; kt < nk; ++kt) {
-        // tile kt landed (this wave's part); tile kt + 1 stays in flight across the barrier
-        if (kt + 1 < nk)
-            asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (ABL != 1 && kt + 2 < nk) {
-            const int sn = (kt + 2) % 3;
-            CONV3_DMA(sn);
-        }
-        const __bf16* as_ = (const __bf16*)(smem3 + (kt % 3) * C3_STAGE);
-        const __bf16* bs_ = as_ + BN * BK2;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-            bf16x8 af[TNS], bfr[4];
-            const int ch = ((4 * kh + fq) ^ (fr & 7)) * 8;  // swizzled slot of chunk 4 kh + fq
-#pragma unroll
-            for (int i = 0; i < TNS; ++i) af[i] = *(const bf16x8*)(as_ + (wn * 64 + 16 * i + fr) * BK2 + ch);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(bs_ + (wm * 64 + 16 * j + fr) * BK2 + ch);
-            if constexpr (ABL == 2) {
-#pragma unroll
-                for (int i = 0; i < TNS; ++i) asm volatile("" ::"v"(af[i]), "v"(bfr[i]));
-                continue;
-            }
-#pragma unroll
-            for (int i = 0; i < TNS; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-    }
-#undef CONV3_DMA
-    __syncthreads();  // every wave is done with the stages (no DMA in flight): reuse them for the epilogue
-    auto orow = [&](int pl) -> int64_t {
-        const int m = m0 + pl;
-        return m < a.M ? (a.mode == 1 ? (int64_t)m : conv_out_row(a, m, cls)) : -1;
-    };
-    if (a.w2) {
-        conv2_tail<NT, BM, TNS, OutT>(a, acc, smem3, n0, wm, wn, wid, fr, fq, orow);
-        return;
-    }
-    conv_epilogue<NT, BM, BN, TNS, OutT>(a, acc, smem3, n0, wm, wn, tid, fr, fq, orow);
 }
 
 // ----------------------------------------------------------------------------------------- conv v4 (bf16, Cout >= 256)
@@ -3001,148 +1913,6 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
     }
 }
 
-// ----------------------------------------------------------------------------------------- wide patch conv
-// Wide stride-1 3x3 convs (Cin a multiple of 64, Cout > 64 in 128-channel tiles).  The im2col kernels
-// (conv2/conv3) stage every input pixel nine times -- once per tap -- through the LDS-DMA path, whose
-// per-CU rate bounds them (profiles/r01b/conv3_ablation.log: the DMA-only variant alone takes as long as
-// the MFMA-only one).  Here the 18 x 18-pixel patch of a 16 x 16 output tile is staged ONCE per 64-channel
-// chunk and the nine taps read their B fragments from it: a 64-deep K-step moves a 16 KiB weight tile
-// plus 1/9 of a 41 KiB patch instead of 48 KiB.
-//   K order: chunk-major, tap-minor: step s = 9 c + t uses weight tile W[s] (rows n0 .. n0 + 127,
-//   k = t Cin + 64 c .. + 63 of the packed [Npad][Kpad] matrix, XOR-swizzled as in conv2) and patch P[c]
-//   (patch_off<8> image).  LDS: 3 weight stages (16 KiB) + 2 patch buffers (48 KiB) = 144 KiB.
-//   8 waves, 4 (pixel rows) x 2 (64-channel halves); acc / epilogue / fused tail as conv2's.
-//   DMA schedule per wave: prologue P[0] (6 instructions), W[0], W[1] (2 each); iteration s issues W[s + 2]
-//   after its barrier and, at s % 9 == 1, P[c + 1].  The wait before iteration s's barrier retires W[s]
-//   with the exact count of what this wave issued after it.
-constexpr int WP_NT = 512, WP_BN = 128, WP_PB = 48 * 1024, WP_WS = WP_BN * 64 * 2;
-constexpr int WP_LDS = 3 * WP_WS + 2 * WP_PB;  // 144 KiB
-static_assert(256 * (WP_BN + 4) * 4 <= WP_LDS, "epilogue tile must fit");
-
-__device__ __forceinline__ void wait_vm_lgkm0(int n) {  // s_waitcnt vmcnt(n) lgkmcnt(0), n in {0, 2, 6, 8}
-    if (n == 0)
-        __builtin_amdgcn_s_waitcnt(0x0070);
-    else if (n == 2)
-        __builtin_amdgcn_s_waitcnt(0x0072);
-    else if (n == 6)
-        __builtin_amdgcn_s_waitcnt(0x0076);
-    else
-        __builtin_amdgcn_s_waitcnt(0x0078);
-}
-
-template <typename OutT>
-__global__ __launch_bounds__(WP_NT) void conv_wp_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntn) {
-    extern __shared__ __align__(16) unsigned char smw[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
-    const int fr = lane & 15, fq = lane >> 4;
-    int bid = blockIdx.x;
-    {  // XCD-aware order: the channel tiles and spatial neighbours of a tile share an XCD's L2
-        const int ntiles = gridDim.x, nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int tn = bid % ntn, sp = bid / ntn;
-    const int tx = sp % tiles_x, t2 = sp / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
-    const int n0 = tn * WP_BN;
-    unsigned char* wstage = smw;
-    unsigned char* pbuf = smw + 3 * WP_WS;
-    const __bf16* __restrict__ X = (const __bf16*)a.x;
-    const __bf16* __restrict__ Wt = (const __bf16*)a.w;
-    const int nck = a.Cin / 64, nsteps = 9 * nck;
-
-    // weight DMA: instruction i (rows 8i .. 8i + 7) for i = wid, wid + 8; lane l: row 8i + (l >> 3), its
-    // slot l & 7 holds chunk (l & 7) ^ (row & 7) = (l & 7) ^ (l >> 3)
-    const int wrow0 = 8 * wid + (lane >> 3), wg = (lane & 7) ^ (lane >> 3);
-    auto stage_w = [&](int s) {
-        const int c = s / 9, t = s - 9 * c;
-        const int kb = t * a.Cin + 64 * c + 8 * wg;
-        unsigned char* dst = wstage + (s % 3) * WP_WS;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const __bf16* src = Wt + (int64_t)(n0 + wrow0 + 64 * h) * a.Kpad + kb;
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(dst + (wid + 8 * h) * 1024), 16, 0, 0);
-        }
-    };
-    // patch DMA: 48 instructions (41 cover the 324 pixels, the rest fetch the zero page into padding),
-    // 6 per wave
-    const int iy0 = PT * ty - 1, ix0 = PT * tx - 1;
-    auto stage_p = [&](int c) {
-        unsigned char* dst = pbuf + (c & 1) * WP_PB;
-#pragma unroll
-        for (int u = 0; u < 6; ++u) {
-            const int i = wid + 8 * u;
-            const int off = i * 1024 + 16 * lane;
-            const int p = off >> 7, ch = ((off >> 4) & 7) ^ patch_swz<8>(p);
-            const int iy = iy0 + p / PW3, ix = ix0 + p % PW3;
-            const bool ok = p < PW3 * PW3 && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-            const void* src = ok ? (const void*)(X + (((int64_t)n * a.H + iy) * a.W + ix) * a.ldx + 64 * c + 8 * ch)
-                                 : (const void*)g_zero_page;
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(dst + i * 1024), 16, 0, 0);
-        }
-    };
-
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    // B fragments of step s + 1 come from a patch that is already resident (the same chunk's, or P[c + 1],
-    // retired at step 9 c + 4), so they are read at the end of step s, before the next barrier: after a
-    // barrier a wave only waits for its 8 A reads
-    bf16x8 bnx[2][4];
-    auto read_b = [&](int s2) {
-        const int c = s2 / 9, t = s2 - 9 * c, ky = t / 3, kx = t - 3 * ky;
-        const unsigned char* cur = pbuf + (c & 1) * WP_PB;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                bnx[kh][j] = *(const bf16x8*)(cur + patch_off<8>((4 * wm + j + ky) * PW3 + fr + kx, 4 * kh + fq));
-    };
-    stage_p(0);
-    stage_w(0);
-    stage_w(1);  // nsteps >= 9
-    for (int s = 0; s < nsteps; ++s) {
-        // retire W[s]: after it this wave issued W[s + 1] (if any) and a patch at iteration s - 2 or s - 1
-        const bool pa = s >= 2 && (s - 2) % 9 == 1 && (s - 2) / 9 + 1 < nck;
-        const bool pb = s >= 1 && (s - 1) % 9 == 1 && (s - 1) / 9 + 1 < nck;
-        wait_vm_lgkm0((s + 1 < nsteps ? 2 : 0) + (pa || pb ? 6 : 0));
-        __builtin_amdgcn_s_barrier();
-        if (s == 0) read_b(0);
-        if (s + 2 < nsteps) stage_w(s + 2);
-        if (s % 9 == 1 && s / 9 + 1 < nck) stage_p(s / 9 + 1);
-        const unsigned char* ws = wstage + (s % 3) * WP_WS;
-        bf16x8 af[2][4], bfr[2][4];
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                af[kh][i] = *(const bf16x8*)(ws + (wn * 64 + 16 * i + fr) * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[kh][j] = bnx[kh][j];
-        }
-        if (s + 1 < nsteps) read_b(s + 1);
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kh][i], bfr[kh][j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();  // every wave is done with the stages (no DMA in flight): reuse them for the epilogue
-    auto orow = [&](int pl) -> int64_t {
-        const int oy = PT * ty + pl / PT, ox = PT * tx + pl % PT;
-        return (oy < a.Ho && ox < a.Wo) ? ((int64_t)n * a.Ho + oy) * a.Wo + ox : -1;
-    };
-    if (a.w2) {
-        conv2_tail<WP_NT, 256, 4, OutT>(a, acc, smw, n0, wm, wn, wid, fr, fq, orow);
-        return;
-    }
-    conv_epilogue<WP_NT, 256, WP_BN, 4, OutT>(a, acc, smw, n0, wm, wn, tid, fr, fq, orow);
-}
-
 template <int TNS, bool TAIL = false, typename OutT = __bf16>
 hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
@@ -3605,7 +2375,7 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
     const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
     int kper = a.Kpad / KS, ks = 1;
-    if (SPL != 16 && a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
+    if (a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
     const int nb = ntiles * ks;
     if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
         hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL>), dim3(nb), dim3(Cfg::NT), 0, st,
@@ -3626,43 +2396,6 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV3=1 moves the wide layers to conv3 (A/B timing; read per launch so one process can compare).
-// Off by default: measured 4-19 % slower than conv2 on every wide layer of the s-seg forward (the deeper
-// prefetch does not pay while the LDS-DMA path itself delivers only ~43 GB/s per CU, profiles/r01/).
-// VA_CONV3_MIN = fewest 256 x 128 tiles for which conv3 is used (default 256: one per CU)
-bool use_conv3(const va_conv_args& a) {
-    const char* e = getenv("VA_CONV3");
-    if (!e || e[0] != '1' || a.bias4) return false;
-    if (a.Cin % 8 || a.ldx % 8 || ((uintptr_t)a.x & 15) || a.Kpad % BK2 || a.Npad % C3_BN) return false;
-    const char* mn = getenv("VA_CONV3_MIN");
-    const int64_t min_tiles = mn ? atoll(mn) : 256;
-    const int64_t tiles = (int64_t)((a.M + C3_BM - 1) / C3_BM) * ((a.Cout + C3_BN - 1) / C3_BN) * (a.mode == 2 ? 4 : 1);
-    return tiles >= min_tiles;
-}
-
-template <typename OutT, int ABL>
-hipError_t launch_conv3_v(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3_kernel<OutT, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                C3_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntm = (a.M + C3_BM - 1) / C3_BM, ntn = (a.Cout + C3_BN - 1) / C3_BN;
-    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3_kernel<OutT, ABL>), dim3(ntiles), dim3(C3_NT), C3_LDS, st, a, ntn, ntiles);
-    return hipGetLastError();
-}
-
-template <typename OutT>
-hipError_t launch_conv3(const va_conv_args& a, hipStream_t st) {
-    const char* e = getenv("VA_CONV3_ABL");  // diagnosis only (wrong results)
-    if (e && e[0] == '1') return launch_conv3_v<OutT, 1>(a, st);
-    if (e && e[0] == '2') return launch_conv3_v<OutT, 2>(a, st);
-    return launch_conv3_v<OutT, 0>(a, st);
-}
-
 // VA_CONV_PATCH=0 keeps the narrow 3x3 layers on conv_dn (A/B timing; read per launch)
 bool use_patch(const va_conv_args& a) {
     const char* e = getenv("VA_CONV_PATCH");
@@ -3674,7 +2407,7 @@ bool use_patch(const va_conv_args& a) {
            (!a.res || (a.ldr % 8 == 0 && ((uintptr_t)a.res & 15) == 0));
 }
 
-template <int TNS, int CPP, bool TAIL, typename OutT, int NW, int ABL>
+template <int TNS, int CPP, bool TAIL, typename OutT, int NW>
 hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const int K = 9 * CPP * 8;
     const int wstride = K + 16;  // +32 bytes per row: conflict-free A-fragment reads
@@ -3683,7 +2416,7 @@ hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const size_t lds = (size_t)16 * TNS * wstride * 2 + 2 * (size_t)patch_bytes;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, ABL>,
+        if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -3694,58 +2427,17 @@ hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const int per_cu = (int)((160 * 1024) / lds);
     int blocks = 256 * (per_cu < 1 ? 1 : per_cu);
     if (blocks > ntiles) blocks = ntiles;
-    hipLaunchKernelGGL((conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, ABL>), dim3(blocks), dim3(64 * NW), lds, st, a,
+    hipLaunchKernelGGL((conv_patch_kernel<TNS, CPP, TAIL, OutT, NW>), dim3(blocks), dim3(64 * NW), lds, st, a,
                        wstride, tiles_x, tiles_y, ntiles, patch_bytes);
     return hipGetLastError();
 }
 
-// 8 waves per workgroup (4 measured 10-25 % slower: one wave per SIMD); VA_PATCH_ABL (diagnosis only,
-// wrong results): 1 = no MFMA, 2 = no in-loop patch DMA, 3 = no epilogue
-template <int TNS, int CPP, bool TAIL, typename OutT>
-hipError_t launch_conv_patch_v(const va_conv_args& a, hipStream_t st) {
-    const char* e = getenv("VA_PATCH_ABL");
-    const int abl = e ? e[0] - '0' : 0;
-    if (abl == 1) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 1>(a, st);
-    if (abl == 2) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 2>(a, st);
-    if (abl == 3) return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 3>(a, st);
-    return launch_conv_patch_t<TNS, CPP, TAIL, OutT, 8, 0>(a, st);
-}
 
 template <bool TAIL, typename OutT>
 hipError_t launch_conv_patch(const va_conv_args& a, hipStream_t st) {
     if (a.Cin == 32)
-        return a.Cout == 32 ? launch_conv_patch_v<2, 4, TAIL, OutT>(a, st) : launch_conv_patch_v<4, 4, TAIL, OutT>(a, st);
-    return a.Cout == 32 ? launch_conv_patch_v<2, 8, TAIL, OutT>(a, st) : launch_conv_patch_v<4, 8, TAIL, OutT>(a, st);
-}
-
-// VA_CONV_WP=1 moves the wide stride-1 3x3 layers to the wide patch kernel (A/B timing; read per launch).
-// Off by default: at P3 (exact 16 x 16 tiling) it ties conv2, on the ragged P4 / P5 tilings it loses 1.4-2x
-// (profiles/r01c/wp_vs_conv2_layers.log) -- the B bytes it saves were not what bounds these layers.
-bool use_wp(const va_conv_args& a) {
-    const char* e = getenv("VA_CONV_WP");
-    if (!e || e[0] != '1') return false;
-    constexpr int OV = 8;  // conv_epilogue's 16-byte runs (bf16); float output runs of 4 are covered too
-    return a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.mode == 0 && a.Cin % 64 == 0 &&
-           a.K == 9 * a.Cin && a.Cout > 64 && a.Npad % WP_BN == 0 && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 &&
-           a.Ho == a.H && a.Wo == a.W && a.Kpad % 64 == 0 &&
-           (a.w2 ? (a.Cout == 128 && a.c2 <= 16 * TAIL_C2F && a.c2 % 4 == 0 && !a.res)
-                 : (a.Cout % OV == 0 && a.ldy % OV == 0 && (!a.res || a.ldr % 8 == 0)));
-}
-
-template <typename OutT>
-hipError_t launch_conv_wp(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv_wp_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                WP_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int tiles_x = (a.Wo + PT - 1) / PT, tiles_y = (a.Ho + PT - 1) / PT;
-    const int ntn = (a.Cout + WP_BN - 1) / WP_BN;
-    const int blocks = a.N * tiles_x * tiles_y * ntn;
-    hipLaunchKernelGGL((conv_wp_kernel<OutT>), dim3(blocks), dim3(WP_NT), WP_LDS, st, a, tiles_x, tiles_y, ntn);
-    return hipGetLastError();
+        return a.Cout == 32 ? launch_conv_patch_t<2, 4, TAIL, OutT, 8>(a, st) : launch_conv_patch_t<4, 4, TAIL, OutT, 8>(a, st);
+    return a.Cout == 32 ? launch_conv_patch_t<2, 8, TAIL, OutT, 8>(a, st) : launch_conv_patch_t<4, 8, TAIL, OutT, 8>(a, st);
 }
 
 // The Cout > 128 layers with at least VA_CONV4_MIN (default 256) 256 x 256 tiles run on conv4 (P3/P4 1x1 and
@@ -3796,21 +2488,18 @@ bool getenv_dn() {
 int f32_split() {
     const char* e = getenv("VA_F32_SPLIT");
     if (!e) return 6;
-    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : (e[0] == '1' && e[1] == '6') ? 16 : 0;
+    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
 }
 
-// VA_CONV3T: 1 = 256-pixel tiles (8 waves, 3 stages), 2 = 128-pixel tiles (4 waves, 2 stages, 2 per CU), 3 = conv3u
-// (128-pixel tiles, 96-byte rows, three A stages, B three steps ahead), 4 = conv3v (conv3u with whole-line B loads a
-// K-step pair at a time; conv3u where Cin % 32 != 0), 5 / 6 = conv3w (B split + stores beside the MFMAs; 6 with an
-// explicit MFMA / VALU / DS interleave), 7 = conv3x (three workgroups per CU), 0 = off
-int conv3t_form() {
+// VA_CONV3T=0 keeps the wide f32 layers on conv2's three-term form (A/B timing; read per launch)
+bool conv3t_off() {
     const char* e = getenv("VA_CONV3T");
-    return e ? e[0] - '0' : 2;
+    return e && e[0] == '0';
 }
 
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
 bool use_conv3t(const va_conv_args& a) {
-    if (!a.w3 || conv3t_form() == 0) return false;
+    if (!a.w3 || conv3t_off()) return false;
     int kper;  // a layer conv2 would split over K (batch-1 shapes) stays on conv2
     const int t2 = ((a.M + 127) / 128) * ((a.Cout + 127) / 128) * (a.mode == 2 ? 4 : 1);
     if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper) > 1) return false;
@@ -3835,107 +2524,13 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
 }
 
 template <typename OutT>
-hipError_t launch_conv3u(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3u_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3U_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
-    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3u_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3U_LDS, st, a, ntn, ntiles);
-    return hipGetLastError();
-}
-
-template <typename OutT>
-hipError_t launch_conv3v(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3v_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3U_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
-    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3v_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3U_LDS, st, a, ntn, ntiles);
-    return hipGetLastError();
-}
-
-template <typename OutT, int SCHED>
-hipError_t launch_conv3w(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3w_kernel<OutT, SCHED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3U_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
-    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3w_kernel<OutT, SCHED>), dim3(ntiles), dim3(T3U_NT), T3U_LDS, st, a, ntn, ntiles);
-    return hipGetLastError();
-}
-
-template <typename OutT>
-hipError_t launch_conv3x(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3x_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3X_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntm = (a.M + T3U_BM - 1) / T3U_BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
-    const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3x_kernel<OutT>), dim3(ntiles), dim3(T3U_NT), T3X_LDS, st, a, ntn, ntiles);
-    return hipGetLastError();
-}
-
-template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
-    const int f = conv3t_form();
-    if (f == 7) return launch_conv3x<OutT>(a, st);
-    if (f == 5) return launch_conv3w<OutT, 0>(a, st);
-    if (f == 6) return launch_conv3w<OutT, 1>(a, st);
-    if (f == 4 && a.Cin % (2 * T3_KS) == 0) return launch_conv3v<OutT>(a, st);
-    if (f == 3 || f == 4) return launch_conv3u<OutT>(a, st);
-    return f == 1 ? launch_conv3t_v<4, 3, OutT>(a, st) : launch_conv3t_v<2, 2, OutT>(a, st);
-}
-
-// conv3n (three-plane kernel, 64-channel tiles) for the narrow f32 layers: 33..64 output channels, the conv3t
-// conditions otherwise.  Off by default: measured neutral against conv2's three-term form (29.73 vs 29.54 ms per
-// 128-frame forward, profiles/r03/conv3n/); VA_CONV3N=1 selects it (A/B; read per launch)
-bool use_conv3n(const va_conv_args& a) {
-    const char* e = getenv("VA_CONV3N");
-    if (!(e && e[0] == '1') || !a.w3 || a.mode != 0 || a.Cout <= 32 || a.Cout > T3N_BN) return false;
-    int kper;
-    const int t2 = ((a.M + 255) / 256) * ((a.Cout + 63) / 64);
-    if (conv2_ksplit(a, t2, a.Kpad / 32, 256, 64, &kper) > 1) return false;
-    return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.ldx % 4 == 0 &&
-           ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2 && a.Cout % 4 == 0 && a.ldy % 4 == 0;
-}
-
-template <typename OutT>
-hipError_t launch_conv3n(const va_conv_args& a, hipStream_t st) {
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3n_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3N_LDS) != hipSuccess)
-            return hipErrorInvalidValue;
-        attr() = true;
-    }
-    const int ntiles = (a.M + T3N_BM - 1) / T3N_BM;
-    hipLaunchKernelGGL((conv3n_kernel<OutT>), dim3(ntiles), dim3(T3N_NT), T3N_LDS, st, a, ntiles);
-    return hipGetLastError();
+    return launch_conv3t_v<2, 2, OutT>(a, st);
 }
 
 template <int SPL, typename OutT>
 hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
     if (SPL == 6 && use_conv3t(a)) return launch_conv3t<OutT>(a, st);
-    if (SPL == 6 && use_conv3n(a)) return launch_conv3n<OutT>(a, st);
     if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
     if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float, SPL>(a, st);
     if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float, SPL>(a, st);
@@ -3958,8 +2553,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
                 a.c2 % 4 == 0 &&
                 a.Kpad % BK2 == 0 && a.ldy % 4 == 0) {
-                if (a.mode == 0 && use_wp(a)) return launch_conv_wp<OutT>(a, st);
-                return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
+                return launch_conv2<2, 2, 4, OutT>(a, st);
             }
         }
         return hipErrorInvalidValue;
@@ -3990,31 +2584,28 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         constexpr int OV = 16 / sizeof(OutT);
         if (a.mode == 2) {  // sub-pixel classes: the 128-wide LDS-staged tile only
             if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && a.Cout > 64)
-                return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
+                return launch_conv2<2, 2, 4, OutT>(a, st);
             return hipErrorInvalidValue;
         }
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
             if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
             if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
-            if (use_wp(a)) return launch_conv_wp<OutT>(a, st);
             if (use_conv4(a)) return launch_conv4<OutT>(a, st);
-            return use_conv3(a) ? launch_conv3<OutT>(a, st) : launch_conv2<2, 2, 4, OutT>(a, st);
+            return launch_conv2<2, 2, 4, OutT>(a, st);
         }
     }
     if constexpr (sizeof(T) == 4) {
-        // exact-f32 parity mode: conv2 with f32 MFMA (K-step 32); VA_CONV_F32_OLD=1 keeps the register-staged
-        // conv_kernel (A/B timing)
-        if (a.Kpad % 32 == 0 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && (a.mode != 1 || (a.Cout / 4) % 4 == 0) &&
-            getenv("VA_CONV_F32_OLD") == nullptr) {
+        // exact-f32 parity mode: the three-term forms (conv3t / conv2 SPL 6); VA_F32_SPLIT=0: conv2 on the f32 MFMA
+        if (a.Kpad % 32 == 0 && a.Cout % 4 == 0 && a.ldy % 4 == 0 && (a.mode != 1 || (a.Cout / 4) % 4 == 0)) {
             switch (f32_split()) {
-                case 16: return launch_conv2_f32<16, OutT>(a, st);
                 case 6: return launch_conv2_f32<6, OutT>(a, st);
                 case 9: return launch_conv2_f32<9, OutT>(a, st);
                 default: return launch_conv2_f32<0, OutT>(a, st);
             }
         }
     }
-    // tile choice: small Cout -> tall pixel tiles
+    // generic fallback for shapes outside the fast kernels' constraints (register-staged conv_kernel; small Cout ->
+    // tall pixel tiles)
     if (a.Cout <= 64) return launch_conv<T, 4, 1, OutT>(a, st);
     return launch_conv<T, 2, 2, OutT>(a, st);
 }

@@ -77,24 +77,28 @@ class FramePipeline:
 
     def load(self, frames: torch.Tensor, stream=None) -> None:
         """Frames (uint8 BGR [B, H, W, 3], on the device or the host) into the network's input buffer, letterboxed
-        if needed, on the current stream; host frames go through a pinned staging buffer (_pinned)."""
+        if needed, on ``stream`` (default: the current stream) -- the H2D copy, the letterbox and the pinned
+        buffer's release event all on that one stream; host frames go through a pinned staging buffer (_pinned)."""
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
         staged = frames.device.type == "cpu" and not frames.is_pinned()
         if staged:
             frames = self._pinned(frames.contiguous())
-        if self.lb is None:
-            self.plan["frames"].copy_(frames, non_blocking=True)
-        else:
-            if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
-                raise _lib.VaError(f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
-            frames = frames.to(self.device, non_blocking=True).contiguous()
-            Hn, Wn, top, left, newh, neww = self.lb
-            with torch.cuda.device(self.device):
-                _lib.check(self.lib.va_letterbox(_lib.stream_ptr(stream, self.device), frames.data_ptr(), self.B,
-                                                 self.H, self.W, self.plan["frames"].data_ptr(), Hn, Wn, top, left,
-                                                 newh, neww), "va_letterbox")
-        if staged:
-            self._pin_ev = torch.cuda.Event()
-            self._pin_ev.record(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            if self.lb is None:
+                self.plan["frames"].copy_(frames, non_blocking=True)
+            else:
+                if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
+                    raise _lib.VaError(
+                        f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
+                frames = frames.to(self.device, non_blocking=True).contiguous()
+                Hn, Wn, top, left, newh, neww = self.lb
+                with torch.cuda.device(self.device):
+                    _lib.check(self.lib.va_letterbox(_lib.stream_ptr(st, self.device), frames.data_ptr(), self.B,
+                                                     self.H, self.W, self.plan["frames"].data_ptr(), Hn, Wn, top,
+                                                     left, newh, neww), "va_letterbox")
+            if staged:
+                self._pin_ev = torch.cuda.Event()
+                self._pin_ev.record(st)
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:
@@ -200,6 +204,10 @@ class SegPostGraph:
     def __init__(self, pipe: FramePipeline, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
                  plant_mode: int = PLANT_NEVER, warmup: int = 2):
         self.pipe = pipe
+        if frames is not None and frames.device.type != "cuda":
+            # a host frame would be staged by a host-side copy into the pinned buffer, which the graph does not
+            # capture: every replay would read whatever that buffer last held
+            raise ValueError("SegPostGraph captures device frames only (copy host frames to the device first)")
         dev = pipe.device
         self.stream = torch.cuda.Stream(device=dev)
         s = self.stream

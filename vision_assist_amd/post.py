@@ -62,6 +62,22 @@ def scale_coords_params(H: int, W: int, H0: int, W0: int) -> tuple[float, float,
     return gain, (W - W0 * gain) / 2, (H - H0 * gain) / 2
 
 
+def scale_boxes(net_hw: tuple[int, int], boxes: torch.Tensor, frame_hw: tuple[int, int]) -> torch.Tensor:
+    """Results.boxes in frame coordinates: Ultralytics' ops.scale_boxes(img1_shape=net, xyxy, img0_shape=frame)
+    (reference's vendored ops.py:139-170 + clip_boxes :366-385) on a float32 host tensor, in place: gain in double,
+    integer pads round(. - 0.1), float32 arithmetic, clamped to the frame.  Bit-equal to the reference's function
+    on its own outputs (tests/test_ops_pinned_cpu.py, tests/golden/ops_goldens.npz)."""
+    gain = min(net_hw[0] / frame_hw[0], net_hw[1] / frame_hw[1])
+    pad_x = round((net_hw[1] - frame_hw[1] * gain) / 2 - 0.1)
+    pad_y = round((net_hw[0] - frame_hw[0] * gain) / 2 - 0.1)
+    for c, p in enumerate((pad_x, pad_y, pad_x, pad_y)):
+        boxes[..., c] -= p
+    boxes[..., :4] /= gain
+    for c, hi in enumerate((frame_hw[1], frame_hw[0], frame_hw[1], frame_hw[0])):
+        boxes[..., c] = boxes[..., c].clamp(0, hi)
+    return boxes
+
+
 def contour_scratch(H: int, W: int, slots: int = CONTOUR_SLOTS, cap: int = CONTOUR_CAP, device=None) -> torch.Tensor:
     lib = _lib.load()
     sb, io, po = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

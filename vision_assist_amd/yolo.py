@@ -22,6 +22,7 @@ import warnings
 import numpy as np
 import torch
 
+from .post import scale_boxes
 from .seg_arch import Arch, fold, synthetic_state_dict
 
 
@@ -38,7 +39,7 @@ class Masks:
 class Results:
     def __init__(self, orig_shape, boxes: np.ndarray, masks: Masks | None):
         self.orig_shape = orig_shape
-        self.boxes = boxes      # float [k, 6]: x1, y1, x2, y2, conf, cls (kept detections, score order)
+        self.boxes = boxes      # float [k, 6]: x1, y1, x2, y2 (frame pixels), conf, cls (kept, score order)
         self.masks = masks      # None when no mask (FrameProcessor.py:68-69)
 
 
@@ -103,6 +104,7 @@ class YOLO:
             o = pipe.plan["out"]
             pipe.post.run(o.levels, o.proto, select=True)
             det, _ = pipe.post.det_tensor(0)
+            scale_boxes((pipe.Hn, pipe.Wn), det[:, :4], (H, W))  # Results.boxes in frame pixels (in place)
             chosen = int(pipe.post.chosen[0])
             masks = None
             if chosen >= 0:
