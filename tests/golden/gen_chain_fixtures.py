@@ -6,7 +6,7 @@ its outputs from here instead of recomputing them on the GPU box.  Inputs are fu
 CPU generator frames, seeded synthetic weights), so the fixture is a function of this script.
 
 Sets:
-  chain/<regime>: frames frame_batch(21, 16), one PathFinder state across the 16 frames, regimes
+  chain/<regime>: frames frame_batch(21, 32), one PathFinder state across the 32 frames, regimes
                   sparse / dense / dense_box (s-seg 640);
   c4/<regime>:    frames frame_batch(7000 + i, 1), i < 8, dealt round-robin to 2 ranks; one PathFinder state
                   per shard, frames in shard order (SURVEY.md §8e per-shard replay); regimes sparse / dense_box.
@@ -31,7 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "chain_oracle.json.gz")
-CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 16, 8, 2, 4
+CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 32, 8, 2, 4
 
 
 def _enc(rec: dict) -> dict:

@@ -567,20 +567,22 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 // epilogue stage 1 of the 32x32-fragment form (conv2_kernel SPL 16): acc[ib][jb] is the 32 x 32 block of channels
 // wn 16 TNS + 32 ib .. and pixels wm 64 + 32 jb ..; lane l holds pixel l % 32, items q: channel 8 (q / 4) + 4 (l / 32)
 // + q % 4 (v_mfma_f32_32x32x16 D layout)
-template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn>
+// pcol(c): tile row (pixel) of accumulator column c (0..31) of a 32 x 32 block (the B operand's row order);
+// mrow(pl): GEMM row m of tile pixel pl (bias4's border table), or -1 when masked
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename MFn, typename PFn>
 __device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&acc)[TNS / 2][2], unsigned char* smem,
-                                                int n0, int wm, int wn, int tid, int lane, RowFn orow, int m0 = 0,
-                                                int cls = 0) {
+                                                int n0, int wm, int wn, int tid, int lane, RowFn orow, MFn mrow,
+                                                PFn pcol, int cls = 0) {
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
     const int r = lane & 31, g = lane >> 5;
     float4 bvs[2][TNS / 2][4];  // loaded up front (see conv_epilogue)
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
-        const int pl = wm * 64 + 32 * jb + r;
+        const int pl = wm * 64 + 32 * jb + pcol(r);
         int brow = n0;
         if (a.bias4) {
-            const int m = m0 + pl;
+            const int m = max(mrow(pl), 0);
             const int wo = m % a.Wo, ho = (m / a.Wo) % a.Ho;
             const int rf = (cls >> 1) ? ho == a.Ho - 1 : ho == 0, cf = (cls & 1) ? wo == a.Wo - 1 : wo == 0;
             brow = ((cls * 2 + rf) * 2 + cf) * a.Npad + n0;
@@ -593,7 +595,7 @@ __device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&
     }
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) {
-        const int pl = wm * 64 + 32 * jb + r;
+        const int pl = wm * 64 + 32 * jb + pcol(r);
 #pragma unroll
         for (int ib = 0; ib < TNS / 2; ++ib) {
 #pragma unroll
@@ -1199,7 +1201,9 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         const int m = m0 + pl;
         return m < a.M ? conv_out_row(a, m, cls) : -1;
     };
-    conv_epilogue32<NT, BM, BN, TNS, OutT, decltype(orow)>(a, acc, smt, n0, wm, wn, tid, lane, orow, m0, cls);
+    auto mrow = [&](int pl) { return m0 + pl; };
+    auto pcol = [](int c) { return c; };
+    conv_epilogue32<NT, BM, BN, TNS, OutT>(a, acc, smt, n0, wm, wn, tid, lane, orow, mrow, pcol, cls);
 }
 
 // ----------------------------------------------------------------------------------------- conv v4 (bf16, Cout >= 256)
