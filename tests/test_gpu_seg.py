@@ -24,7 +24,7 @@ def _net(dtype, scale="s", nc=80, seed=0, cls_bias=None):
 
 
 def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=False, slice_in=0, act=True, ws=None,
-                     B=2):
+                     B=2, w3=False):
     from vision_assist_amd import seg as S
     from vision_assist_amd.seg_arch import Arch
     g = torch.Generator().manual_seed(cin * 1000 + cout + k)
@@ -66,6 +66,8 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
                       y=y.data_ptr() + 8 * y.element_size(), ldy=ld_out,
                       res=res.data_ptr() if res is not None else None, ldr=cout, act=1 if act else 0,
                       mode=1 if deconv else 0, M=B * Ho * Wo, dtype=net.va_dtype, out_f32=0)
+    if w3:  # f32: the pre-split weight planes -> the three-plane kernels (conv3t / conv3h)
+        args.w3 = p.w3.data_ptr()
     if ws is not None:  # split-K workspace (va_conv_args.ws): (slabs uint8, counters int32)
         args.ws, args.ws_bytes, args.wcnt, args.ncnt = ws[0].data_ptr(), ws[0].numel(), ws[1].data_ptr(), ws[1].numel()
     _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), __import__("ctypes").byref(args)), "va_seg_conv")
@@ -348,6 +350,45 @@ def test_conv3t_matches_conv2_f32(B, monkeypatch):
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         d = (g - r).abs().max().item()
         assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3t vs conv2 max diff {d}"
+    if B == 2:
+        torch.set_num_threads(8)
+        want = _ref_heads(arch, fw, frames)
+        for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+            assert (g - r).abs().max().item() <= 1e-3, name
+
+
+@pytest.mark.parametrize("cin,cout,H,W,B,residual", [
+    (128, 224, 80, 80, 2, False),  # TW 16 tiles cover the map exactly; Cout 224: a ragged channel tile
+    (128, 256, 23, 21, 3, True),   # TW 8, ragged columns, tiles straddling images of the stacked map, residual
+    (256, 128, 20, 20, 3, False),  # TW 4 (the P5 map), 32-row tiles spanning two images
+    (64, 96, 40, 40, 2, False),    # four 16-channel chunks, TW 8 with 16-row tiles across the image seam
+])
+def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual):
+    """conv3h (halo-staged B: the tile's input halo loaded and split once per 16-channel chunk, every 3x3 tap read
+    from it; zero rows where a tap leaves the pixel's image) on single f32 ops: within f32 rounding of torch fp32
+    and of conv3t (VA_CONV3H=0: per-tap staging, the same six term products summed in another order)."""
+    got, ref = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
+    scale = max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+    monkeypatch.setenv("VA_CONV3H", "0")
+    got_t, _ = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
+    assert (got - got_t).abs().max().item() <= 2e-5 * scale
+
+
+@pytest.mark.parametrize("B", [2, 3])
+def test_conv3h_matches_conv3t_forward(B, monkeypatch):
+    """The f32 forward with conv3h on its layers (every stride-1 3x3 with Cout > 64: P3-P5 C2f bottlenecks, the
+    head's fused first 3x3 (Cout 224) and cls 3x3s, proto.cv1; the proto sub-pixel fold's 2x2 taps in mode 2) against
+    the same forward on conv3t (VA_CONV3H=0): f32-rounding close, and within the f32 bar of torch."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(B, seed=13)
+    monkeypatch.setenv("VA_CONV3H", "0")
+    ref = _gpu_heads(net, frames)
+    monkeypatch.delenv("VA_CONV3H")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3h vs conv3t max diff {d}"
     if B == 2:
         torch.set_num_threads(8)
         want = _ref_heads(arch, fw, frames)

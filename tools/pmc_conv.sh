@@ -1,0 +1,22 @@
+#!/bin/bash
+# Per-layer SQ / LDS / TA-TD / TCC counters of the f32 s-seg forward (B = 64; tools/pmc_forward.py), one rocprofv3
+# pass per counter set, each under its own time limit; then tools/pmc_summary.py maps them to layer names.
+#   bash tools/pmc_conv.sh OUTDIR [extra env, e.g. VA_CONV3H=0]
+export TMPDIR=/tmp
+O=gpurun_out/$1; shift
+mkdir -p $O
+for kv in "$@"; do export "$kv"; done
+run() {  # name counters...
+  n=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $O/$n -o run -- \
+      python3 tools/pmc_forward.py --dtype f32 --batch 64 --out $O/plan > $O/$n.log 2>&1
+  rc=$?; echo "$n rc=$rc"; return $rc
+}
+run sq SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE && \
+run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD TA_TA_BUSY_sum TD_TD_BUSY_sum \
+    TD_TC_STALL_sum GRBM_GUI_ACTIVE && \
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_BUSY_sum GRBM_GUI_ACTIVE && \
+python3 tools/pmc_summary.py $O/plan.json $O/summary.json $O/sq/*counter_collection.csv $O/lds/*counter_collection.csv \
+    $O/tcc/*counter_collection.csv > $O/summary.log 2>&1
+echo "summary rc=$?"

@@ -1206,6 +1206,234 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     conv_epilogue32<NT, BM, BN, TNS, OutT>(a, acc, smt, n0, wm, wn, tid, lane, orow, mrow, pcol, cls);
 }
 
+// ------------------------------------------------------------------------ conv3h (f32 mode, halo-staged B)
+// conv3t's three-term arithmetic for the stride-1 convs with several taps (3x3 / pad 1, and the proto's sub-pixel
+// classes: 2x2 taps, mode 2), with the activation operand staged ONCE per 16-channel chunk instead of once per tap.
+// conv3t loads B per K-step, i.e. per (tap, chunk): a 3x3 layer moves every input pixel through L2 -> L1 nine
+// times and splits it nine times -- the vector-memory return path and the L2 were the wall (TD busy 0.81, TCC busy
+// 0.94 on the four largest layers).  conv3h tiles the output as TH x TW pixels of the stacked
+// [N * Ho] x Wo map (TW = 4 .. 32 chosen per layer so the tiles cover Wo exactly; TH x TW = 128) and, per chunk of
+// 16 input channels, loads the tile's halo -- (TH + kh - 1) x (TW + kw - 1) <= 204 pixels, 1.4-1.6 x the tile --
+// once, splits it once into three bf16 planes in LDS, and forms all kh x kw taps from it: per chunk the K-steps
+// are the taps, each one A stage (the pre-split weights of (tap, chunk), LDS-DMA two steps ahead, three stages)
+// and the B fragments read from the halo at the tap's offset.  A tile that straddles two images of the stacked
+// map reads zeros (a zero row) where a tap leaves the pixel's own image, so no tile is ragged.  The next chunk's
+// halo is loaded into registers at the chunk's first step (after that step's A DMA: the issue order the counted
+// waits assume, pinned by sched_barrier), split and stored into the other halo buffer at its second step (that
+// buffer was last read in the previous chunk), and is read from the chunk after.  LDS rows are 96 bytes (16
+// channels x 3 planes); chunk c of a weight row r sits in slot c ^ ((r >> 3) & 1), of halo pixel (hy, hx) in
+// slot c ^ ((hy ^ (hx >> 3 if TW >= 16)) & 1), and B-block row r holds pixel t3h_perm(r): each ds_read_b128 lane
+// group then reads 16 consecutive pixels of one tile row -- conflict-free for every TW and tap
+// (tools/lds_conflicts.py).  128 pixels x 128 channels, 4 waves, two workgroups per CU.
+constexpr int T3H_ROW = 96, T3H_BM = 128, T3H_NT = 256, T3H_HMAX = 204, T3H_NSA = 3;
+constexpr int T3H_ASTAGE = T3_BN * T3H_ROW;                   // 12 KiB
+constexpr int T3H_HALO = T3H_HMAX * T3H_ROW;                  // 19,584 B
+constexpr int T3H_ZROW = T3H_NSA * T3H_ASTAGE + 2 * T3H_HALO;  // the zero row
+constexpr int T3H_LDS0 = T3H_ZROW + T3H_ROW;
+constexpr int T3H_EPI = T3H_BM * (T3_BN + 4) * 4;
+constexpr int T3H_LDS = T3H_LDS0 > T3H_EPI ? T3H_LDS0 : T3H_EPI;
+constexpr int T3H_NA = T3H_ASTAGE / 1024 / (T3H_NT / 64);  // A-DMA pieces per wave per K-step (3)
+constexpr int T3H_NU = 2;                                   // halo units (pixel, 8 channels) per thread
+static_assert(T3H_NA * 1024 * (T3H_NT / 64) == T3H_ASTAGE, "A stage in 1 KiB pieces");
+static_assert(2 * T3H_LDS <= 160 * 1024, "two workgroups per CU");
+static_assert(T3H_NU * T3H_NT >= 2 * T3H_HMAX, "halo units");
+
+// B-block row r (0..31) -> pixel of the block: ds_read_b128's lane groups {0-3, 12-15, 20-27} and {4-11, 16-19,
+// 28-31} (MI355X_MICROARCH.md §LDS) take pixels 0..15 and 16..31 in lane order
+__device__ __forceinline__ int t3h_perm(int r) {
+    return r < 4 ? r : r < 12 ? r + 12 : r < 16 ? r - 8 : r < 20 ? r + 8 : r < 28 ? r - 12 : r;
+}
+
+// f(integral_constant<0>) .. f(integral_constant<N - 1>), in order
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void t3h_unroll(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        t3h_unroll<N, I + 1>(f);
+    }
+}
+
+template <int KH, int KW, typename OutT>
+__global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn, int ntiles, int lgw, int tiles_x) {
+    extern __shared__ __align__(16) unsigned char smh[];
+    constexpr int BM = T3H_BM, BN = T3_BN, NT = T3H_NT, WN = 2, TNS = 4, NA = T3H_NA, T = KH * KW;
+    static_assert(T >= 2, "the halo is stored at a chunk's second step");
+    int bid = blockIdx.x;
+    {
+        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int cls = a.mode == 2 ? (bid & 3) : 0;
+    if (a.mode == 2) bid >>= 2;
+    const int tm = bid / ntn, tn = bid % ntn;
+    const int TW = 1 << lgw, TH = BM >> lgw, HW = TW + KW - 1, HHW = (TH + KH - 1) * HW;
+    const int ty = tm / tiles_x, tx = tm - ty * tiles_x;
+    const int r0 = ty * TH, c0 = tx * TW;  // stacked output row / column of the tile's pixel 0
+    const int NR = a.N * a.Ho;
+    const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
+    const int xm = lgw >= 4 ? 1 : 0;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / WN, wn = wid % WN;
+    const int n0 = tn * BN;
+    const int nch = a.Cin / T3_KS;
+    const float* __restrict__ X = (const float*)a.x;
+    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    auto stA = [&](int s) { return smh + s * T3H_ASTAGE; };
+    auto halo = [&](int b) { return smh + T3H_NSA * T3H_ASTAGE + b * T3H_HALO; };
+
+    // ---- A DMA: piece P = wid + 4 j of a stage (1 KiB, linear in LDS); lane l writes bytes 16 l of it: row o / 96,
+    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run
+    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    constexpr int OOR = 0x7ff00000;
+    int aoff[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
+        const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
+        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+    }
+    auto dmaA = [&](int kl, int s, bool live) {  // K-step kl = tap * nch + chunk into stage s; !live: zeros
+        unsigned char* base = stA(s);
+        const int soff = live ? kl * 96 : OOR;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
+    };
+
+    // ---- halo units: u = tid + 256 j -> halo pixel u >> 1 (row hy, column hx), channels 8 (u & 1) .. of a chunk
+    const void* zpage = (const void*)g_zero_page;
+    int64_t hsrc[T3H_NU];  // element offset of the unit's channels in chunk 0, or -1 (outside the map: zeros)
+    int hdst[T3H_NU];      // LDS byte offset of the unit's pixel row in a halo buffer, or -1 (no such pixel)
+    int hbit[T3H_NU];
+#pragma unroll
+    for (int j = 0; j < T3H_NU; ++j) {
+        const int u = tid + NT * j, hp = u >> 1, g = u & 1;
+        const int hy = hp / HW, hx = hp - hy * HW;
+        const int R = r0 - pad_y + hy, Xc = c0 - pad_x + hx;
+        const bool in = hp < HHW;
+        hsrc[j] = in && (unsigned)R < (unsigned)NR && (unsigned)Xc < (unsigned)a.W
+                      ? ((int64_t)R * a.W + Xc) * a.ldx + 8 * g : -1;
+        hdst[j] = in ? hp * T3H_ROW : -1;
+        hbit[j] = (hy ^ ((hx >> 3) & xm)) & 1;
+    }
+    u32x4 rh[T3H_NU][2];
+    auto loadH = [&](int c, bool live) {  // chunk c of every unit into registers (zero page: outside / past the end)
+#pragma unroll
+        for (int j = 0; j < T3H_NU; ++j) {
+            const float* p = live && hsrc[j] >= 0 ? X + hsrc[j] + T3_KS * c : (const float*)zpage;
+            rh[j][0] = *(const u32x4*)p;
+            rh[j][1] = *(const u32x4*)(p + 4);
+        }
+    };
+    auto storeH = [&](int b) {  // split once, three plane chunks per unit into halo buffer b
+        unsigned char* hb = halo(b);
+#pragma unroll
+        for (int j = 0; j < T3H_NU; ++j) {
+            bf16x8 t[3];
+            split3_bf16(rh[j][0], rh[j][1], t);
+            if (hdst[j] >= 0) {
+                const int g = (tid + NT * j) & 1;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *(bf16x8*)(hb + hdst[j] + 16 * ((3 * g + p) ^ hbit[j])) = t[p];
+            }
+        }
+    };
+
+    // ---- B fragment rows of this lane: block jb's row r32 is tile pixel (py, px); vy bit ky: the tap row stays in
+    // the pixel's own image
+    const int r32 = lane & 31, g32 = lane >> 5;
+    int bpy[2], bpx[2], vy[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+        const int p = wm * 64 + 32 * jb + t3h_perm(r32);
+        bpy[jb] = p >> lgw;
+        bpx[jb] = p & (TW - 1);
+        const int h = (r0 + bpy[jb]) % a.Ho;
+        int v = 0;
+#pragma unroll
+        for (int ky = 0; ky < KH; ++ky) v |= ((unsigned)(h - pad_y + ky) < (unsigned)a.Ho) << ky;
+        vy[jb] = v;
+    }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
+    const int nsteps = nch * T;
+    // prologue: A of steps 0, 1 (tap 0 / 1 of chunk 0), chunk 0's halo staged; the zero row
+    dmaA(0, 0, true);
+    dmaA(nch, 1, nsteps > 1);
+    __builtin_amdgcn_sched_barrier(0);
+    loadH(0, true);
+    __builtin_amdgcn_sched_barrier(0);
+    t3_waitvm<0>();
+    storeH(0);
+    if (tid < T3H_ROW / 16) *(u32x4*)(smh + T3H_ZROW + 16 * tid) = (u32x4){0u, 0u, 0u, 0u};
+    __syncthreads();
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    // one K-step (chunk c, tap t): A(k + 2) DMA'd first, at t == 0 the next chunk's halo loads, the fragment reads,
+    // 24 MFMAs, at t == 1 the next chunk's halo stored; then the counted wait for A(k + 1) and a raw barrier
+    auto step = [&](const int c, auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        constexpr int ky = t / KW, kx = t % KW;
+        const int k = c * T + t;
+        {
+            constexpr int t2 = (t + 2) % T, dc = (t + 2) / T;
+            const int c2 = c + dc;
+            dmaA(t2 * nch + c2, (k + 2) % T3H_NSA, c2 < nch);  // stage last read at step k - 1
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (t == 0) {
+            loadH(c + 1, c + 1 < nch);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        bf16x8 ap[2][3], bp[2][3];
+        const unsigned char* as_ = stA(k % T3H_NSA);
+        const unsigned char* hs_ = halo(c & 1);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+            const int row = wn * 64 + 32 * ib + r32, sw = (row >> 3) & 1;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
+        }
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+            const int hy = bpy[jb] + ky, hx = bpx[jb] + kx;
+            const unsigned char* rp = (vy[jb] >> ky) & 1 ? hs_ + (hy * HW + hx) * T3H_ROW : smh + T3H_ZROW;
+            const int sw = (hy ^ ((hx >> 3) & xm)) & 1;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(rp + 16 * ((3 * g32 + p) ^ sw));
+        }
+#pragma unroll
+        for (int tt = 0; tt < 6; ++tt)
+#pragma unroll
+            for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+                for (int jb = 0; jb < 2; ++jb)
+                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[tt]], bp[jb][TB[tt]], acc[ib][jb],
+                                                                          0, 0, 0);
+        if constexpr (t == 1) storeH((c + 1) & 1);  // the buffer chunk c - 1 used; past the last chunk: unread zeros
+        // A(k + 1) landed: younger than its DMAs are this step's NA DMAs and the halo loads of step t == 0 (issued in
+        // this step at t == 0, in the previous one at t == 1)
+        t3_waitvm<(t == 0 || t == 1) ? NA + 2 * T3H_NU : NA>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    for (int c = 0; c < nch; ++c) t3h_unroll<T>([&](auto Tc) { step(c, Tc); });
+    t3_waitvm<0>();  // the zero-page DMAs past the last step land before the epilogue reuses the LDS
+    __syncthreads();
+
+    auto mrow = [&](int pl) -> int {
+        const int R = r0 + (pl >> lgw), Xc = c0 + (pl & (TW - 1));
+        return R < NR && Xc < a.Wo ? R * a.Wo + Xc : -1;
+    };
+    auto orow = [&](int pl) -> int64_t {
+        const int m = mrow(pl);
+        return m >= 0 ? conv_out_row(a, m, cls) : -1;
+    };
+    auto pcol = [](int c) { return t3h_perm(c); };
+    conv_epilogue32<NT, BM, BN, TNS, OutT>(a, acc, smh, n0, wm, wn, tid, lane, orow, mrow, pcol, cls);
+}
+
 // ----------------------------------------------------------------------------------------- conv v4 (bf16, Cout >= 256)
 // 256 output channels x 256 pixels per workgroup with the phase structure of cdna_hip_programming.md §5
 // "The 256² 8-phase template": 8 waves (2 channel halves x 4 pixel quarters; each 128 channels x 64
@@ -2527,8 +2755,53 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing; read per launch)
+bool conv3h_off() {
+    const char* e = getenv("VA_CONV3H");
+    return e && e[0] == '0';
+}
+
+// conv3h's tile width for an output map Wo wide: the TW = 4 .. 32 that covers Wo with the fewest padded columns,
+// then the smallest halo, then the widest (longest contiguous halo rows); -1 when no width fits the halo buffer
+int conv3h_lgw(const va_conv_args& a) {
+    int best = -1, bw = 0, bh = 0;
+    for (int lg = 5; lg >= 2; --lg) {
+        const int tw = 1 << lg, th = T3H_BM / tw, hh = (th + a.kh - 1) * (tw + a.kw - 1);
+        if (hh > T3H_HMAX) continue;
+        const int waste = (a.Wo + tw - 1) / tw * tw - a.Wo;
+        if (best < 0 || waste < bw || (waste == bw && hh < bh)) best = lg, bw = waste, bh = hh;
+    }
+    return best;
+}
+
+bool use_conv3h(const va_conv_args& a) {
+    if (conv3h_off() || a.stride != 1 || a.H != a.Ho || a.W != a.Wo) return false;
+    const bool taps = a.mode == 0 ? (a.kh == 3 && a.kw == 3 && a.pad == 1) : (a.mode == 2 && a.kh == 2 && a.kw == 2);
+    return taps && conv3h_lgw(a) >= 0 && (int64_t)a.N * a.Ho < (1 << 24);
+}
+
+template <int KH, int KW, typename OutT>
+hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                T3H_LDS) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    const int lgw = conv3h_lgw(a);
+    const int tw = 1 << lgw, th = T3H_BM / tw;
+    const int tiles_x = (a.Wo + tw - 1) / tw, tiles_y = (a.N * a.Ho + th - 1) / th;
+    const int ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntiles = tiles_x * tiles_y * ntn * (a.mode == 2 ? 4 : 1);
+    hipLaunchKernelGGL((conv3h_kernel<KH, KW, OutT>), dim3(ntiles), dim3(T3H_NT), T3H_LDS, st, a, ntn, ntiles, lgw,
+                       tiles_x);
+    return hipGetLastError();
+}
+
 template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
+    if (use_conv3h(a)) return a.mode == 2 ? launch_conv3h_v<2, 2, OutT>(a, st) : launch_conv3h_v<3, 3, OutT>(a, st);
     return launch_conv3t_v<2, 2, OutT>(a, st);
 }
 
