@@ -362,6 +362,9 @@ def test_conv3t_matches_conv2_f32(B, monkeypatch):
     (128, 256, 23, 21, 3, True),   # TW 8, ragged columns, tiles straddling images of the stacked map, residual
     (256, 128, 20, 20, 3, False),  # TW 4 (the P5 map), 32-row tiles spanning two images
     (64, 96, 40, 40, 2, False),    # four 16-channel chunks, TW 8 with 16-row tiles across the image seam
+    (64, 64, 80, 80, 2, False),    # the narrow form (64-channel tiles): a C2f bottleneck 3x3 at P3
+    (64, 48, 23, 21, 3, True),     # narrow, ragged channels / columns, image seams, residual
+    (32, 64, 40, 40, 2, False),    # narrow, two chunks
 ])
 def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual):
     """conv3h (halo-staged B: the tile's input halo loaded and split once per 16-channel chunk, every 3x3 tap read

@@ -1226,17 +1226,25 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
 // group then reads 16 consecutive pixels of one tile row -- conflict-free for every TW and tap
 // (tools/lds_conflicts.py).  128 pixels x 128 channels, 4 waves, two workgroups per CU.
 constexpr int T3H_ROW = 96, T3H_BM = 128, T3H_NT = 256, T3H_HMAX = 204, T3H_NSA = 3;
-constexpr int T3H_ASTAGE = T3_BN * T3H_ROW;                   // 12 KiB
-constexpr int T3H_HALO = T3H_HMAX * T3H_ROW;                  // 19,584 B
-constexpr int T3H_ZROW = T3H_NSA * T3H_ASTAGE + 2 * T3H_HALO;  // the zero row
-constexpr int T3H_LDS0 = T3H_ZROW + T3H_ROW;
-constexpr int T3H_EPI = T3H_BM * (T3_BN + 4) * 4;
-constexpr int T3H_LDS = T3H_LDS0 > T3H_EPI ? T3H_LDS0 : T3H_EPI;
-constexpr int T3H_NA = T3H_ASTAGE / 1024 / (T3H_NT / 64);  // A-DMA pieces per wave per K-step (3)
-constexpr int T3H_NU = 2;                                   // halo units (pixel, 8 channels) per thread
-static_assert(T3H_NA * 1024 * (T3H_NT / 64) == T3H_ASTAGE, "A stage in 1 KiB pieces");
-static_assert(2 * T3H_LDS <= 160 * 1024, "two workgroups per CU");
+constexpr int T3H_HALO = T3H_HMAX * T3H_ROW;  // 19,584 B
+constexpr int T3H_NU = 2;                     // halo units (pixel, 8 channels) per thread
 static_assert(T3H_NU * T3H_NT >= 2 * T3H_HMAX, "halo units");
+// per channel-tile width: TNS = 4 -> 128 output channels (waves 2 x 2, each 64 pixels x 64 channels), TNS = 2 -> 64
+// (the narrow layers: waves 2 x 2, each 64 pixels x 32 channels)
+template <int TNS>
+struct T3HCfg {
+    static constexpr int BN = 32 * TNS;
+    static constexpr int ASTAGE = BN * T3H_ROW;                   // 12 / 6 KiB
+    static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6)
+    static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2)
+    static constexpr int ZROW = T3H_NSA * ASTAGE + 2 * T3H_HALO;  // the zero row
+    static constexpr int SINK = ZROW + 128;                       // 1 KiB the idle pieces' zero DMAs land in
+    static constexpr int LDS0 = NP % 4 ? SINK + 1024 : ZROW + T3H_ROW;
+    static constexpr int EPI = T3H_BM * (BN + 4) * 4;
+    static constexpr int LDS = LDS0 > EPI ? LDS0 : EPI;
+    static_assert(NP * 1024 == ASTAGE && 2 * LDS <= 160 * 1024, "A stage in 1 KiB pieces; two workgroups per CU");
+};
+
 
 // B-block row r (0..31) -> pixel of the block: ds_read_b128's lane groups {0-3, 12-15, 20-27} and {4-11, 16-19,
 // 28-31} (MI355X_MICROARCH.md §LDS) take pixels 0..15 and 16..31 in lane order
@@ -1253,10 +1261,11 @@ __device__ __forceinline__ void t3h_unroll(F&& f) {
     }
 }
 
-template <int KH, int KW, typename OutT>
+template <int KH, int KW, int TNS, typename OutT>
 __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn, int ntiles, int lgw, int tiles_x) {
     extern __shared__ __align__(16) unsigned char smh[];
-    constexpr int BM = T3H_BM, BN = T3_BN, NT = T3H_NT, WN = 2, TNS = 4, NA = T3H_NA, T = KH * KW;
+    using Cfg = T3HCfg<TNS>;
+    constexpr int BM = T3H_BM, BN = Cfg::BN, NT = T3H_NT, WN = 2, CB = TNS / 2, T = KH * KW;
     static_assert(T >= 2, "the halo is stored at a chunk's second step");
     int bid = blockIdx.x;
     {
@@ -1278,13 +1287,16 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     const int nch = a.Cin / T3_KS;
     const float* __restrict__ X = (const float*)a.x;
     const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
-    auto stA = [&](int s) { return smh + s * T3H_ASTAGE; };
-    auto halo = [&](int b) { return smh + T3H_NSA * T3H_ASTAGE + b * T3H_HALO; };
+    auto stA = [&](int s) { return smh + s * Cfg::ASTAGE; };
+    auto halo = [&](int b) { return smh + T3H_NSA * Cfg::ASTAGE + b * T3H_HALO; };
 
     // ---- A DMA: piece P = wid + 4 j of a stage (1 KiB, linear in LDS); lane l writes bytes 16 l of it: row o / 96,
-    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run
+    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run.  Every wave issues
+    // NA pieces per K-step (12 over 4 waves; 64-channel tiles: 6, so waves 2-3 send their second piece's zeros to a
+    // sink): a fixed count, no branch, so the counted waits and the compiler's own stay exact
     const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
     constexpr int OOR = 0x7ff00000;
+    constexpr int NA = Cfg::NAW;
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
@@ -1296,7 +1308,11 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
         unsigned char* base = stA(s);
         const int soff = live ? kl * 96 : OOR;
 #pragma unroll
-        for (int j = 0; j < NA; ++j) t3_dma16(W3, w3_bytes, base + (wid + (NT / 64) * j) * 1024, aoff[j], soff);
+        for (int j = 0; j < NA; ++j) {
+            const int P = wid + (NT / 64) * j;
+            const bool real = Cfg::NP % 4 == 0 || P < Cfg::NP;  // wave-uniform: scalar selects, no branch
+            t3_dma16(W3, w3_bytes, real ? base + P * 1024 : smh + Cfg::SINK, aoff[j], real ? soff : OOR);
+        }
     };
 
     // ---- halo units: u = tid + 256 j -> halo pixel u >> 1 (row hy, column hx), channels 8 (u & 1) .. of a chunk
@@ -1354,9 +1370,9 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
         vy[jb] = v;
     }
 
-    f32x16 acc[2][2];
+    f32x16 acc[CB][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < CB; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
     const int nsteps = nch * T;
@@ -1368,7 +1384,7 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     __builtin_amdgcn_sched_barrier(0);
     t3_waitvm<0>();
     storeH(0);
-    if (tid < T3H_ROW / 16) *(u32x4*)(smh + T3H_ZROW + 16 * tid) = (u32x4){0u, 0u, 0u, 0u};
+    if (tid < T3H_ROW / 16) *(u32x4*)(smh + Cfg::ZROW + 16 * tid) = (u32x4){0u, 0u, 0u, 0u};
     __syncthreads();
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
     // one K-step (chunk c, tap t): A(k + 2) DMA'd first, at t == 0 the next chunk's halo loads, the fragment reads,
@@ -1387,19 +1403,19 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
             loadH(c + 1, c + 1 < nch);
             __builtin_amdgcn_sched_barrier(0);
         }
-        bf16x8 ap[2][3], bp[2][3];
+        bf16x8 ap[CB][3], bp[2][3];
         const unsigned char* as_ = stA(k % T3H_NSA);
         const unsigned char* hs_ = halo(c & 1);
 #pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-            const int row = wn * 64 + 32 * ib + r32, sw = (row >> 3) & 1;
+        for (int ib = 0; ib < CB; ++ib) {
+            const int row = wn * 32 * CB + 32 * ib + r32, sw = (row >> 3) & 1;
 #pragma unroll
             for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
         }
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
             const int hy = bpy[jb] + ky, hx = bpx[jb] + kx;
-            const unsigned char* rp = (vy[jb] >> ky) & 1 ? hs_ + (hy * HW + hx) * T3H_ROW : smh + T3H_ZROW;
+            const unsigned char* rp = (vy[jb] >> ky) & 1 ? hs_ + (hy * HW + hx) * T3H_ROW : smh + Cfg::ZROW;
             const int sw = (hy ^ ((hx >> 3) & xm)) & 1;
 #pragma unroll
             for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(rp + 16 * ((3 * g32 + p) ^ sw));
@@ -1407,7 +1423,7 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
 #pragma unroll
         for (int tt = 0; tt < 6; ++tt)
 #pragma unroll
-            for (int ib = 0; ib < 2; ++ib)
+            for (int ib = 0; ib < CB; ++ib)
 #pragma unroll
                 for (int jb = 0; jb < 2; ++jb)
                     acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[tt]], bp[jb][TB[tt]], acc[ib][jb],
@@ -2780,34 +2796,48 @@ bool use_conv3h(const va_conv_args& a) {
     return taps && conv3h_lgw(a) >= 0 && (int64_t)a.N * a.Ho < (1 << 24);
 }
 
-template <int KH, int KW, typename OutT>
+template <int KH, int KW, int TNS, typename OutT>
 hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3HCfg<TNS>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                T3H_LDS) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
     const int lgw = conv3h_lgw(a);
     const int tw = 1 << lgw, th = T3H_BM / tw;
     const int tiles_x = (a.Wo + tw - 1) / tw, tiles_y = (a.N * a.Ho + th - 1) / th;
-    const int ntn = (a.Cout + T3_BN - 1) / T3_BN;
+    const int ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = tiles_x * tiles_y * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3h_kernel<KH, KW, OutT>), dim3(ntiles), dim3(T3H_NT), T3H_LDS, st, a, ntn, ntiles, lgw,
-                       tiles_x);
+    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a, ntn, ntiles,
+                       lgw, tiles_x);
     return hipGetLastError();
+}
+
+// the narrow f32 3x3 layers (33-64 output channels) on conv3h's 64-channel tiles: the conv3t conditions but Cout,
+// and not a layer conv2 would split over K.  (The 32-channel layers stay on conv2: on half-idle 64-channel tiles
+// model.2's 32 -> 32 bottleneck at 160 x 160 measured 1.25-1.35x slower, profiles/r04/conv3h_narrow/.)
+bool use_conv3h_narrow(const va_conv_args& a) {
+    if (!a.w3 || conv3t_off() || a.mode != 0 || a.Cout <= 32 || a.Cout > 64 || !use_conv3h(a)) return false;
+    int kper;
+    const int t2 = ((a.M + 127) / 128) * ((a.Cout + 63) / 64);
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 64, &kper) > 1) return false;
+    return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.Npad % 64 == 0 && a.ldx % 4 == 0 &&
+           ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
 
 template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
-    if (use_conv3h(a)) return a.mode == 2 ? launch_conv3h_v<2, 2, OutT>(a, st) : launch_conv3h_v<3, 3, OutT>(a, st);
+    if (use_conv3h(a)) return a.mode == 2 ? launch_conv3h_v<2, 2, 4, OutT>(a, st) : launch_conv3h_v<3, 3, 4, OutT>(a, st);
     return launch_conv3t_v<2, 2, OutT>(a, st);
 }
 
 template <int SPL, typename OutT>
 hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
     if (SPL == 6 && use_conv3t(a)) return launch_conv3t<OutT>(a, st);
+    if (SPL == 6 && use_conv3h_narrow(a)) return launch_conv3h_v<3, 3, 2, OutT>(a, st);
     if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
     if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT, float, SPL>(a, st);
     if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT, float, SPL>(a, st);
