@@ -70,10 +70,11 @@ def parse():
                    help="detection regime of the synthetic weights (regime_kwargs); the headline is 'sparse': 1-5 "
                         "compact detections per frame through decode / NMS / contours / mask choice, planted "
                         "navigation masks only on frames without a detection")
-    p.add_argument("--extras", default="c4,c2,dropin,bf16,dense,dense_box,c5",
+    p.add_argument("--extras", default="c4,c2,dropin,dealer,bf16,dense,dense_box,c5",
                    help="comma list of extra measurements in the same run: c4 (BASELINE configs[3]: one frame per GPU "
                         "per step, s-seg f32), c2 (configs[1]: n-seg bf16 batch-1 latency, seg-only and end to end), "
                         "dropin (FrameProcessor.__call__ per frame from host numpy frames, answers included), "
+                        "dealer (one frame source dealt to a FrameProcessor worker process per GPU, in-order answers), "
                         "bf16 (the bf16 MFMA pipeline), "
                         "dense (300 detections per frame, the random weights' noise masks), dense_box (300 "
                         "detections per frame with solid box masks, one contour each, as a trained model's compact "
@@ -434,6 +435,28 @@ def dropin_rate(args, dev, calls=200) -> dict:
                         "PathAnalyser answer"}
 
 
+def dealer_rate(args, dev, frames_n: int = 256) -> dict:
+    """SURVEY.md §8e from the drop-in surface: ONE frame source (a reader, as main.py's camera loop) dealing host
+    frames round-robin to one FrameProcessor worker process per visible GPU (vision_assist_amd.shard.FrameDealer:
+    shared-memory frame ring, in-order answers, each worker with its own PathFinder state), f32 s-seg, the
+    regime's network masks.  frames/s of in-order answers over the whole node's workers."""
+    from vision_assist_amd.shard import FrameDealer, dropin_worker
+    G = max(1, torch.cuda.device_count())
+    rng = np.random.default_rng(78)
+    frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
+    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)), list(range(G)),
+                     640, 640, slots=4) as d:
+        for _ in d.map(frames[i % 16] for i in range(4 * G)):  # warm: plans, first launches
+            pass
+        t0 = time.perf_counter()
+        answers = sum(a != [] for a in d.map(frames[i % 16] for i in range(frames_n)))
+        dt = time.perf_counter() - t0
+    return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "frames": frames_n,
+            "frames_with_answer": answers, "dtype": "f32", "regime": args.regime,
+            "workload": "one reader dealing host 640x640 frames round-robin to one FrameProcessor worker process per "
+                        "GPU (vision_assist_amd.shard.FrameDealer), answers back in frame order"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -481,6 +504,10 @@ def main():
         if ex == "dropin":
             if world == 1:
                 extras[ex] = dropin_rate(args, dev)
+            continue
+        if ex == "dealer":
+            if world == 1:
+                extras[ex] = dealer_rate(args, dev)
             continue
         if ex == "c4":
             extras[ex] = c4_rate(args, dev, rank, world, prof)

@@ -1,0 +1,72 @@
+"""The §8e frame dealer (vision_assist_amd.shard.FrameDealer) on the CPU: one reader deals a frame stream
+round-robin to 2 spawned worker processes through the shared-memory ring, results come back in frame order.
+
+The workers run the grid-level path with the oracle standing in for the device pipeline (no GPU here): a frame
+carries a planted corridor mask in its pixels, the worker runs oracle/nav.frame_nav on it with its OWN
+PathFinder angle cache (one per process, as PathFinder.py:32).  Every answer must equal replaying that worker's
+shard (frames i % 2 == w, in order) through a fresh process state -- SURVEY.md §8e's multi-GPU parity
+definition -- and the stream must come back in order even though the two shards finish out of order."""
+import numpy as np
+import pytest
+
+N_FRAMES = 14
+
+
+def _frame(i: int) -> np.ndarray:
+    from workloads.corridors import cells_to_mask, corridor_cells
+    m = cells_to_mask(corridor_cells(4100 + i))
+    return np.repeat(m[:, :, None], 3, axis=2).astype(np.uint8)
+
+
+def _paths(frame: np.ndarray, pf):
+    from oracle import nav as onav
+    mask = frame[:, :, 0]
+    ys, xs = np.nonzero(mask)
+    rect = (int(xs.min()), int(ys.min()), int(xs.max() - xs.min() + 1), int(ys.max() - ys.min() + 1))
+    out = onav.frame_nav(mask, rect, mask.shape[0], mask.shape[1], pf)
+    return [[(c.coords.x, c.coords.y) for c in q[2]] for q in out["queries"]], sorted(pf.angle_cache)
+
+
+class OracleNavWorker:
+    """FrameDealer worker factory (picklable): a per-process PathFinder state, frame -> its A* results."""
+
+    def __call__(self, device):
+        from oracle import nav as onav
+        pf = onav.PathFinderOracle()
+        return lambda frame: _paths(frame, pf)
+
+
+class FailingWorker:
+    def __call__(self, device):
+        def fn(frame):
+            if frame[0, 0, 0] == 7:
+                raise ValueError("bad frame")
+            return int(frame[0, 0, 0])
+        return fn
+
+
+def test_dealer_round_robin_in_order_matches_per_shard_replay():
+    from oracle import nav as onav
+    from vision_assist_amd.shard import FrameDealer, shard_indices
+    frames = [_frame(i) for i in range(N_FRAMES)]
+    with FrameDealer(OracleNavWorker(), [None, None], 640, 640, slots=2) as d:
+        got = list(d.map(frames))
+        assert d.in_flight() == 0
+    assert len(got) == N_FRAMES
+    for w in range(2):
+        pf = onav.PathFinderOracle()
+        for i in shard_indices(N_FRAMES, 2, w):
+            assert got[i] == _paths(frames[i], pf), f"frame {i} (worker {w})"
+
+
+def test_dealer_submit_get_and_worker_errors():
+    from vision_assist_amd.shard import FrameDealer
+    with FrameDealer(FailingWorker(), [None, None, None], 4, 4, slots=1) as d:
+        for v in (1, 2, 3):
+            d.submit(np.full((4, 4, 3), v, np.uint8))
+        assert [d.get(), d.get(), d.get()] == [1, 2, 3]
+        with pytest.raises(ValueError):
+            d.submit(np.zeros((5, 4, 3), np.uint8))
+        d.submit(np.full((4, 4, 3), 7, np.uint8))
+        with pytest.raises(RuntimeError, match="bad frame"):
+            d.get()

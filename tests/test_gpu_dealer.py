@@ -1,0 +1,85 @@
+"""The §8e frame dealer on the GPU: one reader deals the C4 frame stream (frames 7000 + i, s-seg 640, the network's
+own masks) round-robin to 2 worker processes on the test GPU (on a node each worker takes its own GPU; the code
+path is the same), each with a batch-1 f32 FramePipeline and its own PathFinder angle cache.  The in-order
+results must equal each shard's frames replayed in order through the oracle chain with a fresh PathFinder per
+shard -- tests/golden/chain_oracle.json.gz["c4/<regime>"], the same per-shard replay test_gpu_c4.py checks --
+with the f32 bar: every detection matched, the same chosen instance, rect, cells and A* paths and costs.  And
+FrameProcessor.map (the drop-in surface's multi-GPU mode) hands back one answer per frame, in order."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 8
+
+
+class C4RecordWorker:
+    """FrameDealer worker factory: a batch-1 f32 FramePipeline of the regime's weights on the worker's GPU; a
+    frame -> its detections, chosen instance, rect, cells and A* paths / costs (plain numpy / python)."""
+
+    def __init__(self, regime: str):
+        self.regime = regime
+
+    def __call__(self, device):
+        import torch
+
+        from tests.chain_util import weights
+        from vision_assist_amd.pipeline import FramePipeline
+        from vision_assist_amd.post import PLANT_NEVER
+        arch, fw = weights(self.regime)
+        pipe = FramePipeline(arch, fw, 1, 640, 640, dtype="f32", device=torch.device("cuda", device))
+
+        def run(frame):
+            res = pipe.run(torch.from_numpy(frame[None]), plant_mode=PLANT_NEVER)
+            nf = res.frame(0)
+            det, _ = pipe.post.det_tensor(0)
+            return {"det": det.numpy(), "chosen": int(pipe.post.chosen[0]), "rect": pipe.post.rects[0].cpu().tolist(),
+                    "cells": pipe.post.cells[0].cpu().numpy(), "status": nf.status,
+                    "queries": [(q["path"], float(q["cost"]).hex() if q["path"] else None) for q in nf.queries]}
+        return run
+
+
+@pytest.mark.parametrize("regime", ["sparse", "dense_box"])
+def test_dealer_two_workers_vs_per_shard_oracle_replay(regime):
+    import torch
+
+    from tests.chain_util import compare, frame_batch, load_fixture
+    from vision_assist_amd.shard import FrameDealer
+    frames = [frame_batch(7000 + i, 1)[0].numpy() for i in range(N_FRAMES)]
+    want = load_fixture(f"c4/{regime}")
+    with FrameDealer(C4RecordWorker(regime), [0, 0], 640, 640, slots=2) as d:
+        got = list(d.map(frames))
+    bad = []
+    for i, (g, w) in enumerate(zip(got, want)):
+        ok = g["status"] == 0
+        rec = {"det": torch.from_numpy(g["det"]), "chosen": g["chosen"],
+               "rect": tuple(g["rect"]) if g["chosen"] >= 0 else None,
+               "cells": g["cells"] if g["chosen"] >= 0 else None,
+               "paths": [p for p, _ in g["queries"]] if ok else None,
+               "costs": [c for _, c in g["queries"]] if ok else None}
+        c = compare(rec, w, f32=True)
+        frac = 1.0 if regime == "sparse" else 0.98
+        if c["matched"] < frac * max(c["ndet"]) or not c["chosen"] or c["cells_mismatch"] != 0 or not c["paths"]:
+            bad.append((i, c))
+    assert len(got) == N_FRAMES and not bad, bad
+
+
+def test_frameprocessor_map_answers_in_order():
+    import warnings
+
+    from tests.chain_util import frame_batch
+    from vision_assist_amd.FrameProcessor import FrameProcessor
+    from vision_assist_amd.yolo import YOLO
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        model = YOLO("yolov8s-seg.pt", sparse=640, dtype="f32").to("cuda")
+    fp = FrameProcessor(model=model, verbose=False, debug=False)
+    fp.model = model
+    frames = [frame_batch(7100 + i, 1)[0].numpy() for i in range(6)]
+    try:
+        answers = list(fp.map(frames, devices=[0, 0], slots=2))
+    finally:
+        fp.close_map()
+    assert len(answers) == len(frames)
+    assert all(isinstance(a, (str, list)) for a in answers)
+    assert any(a != [] for a in answers)

@@ -379,3 +379,36 @@ class FrameProcessor:
                 self._draw_grid(grid, penalty_calculator.get_penalty_colour(grid.penalty or 0))
 
     process = __call__  # the name BASELINE.json's north_star uses
+
+    # ------- multi-GPU stream -------
+    def map(self, frames, devices=None, slots: int = 4):
+        """Answers of a frame stream in frame order, the frames dealt round-robin to one worker process per GPU
+        (vision_assist_amd.shard.FrameDealer): frame i goes to devices[i % G], each worker running this model in
+        its own FrameProcessor with its own PathFinder angle cache -- per shard the answers of __call__ over that
+        shard's frames in order.  devices: GPU indices (default: every visible GPU).  The first frame fixes the
+        frame size; the dealer is kept for later calls with the same devices and size (close_map ends it)."""
+        from .shard import FrameDealer, dropin_worker
+        it = iter(frames)
+        try:
+            first = next(it)
+        except StopIteration:
+            return
+        H, W = int(first.shape[0]), int(first.shape[1])
+        devices = list(range(torch.cuda.device_count())) if devices is None else list(devices)
+        key = (tuple(devices), H, W, slots)
+        dealers = self.__dict__.setdefault("_dealers", {})
+        if key not in dealers:
+            if not hasattr(self.model, "spec"):
+                raise TypeError("FrameProcessor.map needs a vision_assist_amd.yolo.YOLO model")
+            model, kw = self.model.spec
+            dealers[key] = FrameDealer(dropin_worker(model, **kw), devices, H, W, slots=slots)
+
+        def chain():
+            yield first
+            yield from it
+
+        yield from dealers[key].map(chain())
+
+    def close_map(self) -> None:
+        for d in self.__dict__.pop("_dealers", {}).values():
+            d.close()

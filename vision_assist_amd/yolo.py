@@ -48,6 +48,9 @@ class YOLO:
                  seed: int = 0, cls_bias: float | None = None, sparse: int | None = None, solid_masks: bool = False):
         """model: a .safetensors state dict with Ultralytics key names, or a yolov8{n,s,m}-seg name (seeded
         synthetic weights; cls_bias / sparse / solid_masks select the synthetic regime, seg_arch.synthetic_state_dict)."""
+        # the constructor's arguments: a FrameDealer worker rebuilds this model on its own GPU (shard.dropin_worker)
+        self.spec = (str(model), dict(task=task, dtype=dtype, nc=nc, seed=seed, cls_bias=cls_bias, sparse=sparse,
+                                      solid_masks=solid_masks))
         name = os.path.basename(str(model))
         if str(model).endswith(".safetensors") and os.path.exists(model):
             from safetensors.torch import load_file
