@@ -1,10 +1,11 @@
 """Debug rendering (FrameProcessor(debug=True), PathVisualiser.py / FrameProcessor.py:273-299) on the host frame:
 squares are cv2.fillPoly of an axis-aligned integer square = the inclusive pixel range, penalty colours from the
 nearest gradient key, section colours by position, white section lines and corner dots; later draws cover earlier
-ones.  (cv2 itself is absent: the line / circle rasters are restated and unpinned, the labels are not drawn.)"""
+ones.  (cv2 itself is absent: the line / circle rasters and the label glyphs are restated and unpinned; the label text,
+origin, scale and thickness follow PathVisualiser.py:48-56.)"""
 import numpy as np
 
-from vision_assist_amd.models import Coordinate, Grid, Path
+from vision_assist_amd.models import Coordinate, Corner, Grid, Path
 from vision_assist_amd.PathVisualiser import PathVisualiser, draw_line2, fill_circle, fill_square
 from vision_assist_amd.PenaltyCalculator import penalty_calculator
 
@@ -53,3 +54,27 @@ def test_path_visualiser_draws_sections_in_order():
     assert tuple(f[g0.coords.y + 3, g0.coords.x + 3]) == want
     # the white line through the section's cell centres
     assert tuple(f[s0.start.y + 10, s0.start.x + 10]) == (255, 255, 255)
+
+
+def test_corner_label_text_and_placement():
+    from vision_assist_amd.PathVisualiser import corner_label
+    from vision_assist_amd.strokefont import GLYPHS, put_text, text_size
+    c = Corner(direction="left", sharpness="sharp", shape="inner", start=Coordinate(x=300, y=400),
+               end=Coordinate(x=340, y=300), angle_change=40.0, length=80.0)
+    assert corner_label(0, c) == "1 left inner sharp"
+    words = ["left", "right", "inner", "outer", "optimal", "sharp", "sweeping", "0123456789"]
+    assert all(ch in GLYPHS for w in words for ch in w)
+    f = np.zeros((640, 640, 3), np.uint8)
+    pv = PathVisualiser()
+    pv.frame = f
+    pv._draw_corner_marker(0, c, None)
+    ys, xs = np.nonzero(f[..., 0])
+    # the dots at start/end + 10 and the text whose baseline starts at (end.x - 100, end.y - 5)
+    text = np.zeros_like(f)
+    put_text(text, "1 left inner sharp", (240, 295), 0.5, (255, 255, 255), 2)
+    assert ((f == 255) | (text == 0)).all()  # every text pixel is drawn
+    (w, h), base = text_size("1 left inner sharp", 0.5, 2)
+    ty, tx = np.nonzero(text[..., 0])
+    assert tx.min() >= 240 and tx.max() < 240 + w and ty.min() >= 295 - h and ty.max() <= 295 + base
+    assert tx.max() - tx.min() > 100 and ty.max() - ty.min() >= 9
+    assert f[310, 350, 0] == 255 and f[410, 310, 0] == 255  # the two dots

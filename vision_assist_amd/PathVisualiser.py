@@ -13,8 +13,9 @@ What is drawn, in the reference's order:
 The squares are cv2.fillPoly of an axis-aligned integer square, which is exactly the inclusive pixel range
 [x, x + 20] x [y, y + 20] (clipped to the frame).  OpenCV is absent here, so the thick line (cv2.line, thickness 2)
 and the filled circle (cv2.circle, thickness -1) are restated as a 2-pixel-wide Bresenham line and the disc
-dx^2 + dy^2 <= r^2 + r, and the corner labels (cv2.putText, Hershey font) are not drawn: this rendering's parity
-with cv2 is unpinned (debug output only)."""
+dx^2 + dy^2 <= r^2 + r, and the corner labels (cv2.putText, Hershey simplex, scale 0.5, thickness 2) are drawn
+with strokefont.put_text: the same text, origin, scale and thickness in this module's own stroke glyphs.  This
+rendering's pixel parity with cv2 is unpinned (debug output only)."""
 from __future__ import annotations
 
 from typing import ClassVar, Optional
@@ -23,6 +24,12 @@ import numpy as np
 
 from .config import grid_size
 from .models import Corner, Path, PathColours
+from .strokefont import put_text
+
+
+def corner_label(section_idx: int, corner: Corner) -> str:
+    """The corner marker's text (PathVisualiser.py:50)."""
+    return f"{section_idx + 1} {corner.direction} {corner.shape} {corner.sharpness}"
 
 
 def fill_square(frame: np.ndarray, x: int, y: int, color) -> None:
@@ -93,7 +100,8 @@ class PathVisualiser:
     def _draw_corner_marker(self, section_idx: int, corner: Corner, path: Path) -> None:
         fill_circle(self.frame, corner.start.x + 10, corner.start.y + 10, 5, (255, 255, 255))
         fill_circle(self.frame, corner.end.x + 10, corner.end.y + 10, 5, (255, 255, 255))
-        # the label (cv2.putText) is not drawn: no font rasterizer here
+        put_text(self.frame, corner_label(section_idx, corner), (corner.end.x - 100, corner.end.y - 5), 0.5,
+                 (255, 255, 255), 2)
 
     def _draw_path_sections(self, path: Path, path_idx: int) -> None:
         if not path.sections:
