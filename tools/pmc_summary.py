@@ -68,6 +68,8 @@ def main():
             # the 256 CUs' 4 SIMDs (32 SIMDs per XCD x 8) -> fraction of the SIMD-cycles the kernel spanned
             r["mfma_busy"] = round(r["SQ_VALU_MFMA_BUSY_CYCLES"] / (r["GRBM_GUI_ACTIVE"] / 8 * SIMDS), 4)
             r["clock_ghz"] = round(r["GRBM_GUI_ACTIVE"] / 8 / (r["dur_us"] * 1e3), 3)
+        if "TCP_TCC_READ_REQ_sum" in r:
+            r["l1_l2_read_req"] = r["TCP_TCC_READ_REQ_sum"]  # vL1D -> L2 read requests (one per missed line)
         if "FETCH_SIZE" in r or "WRITE_SIZE" in r:
             r["hbm_bytes"] = round(2 * r.get("FETCH_SIZE", 0) * 1024 + r.get("WRITE_SIZE", 0) * 1024)
         if op.get("flops") and r.get("GRBM_GUI_ACTIVE"):
@@ -85,7 +87,7 @@ def main():
         json.dump(res, f, indent=1)
     for r in out:
         print(json.dumps({k: r.get(k) for k in ("i", "name", "dur_us", "tflops", "mfma_busy", "wait_frac", "stall_frac",
-                                                  "hbm_bytes", "clock_ghz") if k in r}))
+                                                  "hbm_bytes", "clock_ghz", "l1_l2_read_req") if k in r}))
 
 
 if __name__ == "__main__":

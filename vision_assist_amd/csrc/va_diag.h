@@ -7,6 +7,10 @@
 //                             outside it, 27 a bilinear tap row outside the strip, 30 a fill hit past the lattice
 //   nav (va_nav.hip):         31 grid: a rect no frame can hold (v0 = x, v1 = w), treated as no mask
 //                             32 A*: start / end node outside the lattice (v0 = start, v1 = end)
+//                             33 A*: a popped key outside the open list or the lattice (v0 = node, v1 = open count)
+//                             34 A*: a parent chain longer than the lattice (v0 = query slot, v1 = length)
+//                             35 dedupe: a found path's length outside 1..nodes (v0 = query k, v1 = length)
+//                             36 dedupe: a path node outside the lattice (v0 = query k, v1 = node)
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -666,6 +666,9 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         const int slot = (int)(sec & 0xFFFFu);
         const int cx = (int)(sec >> 24), cy = (int)((sec >> 16) & 0xFFu);
         const int cur = cy * LC + cx;
+        // the popped key must name a live open slot and a lattice node (it indexes the global penalties below):
+        // anything else is open-list state no push wrote -- recorded and the query ends (wave-uniform values)
+        if (!VA_DIAG_OK(slot < open_n && cx < LC && cy < a.LR, 33, cur, open_n)) break;
         // the neighbours (lanes 0..3) and their penalties, loaded now and consumed by the relaxation
         int nb = -1;
         if (lane < 4) {
@@ -766,14 +769,19 @@ __global__ __launch_bounds__(64) void nav_astar_kernel(AstarArgs a) {
         qh->miss[1] = miss1;
         qh->unique = 0;
         qh->order = -1;
-        if (found) {
-            uint16_t* path = (uint16_t*)((uint8_t*)qh + a.off_q_path);
-            int len = 1, c = e;
-            while (c != s) {
+        int len = 1;
+        if (found) {  // the parent chain from e must reach s within the lattice (the record holds N nodes)
+            int c = e;
+            while (c != s && len <= N) {
                 c = par[c];
                 ++len;
+                if (c >= N) len = N + 1;
             }
-            c = e;
+            found = VA_DIAG_OK(len <= N, 34, q, len);
+        }
+        if (found) {
+            uint16_t* path = (uint16_t*)((uint8_t*)qh + a.off_q_path);
+            int c = e;
             for (int i = len - 1; i >= 0; --i) {
                 path[i] = (uint16_t)c;
                 if (i) c = par[c];
@@ -867,9 +875,10 @@ __global__ __launch_bounds__(64) void nav_dedupe_kernel(uint8_t* qwork, int64_t 
         va_query_hdr* qh = qhdr(k);
         if (qh->status != VA_QUERY_FOUND) continue;
         const uint16_t* path = (const uint16_t*)((uint8_t*)qh + off_q_path);
-        for (int i = lane; i < qh->len; i += 64) {
+        const int len = VA_DIAG_OK(qh->len > 0 && qh->len <= nodes, 35, k, qh->len) ? qh->len : 0;
+        for (int i = lane; i < len; i += 64) {
             int nd = path[i];
-            atomicOr(&bits[(int64_t)k * words + nd / 64], 1ull << (nd % 64));
+            if (VA_DIAG_OK(nd < nodes, 36, k, nd)) atomicOr(&bits[(int64_t)k * words + nd / 64], 1ull << (nd % 64));
         }
     }
     __syncthreads();
