@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--regime", default="sparse")
     ap.add_argument("--lanes", type=int, default=1)
+    ap.add_argument("--seg-only", action="store_true", help="bench.c2_latency's seg_only leg (run_seg_only) instead")
+    ap.add_argument("--scale", default="n")
+    ap.add_argument("--dtype", default="bf16", help="bf16 (C2) or f32 (the drop-in's batch-1 network)")
     a = ap.parse_args()
     import bench
     from vision_assist_amd.pipeline import FramePipeline
@@ -25,9 +28,9 @@ def main():
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
     from workloads.corridors import cells_rect, corridor_cells
     dev = torch.device("cuda", 0)
-    arch = Arch("n")
+    arch = Arch(a.scale)
     pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, **bench.regime_kwargs(a.regime, 640))),
-                         1, 640, 640, dtype="bf16", device=dev, lanes=bool(a.lanes))
+                         1, 640, 640, dtype=a.dtype, device=dev, lanes=bool(a.lanes))
     g = corridor_cells(11, 32, 32)
     pc = torch.tensor(g[None].astype(np.uint8), device=dev)
     pr = torch.tensor(np.array([cells_rect(g)], dtype=np.int32), device=dev)
@@ -39,12 +42,16 @@ def main():
     with torch.cuda.stream(st):
         for i in range(20 + a.iters):
             t0 = time.perf_counter()
-            pipe.run(frame, pc, pr, PLANT_IF_NONE, stream=st)
+            if a.seg_only:
+                pipe.run_seg_only(stream=st)
+            else:
+                pipe.run(frame, pc, pr, PLANT_IF_NONE, stream=st)
             st.synchronize()
             if i >= 20:
                 ts.append(time.perf_counter() - t0)
     ts = np.array(ts) * 1e3
-    print(json.dumps({"end_to_end_median_ms": round(float(np.median(ts)), 4), "iters": a.iters,
+    key = "seg_only_median_ms" if a.seg_only else "end_to_end_median_ms"
+    print(json.dumps({key: round(float(np.median(ts)), 4), "iters": a.iters,
                       "ndet": int(pipe.post.ndet[0]), "lanes": a.lanes}))
 
 
