@@ -23,7 +23,8 @@ def test_sparse_chain_fixture_recomputes():
     for g, w in zip(got, want):
         _same(g, w)
     assert sum(w["chosen"] >= 0 for w in want) >= len(want) // 2
-    assert all(w["det"].shape[0] <= 8 for w in want)  # the regime: a few detections per frame
+    nd = sorted(w["det"].shape[0] for w in want)  # the regime: a few detections per frame (32 frames: median 2,
+    assert nd[len(nd) // 2] <= 5 and nd[-1] <= 16      # one frame with 12)
 
 
 def test_c4_sparse_fixture_is_the_per_shard_replay():

@@ -20,8 +20,11 @@ def main():
     ap.add_argument("--lanes", type=int, default=1)
     ap.add_argument("--seg-only", action="store_true", help="bench.c2_latency's seg_only leg (run_seg_only) instead")
     ap.add_argument("--scale", default="n")
+    ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", help="bf16 (C2) or f32 (the drop-in's batch-1 network)")
     a = ap.parse_args()
+    if a.batch > 1 and not a.seg_only:
+        raise SystemExit("--batch > 1 only with --seg-only")
     import bench
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_IF_NONE
@@ -30,7 +33,7 @@ def main():
     dev = torch.device("cuda", 0)
     arch = Arch(a.scale)
     pipe = FramePipeline(arch, fold(arch, synthetic_state_dict(arch, seed=0, **bench.regime_kwargs(a.regime, 640))),
-                         1, 640, 640, dtype=a.dtype, device=dev, lanes=bool(a.lanes))
+                         a.batch, 640, 640, dtype=a.dtype, device=dev, lanes=bool(a.lanes))
     g = corridor_cells(11, 32, 32)
     pc = torch.tensor(g[None].astype(np.uint8), device=dev)
     pr = torch.tensor(np.array([cells_rect(g)], dtype=np.int32), device=dev)

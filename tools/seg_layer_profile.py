@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--ab", default="", help="env switch NAME (or NAME:V0:V1): interleave rounds with NAME=0 and "
                                             "NAME=1 (or V0 / V1) (one process, cdna_hip_programming.md §5.4 rule 24)")
     ap.add_argument("--env", action="append", default=[], help="KEY=VAL set before planning")
+    ap.add_argument("--plan-ab", default="", help="planner switch NAME (NAME=0 vs unset): two plans (e.g. fusions "
+                                                 "that change the op list), rounds interleaved, totals and per-op rows")
     args = ap.parse_args()
     for kv in args.env:
         k, v = kv.split("=", 1)
@@ -57,6 +59,31 @@ def main():
         lib.va_prof_stop(kinds, cnt, 8)
         return list(ms)
 
+    if args.plan_ab:
+        name = args.plan_ab
+        os.environ[name] = "0"
+        plan0 = net.plan(B, H, H, tag=7)
+        del os.environ[name]
+        plans = {f"{name}=0": plan0, "default": plan}
+        for p_ in plans.values():
+            p_["frames"].copy_(plan["frames"])
+            net.run_plan(p_)
+        tot = {k: [0.0] * p_["n"] for k, p_ in plans.items()}
+        for rnd in range(args.iters):
+            for k, p_ in plans.items():
+                net.run_plan(p_)
+                _lib.check(lib.va_prof_start(p_["n"] + 8), "va_prof_start")
+                net.run_plan(p_)
+                ms = (ctypes.c_double * p_["n"])()
+                lib.va_prof_stop_ops(ms, p_["n"])
+                kinds, cnt = (ctypes.c_double * 8)(), (ctypes.c_int64 * 8)()
+                lib.va_prof_stop(kinds, cnt, 8)
+                tot[k] = [a + b for a, b in zip(tot[k], ms)]
+        for k, p_ in plans.items():
+            for i, m in enumerate(p_["meta"]):
+                print(json.dumps({"plan": k, "i": i, "name": m["name"], "us": round(1000 * tot[k][i] / args.iters, 2)}))
+        print(json.dumps({"total_us": {k: round(1000 * sum(v) / args.iters, 1) for k, v in tot.items()}}))
+        return
     if args.ab:
         name, v0, v1 = (args.ab.split(":") + ["0", "1"])[:3] if ":" in args.ab else (args.ab, "0", "1")
         tot = {v0: [0.0] * n, v1: [0.0] * n}
