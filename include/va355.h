@@ -183,7 +183,7 @@ typedef struct va_conv_args {
     int32_t M;              /* N * Ho * Wo */
     int32_t dtype;          /* VA_DTYPE_BF16 (MFMA bf16, f32 accumulate) or VA_DTYPE_F32 (exact f32 MFMA) */
     int32_t out_f32;        /* bf16 inputs with a float output (head logits) */
-    int32_t bias4;          /* mode 2 with a fused tail only: bias is a border table [4 classes][2][2][Npad],
+    int32_t bias4;          /* mode 2 only (bf16: with a fused tail): bias is a border table [4 classes][2][2][Npad],
                                entry [c][rf][cf] for output pixels whose class-c taps miss the map's first /
                                last row (rf) or column (cf) -- the folded deconv bias depends on which taps
                                fall inside the map, so no constant-1 input channel is needed */
@@ -191,8 +191,12 @@ typedef struct va_conv_args {
      * c2 <= 64 and the weights fitting 120 KiB of LDS): when w2 != NULL the main conv's activations (bias + act,
      * rounded to bf16 as a stored layer would be) never leave the chip and feed y2 = act2(W2 . a + b2);
      * y / ldy / out_f32 then describe the TAIL output (c2 channels, c2 % 4 == 0).  Replaces a 1x1 layer that
-     * only consumes this one (proto.cv2 -> proto.cv3, head cv2/cv3/cv4 .l.1 -> .l.2). */
-    const void* w2;         /* [>= ceil16(c2)][Cout] bf16, K contiguous */
+     * only consumes this one (proto.cv2 -> proto.cv3, head cv2/cv3/cv4 .l.1 -> .l.2).
+     * f32 (VA_DTYPE_F32 with w3): a stride-1 3x3 / pad 1 conv (or the mode-2 fold) with Cout 64 or 128 (128 for
+     * mode 2), c2 <= 96, no residual; w2 = the tail's weights as three exact bf16 terms [32 ceil(c2 / 32)][Cout / 8]
+     * [3][8] (w3's layout), the main activations kept in f32 and contracted as six exact term products; the tail
+     * output is float. */
+    const void* w2;         /* bf16: [>= ceil16(c2)][Cout], K contiguous; f32: the three-term planes above */
     const float* b2;        /* [>= ceil16(c2)] */
     int32_t c2;
     int32_t act2;           /* 1 = SiLU */

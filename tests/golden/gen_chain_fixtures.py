@@ -10,7 +10,7 @@ Sets:
                   sparse / dense / dense_box (s-seg 640);
   c4/<regime>:    frames frame_batch(7000 + i, 1), i < 8, dealt round-robin to 2 ranks; one PathFinder state
                   per shard, frames in shard order (SURVEY.md §8e per-shard replay); regimes sparse / dense_box.
-  c5/<regime>:    YOLOv8m-seg at 1280 x 1280 (BASELINE configs[4]), frames frame_batch(8000, 4, 1280), one
+  c5/<regime>:    YOLOv8m-seg at 1280 x 1280 (BASELINE configs[4]), frames frame_batch(8000, 8, 1280), one
                   PathFinder state; regimes sparse / dense_box (the fp8 chain test's reference).
 
 Per frame: det float32 [k, 6] (x1 y1 x2 y2 score cls, base64), chosen index, rect, cells uint8 [32, 32]
@@ -31,7 +31,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "chain_oracle.json.gz")
-CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 32, 8, 2, 4
+CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 32, 8, 2, 8
 
 
 def _enc(rec: dict) -> dict:

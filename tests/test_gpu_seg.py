@@ -378,6 +378,78 @@ def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual):
     assert (got - got_t).abs().max().item() <= 2e-5 * scale
 
 
+@pytest.mark.parametrize("cin,cout,c2,act2,H,W,B", [
+    (64, 64, 64, False, 40, 40, 2),    # the box branch: narrow main conv (64-channel tile), 64 float outputs
+    (128, 128, 80, False, 23, 21, 3),  # the cls branch: 80 outputs (a ragged third 32-row block), image seams
+    (128, 128, 32, True, 20, 20, 3),   # proto.cv3's shape: 32 outputs with SiLU
+])
+def test_conv3h_fused_tail_op(cin, cout, c2, act2, H, W, B):
+    """The f32 fused 1x1 tail (va_seg.hip conv_tail32): a stride-1 3x3 conv on conv3h whose whole channel set is one
+    tile, + bias + SiLU, contracted in the epilogue with the tail's pre-split weights (six exact term products per
+    f32 product) + b2 (+ SiLU): within f32 rounding of torch fp32 of the two layers in sequence."""
+    import ctypes
+
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    from vision_assist_amd.seg_arch import Arch
+    g = torch.Generator().manual_seed(cin + 7 * c2 + B)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    w2 = torch.randn(c2, cout, 1, 1, generator=g) * (2.0 / cout) ** 0.5
+    b2 = torch.randn(c2, generator=g) * 0.1
+    x = torch.randn(B, cin, H, W, generator=g)
+    net = S.SegNet.__new__(S.SegNet)
+    net.arch, net.dtype, net.tdtype, net.va_dtype, net.vec = Arch("n"), "f32", torch.float32, S.VA_DTYPE_F32, 4
+    net.device = torch.device("cuda")
+    net.lib = _lib.load()
+    p, p2 = net._pack(w, b), net._pack(w2, b2)
+    planes = S.split3_bf16(p2.w[:32 * ((c2 + 31) // 32), :cout])
+    ld_in = cin + 8
+    xin = torch.zeros(B, H, W, ld_in, dtype=torch.float32, device="cuda")
+    xin[..., :cin] = x.permute(0, 2, 3, 1).cuda()
+    ld_out = c2 + 12
+    y = torch.zeros(B, H, W, ld_out, dtype=torch.float32, device="cuda")
+    args = S.ConvArgs(x=xin.data_ptr(), N=B, H=H, W=W, Cin=p.cin, ldx=ld_in, kh=3, kw=3, stride=1, pad=1, Ho=H,
+                      Wo=W, w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
+                      y=y.data_ptr() + 4 * 4, ldy=ld_out, act=1, mode=0, M=B * H * W, dtype=S.VA_DTYPE_F32,
+                      w3=p.w3.data_ptr(), w2=planes.data_ptr(), b2=p2.b.data_ptr(), c2=c2, act2=1 if act2 else 0)
+    _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(args)), "va_seg_conv")
+    torch.cuda.synchronize()
+    got = y[..., 4:4 + c2].cpu().permute(0, 3, 1, 2)
+    assert int(y[..., :4].abs().sum()) == 0 and int(y[..., 4 + c2:].abs().sum()) == 0  # nothing outside the slice
+    ref = F.conv2d(F.silu(F.conv2d(x.double(), w.double(), b.double(), 1, 1)), w2.double(), b2.double())
+    if act2:
+        ref = F.silu(ref)
+    scale = max(1.0, ref.abs().max().item())
+    assert (got.double() - ref).abs().max().item() <= 2e-5 * scale, (got.double() - ref).abs().max().item()
+
+
+def test_fused_tails_f32_forward(monkeypatch):
+    """The f32 forward with the head's box / cls 1x1s and proto.cv3 in their 3x3s' epilogues (conv3h + conv_tail32;
+    the plan's op names carry the fusion) against the same forward unfused (VA_FUSE_TAIL=0): f32-rounding close,
+    and within the f32 bar of torch."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(3, seed=17)
+    monkeypatch.setenv("VA_FUSE_TAIL", "0")
+    ref = _gpu_heads(net, frames)
+    assert not any("+model.22" in m["name"] or "+cv3" in m["name"] for m in net.plan(3, 640, 640)["meta"])
+    monkeypatch.delenv("VA_FUSE_TAIL")
+    net._plans.clear()
+    # fused where the launch has >= 128 tiles (level 0 and the fold at B = 3); level 1's 38 tiles stay on conv2's
+    # split-K form, unfused
+    names = [m["name"] for m in net.plan(3, 640, 640)["meta"]]
+    assert "model.22.cv3.0.1+model.22.cv3.0.2" in names and "model.22.cv2.0.1+model.22.cv2.0.2" in names
+    assert "model.22.proto.upsample+cv2+cv3 (sub-pixel fold)" in names and "model.22.cv3.1.1" in names
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: fused vs unfused max diff {d}"
+    torch.set_num_threads(8)
+    want = _ref_heads(arch, fw, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+        assert (g - r).abs().max().item() <= 1e-3, name
+
+
 @pytest.mark.parametrize("B", [2, 3])
 def test_conv3h_matches_conv3t_forward(B, monkeypatch):
     """The f32 forward with conv3h on its layers (every stride-1 3x3 with Cout > 64: P3-P5 C2f bottlenecks, the

@@ -569,10 +569,10 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
 // + q % 4 (v_mfma_f32_32x32x16 D layout)
 // pcol(c): tile row (pixel) of accumulator column c (0..31) of a 32 x 32 block (the B operand's row order);
 // mrow(pl): GEMM row m of tile pixel pl (bias4's border table), or -1 when masked
-template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename MFn, typename PFn>
-__device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&acc)[TNS / 2][2], unsigned char* smem,
-                                                int n0, int wm, int wn, int tid, int lane, RowFn orow, MFn mrow,
-                                                PFn pcol, int cls = 0) {
+template <int BN, int TNS, typename MFn, typename PFn>
+__device__ __forceinline__ void conv_epilogue32_fill(const va_conv_args& a, f32x16 (&acc)[TNS / 2][2],
+                                                     unsigned char* smem, int n0, int wm, int wn, int lane, MFn mrow,
+                                                     PFn pcol, int cls) {
     constexpr int CW = BN + 4;
     float* Cs = (float*)smem;
     const int r = lane & 31, g = lane >> 5;
@@ -615,6 +615,13 @@ __device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&
             }
         }
     }
+}
+
+template <int NT, int BM, int BN, int TNS, typename OutT, typename RowFn, typename MFn, typename PFn>
+__device__ __forceinline__ void conv_epilogue32(const va_conv_args& a, f32x16 (&acc)[TNS / 2][2], unsigned char* smem,
+                                                int n0, int wm, int wn, int tid, int lane, RowFn orow, MFn mrow,
+                                                PFn pcol, int cls = 0) {
+    conv_epilogue32_fill<BN, TNS>(a, acc, smem, n0, wm, wn, lane, mrow, pcol, cls);
     __syncthreads();
     conv_epilogue_store<NT, BM, BN, OutT, RowFn, float>(a, smem, n0, tid, orow);
 }
@@ -665,6 +672,73 @@ __device__ __forceinline__ void sk_store16(void* base, int64_t bytes, int off, f
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+
+// f32 fused 1x1 tail (va_conv_args.w2 in f32 mode): the tile's main-conv activations -- every output channel of the
+// conv (Cout <= BN), bias + SiLU applied, f32 in Cs [BM][BN + 4] -- contracted with the tail's weights as exact
+// three-term products: W2 pre-split on the host ([32 nb][Cout / 8][3][8] bf16, h / m / l per 8-channel group, the
+// w3 layout), each activation split here (split3_bf16), the six term products of 32 x 32 x 16 blocks accumulated in
+// f32 -- the arithmetic of the unfused 1x1 layer, in another order.  Wave w takes pixels 32 w .. 32 w + 31 and all
+// nb = ceil(c2 / 32) blocks of tail channels (c2 <= 96); + b2, SiLU if act2; then through LDS (the activations'
+// space, once every wave has read it) to 16-byte runs of consecutive float channels per pixel at a.y / a.ldy.
+constexpr int T3_TAIL_C2 = 96;
+template <int NT, int BM, int BN, typename RowFn>
+__device__ __forceinline__ void conv_tail32(const va_conv_args& a, unsigned char* smem, int tid, int lane,
+                                            RowFn orow) {
+    static_assert(BM == 32 * (NT / 64), "one 32-pixel block per wave");
+    constexpr int CW = BN + 4, CW2 = T3_TAIL_C2 + 4;
+    float* Cs = (float*)smem;
+    const int w = tid >> 6, r = lane & 31, g = lane >> 5;
+    const int K = a.Cout, nb = (a.c2 + 31) >> 5;
+    const __bf16* __restrict__ W2 = (const __bf16*)a.w2;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    f32x16 acc[3];
+#pragma unroll
+    for (int ib = 0; ib < 3; ++ib) acc[ib] = (f32x16){};
+    for (int k0 = 0; k0 < K; k0 += 16) {
+        const float* p = Cs + (32 * w + r) * CW + k0 + 8 * g;
+        bf16x8 bt[3];
+        split3_bf16(*(const u32x4*)p, *(const u32x4*)(p + 4), bt);
+#pragma unroll
+        for (int ib = 0; ib < 3; ++ib) {
+            if (ib < nb) {  // wave-uniform
+                const bf16x8* wp = (const bf16x8*)(W2 + ((int64_t)(32 * ib + r) * (K / 8) + k0 / 8 + g) * 24);
+                const bf16x8 at[3] = {wp[0], wp[1], wp[2]};
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+                    acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(at[TA[t]], bt[TB[t]], acc[ib], 0, 0, 0);
+            }
+        }
+    }
+    __syncthreads();  // every wave's activation reads are done: the tail's outputs reuse the space
+#pragma unroll
+    for (int ib = 0; ib < 3; ++ib) {
+        if (ib < nb) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int col = 32 * ib + 8 * k + 4 * g;  // v_mfma_f32_32x32x16 D layout: lane (r, g) = pixel r
+                const float4 bv = *(const float4*)(a.b2 + col);  // b2 is padded to the tail's Npad
+                float v0 = acc[ib][4 * k] + bv.x, v1 = acc[ib][4 * k + 1] + bv.y, v2 = acc[ib][4 * k + 2] + bv.z,
+                      v3 = acc[ib][4 * k + 3] + bv.w;
+                if (a.act2) {
+                    const f32x2 s01 = fz::silu2((f32x2){v0, v1}), s23 = fz::silu2((f32x2){v2, v3});
+                    v0 = s01[0];
+                    v1 = s01[1];
+                    v2 = s23[0];
+                    v3 = s23[1];
+                }
+                *(float4*)(Cs + (32 * w + r) * CW2 + col) = make_float4(v0, v1, v2, v3);
+            }
+        }
+    }
+    __syncthreads();
+    const int c4 = a.c2 / 4;
+    float* Y = (float*)a.y;
+    for (int c = tid; c < BM * c4; c += NT) {
+        const int pl = c / c4, cl = (c - pl * c4) * 4;
+        const int64_t orw = orow(pl);
+        if (orw >= 0) *(float4*)(Y + orw * a.ldy + cl) = *(const float4*)(Cs + pl * CW2 + cl);
+    }
 }
 
 template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false,
@@ -1230,11 +1304,15 @@ constexpr int T3H_HALO = T3H_HMAX * T3H_ROW;  // 19,584 B
 constexpr int T3H_NU = 2;                     // halo units (pixel, 8 channels) per thread
 static_assert(T3H_NU * T3H_NT >= 2 * T3H_HMAX, "halo units");
 // per channel-tile width: TNS = 4 -> 128 output channels (waves 2 x 2, each 64 pixels x 64 channels), TNS = 2 -> 64
-// (the narrow layers: waves 2 x 2, each 64 pixels x 32 channels)
-template <int TNS>
+// (the narrow layers: waves 2 x 2, each 64 pixels x 32 channels).  TPS = taps per K-step: a stage holds TPS taps'
+// weights of the chunk, one BN x 96-byte block per tap.  (TPS = 2 on the narrow tiles -- the wide tiles' 24 MFMAs per
+// wave and barrier -- measured neutral, 14.10 vs 14.11 ms per 64-frame forward, profiles/r04/conv3h_tps/; the
+// library instantiates TPS = 1 only)
+template <int TNS, int TPS = 1>
 struct T3HCfg {
     static constexpr int BN = 32 * TNS;
-    static constexpr int ASTAGE = BN * T3H_ROW;                   // 12 / 6 KiB
+    static constexpr int ABLK = BN * T3H_ROW;                     // one tap's weights of a chunk: 12 / 6 KiB
+    static constexpr int ASTAGE = TPS * ABLK;
     static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6)
     static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2)
     static constexpr int ZROW = T3H_NSA * ASTAGE + 2 * T3H_HALO;  // the zero row
@@ -1261,12 +1339,13 @@ __device__ __forceinline__ void t3h_unroll(F&& f) {
     }
 }
 
-template <int KH, int KW, int TNS, typename OutT>
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
 __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn, int ntiles, int lgw, int tiles_x) {
     extern __shared__ __align__(16) unsigned char smh[];
-    using Cfg = T3HCfg<TNS>;
+    using Cfg = T3HCfg<TNS, TPS>;
     constexpr int BM = T3H_BM, BN = Cfg::BN, NT = T3H_NT, WN = 2, CB = TNS / 2, T = KH * KW;
-    static_assert(T >= 2, "the halo is stored at a chunk's second step");
+    constexpr int S = (T + TPS - 1) / TPS;  // K-steps per chunk
+    static_assert(S >= 2, "the halo is stored at a chunk's second step");
     int bid = blockIdx.x;
     {
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
@@ -1300,20 +1379,25 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-        const int o = 1024 * (wid + (NT / 64) * j) + 16 * lane;
+        const int o = (1024 * (wid + (NT / 64) * j)) % Cfg::ABLK + 16 * lane;  // offset in the piece's tap block
         const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
         aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
     }
-    auto dmaA = [&](int kl, int s, bool live) {  // K-step kl = tap * nch + chunk into stage s; !live: zeros
+    // stage s <- the weights of taps TPS t .. of chunk c (kl_h = tap * nch + chunk, or -1: zeros); a piece's tap
+    // block is wave-uniform, so the per-tap source offset is a scalar select
+    auto dmaA = [&](int kl0, int kl1, int s) {
         unsigned char* base = stA(s);
-        const int soff = live ? kl * 96 : OOR;
+        const int so0 = kl0 >= 0 ? kl0 * 96 : OOR, so1 = kl1 >= 0 ? kl1 * 96 : OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
             const int P = wid + (NT / 64) * j;
             const bool real = Cfg::NP % 4 == 0 || P < Cfg::NP;  // wave-uniform: scalar selects, no branch
+            const int soff = TPS > 1 && P * 1024 >= Cfg::ABLK ? so1 : so0;
             t3_dma16(W3, w3_bytes, real ? base + P * 1024 : smh + Cfg::SINK, aoff[j], real ? soff : OOR);
         }
     };
+    // the kl of tap slot h of step t of chunk c (-1 past the taps or the chunks)
+    auto klof = [&](int c, int t, int h) { return (c < nch && TPS * t + h < T) ? (TPS * t + h) * nch + c : -1; };
 
     // ---- halo units: u = tid + 256 j -> halo pixel u >> 1 (row hy, column hx), channels 8 (u & 1) .. of a chunk
     const void* zpage = (const void*)g_zero_page;
@@ -1375,10 +1459,9 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     for (int i = 0; i < CB; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nsteps = nch * T;
-    // prologue: A of steps 0, 1 (tap 0 / 1 of chunk 0), chunk 0's halo staged; the zero row
-    dmaA(0, 0, true);
-    dmaA(nch, 1, nsteps > 1);
+    // prologue: A of steps 0, 1 of chunk 0, chunk 0's halo staged; the zero row
+    dmaA(klof(0, 0, 0), klof(0, 0, 1), 0);
+    dmaA(klof(0, 1, 0), klof(0, 1, 1), 1);
     __builtin_amdgcn_sched_barrier(0);
     loadH(0, true);
     __builtin_amdgcn_sched_barrier(0);
@@ -1391,50 +1474,55 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     // 24 MFMAs, at t == 1 the next chunk's halo stored; then the counted wait for A(k + 1) and a raw barrier
     auto step = [&](const int c, auto Tc) {
         constexpr int t = decltype(Tc)::value;
-        constexpr int ky = t / KW, kx = t % KW;
-        const int k = c * T + t;
+        const int k = c * S + t;
         {
-            constexpr int t2 = (t + 2) % T, dc = (t + 2) / T;
-            const int c2 = c + dc;
-            dmaA(t2 * nch + c2, (k + 2) % T3H_NSA, c2 < nch);  // stage last read at step k - 1
+            constexpr int t2 = (t + 2) % S, dc = (t + 2) / S;
+            dmaA(klof(c + dc, t2, 0), klof(c + dc, t2, 1), (k + 2) % T3H_NSA);  // stage last read at step k - 1
         }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (t == 0) {
             loadH(c + 1, c + 1 < nch);
             __builtin_amdgcn_sched_barrier(0);
         }
-        bf16x8 ap[CB][3], bp[2][3];
-        const unsigned char* as_ = stA(k % T3H_NSA);
         const unsigned char* hs_ = halo(c & 1);
+        t3h_unroll<TPS>([&](auto Hc) {
+            constexpr int h = decltype(Hc)::value, tap = TPS * t + h;
+            if constexpr (tap < T) {
+                constexpr int ky = tap / KW, kx = tap % KW;
+                bf16x8 ap[CB][3], bp[2][3];
+                const unsigned char* as_ = stA(k % T3H_NSA) + h * Cfg::ABLK;
 #pragma unroll
-        for (int ib = 0; ib < CB; ++ib) {
-            const int row = wn * 32 * CB + 32 * ib + r32, sw = (row >> 3) & 1;
+                for (int ib = 0; ib < CB; ++ib) {
+                    const int row = wn * 32 * CB + 32 * ib + r32, sw = (row >> 3) & 1;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
-        }
+                    for (int p = 0; p < 3; ++p)
+                        ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
+                }
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
-            const int hy = bpy[jb] + ky, hx = bpx[jb] + kx;
-            const unsigned char* rp = (vy[jb] >> ky) & 1 ? hs_ + (hy * HW + hx) * T3H_ROW : smh + Cfg::ZROW;
-            const int sw = (hy ^ ((hx >> 3) & xm)) & 1;
+                for (int jb = 0; jb < 2; ++jb) {
+                    const int hy = bpy[jb] + ky, hx = bpx[jb] + kx;
+                    const unsigned char* rp = (vy[jb] >> ky) & 1 ? hs_ + (hy * HW + hx) * T3H_ROW : smh + Cfg::ZROW;
+                    const int sw = (hy ^ ((hx >> 3) & xm)) & 1;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(rp + 16 * ((3 * g32 + p) ^ sw));
-        }
+                    for (int p = 0; p < 3; ++p) bp[jb][p] = *(const bf16x8*)(rp + 16 * ((3 * g32 + p) ^ sw));
+                }
 #pragma unroll
-        for (int tt = 0; tt < 6; ++tt)
+                for (int tt = 0; tt < 6; ++tt)
 #pragma unroll
-            for (int ib = 0; ib < CB; ++ib)
+                    for (int ib = 0; ib < CB; ++ib)
 #pragma unroll
-                for (int jb = 0; jb < 2; ++jb)
-                    acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[tt]], bp[jb][TB[tt]], acc[ib][jb],
-                                                                          0, 0, 0);
+                        for (int jb = 0; jb < 2; ++jb)
+                            acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[ib][TA[tt]], bp[jb][TB[tt]],
+                                                                                  acc[ib][jb], 0, 0, 0);
+            }
+        });
         if constexpr (t == 1) storeH((c + 1) & 1);  // the buffer chunk c - 1 used; past the last chunk: unread zeros
         // A(k + 1) landed: younger than its DMAs are this step's NA DMAs and the halo loads of step t == 0 (issued in
         // this step at t == 0, in the previous one at t == 1)
         t3_waitvm<(t == 0 || t == 1) ? NA + 2 * T3H_NU : NA>();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
-    for (int c = 0; c < nch; ++c) t3h_unroll<T>([&](auto Tc) { step(c, Tc); });
+    for (int c = 0; c < nch; ++c) t3h_unroll<S>([&](auto Tc) { step(c, Tc); });
     t3_waitvm<0>();  // the zero-page DMAs past the last step land before the epilogue reuses the LDS
     __syncthreads();
 
@@ -1447,7 +1535,14 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
         return m >= 0 ? conv_out_row(a, m, cls) : -1;
     };
     auto pcol = [](int c) { return t3h_perm(c); };
-    conv_epilogue32<NT, BM, BN, TNS, OutT>(a, acc, smh, n0, wm, wn, tid, lane, orow, mrow, pcol, cls);
+    if constexpr (TAIL) {  // every channel of the conv is in this tile (ntn == 1): the 1x1 tail runs here
+        static_assert(BM * (T3_TAIL_C2 + 4) * 4 <= Cfg::LDS, "tail staging inside the workgroup's LDS");
+        conv_epilogue32_fill<BN, TNS>(a, acc, smh, n0, wm, wn, lane, mrow, pcol, cls);
+        __syncthreads();
+        conv_tail32<NT, BM, BN>(a, smh, tid, lane, orow);
+    } else {
+        conv_epilogue32<NT, BM, BN, TNS, OutT>(a, acc, smh, n0, wm, wn, tid, lane, orow, mrow, pcol, cls);
+    }
 }
 
 // ----------------------------------------------------------------------------------------- conv v4 (bf16, Cout >= 256)
@@ -2790,18 +2885,20 @@ int conv3h_lgw(const va_conv_args& a) {
     return best;
 }
 
-bool use_conv3h(const va_conv_args& a) {
-    if (conv3h_off() || a.stride != 1 || a.H != a.Ho || a.W != a.Wo) return false;
+bool conv3h_shape_ok(const va_conv_args& a) {
+    if (a.stride != 1 || a.H != a.Ho || a.W != a.Wo) return false;
     const bool taps = a.mode == 0 ? (a.kh == 3 && a.kw == 3 && a.pad == 1) : (a.mode == 2 && a.kh == 2 && a.kw == 2);
     return taps && conv3h_lgw(a) >= 0 && (int64_t)a.N * a.Ho < (1 << 24);
 }
 
-template <int KH, int KW, int TNS, typename OutT>
+bool use_conv3h(const va_conv_args& a) { return !conv3h_off() && conv3h_shape_ok(a); }
+
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
 hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
-    using Cfg = T3HCfg<TNS>;
+    using Cfg = T3HCfg<TNS, TPS>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT>,
+        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -2811,8 +2908,8 @@ hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
     const int tiles_x = (a.Wo + tw - 1) / tw, tiles_y = (a.N * a.Ho + th - 1) / th;
     const int ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = tiles_x * tiles_y * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a, ntn, ntiles,
-                       lgw, tiles_x);
+    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a, ntn,
+                       ntiles, lgw, tiles_x);
     return hipGetLastError();
 }
 
@@ -2832,6 +2929,23 @@ template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
     if (use_conv3h(a)) return a.mode == 2 ? launch_conv3h_v<2, 2, 4, OutT>(a, st) : launch_conv3h_v<3, 3, 4, OutT>(a, st);
     return launch_conv3t_v<2, 2, OutT>(a, st);
+}
+
+// f32 fused 1x1 tail (va_conv_args.w2 with w3): the conv on conv3h with the whole channel set in one tile (Cout 64 on
+// 64-channel tiles, 128 on 128-channel ones; the proto's sub-pixel fold as mode 2), the tail in its epilogue
+bool conv3h_tail_ok(const va_conv_args& a) {
+    if (!a.w3 || !a.w2 || !a.b2 || a.res || a.xu || a.c2 <= 0 || a.c2 > T3_TAIL_C2 || a.c2 % 4 || a.ldy % 4 ||
+        ((uintptr_t)a.y & 15) || (a.Cout != 64 && a.Cout != 128) || (a.mode == 2 && a.Cout != 128) ||
+        !conv3h_shape_ok(a))  // (a planned fused op runs on conv3h whatever VA_CONV3H says: the plan has no other form)
+        return false;
+    return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.Npad % 128 == 0 && a.ldx % 4 == 0 &&
+           ((uintptr_t)a.x & 15) == 0;
+}
+
+hipError_t launch_conv3h_tail(const va_conv_args& a, hipStream_t st) {
+    if (!conv3h_tail_ok(a)) return hipErrorInvalidValue;
+    if (a.mode == 2) return launch_conv3h_v<2, 2, 4, float, true>(a, st);
+    return a.Cout == 128 ? launch_conv3h_v<3, 3, 4, float, true>(a, st) : launch_conv3h_v<3, 3, 2, float, true>(a, st);
 }
 
 template <int SPL, typename OutT>
@@ -2863,6 +2977,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
                 return launch_conv2<2, 2, 4, OutT>(a, st);
             }
         }
+        if constexpr (sizeof(T) == 4) return launch_conv3h_tail(a, st);
         return hipErrorInvalidValue;
     }
     if constexpr (sizeof(T) == 2) {
@@ -2960,8 +3075,13 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     if (a->mode == 2 && (a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res || a->Cout <= 64 || a->Kpad % ks))
         return VA_ERR_ARG;
     // bias4: mode 2 only -- bf16 through conv2's fused-tail path, f32 through the plain epilogue
-    if (a->bias4 && (a->mode != 2 || (bf ? (!a->w2 || a->Cout != 128) : a->w2 != nullptr))) return VA_ERR_ARG;
-    if (a->w2 && (a->dtype != VA_DTYPE_BF16 || (a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode == 1 ||
+    if (a->bias4 && (a->mode != 2 || (bf && (!a->w2 || a->Cout != 128)))) return VA_ERR_ARG;
+    // f32 fused tail: conv3h's conditions (launch_conv3h_tail) are checked at dispatch
+    if (a->w2 && a->dtype == VA_DTYPE_F32 &&
+        (!a->w3 || a->res || !a->b2 || a->c2 <= 0 || a->c2 > T3_TAIL_C2 || a->c2 % 4 || a->mode == 1 ||
+         (a->Cout != 64 && a->Cout != 128)))
+        return VA_ERR_ARG;
+    if (a->w2 && a->dtype != VA_DTYPE_F32 && ((a->Cout != 32 && a->Cout != 64 && a->Cout != 128) || a->mode == 1 ||
                   (a->mode == 2 && a->Cout != 128) ||
                   a->res || !a->b2 || a->c2 <= 0 || a->c2 > 16 * (a->Cout == 128 ? TAIL_C2F : DN_TAIL_C2F) ||
                   a->c2 % 4 || a->Kpad % (a->Cout == 128 ? BK2 : 32) ||
