@@ -446,7 +446,7 @@ def dealer_rate(args, dev, frames_n: int = 256) -> dict:
     frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
     with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)), list(range(G)),
                      640, 640, slots=4) as d:
-        for _ in d.map(frames[i % 16] for i in range(4 * G)):  # warm: plans, first launches
+        for _ in d.map(frames[i % 16] for i in range(32 * G)):  # warm: plans, first launches, lanes' streams
             pass
         t0 = time.perf_counter()
         answers = sum(a != [] for a in d.map(frames[i % 16] for i in range(frames_n)))
