@@ -2841,21 +2841,14 @@ bool conv3t_off() {
 }
 
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
-bool use_conv3h(const va_conv_args& a);
-
-// VA_F32_SMALL (A/B timing, read per launch): 0 = a layer conv2 would split over K (batch-1 shapes) stays on conv2;
-// 1 = the stride-1 multi-tap layers go to conv3h anyway; 2 = every three-plane-eligible layer goes to conv3h / conv3t
-int f32_small() {
-    const char* e = getenv("VA_F32_SMALL");
-    return e ? e[0] - '0' : 0;
-}
-
 bool use_conv3t(const va_conv_args& a) {
     if (!a.w3 || conv3t_off()) return false;
-    int kper;  // a layer conv2 would split over K (batch-1 shapes) stays on conv2 (see f32_small)
+    // a layer conv2 would split over K (batch-1 shapes) stays on conv2: on the three-plane kernels instead the batch-1
+    // f32 s-seg forward took 1.77 ms (stride-1 3x3s on conv3h) / 2.08 ms (every eligible layer) against 1.29
+    // (profiles/r04/batch1/small_ab.log)
+    int kper;
     const int t2 = ((a.M + 127) / 128) * ((a.Cout + 127) / 128) * (a.mode == 2 ? 4 : 1);
-    const int sm = f32_small();
-    if (sm < 2 && !(sm == 1 && use_conv3h(a)) && conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper) > 1) return false;
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper) > 1) return false;
     return (a.mode == 0 || a.mode == 2) && a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K &&
            a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
@@ -2930,7 +2923,7 @@ bool use_conv3h_narrow(const va_conv_args& a) {
     if (!a.w3 || conv3t_off() || a.mode != 0 || a.Cout <= 32 || a.Cout > 64 || !use_conv3h(a)) return false;
     int kper;
     const int t2 = ((a.M + 127) / 128) * ((a.Cout + 63) / 64);
-    if (f32_small() < 1 && conv2_ksplit(a, t2, a.Kpad / 32, 128, 64, &kper) > 1) return false;
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 64, &kper) > 1) return false;
     return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.Npad % 64 == 0 && a.ldx % 4 == 0 &&
            ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
