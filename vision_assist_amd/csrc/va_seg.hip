@@ -2695,6 +2695,9 @@ int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* 
     *kper = nk;
     const char* e = getenv("VA_SPLITK");
     if ((e && e[0] == '0') || !a.ws || !a.wcnt || tiles >= 128 || nk < 4 || tiles > a.ncnt) return 1;
+    // cost model (us): K-steps per slice x ts + tw + tc per slice.  Swept in round 4 at batch 1 (tc 0.75 / 3, ts x1.43,
+    // tiles x ks up to 512): the f32 s-seg and bf16 n-seg forwards within 1-2 % of these constants or slower
+    // (profiles/r04/batch1/splitk_sweep.log)
     const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f, tw = 1.0f, tc = 1.5f;
     int best = 1;
     float bt = nk * ts;
