@@ -300,6 +300,20 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 //     chunks are fetched from a zeroed device page.
 constexpr int BK2 = 64;
 __device__ __attribute__((aligned(16))) unsigned int g_zero_page[8];  // 32 zero bytes (conv3t reads two 16-byte words)
+
+// Phase clocks of conv2_kernel (diagnostic build only, -DVA_CONV2_STAMPS, tools/conv2_phases.py): per workgroup the
+// shader clock at its start, after the first stage landed, after the K-loop, after the split-K slab and arrival,
+// after the combine, at its end, and the 100 MHz real-time clock at start / end; lane 0's vector store.
+#ifdef VA_CONV2_STAMPS
+constexpr int C2S_BLOCKS = 4096, C2S_PTS = 8;
+__device__ unsigned long long g_c2s[C2S_BLOCKS][C2S_PTS];
+#define C2S(pt, v)                                                                          \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && blockIdx.x < C2S_BLOCKS) g_c2s[blockIdx.x][pt] = (v);      \
+    } while (0)
+#else
+#define C2S(pt, v)
+#endif
 // store sink: masked-out lanes of an epilogue whose store count must stay fixed (counted vmcnt) write here
 __device__ __attribute__((aligned(16))) unsigned int g_sink[64 * 4];
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -753,6 +767,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     auto As = [&](int s) { return (T*)(smem + s * Cfg::STAGE); };
     auto Bs = [&](int s) { return (T*)(smem + s * Cfg::STAGE + BN * RS * (int)sizeof(T)); };
 
+    C2S(0, __builtin_amdgcn_s_memtime());
+    C2S(6, __builtin_amdgcn_s_memrealtime());
     int bid = blockIdx.x;
     {
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
@@ -926,6 +942,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         CONV2_STORE(0);
     }
     __syncthreads();
+    C2S(1, __builtin_amdgcn_s_memtime());
     const int fr = lane & 15, fq = lane >> 4;
     for (int kt = kt0; kt < kt1; ++kt) {
         const int s = (kt - kt0) & 1;
@@ -1022,6 +1039,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_LOAD
 #undef CONV2_STORE
 #undef CONV2_DMA
+    C2S(2, __builtin_amdgcn_s_memtime());
 
     {
         if (ksplit > 1) {
@@ -1051,7 +1069,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             __syncthreads();
             const bool last = last_s[0] != 0;
             __syncthreads();  // the flag is read before the epilogue reuses the LDS
-            if (!last) return;
+            C2S(3, __builtin_amdgcn_s_memtime());
+            if (!last) {
+                C2S(5, __builtin_amdgcn_s_memtime());
+                C2S(7, __builtin_amdgcn_s_memrealtime());
+                return;
+            }
             const f32x4* sl = (const f32x4*)a.ws + sbase + tid;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) acc[q / 4][q % 4] = sl[q * NT];
@@ -1061,6 +1084,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             }
         }
     }
+    C2S(4, __builtin_amdgcn_s_memtime());
 
     auto orow = [&](int pl) -> int64_t {
         const int m = m0 + pl;
@@ -1073,6 +1097,8 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
         }
     }
     conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
+    C2S(5, __builtin_amdgcn_s_memtime());
+    C2S(7, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------------ conv3t (f32 mode, three-plane K-loop)
@@ -3041,6 +3067,19 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
 }  // namespace
 
 extern "C" {
+
+#ifdef VA_CONV2_STAMPS
+// diagnostic build: copy (and optionally clear) conv2_kernel's phase clocks, [C2S_BLOCKS][8] uint64
+int va_conv2_stamps(unsigned long long* out, int clear) {
+    if (hipDeviceSynchronize() != hipSuccess) return VA_ERR_HIP;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c2s), sizeof(g_c2s)) != hipSuccess) return VA_ERR_HIP;
+    if (clear) {
+        static unsigned long long z[C2S_BLOCKS][C2S_PTS];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_c2s), z, sizeof(z)) != hipSuccess) return VA_ERR_HIP;
+    }
+    return VA_OK;
+}
+#endif
 
 int va_seg_conv(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w || !a->bias || !a->y || a->M <= 0 || a->Kpad % BK || a->Cin <= 0) return VA_ERR_ARG;
