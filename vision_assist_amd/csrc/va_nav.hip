@@ -954,8 +954,20 @@ volatile int32_t* verdict_word(hipStream_t st) {
 
 size_t astar_lds(int nodes) { return ASTAR_TABLES + (size_t)nodes * (8 + 8 + 4 + 2 + 2 + 2 + 1) + 16; }
 
-// speculative rounds over `nslots` query slots
-int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out) {
+// the Jaccard / subset filter of a va_nav_run batch (nav_dedupe_kernel's launch)
+struct DedupeLaunch {
+    uint8_t* queries;
+    int64_t query_bytes, off_q_path;
+    int B, qpf, nodes;
+    size_t lds;
+};
+
+// speculative rounds over `nslots` query slots.  With `dd` the dedupe kernel is enqueued behind every round's
+// validation, before the host waits for the round's verdict: a round that is final (the common case) then needs no
+// launch after the wait; a round that is re-run gets its dedupe again behind the next one (the filter reads the
+// query records afresh and rewrites every unique / order field, so only the last round's counts)
+int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out,
+                 const DedupeLaunch* dd = nullptr) {
     size_t lds = astar_lds(a.LR * a.LC);
     if (lds > 65536 &&
         hipFuncSetAttribute((const void*)nav_astar_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -977,6 +989,11 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
         hipLaunchKernelGGL(nav_validate_kernel, dim3(1), dim3(VAL_THREADS), 0, st, a.starts, a.qwork, a.query_bytes,
                            a.nslots, slot0, seen, ctrl);
         if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
+        if (dd) {
+            hipLaunchKernelGGL(nav_dedupe_kernel, dim3(dd->B), dim3(64), dd->lds, st, dd->queries, dd->query_bytes,
+                               dd->off_q_path, dd->qpf, dd->nodes);
+            if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
+        }
         *rerun_h = -2;
         if (hipMemcpyAsync((void*)rerun_h, ctrl, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
             return VA_ERR_HIP;
@@ -1080,15 +1097,14 @@ int va_nav_run(void* stream, const uint8_t* cells, const int32_t* rects, int32_t
     aa.LR = d.LR;
     aa.LC = d.LC;
     aa.nslots = B * d.MAXPK;
+    const int words = (d.NODES + 63) / 64;
+    const DedupeLaunch dd{w.queries, d.query_bytes, d.off_q_path, B, d.MAXPK, d.NODES,
+                          (size_t)d.MAXPK * words * 8 + 8 * (size_t)d.MAXPK + 16};
     int32_t r = 0;
-    int rc = astar_rounds(st, aa, w.ctrl, seen, &r);
+    int rc = astar_rounds(st, aa, w.ctrl, seen, &r, &dd);
     if (rc != VA_OK) return rc;
     if (rounds) *rounds = r;
-    int words = (d.NODES + 63) / 64;
-    size_t lds = (size_t)d.MAXPK * words * 8 + 8 * (size_t)d.MAXPK + 16;
-    hipLaunchKernelGGL(nav_dedupe_kernel, dim3(B), dim3(64), lds, st, w.queries, d.query_bytes, d.off_q_path,
-                       d.MAXPK, d.NODES);
-    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
+    return VA_OK;
 }
 
 int64_t va_nav_query_bytes(int32_t nodes) {
