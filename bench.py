@@ -303,7 +303,8 @@ class Run:
         rl = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
               "frac": round(achieved / peak, 5), "traffic": None,
               "kernel": f"the {launches:.0f} conv-family launches of one YOLOv8{self.scale}-seg forward "
-                        + (f"(f32 convs on conv3t_kernel's / conv2_kernel's bf16 three-term forms; model.0 on conv0_f32m)" if terms else
+                        + (f"(f32 convs on conv3h_kernel's / conv3t_kernel's / conv2_kernel's bf16 three-term forms; "
+                           "model.0 on conv0_f32m)" if terms else
                            f"({self.dtype} MFMA GEMM kernels: conv/conv2/conv4/conv_dn/conv_patch/pw/c2f/stem)"),
               "flops_per_launch": round(fl_exec), "flops_per_launch_def": "executed GEMM FLOPs of the plan / launch",
               "avg_launch_us": round(avg_s * 1e6, 3),

@@ -15,6 +15,7 @@ if [ -z "$SKIP_TESTS" ]; then
   step smoke
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 fi
+if [ -z "$SKIP_BENCH" ]; then
 step bench
 timeout -k 10 400 python -u bench.py --steps "$STEPS" > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
@@ -24,15 +25,16 @@ cat "$OUT/bench_noprof.json"
 step layers
 timeout -k 10 300 python -u tools/seg_layer_profile.py --batch 64 --iters 10 --json "$OUT/layers.json" > "$OUT/layers.log" 2>&1
 tail -1 "$OUT/layers.log"
+fi
 step rocprof-stats
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 > "$OUT/rocprof_stats.log" 2>&1
+  python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --extras none > "$OUT/rocprof_stats.log" 2>&1
 if [ -z "$SKIP_PMC" ]; then
   step pmc-fetch
   timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof > "$OUT/pmc_fetch.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > "$OUT/pmc_fetch.log" 2>&1
   step pmc-write
   timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof > "$OUT/pmc_write.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > "$OUT/pmc_write.log" 2>&1
 fi
 step done
