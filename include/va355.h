@@ -135,6 +135,19 @@ int va_nav_sample_cells(void* stream, const uint8_t* masks, int64_t pitch, int32
 int va_nav_run(void* stream, const uint8_t* cells, const int32_t* rects, int32_t B, int32_t H, int32_t W,
                uint64_t* seen, void* work, int32_t* rounds);
 
+/* The records va_nav_run leaves at the start of its workspace for B frames: B frame records of
+ * va_nav_dims.frame_bytes, then (16-byte aligned) B * MAXPK query records of query_bytes -- bytes
+ * [0, va_nav_records_bytes) of `work`. */
+int64_t va_nav_records_bytes(int32_t B, int32_t H, int32_t W);
+
+/* va_nav_run with the records read back: host_records (host memory of >= va_nav_records_bytes(B, H, W) bytes;
+ * pinned, or the copy is staged and synchronous) receives them on `stream` behind each speculative round's
+ * kernels and ahead of that round's verdict copy, so the call returns with the final round's records on the
+ * host and the caller needs no second synchronisation (FrameProcessor.py:325-347 reads every one of them on the
+ * host right after).  host_records NULL = va_nav_run. */
+int va_nav_run_rb(void* stream, const uint8_t* cells, const int32_t* rects, int32_t B, int32_t H, int32_t W,
+                  uint64_t* seen, void* work, int32_t* rounds, void* host_records, int64_t host_bytes);
+
 /* Standalone A* over an explicit lattice (PathFinder.find_path surface, PathFinder.py:119-186)
  * for Q queries that share one lattice of LR x LC nodes.
  *   node_flags  device uint8 [LR*LC] (VA_NODE_* bits; multiplicity in bits 3-4)
@@ -473,6 +486,10 @@ int va_destroy(va_handle h);
 int va_handle_device(va_handle h, int32_t* device);
 int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
              int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds);
+/* va_frame whose grid stage is va_nav_run_rb: the nav records land in host_records (NULL = va_frame). */
+int va_frame_rb(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
+                int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds, void* host_records,
+                int64_t host_bytes);
 
 /* Out-of-range state the kernels rejected instead of faulting (a rect no frame holds, an A* node outside the
  * lattice, a traced pixel outside its image, candidate counts past the anchors -- csrc/va_diag.h lists the

@@ -113,3 +113,64 @@ def test_path_model_fixtures_match_reference():
         p = Path(grids=cells, total_cost=100, path_type="path")
         assert _structure(p) == _golden_structure(f), k
         assert _hx(p.angle) == _hx(unhex(f["angle"])) and _hx(p.length) == _hx(unhex(f["length"])), k
+
+
+def _naive_analyser(clock):
+    """A PathAnalyser whose history handling is the reference's literal form: every entry scanned for pairs and
+    the dict rebuilt per call (PathAnalyser.py:185-230, :375-382)."""
+    from vision_assist_amd.PathAnalyser import _HISTORY_MS, _PAIR_WINDOW_MS, PathAnalyser
+    pa = object.__new__(PathAnalyser)
+    pa.paths, pa.previous_instructions, pa.instructions, pa.clock, pa._hist = [], {}, [], clock, None
+    pa._recent = lambda previous, now: [(ts, v) for ts, v in previous.items() if now - ts < _PAIR_WINDOW_MS]
+
+    def remember(now, ins):
+        pa.previous_instructions[now] = ins
+        pa.previous_instructions = {ts: v for ts, v in pa.previous_instructions.items() if now - ts <= _HISTORY_MS}
+    pa._remember = remember
+    return pa
+
+
+def test_history_window_equals_full_scan():
+    """PathAnalyser's history handling (pairs from the suffix inside the pair window, expired entries deleted from
+    the front while the keys arrive in order; the full scan otherwise) against the literal full-scan form, on the
+    golden frames' paths at drop-in call rates (2-3 ms apart: thousands of history entries), with repeated
+    timestamps, clock steps backwards and outside resets of the history: the same answers, history keys and
+    history dangers at every frame."""
+    import random
+
+    from vision_assist_amd.models import Path
+    from vision_assist_amd.PathAnalyser import path_analyser
+    rnd = random.Random(5)
+    frames = []
+    for seq in load_goldens()["sequences"]:
+        for fr in seq["frames"]:
+            if fr.get("error") or fr.get("empty") or not fr["paths"]:
+                continue
+            pens = {}
+            for row in fr["rows"]:
+                for c, p in enumerate(row["pen"]):
+                    pens[(row["x0"] + 20 * c, row["y"])] = unhex(p)
+            frames.append((fr["H"], fr["W"], [([(x, y) for x, y in gp["coords"]], unhex(gp["cost"]), pens)
+                                               for gp in fr["paths"]]))
+    clock = {"t": 2_000_000.0}
+    naive = _naive_analyser(lambda: clock["t"])
+    fast = path_analyser
+    saved = (fast.clock, fast.previous_instructions, fast._hist)
+    fast.clock, fast.previous_instructions = (lambda: clock["t"]), {}
+    try:
+        for k in range(4000):
+            H, W, gps = frames[k % len(frames)]
+            r = rnd.random()
+            clock["t"] += 0.0 if r < 0.05 else -0.4 if r < 0.055 else 0.3 if r < 0.06 else rnd.uniform(0.001, 0.003)
+            if k in (1500, 2600):
+                fast.previous_instructions, naive.previous_instructions = {}, {}
+            mk = lambda: [Path(grids=[_grid(x, y, pens) for x, y in cs], total_cost=cost, path_type="path")
+                          for cs, cost, pens in gps]
+            assert fast(H, W, mk()) == naive(H, W, mk()), k
+            assert list(fast.previous_instructions) == list(naive.previous_instructions), k
+            if k % 97 == 0:
+                assert [[i.danger for i in v] for v in fast.previous_instructions.values()] == \
+                       [[i.danger for i in v] for v in naive.previous_instructions.values()], k
+        assert len(naive.previous_instructions) > 1000
+    finally:
+        fast.clock, fast.previous_instructions, fast._hist = saved

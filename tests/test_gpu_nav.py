@@ -9,6 +9,8 @@
 * against the oracle (oracle/nav.py) on seeded procedural corridors at
   640x640, 1280x1280 and 720x1280 (warm, order-dependent sequences).
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -37,30 +39,54 @@ def _inputs(frames):
     return cells, rects
 
 
-@pytest.mark.parametrize("mode", ["batch", "single"])
+@pytest.mark.parametrize("mode", ["batch", "batch_rb", "single", "single_rb"])
 def test_nav_matches_reference_goldens(mode):
+    """batch / single: va_nav_run + NavBatch's asynchronous copy; *_rb: va_nav_run_rb (records copied to the host
+    inside the call, re-copied by every re-run round -- a whole sequence as one batch takes several)"""
     d = load_goldens()
-    nframes = nq = 0
+    rb = mode.endswith("_rb")
+    nframes = nq = rerun = 0
     for seq in d["sequences"]:
         frames = seq["frames"]
         H, W = frames[0]["H"], frames[0]["W"]
         eng = _engine(H, W, len(frames))
         seen_dev = _seen()
         seen = set()
-        if mode == "batch":
+        if mode.startswith("batch"):
             cells, rects = _inputs(frames)
-            res = eng.run(cells, rects, seen_dev)
+            res = eng.run(cells, rects, seen_dev, readback=rb)
+            rerun += res.rounds > 1
             for i, fr in enumerate(frames):
                 seen = compare_golden_frame(res.frame(i), fr, seen)
         else:
             for fr in frames:
                 cells, rects = _inputs([fr])
-                res = eng.run(cells, rects, seen_dev)
+                res = eng.run(cells, rects, seen_dev, readback=rb)
                 seen = compare_golden_frame(res.frame(0), fr, seen)
         assert seen_dev.keys() == seen
         nframes += len(frames)
         nq += sum(len(f.get("queries", [])) for f in frames)
     assert nframes == 372 and nq == 392
+    if mode == "batch_rb":
+        assert rerun > 0  # the re-copy behind a re-run round is exercised
+
+
+def test_nav_run_rb_checks_host_size():
+    from vision_assist_amd import _lib
+    eng = _engine(640, 640, 2)
+    lib = _lib.load()
+    n = int(lib.va_nav_records_bytes(2, 640, 640))
+    d = eng.dims
+    assert n == ((2 * d.frame_bytes + 15) & ~15) + 2 * d.MAXPK * d.query_bytes
+    assert lib.va_nav_records_bytes(0, 640, 640) == _lib.VA_ERR_ARG
+    cells = torch.zeros((2, d.LR, d.LC), dtype=torch.uint8, device="cuda")
+    rects = torch.zeros((2, 4), dtype=torch.int32, device="cuda")
+    rec = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    rounds = ctypes.c_int32(0)
+    args = (None, cells.data_ptr(), rects.data_ptr(), 2, 640, 640, _seen().t.data_ptr(), eng.work.data_ptr(),
+            ctypes.byref(rounds), rec.data_ptr())
+    assert lib.va_nav_run_rb(*args, n - 1) == _lib.VA_ERR_ARG
+    assert lib.va_nav_run_rb(*args, n) == _lib.VA_OK
 
 
 def _oracle_compare(nf, out, seen_before: set, pf_keys_after: list, src):

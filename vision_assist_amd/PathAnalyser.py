@@ -41,6 +41,7 @@ class PathAnalyser:
             self.previous_instructions: dict[int, list[Instruction]] = {}
             self.instructions: list[Instruction] = []
             self.clock = clock or time.time
+            self._hist = None  # (dict, len, keys non-decreasing in insertion order, newest key): _hist_order
         elif clock is not None:
             self.clock = clock
 
@@ -85,10 +86,57 @@ class PathAnalyser:
     def _analyse_instructions(self, instructions: list[Instruction]) -> list[Instruction]:  # :145-156 (identity)
         return instructions
 
+    def _recent(self, previous, now):
+        """The history entries a pair can come from (dt = now - ts < the pair window: both of the pair tests
+        require it), in insertion order.  The reference visits every entry of its 5 s history per call (O(calls
+        per 5 s): ~2,500 entries at 500 calls/s); when the history's keys were inserted in non-decreasing order
+        and ``now`` is not behind the newest, the candidates are a suffix, found from the end."""
+        mono, last = self._hist_order()
+        if previous is self.previous_instructions and mono and previous and now >= last:
+            tail = []
+            for ts in reversed(previous):
+                if now - ts >= _PAIR_WINDOW_MS:
+                    break
+                tail.append(ts)
+            return [(ts, previous[ts]) for ts in reversed(tail)]
+        return [(ts, v) for ts, v in previous.items() if now - ts < _PAIR_WINDOW_MS]
+
+    def _remember(self, now, instructions):
+        """previous_instructions[now] = instructions, then the entries older than the 5 s history dropped
+        (:375-382).  The reference rebuilds the dict per call; with non-decreasing keys the expired entries are a
+        prefix, deleted from the front (same entries kept, same order)."""
+        mono, last = self._hist_order()
+        prev = self.previous_instructions
+        if now not in prev:
+            mono = mono and (last is None or now >= last)
+            last = now
+        prev[now] = instructions
+        if mono:
+            while True:
+                ts = next(iter(prev))
+                if now - ts <= _HISTORY_MS:
+                    break
+                del prev[ts]
+            self._hist = (prev, len(prev), True, last)
+        else:
+            self.previous_instructions = {ts: v for ts, v in prev.items() if now - ts <= _HISTORY_MS}
+            self._hist = None
+
+    def _hist_order(self):
+        """(keys non-decreasing in insertion order, newest key) of previous_instructions, recomputed whenever the
+        dict is not the one _remember last left (replaced or resized from outside, e.g. a test's reset)."""
+        prev = self.previous_instructions
+        h = self._hist
+        if h is None or h[0] is not prev or h[1] != len(prev):
+            keys = list(prev)
+            h = self._hist = (prev, len(prev), all(a <= b for a, b in zip(keys, keys[1:])),
+                              keys[-1] if keys else None)
+        return h[2], h[3]
+
     def _pairs(self, previous, current, now):
         """Previous/current instruction pairs that describe the same feature (:185-230)."""
         pairs = []
-        for ts, prev_list in previous.items():
+        for ts, prev_list in self._recent(previous, now):
             for p in prev_list:
                 for c in current:
                     if p.instruction_type == "bearing" and c.instruction_type != "bearing":
@@ -161,8 +209,7 @@ class PathAnalyser:
             self.instructions, key=lambda i: (_TYPE_RANK[i.instruction_type], _DANGER_RANK[i.danger]))
         self.filtered_instructions = self._analyse_previous_instructions(self.previous_instructions,
                                                                           self.instructions, now)
-        self.previous_instructions[now] = self.unfiltered_instructions
-        self.previous_instructions = {ts: v for ts, v in self.previous_instructions.items() if now - ts <= _HISTORY_MS}
+        self._remember(now, self.unfiltered_instructions)
         return self.determine_final_instruction(self.filtered_instructions).value
 
 

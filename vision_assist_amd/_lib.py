@@ -49,6 +49,8 @@ SIGNATURES = [
     ("va_nav_workspace_bytes", I64, [I32, I32, I32]),
     ("va_nav_sample_cells", I32, [P, P, I64, I32, I32, I32, P]),
     ("va_nav_run", I32, [P, P, P, I32, I32, I32, P, P, ctypes.POINTER(I32)]),
+    ("va_nav_records_bytes", I64, [I32, I32, I32]),
+    ("va_nav_run_rb", I32, [P, P, P, I32, I32, I32, P, P, ctypes.POINTER(I32), P, I64]),
     ("va_nav_query_bytes", I64, [I32]),
     ("va_astar_workspace_bytes", I64, [I32, I32]),
     ("va_astar_run", I32, [P, P, P, I32, I32, P, P, I32, P, P, ctypes.POINTER(I32)]),
@@ -66,6 +68,7 @@ SIGNATURES = [
     ("va_destroy", I32, [P]),
     ("va_handle_device", I32, [P, ctypes.POINTER(ctypes.c_int32)]),
     ("va_frame", I32, [P, P, P, I32, P, I32, I32, P, P, ctypes.POINTER(ctypes.c_int32)]),
+    ("va_frame_rb", I32, [P, P, P, I32, P, I32, I32, P, P, ctypes.POINTER(ctypes.c_int32), P, I64]),
     ("va_seg_sppf_pool", I32, [P, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_upsample2x", I32, [P, P, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_seg_run", I32, [P, P, I32]),

@@ -58,14 +58,22 @@ int va_handle_device(va_handle h, int32_t* device) {
 
 int va_frame(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
              int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds) {
+    return va_frame_rb(h, stream, ops, nops, post, H0, W0, seen, nav_work, rounds, nullptr, 0);
+}
+
+int va_frame_rb(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, const va_post_args* post, int32_t H0,
+                int32_t W0, uint64_t* seen, void* nav_work, int32_t* rounds, void* host_records,
+                int64_t host_bytes) {
     if (!h || !ops || nops <= 0 || !post || !post->cells || !post->rects || !seen || !nav_work) return VA_ERR_ARG;
+    if (host_records && host_bytes < va_nav_records_bytes(post->B, H0, W0)) return VA_ERR_ARG;
     DeviceScope scope(h->device);
     if (!scope.ok) return VA_ERR_HIP;
     int rc = va_seg_run(stream, ops, nops);
     if (rc != VA_OK) return rc;
     rc = va_post_run(stream, post);
     if (rc != VA_OK) return rc;
-    return va_nav_run(stream, post->cells, post->rects, post->B, H0, W0, seen, nav_work, rounds);
+    return va_nav_run_rb(stream, post->cells, post->rects, post->B, H0, W0, seen, nav_work, rounds, host_records,
+                         host_bytes);
 }
 
 int va_diag(uint32_t* out, int32_t n, int32_t clear) {

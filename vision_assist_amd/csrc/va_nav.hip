@@ -966,8 +966,18 @@ struct DedupeLaunch {
 // validation, before the host waits for the round's verdict: a round that is final (the common case) then needs no
 // launch after the wait; a round that is re-run gets its dedupe again behind the next one (the filter reads the
 // query records afresh and rewrites every unique / order field, so only the last round's counts)
+// the records of a va_nav_run copied to the caller's host memory (va_nav_run_rb)
+struct ReadBack {
+    void* dst;
+    const void* src;
+    int64_t bytes;
+};
+
+// speculative rounds over `nslots` query slots.  With `rb` the records are copied to the host behind every round's
+// kernels and ahead of its verdict copy, so the verdict wait also covers them: a final round (the common case)
+// returns with the records on the host; a re-run round copies them again
 int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out,
-                 const DedupeLaunch* dd = nullptr) {
+                 const DedupeLaunch* dd = nullptr, const ReadBack* rb = nullptr) {
     size_t lds = astar_lds(a.LR * a.LC);
     if (lds > 65536 &&
         hipFuncSetAttribute((const void*)nav_astar_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
@@ -994,6 +1004,8 @@ int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int
                                dd->off_q_path, dd->qpf, dd->nodes);
             if (hipGetLastError() != hipSuccess) return VA_ERR_HIP;
         }
+        if (rb && hipMemcpyAsync(rb->dst, rb->src, (size_t)rb->bytes, hipMemcpyDeviceToHost, st) != hipSuccess)
+            return VA_ERR_HIP;
         *rerun_h = -2;
         if (hipMemcpyAsync((void*)rerun_h, ctrl, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess)
             return VA_ERR_HIP;
@@ -1073,10 +1085,23 @@ int va_nav_sample_cells(void* stream, const uint8_t* masks, int64_t pitch, int32
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
+int64_t va_nav_records_bytes(int32_t B, int32_t H, int32_t W) {
+    Dims d;
+    if (B <= 0 || !make_dims(H, W, &d)) return VA_ERR_ARG;
+    return align16(align16((int64_t)B * d.frame_bytes) + (int64_t)B * d.MAXPK * d.query_bytes);
+}
+
 int va_nav_run(void* stream, const uint8_t* cells, const int32_t* rects, int32_t B, int32_t H, int32_t W,
                uint64_t* seen, void* work, int32_t* rounds) {
+    return va_nav_run_rb(stream, cells, rects, B, H, W, seen, work, rounds, nullptr, 0);
+}
+
+int va_nav_run_rb(void* stream, const uint8_t* cells, const int32_t* rects, int32_t B, int32_t H, int32_t W,
+                  uint64_t* seen, void* work, int32_t* rounds, void* host_records, int64_t host_bytes) {
     Dims d;
     if (!cells || !rects || !seen || !work || B <= 0 || !make_dims(H, W, &d)) return VA_ERR_ARG;
+    const int64_t rec_bytes = va_nav_records_bytes(B, H, W);
+    if (host_records && host_bytes < rec_bytes) return VA_ERR_ARG;
     if (ensure_tables() != hipSuccess) return VA_ERR_HIP;
     hipStream_t st = (hipStream_t)stream;
     Work w;
@@ -1101,7 +1126,8 @@ int va_nav_run(void* stream, const uint8_t* cells, const int32_t* rects, int32_t
     const DedupeLaunch dd{w.queries, d.query_bytes, d.off_q_path, B, d.MAXPK, d.NODES,
                           (size_t)d.MAXPK * words * 8 + 8 * (size_t)d.MAXPK + 16};
     int32_t r = 0;
-    int rc = astar_rounds(st, aa, w.ctrl, seen, &r, &dd);
+    const ReadBack rb{host_records, work, rec_bytes};
+    int rc = astar_rounds(st, aa, w.ctrl, seen, &r, &dd, host_records ? &rb : nullptr);
     if (rc != VA_OK) return rc;
     if (rounds) *rounds = r;
     return VA_OK;

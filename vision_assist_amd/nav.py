@@ -75,14 +75,22 @@ class NavBatch:
     enqueued on, right behind it (so a later run on the same engine cannot overwrite them first and the host
     never reads them before the last kernel of the run has finished); ``host()`` waits for that copy."""
 
-    def __init__(self, engine: "NavEngine", B: int, rounds: int, queries_off: int, stream=None):
+    def __init__(self, engine: "NavEngine", B: int, rounds: int, queries_off: int, stream=None,
+                 records: torch.Tensor | None = None):
+        """records: the run's records already on the host (pinned uint8, va_nav_run_rb / va_frame_rb filled them
+        before returning): read in place, no copy and no wait."""
         self.engine = engine
         self.B = B
         self.rounds = rounds
         self.queries_off = queries_off
         e = engine
-        st = stream if stream is not None else torch.cuda.current_stream(e.device)
         nq = B * e.dims.MAXPK * e.dims.query_bytes
+        if records is not None:
+            r = records.numpy()
+            self._pinned = (records,)
+            self._host = (r[: B * e.dims.frame_bytes], r[queries_off: queries_off + nq])
+            return
+        st = stream if stream is not None else torch.cuda.current_stream(e.device)
         fr = torch.empty(B * e.dims.frame_bytes, dtype=torch.uint8, pin_memory=True)
         qs = torch.empty(nq, dtype=torch.uint8, pin_memory=True)
         with torch.cuda.stream(st):
@@ -174,17 +182,36 @@ class NavEngine:
             raise _lib.VaError("rects must be contiguous int32 [B, 4]")
         return B
 
-    def batch(self, B: int, rounds: int, stream=None) -> NavBatch:
-        """The records of the va_nav_run just enqueued on `stream` (frame records, then query records)."""
+    def batch(self, B: int, rounds: int, stream=None, records: torch.Tensor | None = None) -> NavBatch:
+        """The records of the va_nav_run just enqueued on `stream` (frame records, then query records), or of a
+        va_nav_run_rb / va_frame_rb call that left them in `records` (host_records)."""
         d = self.dims
-        return NavBatch(self, B, rounds, (B * d.frame_bytes + 15) & ~15, stream)
+        return NavBatch(self, B, rounds, (B * d.frame_bytes + 15) & ~15, stream, records)
 
-    def run(self, cells: torch.Tensor, rects: torch.Tensor, seen: AngleSeen, stream=None) -> NavBatch:
-        """cells: uint8 [B, H/20, W/20] (device), rects: int32 [B, 4] (device)."""
+    def host_records(self, B: int) -> torch.Tensor:
+        """A pinned host buffer for va_nav_run_rb / va_frame_rb's records of B frames (fresh per call: a
+        NavBatch keeps reading its own)."""
+        n = int(self.lib.va_nav_records_bytes(B, self.dims.H, self.dims.W))
+        if n <= 0:
+            raise _lib.VaError(f"va_nav_records_bytes({B}) = {n}")
+        return torch.empty(n, dtype=torch.uint8, pin_memory=True)
+
+    def run(self, cells: torch.Tensor, rects: torch.Tensor, seen: AngleSeen, stream=None,
+            readback: bool = False) -> NavBatch:
+        """cells: uint8 [B, H/20, W/20] (device), rects: int32 [B, 4] (device).  readback: va_nav_run_rb (the
+        records copied to the host inside the call, ahead of the A* verdict wait) instead of va_nav_run + an
+        asynchronous copy NavBatch.host() waits for."""
         B = self.check_inputs(cells, rects)
         d = self.dims
         rounds = ctypes.c_int32(0)
         with torch.cuda.device(self.device):
+            if readback:
+                rec = self.host_records(B)
+                _lib.check(self.lib.va_nav_run_rb(_lib.stream_ptr(stream, self.device), cells.data_ptr(),
+                                                  rects.data_ptr(), B, d.H, d.W, seen.t.data_ptr(),
+                                                  self.work.data_ptr(), ctypes.byref(rounds), rec.data_ptr(),
+                                                  rec.numel()), "va_nav_run_rb")
+                return self.batch(B, rounds.value, stream, records=rec)
             _lib.check(self.lib.va_nav_run(_lib.stream_ptr(stream, self.device), cells.data_ptr(), rects.data_ptr(),
                                            B, d.H, d.W, seen.t.data_ptr(), self.work.data_ptr(), ctypes.byref(rounds)),
                        "va_nav_run")

@@ -102,8 +102,9 @@ class FramePipeline:
 
     def run(self, frames: torch.Tensor | None = None, plant_cells=None, plant_rects=None,
             plant_mode: int = PLANT_NEVER, stream=None) -> NavBatch:
-        """One batch through the whole path: frames in, then ONE va_frame call on the device's handle (forward,
-        post-processing and mask choice, grid / penalty / protrusion / A*)."""
+        """One batch through the whole path: frames in, then ONE va_frame_rb call on the device's handle (forward,
+        post-processing and mask choice, grid / penalty / protrusion / A*), which returns with the grid stage's
+        records in host memory (copied ahead of the A* verdict wait: one synchronisation per call)."""
         if frames is not None:
             self.load(frames, stream)
         out = self.plan["out"]
@@ -113,11 +114,13 @@ class FramePipeline:
         B = self.nav.check_inputs(self.post.cells, self.post.rects)
         rounds = ctypes.c_int32(0)
         h = _lib.Handle.for_device(self.device)
+        rec = self.nav.host_records(B)
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.va_frame(h.ptr, _lib.stream_ptr(stream, self.device), self.plan["ops"], self.plan["n"],
-                                         ctypes.byref(a), self.H, self.W, self.seen.t.data_ptr(),
-                                         self.nav.work.data_ptr(), ctypes.byref(rounds)), "va_frame")
-        return self.nav.batch(B, rounds.value, stream)
+            _lib.check(self.lib.va_frame_rb(h.ptr, _lib.stream_ptr(stream, self.device), self.plan["ops"],
+                                            self.plan["n"], ctypes.byref(a), self.H, self.W, self.seen.t.data_ptr(),
+                                            self.nav.work.data_ptr(), ctypes.byref(rounds), rec.data_ptr(),
+                                            rec.numel()), "va_frame_rb")
+        return self.nav.batch(B, rounds.value, stream, records=rec)
 
     def run_seg_only(self, stream=None) -> None:
         self.seg.run_plan(self.plan, stream)
