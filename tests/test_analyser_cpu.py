@@ -120,7 +120,8 @@ def _naive_analyser(clock):
     the dict rebuilt per call (PathAnalyser.py:185-230, :375-382)."""
     from vision_assist_amd.PathAnalyser import _HISTORY_MS, _PAIR_WINDOW_MS, PathAnalyser
     pa = object.__new__(PathAnalyser)
-    pa.paths, pa.previous_instructions, pa.instructions, pa.clock, pa._hist = [], {}, [], clock, None
+    pa.paths, pa.previous_instructions, pa.instructions, pa.clock, pa._rows = [], {}, [], clock, None
+    pa._upgrade_fast = lambda previous, current, now: False
     pa._recent = lambda previous, now: [(ts, v) for ts, v in previous.items() if now - ts < _PAIR_WINDOW_MS]
 
     def remember(now, ins):
@@ -155,7 +156,7 @@ def test_history_window_equals_full_scan():
     clock = {"t": 2_000_000.0}
     naive = _naive_analyser(lambda: clock["t"])
     fast = path_analyser
-    saved = (fast.clock, fast.previous_instructions, fast._hist)
+    saved = (fast.clock, fast.previous_instructions, fast._rows)
     fast.clock, fast.previous_instructions = (lambda: clock["t"]), {}
     try:
         for k in range(4000):
@@ -173,4 +174,4 @@ def test_history_window_equals_full_scan():
                        [[i.danger for i in v] for v in naive.previous_instructions.values()], k
         assert len(naive.previous_instructions) > 1000
     finally:
-        fast.clock, fast.previous_instructions, fast._hist = saved
+        fast.clock, fast.previous_instructions, fast._rows = saved

@@ -82,14 +82,23 @@ def main():
             tin.append(1e3 * (time.perf_counter() - t))
             return r
         pipe.run = timed_run
+        cpu0, wall0 = time.process_time(), time.perf_counter()
         for i in range(args.calls):
             t0 = time.perf_counter()
             fp(frames[i % 16])
             ts.append(1e3 * (time.perf_counter() - t0))
+        cpu_ratio = (time.process_time() - cpu0) / (time.perf_counter() - wall0)
         pipe.run = run0
+        # the same calls paced by a 1 ms sleep: a stall every N calls or every T ms?
+        tsl = []
+        for i in range(args.calls):
+            time.sleep(0.001)
+            t0 = time.perf_counter()
+            fp(frames[i % 16])
+            tsl.append((t0, 1e3 * (time.perf_counter() - t0)))
         # the surface's body step by step (FrameProcessor.__call__, debug off)
         from vision_assist_amd import _lib
-        R = {k: [] for k in ("as_tensor+pipe", "run", "adopt", "checks", "device_paths", "analyser")}
+        R = {k: [] for k in ("as_tensor+pipe", "load", "va_frame", "adopt", "checks", "device_paths", "analyser")}
         for i in range(args.calls):
             frame = frames[i % 16]
             c0 = time.perf_counter()
@@ -98,7 +107,9 @@ def main():
             H, W = int(t.shape[0]), int(t.shape[1])
             p_ = fp._pipe(H, W)
             c1 = time.perf_counter()
-            b = p_.run(t.reshape(1, H, W, 3), plant_mode=PLANT_NEVER)
+            p_.load(t.reshape(1, H, W, 3))
+            c1b = time.perf_counter()
+            b = p_.run(None, plant_mode=PLANT_NEVER)
             c2 = time.perf_counter()
             fp._adopt(p_.nav, b)
             c3 = time.perf_counter()
@@ -116,7 +127,7 @@ def main():
             c5 = time.perf_counter()
             fpm.path_analyser(H, W, paths_)
             c6 = time.perf_counter()
-            for k, a_, b_ in (("as_tensor+pipe", c0, c1), ("run", c1, c2), ("adopt", c2, c3), ("checks", c3, c4),
+            for k, a_, b_ in (("as_tensor+pipe", c0, c1), ("load", c1, c1b), ("va_frame", c1b, c2), ("adopt", c2, c3), ("checks", c3, c4),
                               ("device_paths", c4, c5), ("analyser", c5, c6)):
                 R[k].append(1e3 * (b_ - a_))
         tin = np.array(tin)
@@ -149,7 +160,25 @@ def main():
     out["surface_max_ms"] = round(float(np.max(ts)), 3)
     out["surface_run_pct_ms"] = {q: round(float(np.percentile(tin, q)), 3) for q in (10, 50, 90, 99, 100)}
     out["surface_host_rest_pct_ms"] = {q: round(float(np.percentile(rest, q)), 3) for q in (10, 50, 90, 99, 100)}
-    out["replica_pct_ms"] = {k: [round(float(np.percentile(v, q)), 3) for q in (50, 90, 99)] for k, v in R.items()}
+    out["replica_pct_ms"] = {k: [round(float(np.percentile(v, q)), 3) for q in (50, 90, 99, 100)] for k, v in R.items()}
+    out["env_ROC_ACTIVE_WAIT_TIMEOUT"] = os.environ.get("ROC_ACTIVE_WAIT_TIMEOUT")
+    out["surface_process_cpu_per_wall"] = round(cpu_ratio, 3)
+    try:  # per-thread CPU ticks, busiest first: (name, utime + stime)
+        import glob as _g
+        th = []
+        for d in _g.glob("/proc/self/task/*"):
+            name = open(d + "/comm").read().strip()
+            f = open(d + "/stat").read().rsplit(")", 1)[1].split()
+            th.append((name, int(f[11]) + int(f[12])))
+        out["thread_ticks"] = sorted(th, key=lambda x: -x[1])[:20]
+    except OSError:
+        pass
+    try:
+        out["threads"] = int([l for l in open("/proc/self/status") if l.startswith("Threads")][0].split()[1])
+    except OSError:
+        pass
+    slow = [(round(1e3 * (t - tsl[0][0]), 1), round(d, 2)) for t, d in tsl if d > 5]
+    out["paced_slow_calls_at_ms"] = slow[:20]
     out["surface_slowest"] = [(int(i), round(float(ts[i]), 3)) for i in np.argsort(ts)[-8:]]
     out["surface_gc_off_calls_per_s"] = round(1e3 / float(np.mean(tg)), 1)
     out["surface_gc_off_pct_ms"] = {q: round(float(np.percentile(tg, q)), 3) for q in (50, 90, 99)}

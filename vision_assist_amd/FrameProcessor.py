@@ -64,6 +64,7 @@ class _FrameState:
         self._grids = None
         self._lookup = None
         self._np = None
+        self._pos = None  # object id -> list position (nf.pos_obj is fixed for the frame)
         self.penalties_assigned = False
 
     # object id: main row r -> r, artificial row a -> LR + a (va_nav.hip nav_grid_kernel)
@@ -75,7 +76,9 @@ class _FrameState:
         return o if o < self.dims.LR else (self._obj_y(o) - self.nf.y0) // G
 
     def _pos_of_obj(self) -> dict[int, int]:
-        return {int(o): p for p, o in enumerate(self.nf.pos_obj)}
+        if self._pos is None:
+            self._pos = {int(o): p for p, o in enumerate(self.nf.pos_obj)}
+        return self._pos
 
     def obj(self, o: int, c: int, flags: int | None = None) -> Grid:
         key = (o, c)

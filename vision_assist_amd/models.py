@@ -14,6 +14,8 @@ checked against the reference's own answers in tests/test_surface.py.
 """
 from __future__ import annotations
 
+import math
+
 from enum import Enum
 from typing import Any, Literal
 
@@ -101,12 +103,17 @@ def signed_angle_from_vertical(a: Coordinate, b: Coordinate) -> float:
 
 
 def _first_nearest(point: Coordinate, cells: list[Grid]):
-    """Nearest non-empty cell centre, first one wins on ties (models.py:272-298)."""
+    """Nearest non-empty cell centre, first one wins on ties (models.py:272-298).  math.sqrt, not the
+    reference's np.sqrt: both are the correctly rounded square root of the same float64, so every comparison
+    (and the cell returned) is the same, without numpy's per-scalar call overhead."""
     best, best_d = None, np.inf
+    px, py = point.x, point.y
+    sqrt = math.sqrt
     for c in cells:
         if c.empty:
             continue
-        d = np.sqrt((point.x - c.centre.x) ** 2 + (point.y - c.centre.y) ** 2)
+        ce = c.centre
+        d = sqrt((px - ce.x) ** 2 + (py - ce.y) ** 2)
         if d < best_d:
             best, best_d = c, d
     return best
@@ -118,9 +125,10 @@ def _vertical_runs(cells: list[Grid]) -> list[tuple[int, int]]:
     runs = []
     run_start, run_len, prev_dir = 0, 1, None
     n = len(cells)
+    xy = [(c.coords.x, c.coords.y) for c in cells]
     for i in range(1, n):
-        dx = cells[i].coords.x - cells[i - 1].coords.x
-        dy = cells[i].coords.y - cells[i - 1].coords.y
+        dx = xy[i][0] - xy[i - 1][0]
+        dy = xy[i][1] - xy[i - 1][1]
         d = "vertical" if (dx == 0 and dy != 0) else None
         if i == 1:
             prev_dir = d

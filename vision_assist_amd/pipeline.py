@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -66,13 +67,17 @@ class FramePipeline:
     def _pinned(self, frames: torch.Tensor) -> torch.Tensor:
         """Host frames (a camera's numpy frame, main.py:62-82) copied into a pinned staging buffer, so that the H2D
         copy that follows is asynchronous on the launch stream (a pageable source makes it synchronous and staged
-        by the runtime).  The buffer is reused only after the previous copy out of it has completed (_pin_ev)."""
-        if getattr(self, "_pin", None) is None or self._pin.shape != frames.shape:
+        by the runtime).  The buffer is reused only after the previous copy out of it has completed (_pin_ev).
+        The copy is numpy's (one thread): torch's CPU copy of a frame this size wakes the OpenMP pool, whose
+        workers then spin between calls -- at a call every ~2 ms that kept 15 threads busy, and under the box's
+        16-CPU quota the whole process was throttled ~8 ms in every 100 ms period (tools/dropin_split.py)."""
+        if getattr(self, "_pin", None) is None or self._pin.shape != frames.shape or self._pin.dtype != frames.dtype:
             self._pin = torch.empty(frames.shape, dtype=frames.dtype, pin_memory=True)
+            self._pin_np = self._pin.numpy()
             self._pin_ev = None
         if self._pin_ev is not None:
             self._pin_ev.synchronize()
-        self._pin.copy_(frames)
+        np.copyto(self._pin_np, frames.numpy())
         return self._pin
 
     def load(self, frames: torch.Tensor, stream=None) -> None:
@@ -82,7 +87,7 @@ class FramePipeline:
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         staged = frames.device.type == "cpu" and not frames.is_pinned()
         if staged:
-            frames = self._pinned(frames.contiguous())
+            frames = self._pinned(frames)
         with torch.cuda.stream(st):
             if self.lb is None:
                 self.plan["frames"].copy_(frames, non_blocking=True)
