@@ -91,6 +91,8 @@ def parse():
                         "host blocks in batch k's grid stage")
     p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2],
                    help="network streams of the overlapped pipeline (2: consecutive forwards run concurrently)")
+    p.add_argument("--dropin-only", action="store_true",
+                   help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
 
 
@@ -253,14 +255,17 @@ class Run:
         torch.cuda.synchronize()
         if self.overlap:
             self.opipe.k = 0
+        cpu0, wall0 = time.process_time(), time.perf_counter()
         (rounds, res), elapsed = timed(lambda: self.steps(steps), world, sync=torch.cuda.synchronize)
+        host_cpu = (time.process_time() - cpu0) / (time.perf_counter() - wall0)
         res.host()  # (synchronised snapshot of the last batch's records)
         paths = sum(1 for i in range(B) for q in res.frame(i).queries if q["unique"])
         seg = self.pipe.seg
         gflop_alg = seg.gflop_per_frame(H, H)
         gflop_exec = seg.plan_gflop(self.pipe.plan)  # per B-frame forward
         out = {"value": world * B * steps / elapsed, "elapsed": elapsed, "ms_per_step": 1e3 * elapsed / steps,
-               "rounds": rounds / steps, "paths": paths, "gflop_alg": gflop_alg, "gflop_exec": gflop_exec}
+               "rounds": rounds / steps, "paths": paths, "gflop_alg": gflop_alg, "gflop_exec": gflop_exec,
+               "host_cpu": host_cpu}
         if prof:
             out["roofline"] = self.roofline(_lib.load(), gflop_alg, gflop_exec, elapsed, steps)
         return out
@@ -424,16 +429,34 @@ def dropin_rate(args, dev, calls=200) -> dict:
         for i in range(10):
             fp(frames[i % 16])
         torch.cuda.synchronize()
+        c0 = time.process_time()
         t0 = time.perf_counter()
         for i in range(calls):
             a = fp(frames[i % 16])
             answers += a != []
         dt = time.perf_counter() - t0
+        host_cpu = (time.process_time() - c0) / dt
     return {"value": round(calls / dt, 2), "unit": "frames/s", "ms_per_call": round(1e3 * dt / calls, 4),
             "calls": calls, "calls_with_answer": answers, "dtype": "f32", "regime": args.regime,
+            "host_cpu_per_wall": round(host_cpu, 2),
             "workload": "FrameProcessor.__call__(frame) per frame (main.py:80-82): host numpy 640x640 frame -> pinned "
                         "H2D -> YOLOv8s-seg f32 + post + grid / A* (batch 1) -> host Path sections/corners + "
                         "PathAnalyser answer"}
+
+
+def dropin_child(args) -> dict:
+    """dropin_rate in a fresh child process (`bench.py --dropin-only`): main.py runs FrameProcessor in a process of
+    its own, and the streams this bench process has made by then (overlapped pipelines, C4's, C2's) change which
+    hardware queues the batch-1 forward's lane streams share -- with three extra streams made first the call took
+    1.76 instead of 1.58 ms of device time (profiles/r04/dropin2/streams/)."""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--dropin-only", "--regime", args.regime],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"dropin child failed ({r.returncode}): {r.stderr[-2000:]}")
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    d["process"] = "a fresh child process (bench.py --dropin-only), as main.py runs FrameProcessor"
+    return d
 
 
 def dealer_rate(args, dev, frames_n: int = 256) -> dict:
@@ -470,6 +493,9 @@ def main():
     # rank r on GPU r of the node (a 1-GPU rehearsal box shares cuda:0 between ranks)
     torch.cuda.set_device(local % torch.cuda.device_count() if dist else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.dropin_only:
+        print(json.dumps(dropin_rate(args, dev)), flush=True)
+        return
     B = args.batch or DEFAULT_BATCH[args.dtype]
     prof = not args.no_prof
 
@@ -511,7 +537,7 @@ def main():
             continue
         if ex == "dropin":
             if world == 1:
-                extras[ex] = dropin_rate(args, dev)
+                extras[ex] = dropin_child(args)
             continue
         if ex == "dealer":
             if world == 1:
@@ -590,6 +616,9 @@ def main():
             "extras": extras,
             "astar_rounds_per_step": round(main_res["rounds"], 3),
             "unique_paths_last_batch": main_res["paths"],
+            # host CPU seconds per wall second over the timed region (this process, all threads): a host that
+            # spins (an OpenMP pool left busy-waiting) runs into the box's CPU quota and is throttled
+            "host_cpu_per_wall": round(main_res["host_cpu"], 2),
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -27,7 +27,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=300)
     ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--pre-streams", type=int, default=0, help="create and use N torch streams first")
     args = ap.parse_args()
+    keep = []
+    for _ in range(args.pre_streams):
+        st_ = torch.cuda.Stream()
+        with torch.cuda.stream(st_):
+            keep.append(torch.ones(16, device="cuda") * 2)
+    torch.cuda.synchronize()
     from bench import regime_kwargs
     from vision_assist_amd import FrameProcessor as fpm
     from vision_assist_amd.FrameProcessor import FrameProcessor
