@@ -1,12 +1,12 @@
 #!/bin/bash
 # Per-layer SQ / LDS / TA-TD / TCC counters of the f32 s-seg forward (B = 64; tools/pmc_forward.py), one rocprofv3
 # pass per counter set, each under its own time limit; then tools/pmc_summary.py maps them to layer names.
-#   bash tools/pmc_conv.sh OUTDIR [extra env, e.g. VA_CONV3H=0]      (PASSES="sq lds tcc tcp" by default)
+#   bash tools/pmc_conv.sh OUTDIR [extra env, e.g. VA_CONV3H=0]      (PASSES="sq lds tcc tcp fetch write" by default)
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift
 mkdir -p $O
 for kv in "$@"; do export "$kv"; done
-PASSES=${PASSES:-sq lds tcc tcp}
+PASSES=${PASSES:-sq lds tcc tcp fetch write}
 run() {  # name counters...
   n=$1; shift
   case " $PASSES " in *" $n "*) ;; *) return 0;; esac
@@ -20,6 +20,8 @@ run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD
     TD_TC_STALL_sum GRBM_GUI_ACTIVE && \
 run tcc TCC_HIT_sum TCC_MISS_sum TCC_BUSY_sum GRBM_GUI_ACTIVE && \
 run tcp TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum GRBM_GUI_ACTIVE && \
+run fetch FETCH_SIZE GRBM_GUI_ACTIVE && \
+run write WRITE_SIZE GRBM_GUI_ACTIVE && \
 python3 tools/pmc_summary.py $O/plan.json $O/summary.json $(for n in $PASSES; do echo $O/$n/*counter_collection.csv; done) \
     > $O/summary.log 2>&1
 echo "summary rc=$?"
