@@ -89,8 +89,12 @@ def parse():
     p.add_argument("--pipelines", type=int, default=3,
                    help="batches in flight (buffer sets): 3 lets batch k+2's network be enqueued before the "
                         "host blocks in batch k's grid stage")
-    p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2],
+    p.add_argument("--seg-streams", type=int, default=2, choices=[1, 2, 3, 4],
                    help="network streams of the overlapped pipeline (2: consecutive forwards run concurrently)")
+    p.add_argument("--c4-pipelines", type=int, default=6,
+                   help="frames in flight per GPU in the c4 extra (batch 1: more concurrent forwards fill the chip)")
+    p.add_argument("--c4-seg-streams", type=int, default=3, choices=[1, 2, 3, 4],
+                   help="network streams of the c4 extra (3 + the grid stage's stream: one hardware queue each)")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -179,7 +183,7 @@ def cpu_baseline(arch, fw, frames_u8: np.ndarray, plant_cells, plant_rects, res:
 class Run:
     """One measured configuration: pipelines, resident inputs and the timed steps."""
 
-    def __init__(self, args, dev, rank, dtype, B, regime, scale=None, res=None):
+    def __init__(self, args, dev, rank, dtype, B, regime, scale=None, res=None, pipelines=None, seg_streams=None):
         from vision_assist_amd.pipeline import FramePipeline, OverlappedPipelines
         from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
         self.args, self.dtype, self.B, self.regime = args, dtype, B, regime
@@ -190,7 +194,8 @@ class Run:
         self.overlap = not args.no_overlap
         if self.overlap:
             self.opipe = OverlappedPipelines(self.arch, self.fw, B, H, W, dtype=dtype, device=dev,
-                                             seg_streams=args.seg_streams, depth=args.pipelines)
+                                             seg_streams=seg_streams or args.seg_streams,
+                                             depth=pipelines or args.pipelines)
             self.pipe = self.opipe.a
         else:
             self.pipe = FramePipeline(self.arch, self.fw, B, H, W, dtype=dtype, device=dev)
@@ -346,16 +351,20 @@ class Run:
 
 def c4_rate(args, dev, rank, world, prof) -> dict:
     """C4 (BASELINE.json configs[3]): YOLOv8s-seg 640x640 f32, ONE frame per GPU per step (batch 8 over 8 GPUs),
-    frames dealt round-robin, no collective; the same overlapped pipeline as the headline with batch 1 (three
-    frames in flight per GPU).  value = frames of all ranks / max-over-ranks time."""
+    frames dealt round-robin, no collective; the headline's overlapped pipeline with batch 1, --c4-pipelines frames in
+    flight per GPU on --c4-seg-streams network streams (6 on 3: 1,031 -> 1,456 frames/s against the headline's 3 on
+    2; a 4th network stream shares a hardware queue and fell to 1,015).  value = frames of all ranks /
+    max-over-ranks time."""
     steps = max(200, 10 * args.steps)
-    r = Run(args, dev, rank, "f32", 1, args.regime, scale="s", res=640)
+    r = Run(args, dev, rank, "f32", 1, args.regime, scale="s", res=640, pipelines=args.c4_pipelines,
+            seg_streams=args.c4_seg_streams)
     m = r.measure(steps, 20, world, prof)
     r.release()
     e = {"value": round(m["value"], 2), "unit": "frames/s", "ms_per_step": round(m["ms_per_step"], 4), "steps": steps,
          "dtype": "f32", "batch_per_gpu": 1, "global_batch": world, "regime": args.regime,
          "workload": "C4 (BASELINE.json configs[3]): YOLOv8s-seg 640x640, one frame per GPU per step, network masks "
-                     "(planted only when a frame has no detection) -> contours -> grid / A*, 3 frames in flight per GPU",
+                     f"(planted only when a frame has no detection) -> contours -> grid / A*, {args.c4_pipelines} frames in "
+                     f"flight per GPU on {args.c4_seg_streams} network streams",
          "parity": "tests/test_gpu_c4.py (2 ranks, one frame per rank per step, vs the per-shard oracle-chain replay)"}
     if prof:
         rl = m["roofline"]

@@ -163,8 +163,9 @@ class OverlappedPipelines:
                                               seen=first.seen, seg=first.seg, tag=i, **kw) for i in range(1, depth)]
         self.a, self.b = self.pipes[0], self.pipes[1]
         self.depth = depth
-        s0 = torch.cuda.Stream(device=first.device)
-        self.s_segs = (s0, torch.cuda.Stream(device=first.device) if seg_streams == 2 else s0)
+        if seg_streams < 1:
+            raise ValueError("seg_streams >= 1")
+        self.s_segs = tuple(torch.cuda.Stream(device=first.device) for _ in range(seg_streams))
         self.s_nav = torch.cuda.Stream(device=first.device)
         self.ev = [torch.cuda.Event() for _ in range(depth)]        # network + post of the pipeline's batch
         self.nav_done = [torch.cuda.Event() for _ in range(depth)]  # its grid stage
@@ -174,7 +175,7 @@ class OverlappedPipelines:
         """Enqueue copy + network + post-processing of the next batch on its network stream."""
         i = self.k % self.depth
         p = self.pipes[i]
-        s_seg = self.s_segs[self.k % 2]
+        s_seg = self.s_segs[self.k % len(self.s_segs)]
         s_seg.wait_stream(torch.cuda.current_stream())
         s_seg.wait_event(self.nav_done[i])  # the pipeline's previous batch has left its grid stage
         with torch.cuda.stream(s_seg):
