@@ -95,6 +95,8 @@ def parse():
                    help="frames in flight per GPU in the c4 extra (batch 1: more concurrent forwards fill the chip)")
     p.add_argument("--c4-seg-streams", type=int, default=3, choices=[1, 2, 3, 4],
                    help="network streams of the c4 extra (3 + the grid stage's stream: one hardware queue each)")
+    p.add_argument("--dealer-workers-per-gpu", type=int, default=1,
+                   help="FrameProcessor worker processes per GPU in the dealer extra (each its own PathFinder shard)")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -474,17 +476,18 @@ def dealer_rate(args, dev, frames_n: int = 256) -> dict:
     shared-memory frame ring, in-order answers, each worker with its own PathFinder state), f32 s-seg, the
     regime's network masks.  frames/s of in-order answers over the whole node's workers."""
     from vision_assist_amd.shard import FrameDealer, dropin_worker
-    G = max(1, torch.cuda.device_count())
+    G = max(1, torch.cuda.device_count()) * args.dealer_workers_per_gpu
+    ngpu = max(1, torch.cuda.device_count())
     rng = np.random.default_rng(78)
     frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
-    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)), list(range(G)),
-                     640, 640, slots=4) as d:
+    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)),
+                     [w % ngpu for w in range(G)], 640, 640, slots=4) as d:
         for _ in d.map(frames[i % 16] for i in range(32 * G)):  # warm: plans, first launches, lanes' streams
             pass
         t0 = time.perf_counter()
         answers = sum(a != [] for a in d.map(frames[i % 16] for i in range(frames_n)))
         dt = time.perf_counter() - t0
-    return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "frames": frames_n,
+    return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "gpus": ngpu, "frames": frames_n,
             "frames_with_answer": answers, "dtype": "f32", "regime": args.regime,
             "workload": "one reader dealing host 640x640 frames round-robin to one FrameProcessor worker process per "
                         "GPU (vision_assist_amd.shard.FrameDealer), answers back in frame order"}

@@ -17,6 +17,7 @@ import os
 import time
 from typing import Callable
 
+import numpy as np
 import torch
 
 
@@ -92,6 +93,7 @@ class FrameDealer:
         self.H, self.W, self.slots = H, W, slots
         ctx = tmp.get_context("spawn")
         self.ring = torch.zeros((self.G, slots, H, W, 3), dtype=torch.uint8).share_memory_()
+        self._ring_np = self.ring.numpy()  # frames are copied in by numpy (one thread; see submit)
         self.inq = [ctx.Queue() for _ in range(self.G)]
         self.free = [ctx.Queue() for _ in range(self.G)]
         self.outq = ctx.Queue()
@@ -122,7 +124,9 @@ class FrameDealer:
         if tuple(t.shape) != (self.H, self.W, 3) or t.dtype != torch.uint8:
             raise ValueError(f"frame must be uint8 [{self.H}, {self.W}, 3], got {tuple(t.shape)} {t.dtype}")
         slot = self.free[w].get()
-        self.ring[w, slot].copy_(t)
+        # numpy's copy, not torch's: torch's CPU copy of a frame wakes its OpenMP pool, whose workers then spin
+        # between frames and exhaust the box's CPU quota for every process of it (pipeline.FramePipeline._pinned)
+        np.copyto(self._ring_np[w, slot], t.numpy() if t.device.type == "cpu" else t.cpu().numpy())
         self.inq[w].put((idx, slot))
         self.n += 1
         return idx
