@@ -461,11 +461,15 @@ def dropin_child(args) -> dict:
     hardware queues the batch-1 forward's lane streams share -- with three extra streams made first the call took
     1.76 instead of 1.58 ms of device time (profiles/r04/dropin2/streams/)."""
     import subprocess
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--dropin-only", "--regime", args.regime],
-                       capture_output=True, text=True, timeout=600)
-    if r.returncode != 0:
-        raise RuntimeError(f"dropin child failed ({r.returncode}): {r.stderr[-2000:]}")
-    d = json.loads(r.stdout.strip().splitlines()[-1])
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--dropin-only", "--regime", args.regime],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"exit status {r.returncode}: {r.stderr[-1500:]}")
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # the headline line is still printed; the extra says what failed
+        print(f"dropin child failed: {e}", file=sys.stderr, flush=True)
+        return {"value": None, "error": str(e)[-1500:]}
     d["process"] = "a fresh child process (bench.py --dropin-only), as main.py runs FrameProcessor"
     return d
 
