@@ -217,7 +217,8 @@ class PathAnalyser:
         H, W = self.frame_height, self.frame_width
         weight = w.sy / H
         for c in current:
-            keep = ~w.dist.__gt__(c.distance) & (w.dir == hist.code(c.direction)) & (w.rank <= _DANGER_RANK[c.danger])
+            # ~(p.distance > c.distance), not p.distance <= c.distance: the literal test's result for NaN too
+            keep = ~(w.dist > c.distance) & (w.dir == hist.code(c.direction)) & (w.rank <= _DANGER_RANK[c.danger])
             if c.instruction_type != "bearing":
                 keep &= ~w.bearing
             keep &= (np.abs(w.sy - c.start.y) * weight) < H * 0.2
