@@ -97,6 +97,9 @@ def parse():
                    help="network streams of the c4 extra (3 + the grid stage's stream: one hardware queue each)")
     p.add_argument("--dealer-workers-per-gpu", type=int, default=1,
                    help="FrameProcessor worker processes per GPU in the dealer extra (each its own PathFinder shard)")
+    p.add_argument("--dealer-batch", type=int, default=8,
+                   help="frames a dealer worker runs as one device batch (up to; what waits in its ring)")
+    p.add_argument("--dealer-slots", type=int, default=16, help="ring slots per dealer worker")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -474,7 +477,7 @@ def dropin_child(args) -> dict:
     return d
 
 
-def dealer_rate(args, dev, frames_n: int = 256) -> dict:
+def dealer_rate(args, dev, frames_n: int = 1024) -> dict:
     """SURVEY.md §8e from the drop-in surface: ONE frame source (a reader, as main.py's camera loop) dealing host
     frames round-robin to one FrameProcessor worker process per visible GPU (vision_assist_amd.shard.FrameDealer:
     shared-memory frame ring, in-order answers, each worker with its own PathFinder state), f32 s-seg, the
@@ -484,24 +487,81 @@ def dealer_rate(args, dev, frames_n: int = 256) -> dict:
     ngpu = max(1, torch.cuda.device_count())
     rng = np.random.default_rng(78)
     frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
-    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", **regime_kwargs(args.regime, 640)),
-                     [w % ngpu for w in range(G)], 640, 640, slots=4) as d:
+    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", batch=args.dealer_batch,
+                                   **regime_kwargs(args.regime, 640)),
+                     [w % ngpu for w in range(G)], 640, 640, slots=args.dealer_slots) as d:
         for _ in d.map(frames[i % 16] for i in range(32 * G)):  # warm: plans, first launches, lanes' streams
             pass
         t0 = time.perf_counter()
         answers = sum(a != [] for a in d.map(frames[i % 16] for i in range(frames_n)))
         dt = time.perf_counter() - t0
     return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "gpus": ngpu, "frames": frames_n,
-            "frames_with_answer": answers, "dtype": "f32", "regime": args.regime,
+            "frames_with_answer": answers, "dtype": "f32", "regime": args.regime, "worker_batch": args.dealer_batch,
+            "slots": args.dealer_slots,
             "workload": "one reader dealing host 640x640 frames round-robin to one FrameProcessor worker process per "
-                        "GPU (vision_assist_amd.shard.FrameDealer), answers back in frame order"}
+                        "GPU (vision_assist_amd.shard.FrameDealer), answers back in frame order; each worker runs "
+                        f"up to {args.dealer_batch} waiting frames as one device batch, two batches in flight "
+                        "(pipeline.StreamBatches), answers built frame by frame in order"}
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed.run environment: start N fresh child
+    processes of this script, rank r with RANK = LOCAL_RANK = r, WORLD_SIZE = N and a 127.0.0.1 rendezvous, before
+    this process has made any GPU call (it never makes one: a process that initialised the GPU must not hand its
+    role to another).  Waits for every rank, relays rank 0's JSON line, and returns non-zero if any rank failed
+    (the others are then stopped by their exact PIDs)."""
+    import socket
+    import subprocess
+    import tempfile
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out0 = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # rank 0's stdout (the JSON line) to a file, the other ranks' stdout and everyone's stderr to our stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out0 if r == 0 else sys.stderr, stderr=sys.stderr))
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            if p.poll() not in (None, 0):
+                failed = (r, p.returncode)
+                break
+        time.sleep(0.2)
+    if failed is None:
+        failed = next(((r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0), None)
+    if failed is not None:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        print(f"bench.py --gpus {n}: rank {failed[0]} exited with status {failed[1]}", file=sys.stderr, flush=True)
+        return failed[1] if failed[1] and failed[1] > 0 else 1
+    out0.seek(0)
+    lines = [ln for ln in out0.read().splitlines() if ln.startswith("{")]
+    if len(lines) != 1:
+        print(f"bench.py --gpus {n}: rank 0 printed {len(lines)} JSON lines", file=sys.stderr, flush=True)
+        return 1
+    print(lines[0], flush=True)
+    return 0
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
     dist = world > 1
     if dist:
         import torch.distributed as tdist

@@ -497,6 +497,11 @@ int va_frame_rb(va_handle h, void* stream, const va_seg_op* ops, int32_t nops, c
  * words are zeroed when clear != 0.  Synchronises the current device.  Debug / test surface. */
 int va_diag(uint32_t* out, int32_t n, int32_t clear);
 
+/* The library's A/B switches (environment variables VA_F32_SPLIT, VA_CONV3H, VA_CONV3T, VA_SPLITK, VA_CONV_PATCH,
+ * VA_CONV4, VA_PW, VA_CT_RUNS, VA_CT_WGP) are read once per process, at the first launch that
+ * consults them.  va_switches_reload re-reads them (a test comparing two kernel forms inside one process). */
+int va_switches_reload(void);
+
 /* Library version / build info string; "abi 3": va_post_args as above (sc_* floats, cpts / cpts_cap / max_nms;
  * round 2 changed its layout from round 1's int pad_x / pad_y) -- check va_abi_struct_sizes as well. */
 const char* va_version(void);

@@ -70,3 +70,83 @@ def test_dealer_submit_get_and_worker_errors():
         d.submit(np.full((4, 4, 3), 7, np.uint8))
         with pytest.raises(RuntimeError, match="bad frame"):
             d.get()
+
+
+class BatchingWorker:
+    """The batching protocol (max_batch / begin / end): results carry the batch size each frame ran in; a frame
+    whose first pixel is 7 comes back as an exception object (fails that frame alone)."""
+
+    def __call__(self, device):
+        class Fn:
+            max_batch = 4
+
+            def __call__(self, frame):
+                return int(frame[0, 0, 0]), 1
+
+            def begin(self, frames):
+                return [int(f[0, 0, 0]) for f in frames]  # copied out of the ring slots
+
+            def end(self, tok):
+                return [ValueError("seven") if v == 7 else (v, len(tok)) for v in tok]
+        return Fn()
+
+
+class DyingWorker:
+    def __call__(self, device):
+        import os
+
+        def fn(frame):
+            if frame[0, 0, 0] == 9:
+                os._exit(3)
+            return int(frame[0, 0, 0])
+        return fn
+
+
+def test_dealer_error_then_stream_continues():
+    from vision_assist_amd.shard import FrameDealer
+    with FrameDealer(FailingWorker(), [None, None], 4, 4, slots=2) as d:
+        for v in (1, 7, 3, 4):
+            d.submit(np.full((4, 4, 3), v, np.uint8))
+        assert d.get() == 1
+        with pytest.raises(RuntimeError, match="bad frame"):
+            d.get()
+        assert [d.get(), d.get()] == [3, 4]  # the failed frame does not block the ones after it
+        assert d.in_flight() == 0
+
+
+def test_dealer_batching_protocol_in_order():
+    from vision_assist_amd.shard import FrameDealer
+    vals = [1, 2, 3, 4, 5, 6, 8, 10, 11, 12, 13, 14, 15, 16]
+    with FrameDealer(BatchingWorker(), [None], 4, 4, slots=8) as d:
+        got = list(d.map(np.full((4, 4, 3), v, np.uint8) for v in vals))
+        assert [g[0] for g in got] == vals
+        assert all(1 <= g[1] <= 4 for g in got)
+        d.submit(np.full((4, 4, 3), 7, np.uint8))
+        d.submit(np.full((4, 4, 3), 2, np.uint8))
+        with pytest.raises(RuntimeError, match="seven"):
+            d.get()
+        assert d.get()[0] == 2
+
+
+def test_dealer_map_stopped_early_leaves_nothing_behind():
+    """a consumer that breaks out of map() must not receive the abandoned frames' results next time."""
+    from vision_assist_amd.shard import FrameDealer
+    with FrameDealer(FailingWorker(), [None, None], 4, 4, slots=3) as d:
+        for i, r in enumerate(d.map(np.full((4, 4, 3), v, np.uint8) for v in range(20, 40))):
+            if i == 2:
+                break
+        assert d.in_flight() == 0
+        assert list(d.map(np.full((4, 4, 3), v, np.uint8) for v in (50, 51, 52))) == [50, 51, 52]
+
+
+def test_dealer_dead_worker_raises_instead_of_hanging():
+    from vision_assist_amd.shard import FrameDealer
+    with FrameDealer(DyingWorker(), [None, None], 4, 4, slots=1, poll=0.2) as d:
+        d.submit(np.full((4, 4, 3), 1, np.uint8))
+        d.submit(np.full((4, 4, 3), 9, np.uint8))  # worker 1 dies on it
+        assert d.get() == 1
+        with pytest.raises(RuntimeError, match="exited with status 3"):
+            d.get()
+        assert d.broken
+        with pytest.raises(RuntimeError):
+            d.submit(np.full((4, 4, 3), 2, np.uint8))

@@ -41,3 +41,18 @@ def test_bench_contract_line():
     assert d["extras"]["bf16"]["roofline"]["peak"] == 2500.0 and d["extras"]["dense"]["dtype"] == "f32"
     assert d["extras"]["c5"]["dtype"] == "fp8" and d["extras"]["c5"]["roofline"]["peak"] == 5000.0
     assert "grid_stage_ms_per_frame" in c and "path+analyser" in c["stage_ms_per_frame"]
+
+
+def test_bench_gpus_2_starts_its_own_ranks():
+    """The driver's command form `python bench.py --gpus N` (no torch.distributed.run): bench.py starts N ranks
+    itself (here both share cuda:0, LOCAL_RANK % device_count) and relays rank 0's line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--batch", "8", "--steps", "2", "--warmup", "1",
+                          "--extras", "none", "--no-ingest"], cwd=REPO, capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 16 and d["config"]["batch_per_gpu"] == 8
+    assert d["value"] > 0 and d["scaling"] == "weak" and d["cpu_baseline"] is None

@@ -149,6 +149,32 @@ def test_call_matches_oracle_chain_answers():
     assert got == want
     assert any(a != [] for a in want), "no frame produced a mask: pick another seed / bias"
 
+    # the FrameDealer worker's batched form (shard.dropin_worker batch=k): batches of up to 8 frames (ragged: 8, 8,
+    # 5, 8, 3), two in flight (batch j+1 begun before batch j's answers), answers built frame by frame in order; the
+    # frozen clock reads the frame FrameProcessor is answering
+    from vision_assist_amd.shard import _BatchedFrameProcessor
+    fl = [frames[i] for i in range(B)]
+    at = {id(f): 1_000_000.0 + 0.5 * (i + 1) for i, f in enumerate(fl)}
+
+    class FrameClock:
+        def __call__(self):
+            return at[id(fp.frame)]
+
+    path_analyser.clock = FrameClock()
+    path_analyser.previous_instructions = {}
+    path_finder.reset_angle_cache()
+    worker = _BatchedFrameProcessor(fp, 8)
+    sizes, i, got_b, pend = [8, 8, 5, 8, 3], 0, [], None
+    assert sum(sizes) == B
+    for n in sizes + [0]:
+        tok = worker.begin(fl[i:i + n]) if n else None
+        i += n
+        if pend is not None:
+            got_b += worker.end(pend)
+        pend = tok
+    path_analyser.clock = clock
+    assert got_b == want
+
 
 def test_predict_720x1280_letterboxed_matches_oracle():
     """YOLO.predict on a 720 x 1280 frame (the fixtures' native size): letterboxed on the device to 384 x 640;

@@ -39,15 +39,50 @@ class C4RecordWorker:
         return run
 
 
+class C4BatchRecordWorker(C4RecordWorker):
+    """The same records through the batching protocol (FrameDealer: max_batch / begin / end) on
+    pipeline.StreamBatches -- up to 4 waiting frames per device batch, two batches in flight."""
+
+    def __call__(self, device):
+        import torch
+
+        from tests.chain_util import weights
+        from vision_assist_amd.pipeline import StreamBatches
+        arch, fw = weights(self.regime)
+        sb = StreamBatches(arch, fw, 4, 640, 640, dtype="f32", device=torch.device("cuda", device))
+
+        class Fn:
+            max_batch = 4
+
+            def begin(self, frames):
+                return sb.begin(frames)
+
+            def end(self, tok):
+                res = sb.end(tok)
+                post = sb.pipes[tok[0] % 2].post
+                out = []
+                for i in range(tok[1]):
+                    nf = res.frame(i)
+                    det, _ = post.det_tensor(i)
+                    out.append({"det": det.numpy(), "chosen": int(post.chosen[i]), "rect": post.rects[i].cpu().tolist(),
+                                "cells": post.cells[i].cpu().numpy(), "status": nf.status,
+                                "queries": [(q["path"], float(q["cost"]).hex() if q["path"] else None)
+                                            for q in nf.queries]})
+                return out
+        return Fn()
+
+
+@pytest.mark.parametrize("batched", [False, True])
 @pytest.mark.parametrize("regime", ["sparse", "dense_box"])
-def test_dealer_two_workers_vs_per_shard_oracle_replay(regime):
+def test_dealer_two_workers_vs_per_shard_oracle_replay(regime, batched):
     import torch
 
     from tests.chain_util import compare, frame_batch, load_fixture
     from vision_assist_amd.shard import FrameDealer
     frames = [frame_batch(7000 + i, 1)[0].numpy() for i in range(N_FRAMES)]
     want = load_fixture(f"c4/{regime}")
-    with FrameDealer(C4RecordWorker(regime), [0, 0], 640, 640, slots=2) as d:
+    worker = C4BatchRecordWorker(regime) if batched else C4RecordWorker(regime)
+    with FrameDealer(worker, [0, 0], 640, 640, slots=4 if batched else 2) as d:
         got = list(d.map(frames))
     bad = []
     for i, (g, w) in enumerate(zip(got, want)):

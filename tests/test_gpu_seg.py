@@ -136,14 +136,14 @@ def test_conv_split_k(dtype, cin, cout, k, stride, H, W, residual, slice_in):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_forward_batch1_split_k_matches_unsplit(dtype, monkeypatch):
+def test_forward_batch1_split_k_matches_unsplit(dtype, monkeypatch, switch):
     """The batch-1 n-seg forward with split-K (the C2 shape) against the same forward with VA_SPLITK=0: f32 to
     f32 rounding of the reordered sums, bf16 to bf16 rounding of the stored activations."""
     arch, fw, net = _net(dtype, "n", seed=5)
     frames = _frames(1, seed=8)
-    monkeypatch.setenv("VA_SPLITK", "1")
+    switch("VA_SPLITK", "1")
     a = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_SPLITK", "0")
+    switch("VA_SPLITK", "0")
     b = _gpu_heads(net, frames)
     for name, x, y in zip(("box", "cls", "coef", "proto"), a, b):
         err = ((x - y).abs().max() / y.abs().max()).item()
@@ -169,8 +169,8 @@ def _frames(B, H=640, W=640, seed=0):
 
 
 @pytest.mark.parametrize("form", ["6", "0"])  # three-term bf16 products (default) / the f32 MFMA (VA_F32_SPLIT=0)
-def test_forward_f32_within_1e3_of_torch_reference(form, monkeypatch):
-    monkeypatch.setenv("VA_F32_SPLIT", form)  # read by the library per launch
+def test_forward_f32_within_1e3_of_torch_reference(form, monkeypatch, switch):
+    switch("VA_F32_SPLIT", form)  # the library re-reads its switches (va_switches_reload)
     torch.set_num_threads(8)
     arch, fw, net = _net("f32", "s")
     frames = _frames(2)
@@ -336,16 +336,16 @@ def test_conv0_f32_mfma_matches_fp32(cout, H, W):
 
 
 @pytest.mark.parametrize("B", [2, 3])
-def test_conv3t_matches_conv2_f32(B, monkeypatch):
+def test_conv3t_matches_conv2_f32(B, monkeypatch, switch):
     """conv3t (pre-split weight planes by LDS-DMA, activations split once per workgroup, 32 x 32 blocks) against
     conv2's three-term form (VA_CONV3T=0) on the f32 forward's wide layers -- 3x3 and 1x1, stride 2, Cout 224 (a
     ragged channel tile), the proto sub-pixel fold (mode 2), ragged pixel tiles at B = 3: the same six exact term
     products per f32 product summed in another order, so f32-rounding close; and within the f32 bar of torch."""
     arch, fw, net = _net("f32", "s", seed=5)
     frames = _frames(B, seed=11)
-    monkeypatch.setenv("VA_CONV3T", "0")
+    switch("VA_CONV3T", "0")
     ref = _gpu_heads(net, frames)
-    monkeypatch.delenv("VA_CONV3T")
+    switch("VA_CONV3T")
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         d = (g - r).abs().max().item()
@@ -366,14 +366,14 @@ def test_conv3t_matches_conv2_f32(B, monkeypatch):
     (64, 48, 23, 21, 3, True),     # narrow, ragged channels / columns, image seams, residual
     (32, 64, 40, 40, 2, False),    # narrow, two chunks
 ])
-def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual):
+def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual, switch):
     """conv3h (halo-staged B: the tile's input halo loaded and split once per 16-channel chunk, every 3x3 tap read
     from it; zero rows where a tap leaves the pixel's image) on single f32 ops: within f32 rounding of torch fp32
     and of conv3t (VA_CONV3H=0: per-tap staging, the same six term products summed in another order)."""
     got, ref = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
     scale = max(1.0, ref.abs().max().item())
     assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
-    monkeypatch.setenv("VA_CONV3H", "0")
+    switch("VA_CONV3H", "0")
     got_t, _ = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
     assert (got - got_t).abs().max().item() <= 2e-5 * scale
 
@@ -451,15 +451,15 @@ def test_fused_tails_f32_forward(monkeypatch):
 
 
 @pytest.mark.parametrize("B", [2, 3])
-def test_conv3h_matches_conv3t_forward(B, monkeypatch):
+def test_conv3h_matches_conv3t_forward(B, monkeypatch, switch):
     """The f32 forward with conv3h on its layers (every stride-1 3x3 with Cout > 64: P3-P5 C2f bottlenecks, the
     head's fused first 3x3 (Cout 224) and cls 3x3s, proto.cv1; the proto sub-pixel fold's 2x2 taps in mode 2) against
     the same forward on conv3t (VA_CONV3H=0): f32-rounding close, and within the f32 bar of torch."""
     arch, fw, net = _net("f32", "s", seed=5)
     frames = _frames(B, seed=13)
-    monkeypatch.setenv("VA_CONV3H", "0")
+    switch("VA_CONV3H", "0")
     ref = _gpu_heads(net, frames)
-    monkeypatch.delenv("VA_CONV3H")
+    switch("VA_CONV3H")
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         d = (g - r).abs().max().item()
@@ -471,7 +471,7 @@ def test_conv3h_matches_conv3t_forward(B, monkeypatch):
             assert (g - r).abs().max().item() <= 1e-3, name
 
 
-def test_patch_conv_matches_dn(monkeypatch):
+def test_patch_conv_matches_dn(monkeypatch, switch):
     """The patch-staged narrow 3x3 kernel (input patch in LDS once per 16 x 16 tile) against the im2col
     narrow-layer kernel on a whole bf16 forward (P2/P3 bottlenecks with residuals, the fused head tails).
     The 3x3 GEMMs use the same fragments and K order (bit-identical: cls and proto, which only see those);
@@ -479,9 +479,9 @@ def test_patch_conv_matches_dn(monkeypatch):
     kernel's channel-permuted weights make the tail's K order natural), so those agree to f32 rounding."""
     arch, fw, net = _net("bf16", "s", seed=8)
     frames = _frames(2, seed=9)
-    monkeypatch.setenv("VA_CONV_PATCH", "0")
+    switch("VA_CONV_PATCH", "0")
     ref = _gpu_heads(net, frames)
-    monkeypatch.delenv("VA_CONV_PATCH")
+    switch("VA_CONV_PATCH")
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         if name in ("cls", "proto"):
@@ -496,26 +496,24 @@ def test_patch_conv_matches_dn(monkeypatch):
     (128, 224, 3, 2, 40, 38, False),  # stride 2, ragged channel tile (head.l.0 width)
     (256, 384, 1, 1, 17, 30, True),   # 1x1, two channel tiles, residual
 ])
-def test_conv4_op(monkeypatch, cin, cout, k, stride, H, W, residual):
+def test_conv4_op(monkeypatch, cin, cout, k, stride, H, W, residual, switch):
     """conv4 (256 x 256 tiles, four-phase K-tile with counted vmcnt, permuted weight rows, epilogue from the
     accumulators) forced on single ops vs torch fp32 on the same bf16-rounded inputs."""
-    monkeypatch.setenv("VA_CONV4", "1")
-    monkeypatch.setenv("VA_CONV4_MIN", "1")
+    switch("VA_CONV4", "all")
     got, ref = _run_single_conv("bf16", cin, cout, k, stride, H, W, residual, False, 0, act=True)
     err = (got - ref).abs().max() / ref.abs().max()
     assert err < 2e-2, err
 
 
-def test_conv4_matches_conv2(monkeypatch):
+def test_conv4_matches_conv2(monkeypatch, switch):
     """conv4 forced onto every eligible layer of a bf16 forward (Cout > 128, Cin % 64 == 0) against conv2:
     same 32-deep MFMA k-sequence per output, so bit-identical."""
     arch, fw, net = _net("bf16", "s", seed=12)
     frames = _frames(2, seed=13)
-    monkeypatch.setenv("VA_SPLITK", "0")  # conv2 slicing the P5 layers' K loops would sum in another order
-    monkeypatch.setenv("VA_CONV4", "0")
+    switch("VA_SPLITK", "0")  # conv2 slicing the P5 layers' K loops would sum in another order
+    switch("VA_CONV4", "0")
     ref = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_CONV4", "1")
-    monkeypatch.setenv("VA_CONV4_MIN", "1")
+    switch("VA_CONV4", "all")
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: conv4 vs conv2 max diff {(g - r).abs().max().item()}"
@@ -737,7 +735,7 @@ def test_fpn_upsample_read_in_place(monkeypatch):
         assert torch.equal(g_, r), f"{name}: in-place upsample vs materialised, max diff {(g_ - r).abs().max().item()}"
 
 
-def test_forward_large_batch_pw_matches_conv2(monkeypatch):
+def test_forward_large_batch_pw_matches_conv2(monkeypatch, switch):
     """At bench batch sizes the persistent kernels loop over many tiles per wave (the 4-frame tests run one
     tile per wave): a 64-frame forward is finite, repeatable, and the streaming 1x1 layers agree with the same
     layers on conv2 (VA_PW=0) to bf16 rounding."""
@@ -749,9 +747,9 @@ def test_forward_large_batch_pw_matches_conv2(monkeypatch):
         torch.cuda.synchronize()
         return torch.cat([t.float().flatten(1, 2) for t in out.levels], 1), out.proto.float()
 
-    monkeypatch.setenv("VA_PW", "1")
+    switch("VA_PW", "1")
     a, b = run(), run()
-    monkeypatch.setenv("VA_PW", "0")
+    switch("VA_PW", "0")
     c = run()
     for x, y, z in zip(a, b, c):
         assert torch.isfinite(x).all()

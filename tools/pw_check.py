@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from vision_assist_amd import _lib  # noqa: E402
 from vision_assist_amd.seg import SegNet  # noqa: E402
 from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict  # noqa: E402
 
@@ -33,6 +34,7 @@ def main():
         frames = torch.randint(0, 256, (B, 640, 640, 3), generator=torch.Generator().manual_seed(B),
                                dtype=torch.uint8).cuda()
         os.environ["VA_PW"] = "1"
+        _lib.reload_switches()
         first = heads(net, frames)
         bad = 0
         for _ in range(args.reps):
@@ -42,8 +44,10 @@ def main():
                     bad += 1
         nonfin = [int((~torch.isfinite(t)).sum()) for t in first]
         os.environ["VA_PW"] = "0"
+        _lib.reload_switches()
         ref = heads(net, frames)
         os.environ["VA_PW"] = "1"
+        _lib.reload_switches()
         d = [((g - r).abs().max() / r.abs().max()).item() for g, r in zip(first, ref)]
         cls = lambda lv: int((lv[..., 64:64 + arch.nc].amax(-1) > 0).sum())  # noqa: E731
         print(f"B={B}: run-to-run mismatches {bad}, non-finite {nonfin}, pw vs conv2 rel max diff {d}, "

@@ -90,6 +90,7 @@ def main():
         for rnd in range(args.iters):
             for v in (v0, v1):
                 os.environ[name] = v
+                _lib.reload_switches()  # the library reads its switches once per process otherwise
                 net.run_plan(plan)  # one untimed forward after the switch
                 t = timed(1)
                 tot[v] = [a + b for a, b in zip(tot[v], t)]

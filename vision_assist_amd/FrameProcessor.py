@@ -250,8 +250,10 @@ class FrameProcessor:
         return cache[(H, W)]
 
     def _adopt(self, nav, batch, seen_after=None):
-        nf = batch.frame(0)
-        self._state = _FrameState(nf, nav.dims)
+        self._adopt_frame(nav.dims, batch.frame(0), seen_after)
+
+    def _adopt_frame(self, dims, nf, seen_after=None):
+        self._state = _FrameState(nf, dims)
         self._pending_seen = seen_after
         if nf.status == _lib.VA_FRAME_INDEX_ERROR:
             self._state = None
@@ -347,7 +349,11 @@ class FrameProcessor:
         pipe = self._pipe(H, W)
         from .post import PLANT_NEVER
         batch = pipe.run(t.reshape(1, H, W, 3), plant_mode=PLANT_NEVER)
-        self._adopt(pipe.nav, batch)
+        return self._answer(pipe.nav.dims, batch.frame(0), H, W)
+
+    def _answer(self, dims, nf, H: int, W: int):
+        """FrameProcessor.py:325-360 for one frame's device record: adopt it, then paths and the answer."""
+        self._adopt_frame(dims, nf)
         if not self._has_grids():
             self._state = None
             return (self.frame, []) if self.debug else []
@@ -383,13 +389,44 @@ class FrameProcessor:
 
     process = __call__  # the name BASELINE.json's north_star uses
 
+    # ------- a frame stream in device batches (the FrameDealer worker's form) -------
+    def _begin_batch(self, frames, max_batch: int):
+        """Enqueue up to max_batch host frames (uint8 [H, W, 3] each, one size) as one device batch
+        (YOLO.stream_batches: two batches in flight); the frames are copied out before this returns."""
+        if self.debug:
+            raise ValueError("debug frames are drawn per call: use __call__")
+        if self.model is None or not hasattr(self.model, "stream_batches"):
+            raise TypeError("FrameProcessor needs a vision_assist_amd.yolo.YOLO model (the device pipeline)")
+        H, W = int(frames[0].shape[0]), int(frames[0].shape[1])
+        sb = self.model.stream_batches(H, W, max_batch, seen=path_finder.seen)
+        return sb, sb.begin(frames), list(frames), H, W
+
+    def _end_batch(self, token) -> list:
+        """The answers of a begun batch, frame by frame in stream order -- __call__'s on each frame (the grid
+        stage ran the frames in order against the one angle cache); an IndexError object in the place of a frame
+        whose __call__ would raise it."""
+        sb, tok, frames, H, W = token
+        res = sb.end(tok)
+        dims = sb.pipes[0].nav.dims
+        out = []
+        for i, fr in enumerate(frames):
+            self.frame = fr
+            try:
+                out.append(self._answer(dims, res.frame(i), H, W))
+            except IndexError as e:
+                out.append(e)
+        return out
+
     # ------- multi-GPU stream (SURVEY.md §8e) -------
-    def map(self, frames, devices=None, slots: int = 4):
+    def map(self, frames, devices=None, slots: int = 16, batch: int = 8):
         """Answers of a frame stream in frame order, the frames dealt round-robin to one worker process per GPU
         (vision_assist_amd.shard.FrameDealer): frame i goes to devices[i % G], each worker running this model in
         its own FrameProcessor with its own PathFinder angle cache -- per shard the answers of __call__ over that
-        shard's frames in order.  devices: GPU indices (default: every visible GPU).  The first frame fixes the
-        frame size; the dealer is kept for later calls with the same devices and size (close_map ends it)."""
+        shard's frames in order.  devices: GPU indices (default: every visible GPU); batch: frames a worker runs as
+        one device batch (up to; what is waiting in its ring of ``slots`` frames).  The first frame fixes the
+        frame size; the dealer is kept for later calls with the same devices, size and model settings (close_map
+        ends it); a consumer that stops early leaves nothing behind for the next call (FrameDealer.map), and a
+        dealer whose worker died is dropped."""
         from .shard import FrameDealer, dropin_worker
         it = iter(frames)
         try:
@@ -398,19 +435,27 @@ class FrameProcessor:
             return
         H, W = int(first.shape[0]), int(first.shape[1])
         devices = list(range(torch.cuda.device_count())) if devices is None else list(devices)
-        key = (tuple(devices), H, W, slots)
+        if not hasattr(self.model, "spec"):
+            raise TypeError("FrameProcessor.map needs a vision_assist_amd.yolo.YOLO model")
+        calib = getattr(self.model, "fp8_calib", None)  # set after construction: travels with the worker spec
+        key = (tuple(devices), H, W, slots, batch, id(calib))
         dealers = self.__dict__.setdefault("_dealers", {})
         if key not in dealers:
-            if not hasattr(self.model, "spec"):
-                raise TypeError("FrameProcessor.map needs a vision_assist_amd.yolo.YOLO model")
             model, kw = self.model.spec
-            dealers[key] = FrameDealer(dropin_worker(model, **kw), devices, H, W, slots=slots)
+            dealers[key] = FrameDealer(dropin_worker(model, batch=batch, fp8_calib=calib, **kw), devices, H, W,
+                                       slots=slots)
+        d = dealers[key]
 
         def chain():
             yield first
             yield from it
 
-        yield from dealers[key].map(chain())
+        try:
+            yield from d.map(chain())
+        finally:
+            if d.broken:
+                dealers.pop(key, None)
+                d.close()
 
     def close_map(self) -> None:
         for d in self.__dict__.pop("_dealers", {}).values():

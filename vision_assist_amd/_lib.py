@@ -84,6 +84,7 @@ SIGNATURES = [
     ("va_letterbox", I32, [P, P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32]),
     ("va_abi_struct_sizes", I32, [P, I32]),
     ("va_diag", I32, [P, I32, I32]),
+    ("va_switches_reload", I32, []),
     ("va_version", ctypes.c_char_p, []),
 ]
 
@@ -108,6 +109,13 @@ def load(path: str = LIB_PATH):
 def check(rc: int, what: str) -> None:
     if rc != VA_OK:
         raise VaError(f"{what} failed with status {rc}")
+
+
+def reload_switches() -> None:
+    """Re-read the library's A/B switches from the environment (va_switches_reload; they are read once per process
+    otherwise).  For tests that hold two kernel forms against each other inside one process."""
+    if _LIB is not None:
+        check(_LIB.va_switches_reload(), "va_switches_reload")
 
 
 DIAG_UNITS = ("post", "contour", "nav")

@@ -82,7 +82,6 @@ __device__ __forceinline__ int cf_addr(int p, int c) { return p * CF_PS + 16 * c
 
 struct CfGeom {
     int N, H, W, ldx, ldy, tx, tpf, ntiles;
-    int getenv_rt;              // debug: trace with the 100 MHz real-time counter instead of the shader clock
     unsigned long long* trace;  // debug (va_c2f_trace): [grid][NW waves][CF_TR_TILES][CF_TR_PTS] clocks, or null
 };
 constexpr int CF_TR_TILES = 32, CF_TR_PTS = 6;
@@ -181,7 +180,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
     // stage boundary clocks of the first CF_TR_TILES tiles (debug only; one vector store per point)
     auto mark = [&](int k, int pt) {
         if (g.trace && k <= CF_TR_TILES && (tid & 63) == 0)
-            g.trace[((blockIdx.x * NW + wid) * CF_TR_TILES + k - 1) * CF_TR_PTS + pt] = (g.getenv_rt ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime());
+            g.trace[((blockIdx.x * NW + wid) * CF_TR_TILES + k - 1) * CF_TR_PTS + pt] = __builtin_amdgcn_s_memtime();
     };
     for (int k = 1; t >= 0; ++k) {
         mark(k, 0);
@@ -390,14 +389,12 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
     }
 }
 
-// configurations (VA_C2F_CFG): 0 = 16 x 16 tiles, 8 waves, one workgroup per CU, all weights in LDS;
-// 1 = the same with 16 waves; 2 = 8 x 16 tiles, 4 waves, two workgroups per CU (their phases drift
-// apart, so one's SiLU epilogues overlap the other's MFMAs), 1x1 weights in registers
-using CfA = CfCfg<16, 8, 1, false>;
-using CfB = CfCfg<16, 16, 1, false>;
+// the configuration: 8 x 16 tiles, 4 waves, two workgroups per CU (their phases drift apart, so one's SiLU
+// epilogues overlap the other's MFMAs), 1x1 weights in registers -- measured best in round 1 against 16 x 16
+// tiles with all weights in LDS and 8 or 16 waves per workgroup (one workgroup per CU), which were removed
 using CfC = CfCfg<8, 4, 2, true>;
 
-int g_cus = 0, g_cfg = 2;
+int g_cus = 0;
 unsigned long long* g_trace = nullptr;
 
 template <class C>
@@ -435,21 +432,16 @@ extern "C" int va_seg_c2f(void* stream, const va_conv_args* a) {
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return VA_ERR_HIP;
-        const char* e = getenv("VA_C2F_CFG");  // A/B timing of the configurations
-        g_cfg = e ? atoi(e) : 2;
     }
     CfGeom g;
     g.trace = g_trace;
-    g.getenv_rt = getenv("VA_C2F_TRACE_RT") != nullptr;
     g.N = a->N;
     g.H = a->H;
     g.W = a->W;
     g.ldx = a->ldx;
     g.ldy = a->ldy;
     hipStream_t st = (hipStream_t)stream;
-    const hipError_t rc = g_cfg == 0   ? cf_launch<CfA>(a, g, g_cus, st)
-                          : g_cfg == 1 ? cf_launch<CfB>(a, g, g_cus, st)
-                                       : cf_launch<CfC>(a, g, g_cus, st);
+    const hipError_t rc = cf_launch<CfC>(a, g, g_cus, st);
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

@@ -37,6 +37,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_switch.h"
 #include "va_contour.h"
 #include "va_dev.h"
 #include "va_diag.h"
@@ -1515,17 +1516,10 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     ca.polys = polys;
     ca.poly_n = poly_n;
     ca.poly_cap = poly_cap;
-    static const int gate_env = getenv("VA_CT_GATE") ? atoi(getenv("VA_CT_GATE")) : 1;  // A/B knob
-    ca.gate = gate_env;
-    static const int runs_env = getenv("VA_CT_RUNS") ? atoi(getenv("VA_CT_RUNS")) : 1;  // A/B knob
-    ca.runs = runs_env;
-    // images needing more than VA_CT_POOL_PAGES pages (default all 32) run in global memory (A/B knob)
-    // the pool kernel's LDS: VA_CT_PAGES pages (default all 32 = 160 KiB; fewer leave LDS for a concurrent conv
-    // workgroup of the next batch's forward on the same CU)
-    static const int pages_env = getenv("VA_CT_PAGES") ? atoi(getenv("VA_CT_PAGES")) : CP_PAGES;
-    ca.pages = pages_env < 1 ? 1 : (pages_env > CP_PAGES ? CP_PAGES : pages_env);
-    static const int pool_pages = getenv("VA_CT_POOL_PAGES") ? atoi(getenv("VA_CT_POOL_PAGES")) : CP_PAGES;
-    ca.pool_max = (int64_t)(pool_pages < ca.pages ? pool_pages : ca.pages) * CP_PAGE;
+    ca.gate = 1;
+    ca.runs = va_sw().ct_runs ? 1 : 0;  // VA_CT_RUNS=0: border following pixel by pixel (A/B, va_switch.h)
+    ca.pages = CP_PAGES;                // the pool form's LDS: all 32 pages (160 KiB)
+    ca.pool_max = (int64_t)CP_PAGES * CP_PAGE;
     const int64_t items = (int64_t)src.B * max_det;
     static DevVal<int> n_cu;  // per device: one pool block per CU
     if (n_cu() <= 0) {
@@ -1537,22 +1531,16 @@ hipError_t va_contour_launch(const CtSrc& src, const CtFrame& f, const CtScratch
     }
     const int pgrid = (int)(items < n_cu() ? items : n_cu());
     const int grid = (int)(items < sc.nslots ? items : sc.nslots);
-    // a slot per detection (small batches): the workgroup-per-detection form; VA_CT_WG=0 keeps the pool form (A/B)
-    static const bool wg_env = !(getenv("VA_CT_WG") && getenv("VA_CT_WG")[0] == '0');
-    // larger batches: the persistent workgroup form (VA_CT_WGP=0 keeps the pool form, A/B); its claim counter and
-    // frame prefix live in the last scratch slot
-    static const bool wgp_env = !(getenv("VA_CT_WGP") && getenv("VA_CT_WGP")[0] == '0');
+    // a slot per detection (small batches): the workgroup-per-detection form
+    // larger batches: the persistent workgroup form, one 160 KiB workgroup per CU (VA_CT_WGP=0 keeps the pool form,
+    // A/B, va_switch.h); its claim counter and frame prefix live in the last scratch slot
     int32_t* cbuf = (int32_t*)(sc.base + (int64_t)(sc.nslots - 1) * sc.slot_bytes);
-    if (wg_env && items <= sc.nslots) {
+    if (items <= sc.nslots) {
         hipLaunchKernelGGL(post_contour_wg_kernel, dim3((int)items), dim3(CT_WG_THREADS), CT_WG_LDS, st, ca);
-    } else if (wg_env && wgp_env && sc.nslots >= 2 && (int64_t)(src.B + 2) * 4 <= sc.slot_bytes) {
+    } else if (va_sw().ct_wgp && sc.nslots >= 2 && (int64_t)(src.B + 2) * 4 <= sc.slot_bytes) {
         hipLaunchKernelGGL(ct_prefix_kernel, dim3(1), dim3(1024), 0, st, src.ndet, src.B, max_det, cbuf);
-        // VA_CT_WGP_KB: LDS per workgroup in KiB (default: the whole pool, one per CU; 80 = two, a region past it in
-        // the workgroup's slot) -- A/B knob
-        static const int wgp_kb = getenv("VA_CT_WGP_KB") ? atoi(getenv("VA_CT_WGP_KB")) : 0;
-        const int lds = wgp_kb <= 0 ? CT_WG_LDS : (wgp_kb < 16 ? 16 : wgp_kb > CT_WG_LDS / 1024 ? CT_WG_LDS / 1024 : wgp_kb) * 1024;
-        const int per_cu = CT_WG_LDS / lds;
-        const int g = n_cu() * per_cu < sc.nslots - 1 ? n_cu() * per_cu : sc.nslots - 1;
+        const int lds = CT_WG_LDS;
+        const int g = n_cu() < sc.nslots - 1 ? n_cu() : sc.nslots - 1;
         hipLaunchKernelGGL(post_contour_wgp_kernel, dim3(g), dim3(CT_WG_THREADS), lds, st, ca, cbuf, lds);
     } else {
         hipLaunchKernelGGL(post_contour_pool_kernel, dim3(pgrid), dim3(CP_THREADS), (size_t)ca.pages * CP_PAGE, st,

@@ -6,10 +6,14 @@
 // current for the call and restored after it (a process may drive several GPUs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <mutex>
 
 #include "../../include/va355.h"
 #include "va_diag.h"
+#include "va_switch.h"
 
 struct va_handle_s {
     int32_t device;
@@ -28,9 +32,41 @@ struct DeviceScope {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+VaSwitches g_sw;
+std::once_flag g_sw_once;
+
+bool env_off(const char* name) {
+    const char* e = getenv(name);
+    return e && e[0] == '0';
+}
+
+void read_switches(VaSwitches& s) {
+    const char* e = getenv("VA_F32_SPLIT");
+    s.f32_split = !e ? 6 : e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
+    s.conv3h = !env_off("VA_CONV3H");
+    s.conv3t = !env_off("VA_CONV3T");
+    s.splitk = !env_off("VA_SPLITK");
+    s.patch = !env_off("VA_CONV_PATCH");
+    e = getenv("VA_CONV4");
+    s.conv4_min = !e ? 256 : e[0] == '0' ? -1 : strcmp(e, "all") == 0 ? 1 : 256;
+    s.pw = !env_off("VA_PW");
+    s.ct_runs = !env_off("VA_CT_RUNS");
+    s.ct_wgp = !env_off("VA_CT_WGP");
+}
 }  // namespace
 
+const VaSwitches& va_sw() {
+    std::call_once(g_sw_once, [] { read_switches(g_sw); });
+    return g_sw;
+}
+
 extern "C" {
+
+int va_switches_reload(void) {
+    va_sw();
+    read_switches(g_sw);
+    return VA_OK;
+}
 
 int va_create(int32_t device, uint32_t flags, va_handle* out) {
     if (!out || flags != 0) return VA_ERR_ARG;

@@ -962,10 +962,6 @@ struct DedupeLaunch {
     size_t lds;
 };
 
-// speculative rounds over `nslots` query slots.  With `dd` the dedupe kernel is enqueued behind every round's
-// validation, before the host waits for the round's verdict: a round that is final (the common case) then needs no
-// launch after the wait; a round that is re-run gets its dedupe again behind the next one (the filter reads the
-// query records afresh and rewrites every unique / order field, so only the last round's counts)
 // the records of a va_nav_run copied to the caller's host memory (va_nav_run_rb)
 struct ReadBack {
     void* dst;
@@ -973,9 +969,13 @@ struct ReadBack {
     int64_t bytes;
 };
 
-// speculative rounds over `nslots` query slots.  With `rb` the records are copied to the host behind every round's
-// kernels and ahead of its verdict copy, so the verdict wait also covers them: a final round (the common case)
-// returns with the records on the host; a re-run round copies them again
+// speculative rounds over `nslots` query slots.  With `dd` the dedupe kernel is enqueued behind every round's
+// validation, before the host waits for the round's verdict: a round that is final (the common case) then needs no
+// launch after the wait; a round that is re-run gets its dedupe again behind the next one (the filter reads the
+// query records afresh and rewrites every unique / order field, so only the last round's counts).  With `rb` the
+// records are copied to the host behind every round's kernels and ahead of its verdict copy, so the verdict wait
+// also covers them: a final round (the common case) returns with the records on the host; a re-run round copies
+// them again
 int astar_rounds(hipStream_t st, AstarArgs a, int32_t* ctrl, uint64_t* seen, int32_t* rounds_out,
                  const DedupeLaunch* dd = nullptr, const ReadBack* rb = nullptr) {
     size_t lds = astar_lds(a.LR * a.LC);

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_switch.h"
 #include "va_dev.h"
 #include "va_fuse.h"
 
@@ -150,8 +151,7 @@ int g_cus = 0;
 // 1x1 / stride 1 / mode 0 / Cout 128 / bf16 in and out, no residual or tail, K = Cin a multiple of 64 up to
 // 448 (the weights fit LDS), 16-byte aligned operands, every offset within 31 bits
 bool va_pw_eligible(const va_conv_args& a) {
-    const char* e = getenv("VA_PW");  // 0: keep these layers on conv2 (A/B timing; read per call)
-    if (e && e[0] == '0') return false;
+    if (!va_sw().pw) return false;  // VA_PW=0: keep these layers on conv2 (A/B timing, va_switch.h)
     if (a.dtype != VA_DTYPE_BF16 || a.out_f32 || a.kh != 1 || a.kw != 1 || a.stride != 1 || a.pad != 0 ||
         a.mode != 0 || a.w2 || a.res || a.Cout != 128 || a.Cin != a.K || a.K % 64 || a.K > PW_KMAX ||
         a.ldx % 8 || a.ldy % 8 || ((uintptr_t)a.x & 15) || ((uintptr_t)a.y & 15) || ((uintptr_t)a.w & 15) ||

@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include "../../include/va355.h"
+#include "va_switch.h"
 #include "va_dev.h"
 #include "va_fuse.h"
 
@@ -2699,28 +2700,17 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV_GLDS=0 stages through registers instead of LDS-DMA (A/B timing)
-bool getenv_glds() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("VA_CONV_GLDS");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 // Split-K policy (va_conv_args.ws): a launch of fewer than 128 tiles leaves most of the 256 CUs idle while each
 // tile walks its whole K loop, one LDS-DMA round trip + barrier per K-step -- the batch-1 forward's cost.  Cost
 // model per tile (us, measured at batch 1, profiles/r03/splitk/): ts per K-step (f32 three-term 1.4, bf16 0.6);
 // splitting into ks slices costs a slab write + ticket (1.0) and ~1.5 per slice of the combine (one workgroup reads
 // ks x 64 KiB).  Pick the ks <= 16
 // with tiles x ks <= 256 that minimises ceil(nk / ks) ts + 1.0 + 1.5 ks, if it beats the unsplit nk ts by 15 %.
-// VA_SPLITK=0 disables it (A/B timing; read per launch).  Returns the slice count (1 = no split); *kper = K-steps
+// VA_SPLITK=0 disables it (A/B timing, va_switch.h).  Returns the slice count (1 = no split); *kper = K-steps
 // per slice (every slice non-empty).
 int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* kper) {
     *kper = nk;
-    const char* e = getenv("VA_SPLITK");
-    if ((e && e[0] == '0') || !a.ws || !a.wcnt || tiles >= 128 || nk < 4 || tiles > a.ncnt) return 1;
+    if (!va_sw().splitk || !a.ws || !a.wcnt || tiles >= 128 || nk < 4 || tiles > a.ncnt) return 1;
     // cost model (us): K-steps per slice x ts + tw + tc per slice.  Swept in round 4 at batch 1 (tc 0.75 / 3, ts x1.43,
     // tiles x ks up to 512): the f32 s-seg and bf16 n-seg forwards within 1-2 % of these constants or slower
     // (profiles/r04/batch1/splitk_sweep.log)
@@ -2745,7 +2735,7 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
-    const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && getenv("VA_CONV_FK") == nullptr;
+    const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K;
     int kper = a.Kpad / KS, ks = 1;
     if (a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
     const int nb = ntiles * ks;
@@ -2754,7 +2744,7 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
                            a, ntn, nb, ks, kper);
         return hipGetLastError();
     }
-    if (getenv_glds() && a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
+    if (a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
             hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL>), dim3(nb), dim3(Cfg::NT), 0,
                                st, a, ntn, nb, ks, kper);
@@ -2768,10 +2758,9 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV_PATCH=0 keeps the narrow 3x3 layers on conv_dn (A/B timing; read per launch)
+// VA_CONV_PATCH=0 keeps the narrow 3x3 layers on conv_dn (A/B timing, va_switch.h)
 bool use_patch(const va_conv_args& a) {
-    const char* e = getenv("VA_CONV_PATCH");
-    if (e && e[0] == '0') return false;
+    if (!va_sw().patch) return false;
     if (a.w2 && a.c2 > a.Cout) return false;  // the tail runs TNS = Cout/16 output fragments
     return a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.mode == 0 && (a.Cin == 32 || a.Cin == 64) &&
            (a.Cout == 32 || a.Cout == 64) && a.K == 9 * a.Cin && a.ldx % 8 == 0 && ((uintptr_t)a.x & 15) == 0 &&
@@ -2812,18 +2801,18 @@ hipError_t launch_conv_patch(const va_conv_args& a, hipStream_t st) {
     return a.Cout == 32 ? launch_conv_patch_t<2, 8, TAIL, OutT, 8>(a, st) : launch_conv_patch_t<4, 8, TAIL, OutT, 8>(a, st);
 }
 
-// The Cout > 128 layers with at least VA_CONV4_MIN (default 256) 256 x 256 tiles run on conv4 (P3/P4 1x1 and
-// 3x3 layers 2-18 % faster than conv2, profiles/r01g); VA_CONV4=0 keeps them on conv2 (A/B timing; read per launch)
+// The Cout > 128 layers with at least 256 256 x 256 tiles run on conv4 (P3/P4 1x1 and 3x3 layers 2-18 % faster
+// than conv2, profiles/r01g); VA_CONV4=0 keeps them on conv2, VA_CONV4=all sends every eligible layer (A/B timing
+// and the parity tests, va_switch.h)
 bool use_conv4(const va_conv_args& a) {
-    const char* e = getenv("VA_CONV4");
-    if (e && e[0] == '0') return false;
+    const int mn = va_sw().conv4_min;
+    if (mn < 0) return false;
     if (a.mode != 0 || a.w2 || a.Cout <= 128 || a.Cin % 64 || a.K != a.kh * a.kw * a.Cin || a.Kpad != a.K ||
         a.ldx % 8 || ((uintptr_t)a.x & 15) || a.ldy % 8 || ((uintptr_t)a.y & 15) || a.Npad % 256 ||
         (a.res && (a.ldr % 8 || ((uintptr_t)a.res & 15))))
         return false;
-    const char* mn = getenv("VA_CONV4_MIN");
     const int64_t tiles = (int64_t)((a.M + 255) / 256) * ((a.Cout + 255) / 256);
-    return tiles >= (mn ? atoll(mn) : 256);
+    return tiles >= mn;
 }
 
 template <typename OutT>
@@ -2845,29 +2834,12 @@ hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV_DN=0 disables the narrow-layer kernel (A/B timing)
-bool getenv_dn() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("VA_CONV_DN");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 // f32 mode's MFMA form (conv2_kernel SPL): VA_F32_SPLIT = 0 (exact f32 MFMA), 6 (default) or 9 bf16 term
-// products; read per launch (A/B timing)
-int f32_split() {
-    const char* e = getenv("VA_F32_SPLIT");
-    if (!e) return 6;
-    return e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
-}
+// products (A/B timing, va_switch.h)
+int f32_split() { return va_sw().f32_split; }
 
-// VA_CONV3T=0 keeps the wide f32 layers on conv2's three-term form (A/B timing; read per launch)
-bool conv3t_off() {
-    const char* e = getenv("VA_CONV3T");
-    return e && e[0] == '0';
-}
+// VA_CONV3T=0 keeps the wide f32 layers on conv2's three-term form (A/B timing, va_switch.h)
+bool conv3t_off() { return !va_sw().conv3t; }
 
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
 bool use_conv3t(const va_conv_args& a) {
@@ -2898,11 +2870,8 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-// VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing; read per launch)
-bool conv3h_off() {
-    const char* e = getenv("VA_CONV3H");
-    return e && e[0] == '0';
-}
+// VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing, va_switch.h)
+bool conv3h_off() { return !va_sw().conv3h; }
 
 // conv3h's tile width for an output map Wo wide: the TW = 4 .. 32 that covers Wo with the fewest padded columns,
 // then the smallest halo, then the widest (longest contiguous halo rows); -1 when no width fits the halo buffer
@@ -3026,7 +2995,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             // workgroup, which a handful of tiles cannot amortise -- batch-1 model.16, 23.6 -> 16.7 us,
             // profiles/r03/batch1/)
             if (a.mode == 0 && a.Cout <= 64 && a.Cin % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 32 == 0 && a.M >= 4096 &&
-                (size_t)16 * ((a.Cout + 15) / 16) * (a.Kpad + 8) * 2 <= 120 * 1024 && getenv_dn()) {
+                (size_t)16 * ((a.Cout + 15) / 16) * (a.Kpad + 8) * 2 <= 120 * 1024) {
                 switch ((a.Cout + 15) / 16) {
                     case 1: return launch_conv_dn<1>(a, st);
                     case 2: return launch_conv_dn<2>(a, st);
@@ -3088,8 +3057,7 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
         hipStream_t st = (hipStream_t)stream;
         // e4m3 input: conv2's LDS-DMA tiles (narrow layers get the tall 256-pixel tiles), e4m3 or float output;
         // a bf16 input (model.0's map) or a bf16 output / residual: va_fp8.hip's register-staged kernel
-        const bool c2 = a->x8 && (a->out_f32 || a->yscale > 0.0f) && (!a->res || a->rscale > 0.0f) &&
-                        getenv("VA_FP8_CONV8") == nullptr;
+        const bool c2 = a->x8 && (a->out_f32 || a->yscale > 0.0f) && (!a->res || a->rscale > 0.0f);
         if (c2) {
             const int ov = a->out_f32 ? 4 : 16, cd = a->mode == 1 ? a->Cout / 4 : a->Cout;
             if (a->Cout % ov == 0 && cd % ov == 0 && a->ldy % ov == 0 && ((uintptr_t)a->y & 15) == 0 &&

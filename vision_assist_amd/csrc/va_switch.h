@@ -1,0 +1,19 @@
+// va_switch.h -- the library's A/B switches.  Every default is the measured-best form; the other
+// settings are kept for same-box comparisons and for the parity tests that hold two forms against each other.
+// They are read from the environment ONCE per process, at the first launch that consults them, never per launch;
+// va_switches_reload() (va355.h) re-reads them, for a test that changes one inside a process.
+#pragma once
+
+struct VaSwitches {
+    int f32_split;   // VA_F32_SPLIT: bf16 term products per f32 product, 6 (default) or 9; 0 = the f32 MFMA
+    bool conv3h;     // VA_CONV3H=0: the stride-1 multi-tap f32 layers on conv3t instead of the halo-staged kernel
+    bool conv3t;     // VA_CONV3T=0: the wide f32 layers on conv2's three-term form
+    bool splitk;     // VA_SPLITK=0: no split-K for launches of few tiles
+    bool patch;      // VA_CONV_PATCH=0: the narrow bf16 3x3 layers on conv_dn instead of the patch kernel
+    int conv4_min;   // VA_CONV4: 0 = conv4 off (-1 here), "all" = every eligible layer (1), default 256 tiles
+    bool pw;         // VA_PW=0: the bf16 128-channel 1x1 layers on conv2 instead of pw_kernel
+    bool ct_runs;    // VA_CT_RUNS=0: border following pixel by pixel (no straight-run probe)
+    bool ct_wgp;     // VA_CT_WGP=0: large-batch contours on the pool form instead of the persistent workgroups
+};
+
+const VaSwitches& va_sw();

@@ -71,34 +71,53 @@ class FramePipeline:
         The copy is numpy's (one thread): torch's CPU copy of a frame this size wakes the OpenMP pool, whose
         workers then spin between calls -- at a call every ~2 ms that kept 15 threads busy, and under the box's
         16-CPU quota the whole process was throttled ~8 ms in every 100 ms period (tools/dropin_split.py)."""
-        if getattr(self, "_pin", None) is None or self._pin.shape != frames.shape or self._pin.dtype != frames.dtype:
-            self._pin = torch.empty(frames.shape, dtype=frames.dtype, pin_memory=True)
+        frames = [frames] if isinstance(frames, torch.Tensor) else frames
+        n = sum(int(f.shape[0]) if f.ndim == 4 else 1 for f in frames)
+        if getattr(self, "_pin", None) is None:
+            self._pin = torch.empty((self.B, self.H, self.W, 3), dtype=torch.uint8, pin_memory=True)
             self._pin_np = self._pin.numpy()
             self._pin_ev = None
+        if n > self.B:
+            raise _lib.VaError(f"{n} frames for a pipeline of batch {self.B}")
         if self._pin_ev is not None:
             self._pin_ev.synchronize()
-        np.copyto(self._pin_np, frames.numpy())
-        return self._pin
+        i = 0
+        for f in frames:
+            a = f.numpy() if isinstance(f, torch.Tensor) else f
+            k = a.shape[0] if a.ndim == 4 else 1
+            np.copyto(self._pin_np[i:i + k], a.reshape(k, self.H, self.W, 3))
+            i += k
+        return self._pin[:n]
 
-    def load(self, frames: torch.Tensor, stream=None) -> None:
-        """Frames (uint8 BGR [B, H, W, 3], on the device or the host) into the network's input buffer, letterboxed
-        if needed, on ``stream`` (default: the current stream) -- the H2D copy, the letterbox and the pinned
-        buffer's release event all on that one stream; host frames go through a pinned staging buffer (_pinned)."""
+    def load(self, frames, stream=None) -> None:
+        """Frames (uint8 BGR [n, H, W, 3] with n <= B, on the device or the host; or a list of host frames, each
+        [H, W, 3]) into the first n entries of the network's input buffer, letterboxed if needed, on ``stream``
+        (default: the current stream) -- the H2D copy, the letterbox and the pinned buffer's release event all on
+        that one stream; host frames go through a pinned staging buffer (_pinned).  The network always runs B
+        frames: entries past n keep what they held (their results are simply not read, see nav_run)."""
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        staged = frames.device.type == "cpu" and not frames.is_pinned()
+        if isinstance(frames, (list, tuple)):
+            for f in frames:
+                if tuple(f.shape) != (self.H, self.W, 3) or f.dtype != np.uint8:
+                    raise _lib.VaError(f"frames must be uint8 [{self.H}, {self.W}, 3], got {tuple(f.shape)}")
+            staged = True
+        else:
+            if frames.ndim != 4 or tuple(frames.shape[1:]) != (self.H, self.W, 3) or frames.dtype != torch.uint8 \
+                    or frames.shape[0] > self.B:
+                raise _lib.VaError(f"frames must be uint8 [n <= {self.B}, {self.H}, {self.W}, 3], "
+                                   f"got {tuple(frames.shape)} {frames.dtype}")
+            staged = frames.device.type == "cpu" and not frames.is_pinned()
         if staged:
             frames = self._pinned(frames)
+        n = int(frames.shape[0])
         with torch.cuda.stream(st):
             if self.lb is None:
-                self.plan["frames"].copy_(frames, non_blocking=True)
+                self.plan["frames"][:n].copy_(frames, non_blocking=True)
             else:
-                if tuple(frames.shape) != (self.B, self.H, self.W, 3) or frames.dtype != torch.uint8:
-                    raise _lib.VaError(
-                        f"frames must be uint8 [{self.B}, {self.H}, {self.W}, 3], got {tuple(frames.shape)}")
                 frames = frames.to(self.device, non_blocking=True).contiguous()
                 Hn, Wn, top, left, newh, neww = self.lb
                 with torch.cuda.device(self.device):
-                    _lib.check(self.lib.va_letterbox(_lib.stream_ptr(st, self.device), frames.data_ptr(), self.B,
+                    _lib.check(self.lib.va_letterbox(_lib.stream_ptr(st, self.device), frames.data_ptr(), n,
                                                      self.H, self.W, self.plan["frames"].data_ptr(), Hn, Wn, top,
                                                      left, newh, neww), "va_letterbox")
             if staged:
@@ -137,9 +156,12 @@ class FramePipeline:
         out = self.plan["out"]
         self.post.run(out.levels, out.proto, plant_cells, plant_rects, plant_mode, select=True, stream=stream)
 
-    def nav_run(self, stream=None) -> NavBatch:
-        """Grid stage of the batch whose seg_post was enqueued (synchronises `stream`)."""
-        return self.nav.run(self.post.cells, self.post.rects, self.seen, stream)
+    def nav_run(self, stream=None, n: int | None = None, readback: bool = False) -> NavBatch:
+        """Grid stage of the batch whose seg_post was enqueued (synchronises `stream`): its first ``n`` frames
+        (default all B; frames past n never reach A*, so the angle cache advances over the n real frames only).
+        readback: the records land in host memory inside the call (va_nav_run_rb, one synchronisation)."""
+        n = self.B if n is None else n
+        return self.nav.run(self.post.cells[:n], self.post.rects[:n], self.seen, stream, readback=readback)
 
 
 class OverlappedPipelines:
@@ -195,7 +217,63 @@ class OverlappedPipelines:
         return res
 
 
-__all__ = ["FramePipeline", "OverlappedPipelines", "PLANT_IF_NONE", "PLANT_NEVER"]
+class StreamBatches:
+    """A frame stream in batches of up to B host frames with two batches in flight: ``begin(frames)`` stages the
+    frames in pinned memory and enqueues copy + network + post-processing on one of two network streams (it
+    returns as soon as the frames are copied out of the caller's memory), ``end(token)`` runs that batch's grid
+    stage on the grid stream -- in begin order, so the angle cache advances frame by frame in stream order -- and
+    returns its records on the host.  A caller that begins batch j + 1 before it ends batch j keeps the GPU on
+    batch j + 1's network while the host builds batch j's answers.  Two FramePipelines share one SegNet (the
+    weights) and the angle cache; a batch of n < B frames runs the network on B entries but only its n frames
+    reach the grid stage (FramePipeline.nav_run)."""
+
+    def __init__(self, arch, folded, B: int, H: int, W: int, dtype: str = "f32", device=None, seen=None,
+                 seg=None, **kw):
+        kw.setdefault("lanes", False)  # two whole forwards overlap already (as OverlappedPipelines)
+        first = FramePipeline(arch, folded, B, H, W, dtype=dtype, device=device, seen=seen, seg=seg, tag=0, **kw)
+        self.pipes = [first, FramePipeline(arch, folded, B, H, W, dtype=dtype, device=first.device, seen=first.seen,
+                                           seg=first.seg, tag=1, **kw)]
+        self.device, self.B = first.device, B
+        self.s_segs = tuple(torch.cuda.Stream(device=self.device) for _ in self.pipes)
+        self.s_nav = torch.cuda.Stream(device=self.device)
+        self.ready = [torch.cuda.Event() for _ in self.pipes]
+        self.k = 0      # batches begun
+        self.done = 0   # batches ended
+
+    def begin(self, frames) -> tuple[int, int]:
+        """Host frames (a list of uint8 [H, W, 3], at most B) -> a token for end().  At most two batches may be
+        begun and not ended."""
+        if not 0 < len(frames) <= self.B:
+            raise ValueError(f"1..{self.B} frames per batch, got {len(frames)}")
+        if self.k - self.done >= len(self.pipes):
+            raise RuntimeError("two batches are in flight: end() the older one first")
+        i = self.k % len(self.pipes)
+        p, st = self.pipes[i], self.s_segs[i]
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            p.load(list(frames), stream=st)
+            p.seg_post(stream=st)
+            self.ready[i].record(st)
+        tok = (self.k, len(frames))
+        self.k += 1
+        return tok
+
+    def end(self, token) -> NavBatch:
+        """The grid stage of a begun batch (tokens in begin order); returns with the records on the host."""
+        j, n = token
+        if j != self.done:
+            raise RuntimeError(f"batches end in begin order: expected {self.done}, got {j}")
+        i = j % len(self.pipes)
+        self.s_nav.wait_event(self.ready[i])
+        with torch.cuda.stream(self.s_nav):
+            res = self.pipes[i].nav_run(stream=self.s_nav, n=n, readback=True)
+        # the next begin() on this pipeline rewrites cells / rects the grid stage just read: order it after it
+        self.s_segs[i].wait_stream(self.s_nav)
+        self.done += 1
+        return res
+
+
+__all__ = ["FramePipeline", "OverlappedPipelines", "StreamBatches", "PLANT_IF_NONE", "PLANT_NEVER"]
 
 
 class SegPostGraph:

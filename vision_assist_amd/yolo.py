@@ -87,12 +87,31 @@ class YOLO:
         from .pipeline import FramePipeline
         key = (H, W, conf, iou, max_det, imgsz)
         if key not in self._pipes:
-            if self.device is None:
-                self.to("cuda")
             self._pipes[key] = FramePipeline(self.arch, self.folded, 1, H, W, dtype=self.dtype, conf=conf, iou=iou,
                                              max_det=max_det, device=self.device, seen=seen, imgsz=imgsz,
-                                             fp8_calib=self.fp8_calib)
+                                             fp8_calib=self.fp8_calib, seg=self._segnet())
         return self._pipes[key]
+
+    def stream_batches(self, H: int, W: int, B: int, seen=None, conf: float = 0.5, iou: float = 0.7,
+                       max_det: int = 300, imgsz: int | None = 640):
+        """A frame stream in device batches of up to B frames (pipeline.StreamBatches, cached), on the same
+        weights as ``pipeline`` and predict's defaults: FrameProcessor's batched form (FrameDealer workers)."""
+        from .pipeline import StreamBatches
+        key = ("batches", H, W, B, conf, iou, max_det, imgsz)
+        if key not in self._pipes:
+            self._pipes[key] = StreamBatches(self.arch, self.folded, B, H, W, dtype=self.dtype, conf=conf, iou=iou,
+                                             max_det=max_det, device=self.device, seen=seen, imgsz=imgsz,
+                                             fp8_calib=self.fp8_calib, seg=self._segnet())
+        return self._pipes[key]
+
+    def _segnet(self):
+        """The packed weights on the device, one SegNet shared by every pipeline of this model."""
+        from .seg import SegNet
+        if self.device is None:
+            self.to("cuda")
+        if getattr(self, "_seg", None) is None or self._seg.device != self.device:
+            self._seg = SegNet(self.arch, self.folded, dtype=self.dtype, device=self.device)
+        return self._seg
 
     def predict(self, source, conf: float = 0.5, verbose: bool = False, iou: float = 0.7, max_det: int = 300,
                 imgsz: int | None = 640):
