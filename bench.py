@@ -97,9 +97,9 @@ def parse():
                    help="network streams of the c4 extra (3 + the grid stage's stream: one hardware queue each)")
     p.add_argument("--dealer-workers-per-gpu", type=int, default=1,
                    help="FrameProcessor worker processes per GPU in the dealer extra (each its own PathFinder shard)")
-    p.add_argument("--dealer-batch", type=int, default=8,
+    p.add_argument("--dealer-batch", type=int, default=32,
                    help="frames a dealer worker runs as one device batch (up to; what waits in its ring)")
-    p.add_argument("--dealer-slots", type=int, default=16, help="ring slots per dealer worker")
+    p.add_argument("--dealer-slots", type=int, default=64, help="ring slots per dealer worker")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -487,7 +487,7 @@ def dealer_rate(args, dev, frames_n: int = 1024) -> dict:
     ngpu = max(1, torch.cuda.device_count())
     rng = np.random.default_rng(78)
     frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
-    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", batch=args.dealer_batch,
+    with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", batch=args.dealer_batch, quiet=True,
                                    **regime_kwargs(args.regime, 640)),
                      [w % ngpu for w in range(G)], 640, 640, slots=args.dealer_slots) as d:
         for _ in d.map(frames[i % 16] for i in range(32 * G)):  # warm: plans, first launches, lanes' streams

@@ -866,3 +866,28 @@ def test_forward_bf16_medium_1280_close():
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, c["ref"]):
         rel = ((g - r).norm() / r.norm()).item()
         assert rel < 5e-2, f"{name}: relative L2 error {rel}"
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_c2_plan_nseg_bf16_batch1_vs_fp32_oracle(seed):
+    """C2's own configuration (BASELINE.json configs[1]: YOLOv8n-seg 640x640 bf16, batch 1; the weights of bench.py's
+    c2 extra, the sparse regime) through the plan the planner builds for it -- the laned list (head levels 0 / 1 and
+    proto on lanes 1 / 2 beside the neck), split-K on the few-tile layers, model.0 fused with the preprocess, the
+    patch kernel on the narrow 3x3 layers -- against the plain-PyTorch fp32 oracle (oracle/yolo_ref.py) at the bf16
+    bar: relative L2 < 5e-2 per head output (the other batch-1 tests hold this plan only against itself)."""
+    from vision_assist_amd.seg import SegNet
+    from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
+    arch = Arch("n")
+    fw = fold(arch, synthetic_state_dict(arch, seed=0, sparse=640))
+    net = SegNet(arch, fw, dtype="bf16")
+    p = net.plan(1, 640, 640)
+    assert {op.lane for op in p["ops"]} == {0, 1, 2}, "the batch-1 plan is laned"
+    assert p["meta"][0]["name"] == "model.0"  # preprocess fused into model.0 (conv0)
+    torch.set_num_threads(8)
+    frames = _frames(1, seed=seed)
+    got = _gpu_heads(net, frames)
+    ref = _ref_heads(arch, fw, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.isfinite(g).all(), name
+        rel = ((g - r).norm() / r.norm()).item()
+        assert rel < 5e-2, f"{name}: relative L2 error {rel}"

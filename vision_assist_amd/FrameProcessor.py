@@ -418,7 +418,7 @@ class FrameProcessor:
         return out
 
     # ------- multi-GPU stream -------
-    def map(self, frames, devices=None, slots: int = 16, batch: int = 8):
+    def map(self, frames, devices=None, slots: int = 64, batch: int = 32):
         """Answers of a frame stream in frame order, the frames dealt round-robin to one worker process per GPU
         (vision_assist_amd.shard.FrameDealer): frame i goes to devices[i % G], each worker running this model in
         its own FrameProcessor with its own PathFinder angle cache -- per shard the answers of __call__ over that

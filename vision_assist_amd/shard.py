@@ -321,15 +321,21 @@ class dropin_worker:
     frames one by one.  Picklable (the YOLO constructor's arguments plus post-construction settings such as
     ``fp8_calib``; the weights are built inside the worker)."""
 
-    def __init__(self, model: str = "yolov8s-seg.pt", batch: int = 8, fp8_calib=None, **yolo_kw):
-        self.model, self.kw, self.batch = model, yolo_kw, batch
+    def __init__(self, model: str = "yolov8s-seg.pt", batch: int = 8, fp8_calib=None, quiet: bool = False,
+                 **yolo_kw):
+        """quiet: the worker's stdout to /dev/null (FrameProcessor prints "No path found." as the reference does)."""
+        self.model, self.kw, self.batch, self.quiet = model, yolo_kw, batch, quiet
         self.fp8_calib = None if fp8_calib is None else np.asarray(torch.as_tensor(fp8_calib).cpu())
 
     def __call__(self, device):
+        import os
+        import sys
         import warnings
 
         from .FrameProcessor import FrameProcessor
         from .yolo import YOLO
+        if self.quiet:
+            sys.stdout = open(os.devnull, "w")
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")
             yolo = YOLO(self.model, **self.kw).to(torch.device("cuda", device))
