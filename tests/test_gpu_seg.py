@@ -373,6 +373,9 @@ def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual, switch):
     got, ref = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
     scale = max(1.0, ref.abs().max().item())
     assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+    switch("VA_CONV3H", "af")  # the A stage as f32, split in registers: the same terms, the same products
+    got_af, _ = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
+    assert torch.equal(got_af, got), (got_af - got).abs().max().item()
     switch("VA_CONV3H", "0")
     got_t, _ = _run_single_conv("f32", cin, cout, 3, 1, H, W, residual, w3=True, B=B)
     assert (got - got_t).abs().max().item() <= 2e-5 * scale
@@ -891,3 +894,19 @@ def test_c2_plan_nseg_bf16_batch1_vs_fp32_oracle(seed):
         assert torch.isfinite(g).all(), name
         rel = ((g - r).norm() / r.norm()).item()
         assert rel < 5e-2, f"{name}: relative L2 error {rel}"
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_conv3h_f32_a_stage_forward_bit_identical(B, switch):
+    """conv3h with its A stage as f32 weights split in registers (VA_CONV3H=af: 4 instead of 6 L2 -> LDS bytes per
+    weight) against the pre-split planes (the device split3 and the host's split3_bf16 give the same three terms, and
+    the MFMA order is unchanged): the whole f32 forward -- every conv3h layer incl. the fused tails and the proto's
+    sub-pixel classes -- bit-identical."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(B, seed=19)
+    switch("VA_CONV3H", "planes")
+    ref = _gpu_heads(net, frames)
+    switch("VA_CONV3H", "af")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.equal(g, r), f"{name}: af vs planes max diff {(g - r).abs().max().item()}"

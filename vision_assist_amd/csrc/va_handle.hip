@@ -43,7 +43,8 @@ bool env_off(const char* name) {
 void read_switches(VaSwitches& s) {
     const char* e = getenv("VA_F32_SPLIT");
     s.f32_split = !e ? 6 : e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
-    s.conv3h = !env_off("VA_CONV3H");
+    e = getenv("VA_CONV3H");
+    s.conv3h = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
     s.conv3t = !env_off("VA_CONV3T");
     s.splitk = !env_off("VA_SPLITK");
     s.patch = !env_off("VA_CONV_PATCH");

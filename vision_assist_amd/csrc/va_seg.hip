@@ -1335,13 +1335,18 @@ static_assert(T3H_NU * T3H_NT >= 2 * T3H_HMAX, "halo units");
 // weights of the chunk, one BN x 96-byte block per tap.  (TPS = 2 on the narrow tiles -- the wide tiles' 24 MFMAs per
 // wave and barrier -- measured neutral, 14.10 vs 14.11 ms per 64-frame forward, profiles/r04/conv3h_tps/; the
 // library instantiates TPS = 1 only)
-template <int TNS, int TPS = 1>
+// AF: the A stage holds the weights as f32 (64-byte rows of 16 channels, DMA'd from va_conv_args.w) and every wave
+// splits its A fragments into the three bf16 terms in registers (split3_bf16: the same terms the host's split3_bf16
+// pre-splits, so the same products) -- 4 instead of 6 L2 -> LDS bytes per weight, the stream that fills the L2 on
+// the 128-channel layers
+template <int TNS, int TPS = 1, bool AF = false>
 struct T3HCfg {
     static constexpr int BN = 32 * TNS;
-    static constexpr int ABLK = BN * T3H_ROW;                     // one tap's weights of a chunk: 12 / 6 KiB
+    static constexpr int AROW = AF ? 64 : T3H_ROW;                // LDS bytes per weight row of a (tap, chunk)
+    static constexpr int ABLK = BN * AROW;                        // one tap's weights of a chunk: 12 / 6 KiB (AF 8 / 4)
     static constexpr int ASTAGE = TPS * ABLK;
-    static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6)
-    static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2)
+    static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6; AF 8 / 4)
+    static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2; AF 2 / 1)
     static constexpr int ZROW = T3H_NSA * ASTAGE + 2 * T3H_HALO;  // the zero row
     static constexpr int SINK = ZROW + 128;                       // 1 KiB the idle pieces' zero DMAs land in
     static constexpr int LDS0 = NP % 4 ? SINK + 1024 : ZROW + T3H_ROW;
@@ -1366,10 +1371,10 @@ __device__ __forceinline__ void t3h_unroll(F&& f) {
     }
 }
 
-template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1, bool AF = false>
 __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn, int ntiles, int lgw, int tiles_x) {
     extern __shared__ __align__(16) unsigned char smh[];
-    using Cfg = T3HCfg<TNS, TPS>;
+    using Cfg = T3HCfg<TNS, TPS, AF>;
     constexpr int BM = T3H_BM, BN = Cfg::BN, NT = T3H_NT, WN = 2, CB = TNS / 2, T = KH * KW;
     constexpr int S = (T + TPS - 1) / TPS;  // K-steps per chunk
     static_assert(S >= 2, "the halo is stored at a chunk's second step");
@@ -1392,35 +1397,44 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     const int n0 = tn * BN;
     const int nch = a.Cin / T3_KS;
     const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    // A source: the pre-split planes (w3), or with AF the f32 weights (w); mode 2: the sub-pixel class's matrix
+    const void* WA = AF ? (const void*)((const float*)a.w + (int64_t)cls * a.Npad * a.Kpad)
+                        : (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
     auto stA = [&](int s) { return smh + s * Cfg::ASTAGE; };
     auto halo = [&](int b) { return smh + T3H_NSA * Cfg::ASTAGE + b * T3H_HALO; };
 
     // ---- A DMA: piece P = wid + 4 j of a stage (1 KiB, linear in LDS); lane l writes bytes 16 l of it: row o / 96,
-    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run.  Every wave issues
-    // NA pieces per K-step (12 over 4 waves; 64-channel tiles: 6, so waves 2-3 send their second piece's zeros to a
-    // sink): a fixed count, no branch, so the counted waits and the compiler's own stay exact
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run (AF: row o / 64,
+    // slot (o % 64) / 16 -> f32 quarter slot ^ ((row >> 2) & 3)).  Every wave issues NA pieces per K-step (12 over 4
+    // waves; 64-channel tiles: 6, so waves 2-3 send their second piece's zeros to a sink; AF: 8 / 4, even): a fixed
+    // count, no branch, so the counted waits and the compiler's own stay exact
+    const int wa_bytes = AF ? a.Npad * a.Kpad * 4 : a.Npad * a.Kpad * 3 * 2;
     constexpr int OOR = 0x7ff00000;
     constexpr int NA = Cfg::NAW;
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
         const int o = (1024 * (wid + (NT / 64) * j)) % Cfg::ABLK + 16 * lane;  // offset in the piece's tap block
-        const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
-        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+        if constexpr (AF) {
+            const int row = o / 64, q = ((o - row * 64) >> 4) ^ ((row >> 2) & 3);
+            aoff[j] = ((n0 + row) * a.Kpad + 4 * q) * 4;
+        } else {
+            const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
+            aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
+        }
     }
     // stage s <- the weights of taps TPS t .. of chunk c (kl_h = tap * nch + chunk, or -1: zeros); a piece's tap
     // block is wave-uniform, so the per-tap source offset is a scalar select
     auto dmaA = [&](int kl0, int kl1, int s) {
         unsigned char* base = stA(s);
-        const int so0 = kl0 >= 0 ? kl0 * 96 : OOR, so1 = kl1 >= 0 ? kl1 * 96 : OOR;
+        constexpr int KLB = AF ? 64 : 96;  // source bytes of one (tap, chunk) run of a row
+        const int so0 = kl0 >= 0 ? kl0 * KLB : OOR, so1 = kl1 >= 0 ? kl1 * KLB : OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
             const int P = wid + (NT / 64) * j;
             const bool real = Cfg::NP % 4 == 0 || P < Cfg::NP;  // wave-uniform: scalar selects, no branch
             const int soff = TPS > 1 && P * 1024 >= Cfg::ABLK ? so1 : so0;
-            t3_dma16(W3, w3_bytes, real ? base + P * 1024 : smh + Cfg::SINK, aoff[j], real ? soff : OOR);
+            t3_dma16(WA, wa_bytes, real ? base + P * 1024 : smh + Cfg::SINK, aoff[j], real ? soff : OOR);
         }
     };
     // the kl of tap slot h of step t of chunk c (-1 past the taps or the chunks)
@@ -1520,10 +1534,18 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
                 const unsigned char* as_ = stA(k % T3H_NSA) + h * Cfg::ABLK;
 #pragma unroll
                 for (int ib = 0; ib < CB; ++ib) {
-                    const int row = wn * 32 * CB + 32 * ib + r32, sw = (row >> 3) & 1;
+                    const int row = wn * 32 * CB + 32 * ib + r32;
+                    if constexpr (AF) {  // this lane's 8 f32 weights (two 16-byte quarters), split here
+                        const int sw = (row >> 2) & 3;
+                        const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
+                        const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
+                        split3_bf16(lo, hi, ap[ib]);
+                    } else {
+                        const int sw = (row >> 3) & 1;
 #pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
+                        for (int p = 0; p < 3; ++p)
+                            ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
+                    }
                 }
 #pragma unroll
                 for (int jb = 0; jb < 2; ++jb) {
@@ -2871,7 +2893,7 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
 }
 
 // VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing, va_switch.h)
-bool conv3h_off() { return !va_sw().conv3h; }
+bool conv3h_off() { return va_sw().conv3h == 0; }
 
 // conv3h's tile width for an output map Wo wide: the TW = 4 .. 32 that covers Wo with the fewest padded columns,
 // then the smallest halo, then the widest (longest contiguous halo rows); -1 when no width fits the halo buffer
@@ -2894,12 +2916,12 @@ bool conv3h_shape_ok(const va_conv_args& a) {
 
 bool use_conv3h(const va_conv_args& a) { return !conv3h_off() && conv3h_shape_ok(a); }
 
-template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
-hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
-    using Cfg = T3HCfg<TNS, TPS>;
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1, bool AF = false>
+hipError_t launch_conv3h_af(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3HCfg<TNS, TPS, AF>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>,
+        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS, AF>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -2909,9 +2931,17 @@ hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
     const int tiles_x = (a.Wo + tw - 1) / tw, tiles_y = (a.N * a.Ho + th - 1) / th;
     const int ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = tiles_x * tiles_y * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a, ntn,
-                       ntiles, lgw, tiles_x);
+    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS, AF>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a,
+                       ntn, ntiles, lgw, tiles_x);
     return hipGetLastError();
+}
+
+// the A stage's form (VA_CONV3H, va_switch.h): the pre-split planes, or f32 split in registers (AF) -- the f32
+// weights (va_conv_args.w) are always there in f32 mode
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
+hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
+    if (va_sw().conv3h == 2) return launch_conv3h_af<KH, KW, TNS, OutT, TAIL, TPS, true>(a, st);
+    return launch_conv3h_af<KH, KW, TNS, OutT, TAIL, TPS, false>(a, st);
 }
 
 // the narrow f32 3x3 layers (33-64 output channels) on conv3h's 64-channel tiles: the conv3t conditions but Cout,
