@@ -332,19 +332,36 @@ def test_fp8_forward_real_frames_vs_fp32_oracle(calib):
 FP8_CHAIN_FLOOR = {"dense_box": {"chosen": 0.125, "cells": 0.625, "paths": 0.625}, "sparse": {}}
 
 
+# the weight-only form (SegNet dtype "w8a16": e4m3 weights dequantized into bf16, bf16 activations): measured on the
+# GPU before these floors were set (profiles/r05/c5/), floors one frame below; a CPU simulation with fp32 activations
+# (tools/w8a16_sim.py, profiles/r05/w8a16_sim_dense_box.json) gave dense_box chosen 0.75, cells / paths 0.875
+W8A16_CHAIN_FLOOR = {"dense_box": {}, "sparse": {}}
+
+
+@pytest.mark.parametrize("regime", ["dense_box", "sparse"])
+def test_w8a16_chain_1280_vs_fp32_oracle(regime):
+    """C5's weight-only form down the whole chain (m@1280, 8 frames) against the fp32 oracle chain, as
+    test_fp8_chain_1280_vs_fp32_oracle does for the e4m3 MFMA form: rates written out, held to measured floors."""
+    _chain_1280("w8a16", regime, W8A16_CHAIN_FLOOR[regime])
+
+
 @pytest.mark.parametrize("regime", ["dense_box", "sparse"])
 def test_fp8_chain_1280_vs_fp32_oracle(regime):
     """C5's whole chain at fp8 (BASELINE configs[4]: YOLOv8m-seg 1280 on e4m3 MFMA): the network's own detections
     through NMS, contours, the mask choice and grid / A* on 4 frames, against the fp32 oracle chain
     (tests/golden/chain_oracle.json.gz["c5/*"]): detections matched (boxes within 2 px, scores within 2e-2), the
     same chosen instance, cells and A* paths -- rates written out and held to measured floors."""
+    _chain_1280("fp8", regime, FP8_CHAIN_FLOOR[regime])
+
+
+def _chain_1280(dtype, regime, floors):
     from tests.chain_util import compare, frame_batch, load_fixture, rates, weights
     from vision_assist_amd.pipeline import FramePipeline
     from vision_assist_amd.post import PLANT_NEVER
     arch, fw = weights(regime, scale="m")
     want = load_fixture(f"c5/{regime}")
     B = len(want)
-    pipe = FramePipeline(arch, fw, B, 1280, 1280, dtype="fp8")
+    pipe = FramePipeline(arch, fw, B, 1280, 1280, dtype=dtype)
     res = pipe.run(frame_batch(8000, B, 1280).cuda(), plant_mode=PLANT_NEVER)
     torch.cuda.synchronize()
     cmps = []
@@ -360,8 +377,8 @@ def test_fp8_chain_1280_vs_fp32_oracle(regime):
                "costs": [float(q["cost"]).hex() if q["path"] else None for q in nf.queries] if ok else None}
         cmps.append(compare(got, w, f32=False))
     rr = rates(cmps)
-    _FP8_REPORT[f"chain_1280/{regime}"] = rr
+    _FP8_REPORT[f"chain_1280/{regime}" if dtype == "fp8" else f"{dtype}_chain_1280/{regime}"] = rr
     _write_report()
-    print("fp8 chain", regime, rr)
-    for k, floor in FP8_CHAIN_FLOOR[regime].items():
+    print(dtype, "chain", regime, rr)
+    for k, floor in floors.items():
         assert rr[k] >= floor, (k, rr[k], floor)

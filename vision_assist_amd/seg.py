@@ -81,6 +81,24 @@ class Packed:
     w3: torch.Tensor | None = None  # f32 mode: the weights as three exact bf16 terms (split3_bf16, va_conv_args.w3)
 
 
+def quantize_weights_e4m3(folded: dict) -> dict:
+    """The folded weights with every conv but model.0 rounded to e4m3 values times one f32 scale per output channel
+    (the channel's largest |w| maps to 448, round to nearest even: _pack_fp8's quantization), returned in float32."""
+    out = {}
+    for k, v in folded.items():
+        w, b = v
+        if k == "model.0" or w.dim() != 4:
+            out[k] = v
+            continue
+        wf = w.float()
+        amax = wf.abs().flatten(1).amax(1) if not k.endswith("upsample") else wf.abs().transpose(0, 1).flatten(1).amax(1)
+        sw = torch.where(amax > 0, amax / F8_MAX, torch.ones_like(amax))
+        shape = (-1, 1, 1, 1) if not k.endswith("upsample") else (1, -1, 1, 1)
+        q = (wf / sw.view(shape)).clamp(-F8_MAX, F8_MAX).to(torch.float8_e4m3fn).float()
+        out[k] = (q * sw.view(shape), b)
+    return out
+
+
 def split3_bf16(w: torch.Tensor) -> torch.Tensor:
     """f32 [..., K] (K % 8 == 0) -> bf16 [..., K / 8, 3, 8]: per 8-element group the round-to-nearest bf16 h of each
     value, then m = bf16(x - h), then l = bf16(x - h - m) -- x == h + m + l exactly (both subtractions are exact in
@@ -129,8 +147,15 @@ class SegNet:
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
-        if dtype not in ("bf16", "f32", "fp8"):
-            raise ValueError(f"dtype {dtype!r}: bf16, f32 or fp8")
+        if dtype not in ("bf16", "f32", "fp8", "w8a16"):
+            raise ValueError(f"dtype {dtype!r}: bf16, f32, fp8 or w8a16")
+        # w8a16 (C5's weight-only form): every conv's weights quantized to e4m3 with one scale per output channel, as
+        # the fp8 mode packs them (_pack_fp8), and dequantized once into the bf16 weights; activations bf16, the bf16
+        # MFMA kernels -- so only the weights carry e4m3's 3-bit mantissa (model.0 stays bf16, as in the fp8 mode)
+        self.form = dtype
+        if dtype == "w8a16":
+            folded = quantize_weights_e4m3(folded)
+            dtype = "bf16"
         self.dtype = dtype
         self.tdtype = torch.bfloat16 if self.store == "bf16" else torch.float32
         self.va_dtype = VA_DTYPE_BF16 if self.store == "bf16" else VA_DTYPE_F32
