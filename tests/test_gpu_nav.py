@@ -158,3 +158,38 @@ def test_nav_rect_past_the_frame(rect, err):
     else:
         out = onav.frame_nav(cells_to_mask(g), rect, H, W, onav.PathFinderOracle())
         _oracle_compare(nf, out, set(), [q[4] for q in out["queries"]], str(rect))
+
+
+def test_standalone_singletons_on_caller_built_grids():
+    """PenaltyCalculator.calculate_penalty and ProtrusionDetector()(frame, grids, lookup) on grids built OUTSIDE this
+    package's FrameProcessor -- here by the oracle's builder, pinned to the reference's -- as the reference's
+    FrameProcessor._calculate_penalties / __call__ drive them (/root/reference FrameProcessor.py:180-182, :341): the
+    device grid stage runs on the frame the grids imply (FrameProcessor.device_frame_for) and serves every penalty
+    bit-exact with its python type, and the peaks, against the reference-run goldens (the fixtures, corridors and
+    edge cases of tests/test_standalone_cpu.py)."""
+    from tests.golden_io import unhex
+    from tests.test_standalone_cpu import _as_grids, _frames
+    from vision_assist_amd.FrameProcessor import FrameProcessor
+    from vision_assist_amd.PenaltyCalculator import penalty_calculator
+    from vision_assist_amd.PathFinder import path_finder
+    from vision_assist_amd.ProtrusionDetector import ProtrusionDetector
+    fp = FrameProcessor(model=None)
+    seen_before = path_finder.seen.t.clone()
+    for name, fr in _frames()[:40]:
+        H, W = fr["H"], fr["W"]
+        st = onav.build_grids(cells_to_mask(cells_of(fr)), tuple(fr["rect"]), H, W)
+        grids, lookup = _as_grids(st)
+        fp.frame = np.zeros((H, W, 3), np.uint8)
+        fp._state = None  # not FrameProcessor's own frame
+        penalty_calculator._pre_compute_easy_segments(st.np_grids, grids)
+        for row, grow in zip(grids, fr["rows"]):
+            for g, want in zip(row, grow["pen"]):
+                got = penalty_calculator.calculate_penalty(g, lookup)
+                w = unhex(want)
+                if g.empty:
+                    assert got == 0
+                else:
+                    assert _ptype(got) == _ptype(w), (name, g.coords)
+        peaks = ProtrusionDetector()(fp.frame, grids, lookup)
+        assert [[p.x, p.y] for p in peaks] == fr["peaks"], name
+    assert torch.equal(path_finder.seen.t, seen_before), "the process angle cache is left as it was"

@@ -193,6 +193,83 @@ class _FrameState:
         return out
 
 
+def _same_grid(a: Grid | None, b: Grid | None) -> bool:
+    if a is None or b is None:
+        return a is b
+    return (a.coords.x, a.coords.y, a.centre.x, a.centre.y, a.row, a.col, a.empty, a.artificial) == \
+        (b.coords.x, b.coords.y, b.centre.x, b.centre.y, b.row, b.col, b.empty, b.artificial)
+
+
+def implied_grid_inputs(grids: list, grid_lookup: dict, H: int, W: int):
+    """What the reference's grid builder (FrameProcessor.py:50-171) must have been given to make ``grids`` /
+    ``grid_lookup`` in an H x W frame: the rect rounded to the 20-px lattice and the mask samples at the cell centres.
+    The rect's origin comes from any grid (x - 20 col, y - 20 row: both the main and the artificial rows set row =
+    (y - rect y) / 20), its width from the columns; a main-row cell was in the mask iff its FINAL grid in the lookup
+    is non-empty and not artificial (an artificial row keeps a non-empty cell non-empty and marks a formerly empty
+    one artificial, :138-151).  The rect's height is ambiguous where the main rows run under the artificial ones:
+    -> (x0, y0, w, [(h, cells uint8 [H/20, W/20]) for every candidate height, shortest first])."""
+    rows = [r for r in grids if r]
+    if not rows or not grid_lookup:
+        raise ValueError("no grids")
+    g0 = rows[0][0]
+    x0, y0 = g0.coords.x - G * g0.col, g0.coords.y - G * g0.row
+    xs = sorted({x for x, _ in grid_lookup})
+    ys = sorted({y for _, y in grid_lookup})
+    w = xs[-1] - x0 + G
+    if H % G or W % G or x0 % G or y0 % G or x0 < 0 or y0 < 0 or w <= 0:
+        raise ValueError("grids not on the 20-px lattice of an H x W frame")
+    LR, LC = H // G, W // G
+    out = []
+    for h in range(G, ys[-1] - y0 + 2 * G, G):
+        cells = np.zeros((LR, LC), dtype=np.uint8)
+        for r in range(h // G):
+            for c in range(w // G):
+                x, y = x0 + G * c, y0 + G * r
+                g = grid_lookup.get((x, y))
+                if g is not None and not g.empty and not g.artificial and y // G < LR and x // G < LC:
+                    cells[y // G, x // G] = 1
+        if cells.any():
+            out.append((h, cells))
+    return x0, y0, w, out
+
+
+def device_frame_for(grids: list, grid_lookup: dict, H: int, W: int) -> "_FrameState":
+    """The device grid stage for a grid list built outside this package's FrameProcessor (the standalone
+    PenaltyCalculator / ProtrusionDetector surfaces, PenaltyCalculator.py:112-142, ProtrusionDetector.py:419-535).
+
+    The reference's penalties and peaks depend only on what its grid builder was given (the frame size, the rounded
+    rect and the mask samples; implied_grid_inputs reads them back from the grids), so the device stage
+    (va_nav_run) run on those gives the reference's values.  Of the candidate rect heights the one whose device grid
+    list and lookup equal the caller's in every Grid field, in order, is taken; any other list (not one the
+    reference's builder makes of some mask) raises ValueError.  A* runs against a scratch copy of the angle cache
+    (the process cache is left as it was)."""
+    from .nav import AngleSeen, NavEngine
+    x0, y0, w, cands = implied_grid_inputs(grids, grid_lookup, H, W)
+    LR, LC = H // G, W // G
+    dev = torch.device("cuda", torch.cuda.current_device())
+    navs = device_frame_for.__dict__.setdefault("_navs", {})
+    if (H, W) not in navs:
+        navs[(H, W)] = NavEngine(H, W, max_batch=1)
+    nav = navs[(H, W)]
+    for h, cells in cands:
+        scratch = AngleSeen(dev)
+        scratch.t.copy_(path_finder.seen.t)
+        res = nav.run(torch.from_numpy(cells).to(dev).reshape(1, LR, LC).contiguous(),
+                      torch.tensor([[x0, y0, w, h]], dtype=torch.int32, device=dev), scratch, readback=True)
+        nf = res.frame(0)
+        if nf.status != _lib.VA_FRAME_OK:
+            continue
+        st = _FrameState(nf, nav.dims)
+        st.penalties_assigned = True
+        dg, dl = st.grids, st.grid_lookup
+        if len(dg) == len(grids) and all(len(a) == len(b) and all(_same_grid(u, v) for u, v in zip(a, b))
+                                         for a, b in zip(dg, grids)) and \
+                list(dl) == list(grid_lookup) and all(_same_grid(dl[k], grid_lookup[k]) for k in dl):
+            return st
+    raise ValueError(f"these grids are not what the reference's grid builder makes of any mask in a {H} x {W} frame "
+                     f"(rect origin ({x0}, {y0}), width {w}, heights tried {[h for h, _ in cands]})")
+
+
 class _DeviceGraph(defaultdict):
     """The graph dict of _create_graph, tagged with the frame it was built from."""
     _state = None

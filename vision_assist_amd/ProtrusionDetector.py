@@ -4,8 +4,11 @@ The live path of the reference (ProtrusionDetector.py:419-439, 535: raster the
 non-empty cells, top-most pixel row, runs split at gaps > grid_size // 4, run
 centres) runs on the GPU inside ``nav_grid_kernel`` for every frame.  This
 singleton keeps the reference's call signature ``(frame, grids, grid_lookup) ->
-list[Coordinate]`` for the grids of the frame FrameProcessor holds; the
-defect / quadrilateral code the reference comments out (:445-504) is not built.
+list[Coordinate]``: for the grids of the frame FrameProcessor holds it returns
+that frame's device peaks; for grids built elsewhere it runs the device grid
+stage on the frame they imply (FrameProcessor.device_frame_for) and returns its
+peaks.  The defect / quadrilateral code the reference comments out (:445-504)
+is not built.
 """
 from __future__ import annotations
 
@@ -44,6 +47,6 @@ class ProtrusionDetector:
         self.frames_processed += 1
         st = fp._state if fp is not None else None
         if st is None or grids is not st.grids:
-            raise ValueError("ProtrusionDetector: the peaks are computed on the GPU for the grids of the frame "
-                             "vision_assist_amd.FrameProcessor holds; pass processor.grids")
+            from .FrameProcessor import device_frame_for
+            st = device_frame_for(grids, grid_lookup, self.height, self.width)
         return st.peaks()
