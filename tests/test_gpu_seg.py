@@ -910,3 +910,17 @@ def test_conv3h_f32_a_stage_forward_bit_identical(B, switch):
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: af vs planes max diff {(g - r).abs().max().item()}"
+
+
+@pytest.mark.parametrize("B", [2, 3])
+def test_conv3t_f32_a_stage_forward_bit_identical(B, switch):
+    """conv3t with its A stage as f32 weights split in registers (VA_CONV3T=af) against the pre-split planes: the f32
+    forward's conv3t layers (the stride-2 and 1x1 wide layers, ragged pixel tiles at B = 3) bit-identical."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(B, seed=23)
+    switch("VA_CONV3T", "planes")
+    ref = _gpu_heads(net, frames)
+    switch("VA_CONV3T", "af")
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        assert torch.equal(g, r), f"{name}: af vs planes max diff {(g - r).abs().max().item()}"

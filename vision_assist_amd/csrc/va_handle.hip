@@ -45,7 +45,8 @@ void read_switches(VaSwitches& s) {
     s.f32_split = !e ? 6 : e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
     e = getenv("VA_CONV3H");
     s.conv3h = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
-    s.conv3t = !env_off("VA_CONV3T");
+    e = getenv("VA_CONV3T");
+    s.conv3t = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
     s.splitk = !env_off("VA_SPLITK");
     s.patch = !env_off("VA_CONV_PATCH");
     e = getenv("VA_CONV4");

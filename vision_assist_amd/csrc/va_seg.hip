@@ -1115,12 +1115,14 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 // LDS row: 128 bytes = 8 slots of 16 B; chunk c = 3 g + p (c < 6) sits in slot c ^ (r & 7) ^ ((r >> 4) & 1) -- the
 // 32-row fragment reads are conflict-free, slots 6-7 of a chunk are DMA'd from the zero page.
 constexpr int T3_BN = 128, T3_KS = 16, T3_ROW = 128;
-template <int WM, int NSTAGE>
+// AF: the A rows as f32 (64 bytes: 16 channels, DMA'd from va_conv_args.w; conv3h's AF), split into the three
+// terms in registers -- 8 instead of 16 KiB of A DMA per K-step (12 of them weight bytes, 4 the zero page's)
+template <int WM, int NSTAGE, bool AF = false>
 struct T3Cfg {
     static constexpr int BM = 64 * WM, NT = 128 * WM, STAGE = (BM + T3_BN) * T3_ROW;
     static constexpr int EPI = BM * (T3_BN + 4) * 4;
     static constexpr int LDS = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
-    static constexpr int NA = 16 / (2 * WM);  // A-DMA instructions per wave per K-step (16 KiB of A rows)
+    static constexpr int NA = (AF ? 8 : 16) / (2 * WM);  // A-DMA instructions per wave per K-step (16 / 8 KiB of A)
     static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -1140,9 +1142,9 @@ __device__ __forceinline__ void t3_waitvm() {
 // WM = 4, NSTAGE = 3: 256-pixel tiles, 8 waves, one workgroup per CU, A DMA'd two K-steps ahead;
 // WM = 2, NSTAGE = 2: 128-pixel tiles, 4 waves, two workgroups per CU, A one K-step ahead.  B registers always
 // two K-steps ahead.
-template <int WM, int NSTAGE, typename OutT>
+template <int WM, int NSTAGE, typename OutT, bool AF = false>
 __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int ntn, int ntiles) {
-    using Cfg = T3Cfg<WM, NSTAGE>;
+    using Cfg = T3Cfg<WM, NSTAGE, AF>;
     extern __shared__ __align__(16) unsigned char smt[];
     constexpr int BM = Cfg::BM, BN = T3_BN, NT = Cfg::NT, WN = 2, TNS = 4, NA = Cfg::NA;
     int bid = blockIdx.x;
@@ -1157,7 +1159,8 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
     const float* __restrict__ X = (const float*)a.x;
-    const __bf16* __restrict__ W3 = (const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3;
+    const void* WA = AF ? (const void*)((const float*)a.w + (int64_t)cls * a.Npad * a.Kpad)
+                        : (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     auto stA = [&](int s) { return smt + s * Cfg::STAGE; };
     auto stB = [&](int s) { return smt + s * Cfg::STAGE + BN * T3_ROW; };
@@ -1183,22 +1186,29 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     // buffer_load ... lds, not global_load_lds: the compiler's wait pass takes a pending FLAT-encoded LDS DMA as
     // "VM and LGKM out of order" and answers the next register dependency with vmcnt(0), draining the B loads two
     // steps ahead.  Chunks 6-7 (and K-steps past the last) use an offset past the descriptor's range: zeros.
+    // AF: instruction i = wid + 2 WM j holds rows 16 i .. 16 i + 15 as 64-byte f32 rows; lane l: row 16 i + (l >> 2),
+    // slot l & 3 -> f32 quarter slot ^ ((row >> 2) & 3)
     const void* zpage = (const void*)g_zero_page;
-    const int w3_bytes = a.Npad * a.Kpad * 3 * 2;
+    const int wa_bytes = AF ? a.Npad * a.Kpad * 4 : a.Npad * a.Kpad * 3 * 2;
     constexpr int T3_OOR = 0x7ff00000;
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-        const int row = 8 * (wid + 2 * WM * j) + (lane >> 3);
-        const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
-        aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
+        if constexpr (AF) {
+            const int row = 16 * (wid + 2 * WM * j) + (lane >> 2), q = (lane & 3) ^ ((row >> 2) & 3);
+            aoff[j] = ((n0 + row) * a.Kpad + 4 * q) * 4;
+        } else {
+            const int row = 8 * (wid + 2 * WM * j) + (lane >> 3);
+            const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
+            aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
+        }
     }
     auto dmaA = [&](int k, int s, bool live) {  // K-step k (channels 16 k ..) into stage s; !live: zeros
         unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
+        const int soff = live ? k * (AF ? 64 : 96) : T3_OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j)
-            t3_dma16(W3, w3_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
+            t3_dma16(WA, wa_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
     };
     // K-step -> (tap, channel) of the im2col row, advanced per load (uniform)
     int ld_ky = 0, ld_kx = 0, ld_c = 0;
@@ -1266,8 +1276,16 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib) {
             const int row = wn * 64 + 32 * ib + r32;
+            if constexpr (AF) {
+                const int sw = (row >> 2) & 3;
+                const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
+                const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
+                split3_bf16(lo, hi, ap[ib]);
+            } else {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
+                for (int p = 0; p < 3; ++p)
+                    ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
+            }
         }
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
@@ -2861,7 +2879,7 @@ hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
 int f32_split() { return va_sw().f32_split; }
 
 // VA_CONV3T=0 keeps the wide f32 layers on conv2's three-term form (A/B timing, va_switch.h)
-bool conv3t_off() { return !va_sw().conv3t; }
+bool conv3t_off() { return va_sw().conv3t == 0; }
 
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
 bool use_conv3t(const va_conv_args& a) {
@@ -2876,20 +2894,28 @@ bool use_conv3t(const va_conv_args& a) {
            a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
 
-template <int WM, int NSTAGE, typename OutT>
-hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
-    using Cfg = T3Cfg<WM, NSTAGE>;
+template <int WM, int NSTAGE, typename OutT, bool AF>
+hipError_t launch_conv3t_af(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3Cfg<WM, NSTAGE, AF>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Cfg::LDS) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT, AF>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn, ntiles);
+    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT, AF>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn,
+                       ntiles);
     return hipGetLastError();
+}
+
+// the A stage's form (VA_CONV3T, va_switch.h): the pre-split planes, or f32 split in registers (AF)
+template <int WM, int NSTAGE, typename OutT>
+hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
+    if (va_sw().conv3t == 2) return launch_conv3t_af<WM, NSTAGE, OutT, true>(a, st);
+    return launch_conv3t_af<WM, NSTAGE, OutT, false>(a, st);
 }
 
 // VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing, va_switch.h)

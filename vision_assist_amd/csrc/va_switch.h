@@ -8,7 +8,8 @@ struct VaSwitches {
     int f32_split;   // VA_F32_SPLIT: bf16 term products per f32 product, 6 (default) or 9; 0 = the f32 MFMA
     int conv3h;      // VA_CONV3H: 0 = the stride-1 multi-tap f32 layers on conv3t instead of the halo-staged kernel;
                      // its A stage: 1 = the pre-split weight planes ("planes"), 2 = f32, split in registers ("af")
-    bool conv3t;     // VA_CONV3T=0: the wide f32 layers on conv2's three-term form
+    int conv3t;      // VA_CONV3T: 0 = the wide f32 layers on conv2's three-term form; conv3t's A stage: 1 = the
+                     // pre-split planes ("planes"), 2 = f32, split in registers ("af")
     bool splitk;     // VA_SPLITK=0: no split-K for launches of few tiles
     bool patch;      // VA_CONV_PATCH=0: the narrow bf16 3x3 layers on conv_dn instead of the patch kernel
     int conv4_min;   // VA_CONV4: 0 = conv4 off (-1 here), "all" = every eligible layer (1), default 256 tiles
