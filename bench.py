@@ -312,7 +312,8 @@ class Run:
             # the MFMA the f32 convs execute is bf16 (terms products per f32 product): price the executed bf16
             # MFMA work against the bf16 peak; model.0 is counted once at K = 27 (it runs three term products on
             # the MFMA at K = 32, conv0_f32m, or on the VALU: counting it once under-states, never over-states)
-            fl_c0 = sum(2.0 * m["M"] * m["N"] * m["K"] for m in pipe.plan["meta"] if m["name"] == "model.0") / launches
+            fl_c0 = sum(m.get("flops_c0", 2.0 * m["M"] * m["N"] * m["K"] if m["name"] == "model.0" else 0.0)
+                        for m in pipe.plan["meta"]) / launches
             f32eq = {"achieved": round(achieved, 2), "peak": PEAK_TFLOPS["f32"],
                      "frac": round(achieved / PEAK_TFLOPS["f32"], 5),
                      "def": "f32 GEMM FLOPs per launch / launch time against the f32 MFMA peak (what the exact-f32 "

@@ -270,6 +270,16 @@ int va_seg_c2f(void* stream, const va_conv_args* a);
  *   a.w    bf16 weight blob in MFMA fragment order (20480 values; layout: seg.py SegNet._pack_stem)
  *   a.bias float [96] = model.0 [32] | model.1 [64] */
 int va_seg_stem(void* stream, const va_conv_args* a);
+/* The stem in f32 (the headline's precision) as ONE launch: uint8 BGR frames [N][H][W][3] -> model.0 (the
+ * three exact bf16 terms of its weights x the frame bytes, x 1/255, + bias, SiLU) -> model.1 Conv(32, 64, 3x3, s2)
+ * + SiLU as six exact bf16 term products -> float a.y [N][ceil(H/4)][ceil(W/4)] (channel stride a.ldy % 4 == 0);
+ * the 32-channel f32 model.0 map never leaves the chip.  Replaces va_seg_conv0_f32m + the model.1 va_seg_conv.
+ * a.dtype = VA_DTYPE_F32, a.Cin = 32, a.Cout = 64, (W * 3) % 16 == 0, and:
+ *   a.w3   model.0's K-padded weights as three exact bf16 terms [32][4][3][8] (va_seg_conv0_f32m's w3)
+ *   a.bias model.0's bias float [32]
+ *   a.w    model.1's packed f32 weights [Npad][Kpad], K = Kpad = 288 ordered (ky, kx, ci)
+ *   a.b2   model.1's bias float [64] */
+int va_seg_stem_f32(void* stream, const va_conv_args* a);
 /* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
  * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
 int va_c2f_trace(void* buf);
@@ -326,7 +336,7 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
                                a.Cout, a.y, a.ldy, a.dtype (FP8: e4m3 output with a.yscale; F32 with a.w3: the
                                MFMA form) -- see va_seg_conv0 / va_seg_conv0_f32(m) / va_seg_conv0_e4m3 */
 #define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
-#define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: see va_seg_stem */
+#define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: va_seg_stem (bf16), va_seg_stem_f32 (f32) */
 /* Branch-parallel lists (small batches, where one layer does not fill the 256 CUs): an op with lane L > 0
  * is issued on auxiliary stream L of the calling stream (VA_LANES - 1 of them, created on first use per
  * (device, calling stream) and kept for the process).  FORK (a.N = L): lane L waits for everything issued

@@ -924,3 +924,58 @@ def test_conv3t_f32_a_stage_forward_bit_identical(B, switch):
     got = _gpu_heads(net, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         assert torch.equal(g, r), f"{name}: af vs planes max diff {(g - r).abs().max().item()}"
+
+
+@pytest.mark.parametrize("H,W,B", [(72, 112, 2), (640, 640, 1)])
+def test_stem_f32_op_vs_fp64(H, W, B):
+    """va_seg_stem_f32 (uint8 frame -> model.0 -> model.1 in f32 as one kernel, model.0's map kept in LDS as three
+    exact bf16 planes) on single ops against float64 torch of the two layers (x / 255, conv, SiLU, conv s2, SiLU):
+    within f32 rounding; ragged model.1 tiles at 72 x 112 (18 x 28: 4 x 16 tiles), frame edges, a full 640 frame."""
+    import ctypes
+
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    arch, fw, net = _net("f32", "s", seed=29)
+    lib = _lib.load()
+    frames = _frames(B, H, W, seed=H + W)
+    Ho1, Wo1 = ((H + 1) // 2 + 1) // 2, ((W + 1) // 2 + 1) // 2
+    y = torch.full((B, Ho1, Wo1, 64 + 8), float("nan"), device="cuda")
+    p1 = net.w["model.1"]
+    a = S.ConvArgs(x=frames.cuda().data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=net.w0_3.data_ptr(),
+                   bias=net.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K, Kpad=p1.Kpad,
+                   y=y.data_ptr(), ldy=72, dtype=S.VA_DTYPE_F32)
+    fd = frames.cuda()
+    a.x = fd.data_ptr()
+    _lib.check(lib.va_seg_stem_f32(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_stem_f32")
+    torch.cuda.synchronize()
+    w0, b0 = fw["model.0"]
+    w1, b1 = fw["model.1"]
+    x = (frames.flip(-1).double() / 255.0).permute(0, 3, 1, 2)
+    ref = F.silu(F.conv2d(F.silu(F.conv2d(x, w0.double(), b0.double(), 2, 1)), w1.double(), b1.double(), 2, 1))
+    got = y[..., :64].cpu().permute(0, 3, 1, 2).double()
+    assert torch.isfinite(y[..., :64]).all() and torch.isnan(y[..., 64:]).all()  # nothing past the slice
+    scale = max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+
+
+def test_stem_f32_forward(monkeypatch):
+    """The f32 s-seg plan runs model.0 + model.1 as one op (va_seg_stem_f32); heads against the same forward with
+    the two layers apart (VA_STEM=0: conv0_f32m, then conv2's three-term form): f32-rounding close, and within the
+    f32 bar of torch."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(2, seed=31)
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "model.0+model.1 (fused f32 stem)" in names and "model.1" not in names
+    got = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_STEM", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="f32")
+    assert "model.1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
+    ref = _gpu_heads(net2, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: fused vs unfused stem max diff {d}"
+    torch.set_num_threads(8)
+    want = _ref_heads(arch, fw, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+        assert (g - r).abs().max().item() <= 1e-3, name

@@ -197,6 +197,10 @@ class SegNet:
             w1, b1 = folded["model.1"]
             if tuple(w1.shape) == (64, 32, 3, 3):
                 self.stem = self._pack_stem(w0p, b0, w1, b1)
+        # f32: the same fusion in the f32 arithmetic (va355.h va_seg_stem_f32): model.0's three-term weights and
+        # model.1's packed f32 weights; VA_STEM=0 keeps the two layers apart (A/B)
+        self.stem32 = (dtype == "f32" and self.fuse_first and self.w0_3 is not None and w0.shape[0] == 32 and
+                       tuple(folded["model.1"][0].shape) == (64, 32, 3, 3) and os.environ.get("VA_STEM", "1") != "0")
         # C2f blocks the fused kernel covers (va355.h va_seg_c2f): n = 1, shortcut, 64 -> 64 (model.2 of 's')
         self.c2f_fused = {}
         if dtype == "bf16" and os.environ.get("VA_C2F", "1") != "0":
@@ -633,6 +637,18 @@ class SegNet:
             meta.append({"name": "model.0+model.1 (fused stem)", "kind": "conv", "M": B * h2 * w2, "N": 64,
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
                          "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
+        elif self.stem32 and (W * 3) % 16 == 0:
+            a1 = new(h2, w2, a.c2)
+            p1 = self.w["model.1"]
+            ops.append(SegOp(kind=VA_OP_STEM, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64,
+                                                          w3=self.w0_3.data_ptr(), bias=self.w0[1].data_ptr(),
+                                                          w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K,
+                                                          Kpad=p1.Kpad, y=a1.ptr, ldy=a1.ld, dtype=VA_DTYPE_F32)))
+            macs = 27 * 32 * 4 + 288 * 64  # per model.1 output pixel: 4 model.0 pixels + model.1
+            meta.append({"name": "model.0+model.1 (fused f32 stem)", "kind": "conv", "M": B * h2 * w2, "N": 64,
+                         "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
+                         "flops_c0": 2 * B * h2 * w2 * 27 * 32 * 4,  # model.0's share (three term products, once)
+                         "bytes": B * H * W * 3 + 4 * B * h2 * w2 * 64})
         else:
             # fp8: e4m3 straight from the fused model.0 (else bf16, and model.1 quantizes it while staging)
             a0 = new(h1, w1, a.c1, None if self.fuse_first else self.tdtype)
