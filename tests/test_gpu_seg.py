@@ -979,3 +979,62 @@ def test_stem_f32_forward(monkeypatch):
     want = _ref_heads(arch, fw, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
         assert (g - r).abs().max().item() <= 1e-3, name
+
+
+@pytest.mark.parametrize("H,W,B", [(44, 56, 2), (160, 160, 1)])
+def test_c2f_f32_op_vs_fp64(H, W, B):
+    """va_seg_c2f_f32 (model.2's C2f in f32 as one kernel: cv1 -> Bottleneck(3x3, 3x3, + residual) -> cat -> cv2, the
+    intermediates on the chip as exact bf16 planes) against float64 torch of the block (block.py C2f.forward, BN
+    folded): within f32 rounding; ragged 8 x 16 tiles at 44 x 56, image borders, a full 160 x 160 map; the output
+    slice written and nothing past it."""
+    import ctypes
+
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    arch, fw, net = _net("f32", "s", seed=37)
+    assert 2 in net.c2f32
+    blob, bias = net.c2f32[2]
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(H * W + B)
+    x = torch.rand(B, 64, H, W, generator=g) * 3 - 0.5
+    xin = torch.zeros(B, H, W, 72, device="cuda")
+    xin[..., :64] = x.permute(0, 2, 3, 1).cuda()
+    y = torch.full((B, H, W, 68), float("nan"), device="cuda")
+    a = S.ConvArgs(x=xin.data_ptr(), N=B, H=H, W=W, Cin=64, ldx=72, w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                   y=y.data_ptr(), ldy=68, dtype=S.VA_DTYPE_F32)
+    _lib.check(lib.va_seg_c2f_f32(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_c2f_f32")
+    torch.cuda.synchronize()
+
+    def conv(t, name, k):
+        w_, b_ = fw[f"model.2.{name}"]
+        return F.silu(F.conv2d(t, w_.double(), b_.double(), 1, k // 2))
+    t = conv(x.double(), "cv1", 1)
+    a_, b_ = t[:, :32], t[:, 32:]
+    c_ = b_ + conv(conv(b_, "m.0.cv1", 3), "m.0.cv2", 3)
+    ref = conv(torch.cat([a_, b_, c_], 1), "cv2", 1)
+    got = y[..., :64].cpu().permute(0, 3, 1, 2).double()
+    assert torch.isfinite(y[..., :64]).all() and torch.isnan(y[..., 64:]).all()
+    scale = max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+
+
+def test_c2f_f32_forward(monkeypatch):
+    """The f32 s-seg plan runs model.2 as one op (va_seg_c2f_f32); heads against the same forward with the block's
+    four convs apart (VA_C2F=0): f32-rounding close, and within the f32 bar of torch."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(2, seed=41)
+    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+    assert "model.2 (fused f32 C2f)" in names and "model.2.cv1" not in names
+    got = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_C2F", "0")
+    from vision_assist_amd.seg import SegNet
+    net2 = SegNet(arch, fw, dtype="f32")
+    assert "model.2.cv1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
+    ref = _gpu_heads(net2, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: fused vs unfused C2f max diff {d}"
+    torch.set_num_threads(8)
+    want = _ref_heads(arch, fw, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+        assert (g - r).abs().max().item() <= 1e-3, name

@@ -207,6 +207,12 @@ class SegNet:
             for i, ci, co, n, shortcut in arch.c2f_plan():
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
+        # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32); VA_C2F=0 keeps it unfused (A/B)
+        self.c2f32 = {}
+        if dtype == "f32" and os.environ.get("VA_C2F", "1") != "0":
+            for i, ci, co, n, shortcut in arch.c2f_plan():
+                if ci == 64 and co == 64 and n == 1 and shortcut:
+                    self.c2f32[i] = self._pack_c2f32(folded, i)
         self._plans = {}
         # fp8: e4m3 weights with per-output-channel scales (the convs whose input channels come in 16s), and
         # the per-conv activation scales of calibrate_fp8
@@ -223,6 +229,18 @@ class SegNet:
             for prefix, p in self.w.items():
                 if p.cin % 16 == 0:
                     self.w8[prefix] = self._pack_fp8(p)
+
+    def _pack_c2f32(self, folded: dict, i: int):
+        """(weight blob, bias blob) of va_seg_c2f_f32: the four convs' f32 weights row-major [Cout][K] with K ordered
+        (ky, kx, ci) -- cv1 64 x 64, m.0.cv1 32 x 288, m.0.cv2 32 x 288, cv2 64 x 96 -- and their biases."""
+        parts, bias = [], []
+        for name in ("cv1", "m.0.cv1", "m.0.cv2", "cv2"):
+            w, b = folded[f"model.{i}.{name}"]
+            parts.append(w.float().permute(0, 2, 3, 1).reshape(w.shape[0], -1).reshape(-1))
+            bias.append(b.float())
+        blob = torch.cat(parts)
+        assert blob.numel() == 28672, blob.numel()
+        return blob.to(self.device).contiguous(), torch.cat(bias).to(self.device).contiguous()
 
     def _pack_fp8(self, p: Packed):
         """(e4m3 bytes [Npad][Kpad128], per-output-channel scale float [Npad]) of a packed bf16 conv: the
@@ -523,6 +541,16 @@ class SegNet:
 
         def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None):
             _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
+            if i in self.c2f32 and src.c == 64 and src.ld % 4 == 0 and dst.ld % 4 == 0 and up is None:
+                blob, bias = self.c2f32[i]
+                ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
+                                                             w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                                                             y=dst.ptr, ldy=dst.ld, dtype=VA_DTYPE_F32)))
+                macs = 64 * 64 + 2 * 32 * 288 + 64 * 96  # per pixel, the four convs
+                meta.append({"name": f"model.{i} (fused f32 C2f)", "kind": "conv", "M": B * h * w, "N": 64,
+                             "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
+                             "bytes": 4 * B * h * w * 128})
+                return
             if i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
                 ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld, w=blob.data_ptr(),
