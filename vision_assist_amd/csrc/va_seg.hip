@@ -3019,15 +3019,16 @@ __global__ __launch_bounds__(CF32_NT) void c2f32_kernel(const float* __restrict_
     {
         f32x16 acc = (f32x16){};
         const int p = 32 * (wid >> 1) + r32, ib = wid & 1, py = p / CF32_TW, px = p % CF32_TW;
-        const unsigned char* src[3] = {cs + CF32_A + p * CF32_PS, cs + CF32_S1 + ((py + 2) * CF32_R1W + px + 2) * CF32_PS,
-                                       cs + CF32_C + p * CF32_PS};
+        const unsigned char* srcA = cs + CF32_A + p * CF32_PS;
+        const unsigned char* srcB = cs + CF32_S1 + ((py + 2) * CF32_R1W + px + 2) * CF32_PS;
+        const unsigned char* srcC = cs + CF32_C + p * CF32_PS;
         for (int kl = 0; kl < 6; ++kl) {
             const int g = 40 + kl;
             dmaA(g + 2);
             __builtin_amdgcn_sched_barrier(0);
             bf16x8 ap[3], bp[3];
             afrag(g, 32 * ib + r32, ap);
-            bfrag(src[kl >> 1] + (kl & 1) * 96 + 16 * g32, bp);
+            bfrag((kl < 2 ? srcA : kl < 4 ? srcB : srcC) + (kl & 1) * 96 + 16 * g32, bp);
 #pragma unroll
             for (int t = 0; t < 6; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc, 0, 0, 0);
             t3_waitvm<1>();
