@@ -991,7 +991,9 @@ def test_c2f_f32_op_vs_fp64(H, W, B):
 
     from vision_assist_amd import _lib
     from vision_assist_amd import seg as S
-    arch, fw, net = _net("f32", "s", seed=37)
+    from vision_assist_amd.seg import SegNet
+    arch, fw, _ = _net("f32", "s", seed=37)
+    net = SegNet(arch, fw, dtype="f32", c2f32=True)
     assert 2 in net.c2f32
     blob, bias = net.c2f32[2]
     lib = _lib.load()
@@ -1018,16 +1020,16 @@ def test_c2f_f32_op_vs_fp64(H, W, B):
     assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
 
 
-def test_c2f_f32_forward(monkeypatch):
-    """The f32 s-seg plan runs model.2 as one op (va_seg_c2f_f32); heads against the same forward with the block's
-    four convs apart (VA_C2F=0): f32-rounding close, and within the f32 bar of torch."""
-    arch, fw, net = _net("f32", "s", seed=5)
+def test_c2f_f32_forward():
+    """An f32 s-seg plan with model.2 as one op (SegNet(c2f32=True): va_seg_c2f_f32); heads against the default plan
+    with the block's four convs apart: f32-rounding close, and within the f32 bar of torch."""
+    from vision_assist_amd.seg import SegNet
+    arch, fw, _ = _net("f32", "s", seed=5)
+    net = SegNet(arch, fw, dtype="f32", c2f32=True)
     frames = _frames(2, seed=41)
     names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
     assert "model.2 (fused f32 C2f)" in names and "model.2.cv1" not in names
     got = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_C2F", "0")
-    from vision_assist_amd.seg import SegNet
     net2 = SegNet(arch, fw, dtype="f32")
     assert "model.2.cv1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
     ref = _gpu_heads(net2, frames)

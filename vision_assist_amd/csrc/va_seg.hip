@@ -2617,64 +2617,60 @@ __global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restri
 // ----------------------------------------------------------------------------------------- f32 stem
 // The f32 stem as ONE launch: uint8 BGR frames -> model.0 Conv(3, 32, 3x3, s2) + SiLU (conv0_f32m's arithmetic: the
 // three exact bf16 weight terms x the exact frame bytes on the MFMA, the sum x 1/255 + bias, SiLU) -> model.1 Conv(32,
-// 64, 3x3, s2) + SiLU (conv3h's arithmetic: six exact term products, the A stage f32 split in registers) -> f32
-// NHWC.  Unfused, model.0's 320 x 320 x 32 f32 map (13 MB per 640 x 640 frame) is written and read back; here a
-// workgroup owns a 4 x 16 tile of the model.1 map, computes model.0 on the 9 x 33 pixels its taps read (zero
-// outside model.0's map: model.1's padding) straight into LDS as three bf16 planes (exact: h + m + l = the f32
-// value), and runs model.1's 18 K-steps (tap x 16-channel chunk) from there, the weights streamed through a
-// three-stage LDS-DMA ring two steps ahead (conv3h's discipline: a fixed DMA count per wave, counted waits).
-// LDS: model.0 planes 297 px x 208 B (192 used: chunk c, plane p, half g at 96 c + 32 p + 16 g; the 208-byte
-// pitch keeps model.1's stride-2 B reads at most 2-way bank conflicted), the frame patch 19 rows x 208 B, the ring
-// 3 x 4 KiB -- two workgroups per CU.  4 waves: wave (wm, wn) computes 32 pixels x 32 channels of model.1.
+// 64, 3x3, s2) + SiLU (six exact bf16 term products per f32 product, the weights f32 split in registers) -> f32
+// NHWC.  Unfused, model.0's 320 x 320 x 32 f32 map (13 MB per 640 x 640 frame) is written and read back; here it
+// never leaves the chip.  Persistent: one workgroup per CU keeps model.1's whole weight matrix in LDS (64 rows x 288
+// f32, loaded once) and walks 4 x 16 tiles of the model.1 map (XCD-contiguous runs): per tile, model.0 on the 9 x 33
+// pixels the tile's taps read (zero outside model.0's map: model.1's padding) straight into LDS as three bf16 planes
+// (exact: h + m + l = the f32 value), then model.1's 18 K-steps (tap x 16-channel chunk) from there with no barrier
+// inside the K-loop; the next tile's frame patch is loaded into registers while this tile's model.0 runs.  A ring of
+// per-K-step weight stages with a barrier per step (6 MFMAs per wave between barriers) measured 675 us per 64 frames,
+// barely under the two unfused launches (~700 us, profiles/r05/stem/).
+// LDS: weights 64 rows x 1168 B (1152 used: an odd number of 16-byte slots per row, so 16 consecutive rows' reads
+// are conflict-free), model.0 planes 297 px x 208 B (chunk c, plane p, half g at 96 c + 32 p + 16 g: model.1's
+// stride-2 B reads at most 2-way bank conflicted), the frame patch 19 rows x 208 B.  4 waves: wave (wm, wn) computes
+// 32 pixels x 32 channels of model.1, the six term products in two independent accumulator chains.
 constexpr int S32_TH = 4, S32_TW = 16, S32_NT = 256;
 constexpr int S32_MR = 2 * S32_TH + 1, S32_MC = 2 * S32_TW + 1, S32_MP = S32_MR * S32_MC;  // 9 x 33 = 297
 constexpr int S32_PS = 208;                           // LDS bytes per model.0 pixel
 constexpr int S32_PR = 2 * S32_MR + 1, S32_PP = 208;  // frame patch: 19 rows x 208 bytes (13 chunks of 16)
-constexpr int S32_M0 = 0, S32_PATCH = S32_M0 + S32_MP * S32_PS, S32_RING = S32_PATCH + S32_PR * S32_PP;
-constexpr int S32_STAGE = 64 * 64;                    // one K-step of model.1's weights: 64 rows x 16 f32
-constexpr int S32_LDS = S32_RING + 3 * S32_STAGE;
-static_assert(2 * S32_LDS <= 160 * 1024, "two workgroups per CU");
-static_assert(S32_STAGE == 4 * 1024, "one 1 KiB A piece per wave and K-step");
+constexpr int S32_WR = 1168;                          // LDS bytes per weight row (288 f32 + 16)
+constexpr int S32_W = 0, S32_M0 = S32_W + 64 * S32_WR, S32_PATCH = S32_M0 + S32_MP * S32_PS;
+constexpr int S32_LDS = S32_PATCH + S32_PR * S32_PP;
+constexpr int S32_NPC = S32_PR * (S32_PP / 16);       // patch chunks (247 <= threads: one per thread)
+static_assert(S32_LDS <= 160 * 1024 && S32_NPC <= S32_NT, "LDS / patch chunks");
 
-__global__ __launch_bounds__(S32_NT) void stem32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
-                                                        const __bf16* __restrict__ w03, const float* __restrict__ b0,
-                                                        const float* __restrict__ w1, int w1_bytes, int Kpad,
-                                                        const float* __restrict__ b1, float* __restrict__ y, int ldy,
-                                                        int tiles_x, int tiles_y, int ntiles) {
+__global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
+                                                           const __bf16* __restrict__ w03, const float* __restrict__ b0,
+                                                           const float* __restrict__ w1, int Kpad,
+                                                           const float* __restrict__ b1, float* __restrict__ y, int ldy,
+                                                           int tiles_x, int tiles_y, int ntiles) {
     extern __shared__ __align__(16) unsigned char s32[];
-    int bid = blockIdx.x;
-    {  // XCD-contiguous runs: neighbouring tiles (shared frame rows) on one L2
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int tx = bid % tiles_x, t2 = bid / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
-    const int Ho0 = (H + 1) / 2, Wo0 = (W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
-    const int oy0 = ty * S32_TH, ox0 = tx * S32_TW;  // model.1 tile origin
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    // ---- model.1 weight ring: K-step kl = tap * 2 + chunk (16 f32 of every row); wave wid DMAs rows 16 wid ..
-    // 16 wid + 15 (lane l: row 16 wid + l / 4, f32 quarter (l & 3) ^ ((row >> 2) & 3))
-    const int arow = 16 * wid + (lane >> 2);
-    const int aoff = (arow * Kpad + 4 * ((lane & 3) ^ ((arow >> 2) & 3))) * 4;
-    auto dmaA = [&](int kl) {  // kl < 18, stage kl % 3; past the last step: zeros (offset past the range)
-        t3_dma16(w1, w1_bytes, s32 + S32_RING + (kl % 3) * S32_STAGE + wid * 1024, aoff, kl < 18 ? kl * 64 : 0x7ff00000);
-    };
-    dmaA(0);
-    dmaA(1);
-    __builtin_amdgcn_sched_barrier(0);
-
-    // ---- frame patch: rows 4 oy0 - 3 .., bytes [12 ox0 - 16, 12 ox0 + 192) of each row (16-byte aligned: W * 3 % 16 == 0)
-    {
-        const uint8_t* img = frames + (int64_t)n * H * W * 3;
-        const int iy0 = 4 * oy0 - 3, rb0 = 12 * ox0 - 16;
-        for (int i = tid; i < S32_PR * (S32_PP / 16); i += S32_NT) {
-            const int r = i / (S32_PP / 16), c = i - r * (S32_PP / 16);
-            const int iy = iy0 + r, rb = rb0 + 16 * c;
-            u32x4 v = {0u, 0u, 0u, 0u};
-            if ((unsigned)iy < (unsigned)H && rb >= 0 && rb < 3 * W) v = *(const u32x4*)(img + (int64_t)iy * W * 3 + rb);
-            *(u32x4*)(s32 + S32_PATCH + r * S32_PP + 16 * c) = v;
-        }
+    const int Ho0 = (H + 1) / 2, Wo0 = (W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
+    int t = fz::tile(ntiles, 0);
+    if (t < 0) return;
+    // model.1's weights, once: row r, f32 k at r * 1168 + 4 k
+    for (int i = tid; i < 64 * 72; i += S32_NT) {
+        const int r = i / 72, c = i - r * 72;
+        *(u32x4*)(s32 + S32_W + r * S32_WR + 16 * c) = *(const u32x4*)(w1 + (int64_t)r * Kpad + 4 * c);
     }
+    // the frame patch of tile tt: rows 4 oy0 - 3 .., bytes [12 ox0 - 16, 12 ox0 + 192) (16-byte aligned: W * 3 % 16 == 0)
+    u32x4 pf;
+    auto load_patch = [&](int tt) {
+        const int tx = tt % tiles_x, t2 = tt / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+        const int r = tid / (S32_PP / 16), c = tid - r * (S32_PP / 16);
+        const int iy = 4 * ty * S32_TH - 3 + r, rb = 12 * tx * S32_TW - 16 + 16 * c;
+        pf = (u32x4){0u, 0u, 0u, 0u};
+        if (tid < S32_NPC && (unsigned)iy < (unsigned)H && rb >= 0 && rb < 3 * W)
+            pf = *(const u32x4*)(frames + (int64_t)n * H * W * 3 + (int64_t)iy * W * 3 + rb);
+    };
+    auto store_patch = [&]() {
+        if (tid < S32_NPC) *(u32x4*)(s32 + S32_PATCH + 16 * tid) = pf;  // row r, chunk c at r * 208 + 16 c = 16 tid
+    };
+    load_patch(t);
+    store_patch();
+
     const int fr = lane & 15, fq = lane >> 4;
     // model.0 A fragments (conv0_f32m's permutation: fragment i, row r -> channel 8 (r / 4) + 4 i + r % 4, so lane
     // (fr, fq)'s two results are channels 8 fq .. 8 fq + 7 of pixel fr)
@@ -2693,81 +2689,87 @@ __global__ __launch_bounds__(S32_NT) void stem32_kernel(const uint8_t* __restric
         koff[e] = k < 27 ? (tap / 3) * S32_PP + (tap % 3) * 3 + (2 - c) : -1;
     }
     const float4 bl = *(const float4*)(b0 + 8 * fq), bh = *(const float4*)(b0 + 8 * fq + 4);
-    __syncthreads();
-
-    // ---- model.0 on the 9 x 33 region: group g = 16 region pixels (the last group ragged); region pixel q <->
-    // model.0 (2 oy0 - 1 + q / 33, 2 ox0 - 1 + q % 33); its window starts at patch row 2 (q / 33), byte 6 (q % 33) + 7
-    constexpr float inv255 = 1.0f / 255.0f;
-    for (int g = wid; g < (S32_MP + 15) / 16; g += S32_NT / 64) {
-        const int q = 16 * g + fr;
-        const int qi = q < S32_MP ? q / S32_MC : 0, qj = q < S32_MP ? q % S32_MC : 0;
-        const int base = S32_PATCH + 2 * qi * S32_PP + 6 * qj + 7;
-        bf16x8 bfr;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bfr[e] = koff[e] >= 0 ? (__bf16)(float)s32[base + koff[e]] : (__bf16)0.0f;
-        f32x4 acc[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bfr, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr, acc[i], 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr, acc[i], 0, 0, 0);
-        }
-        const int Y = 2 * oy0 - 1 + qi, X = 2 * ox0 - 1 + qj;
-        const bool in = (unsigned)Y < (unsigned)Ho0 && (unsigned)X < (unsigned)Wo0;
-        f32x4 lo = fz::act((f32x4){acc[0][0] * inv255 + bl.x, acc[0][1] * inv255 + bl.y, acc[0][2] * inv255 + bl.z,
-                                   acc[0][3] * inv255 + bl.w});
-        f32x4 hi = fz::act((f32x4){acc[1][0] * inv255 + bh.x, acc[1][1] * inv255 + bh.y, acc[1][2] * inv255 + bh.z,
-                                   acc[1][3] * inv255 + bh.w});
-        if (!in) lo = hi = (f32x4){0.f, 0.f, 0.f, 0.f};
-        bf16x8 t[3];
-        split3_bf16(__builtin_bit_cast(u32x4, lo), __builtin_bit_cast(u32x4, hi), t);
-        if (q < S32_MP) {
-            unsigned char* d = s32 + S32_M0 + q * S32_PS + (fq >> 1) * 96 + (fq & 1) * 16;
-#pragma unroll
-            for (int p = 0; p < 3; ++p) *(bf16x8*)(d + 32 * p) = t[p];
-        }
-    }
-    t3_waitvm<1>();  // A of K-step 0 landed (step 1's DMA may still fly)
-    __syncthreads();
-
-    // ---- model.1: wave (wm, wn) = pixels 32 wm .. (tile rows 2 wm, 2 wm + 1) x channels 32 wn ..
     const int wm = wid >> 1, wn = wid & 1, r32 = lane & 31, g32 = lane >> 5;
-    const int py = 2 * wm + (r32 >> 4), px = r32 & 15;  // this lane's B pixel in the tile
-    f32x16 acc = (f32x16){};
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    const int py = 2 * wm + (r32 >> 4), px = r32 & 15;  // this lane's model.1 pixel in the tile
+    float4 bo[4];
 #pragma unroll
-    for (int kl = 0; kl < 18; ++kl) {
-        dmaA(kl + 2);  // into the stage step kl - 1 read (every wave passed the barrier after it)
-        __builtin_amdgcn_sched_barrier(0);
-        const int tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
-        const unsigned char* as_ = s32 + S32_RING + (kl % 3) * S32_STAGE;
-        const int row = 32 * wn + r32, sw = (row >> 2) & 3;
-        bf16x8 ap[3], bp[3];
-        {
-            const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
-            const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
-            split3_bf16(lo, hi, ap);
-        }
-        const unsigned char* bs = s32 + S32_M0 + ((2 * py + ky) * S32_MC + 2 * px + kx) * S32_PS + ch * 96 + 16 * g32;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) bp[p] = *(const bf16x8*)(bs + 32 * p);
-#pragma unroll
-        for (int t = 0; t < 6; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc, 0, 0, 0);
-        t3_waitvm<1>();  // A of step kl + 1 landed (this step's DMA stays in flight)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    t3_waitvm<0>();  // the zero DMAs past the last step land before the workgroup ends
+    for (int j = 0; j < 4; ++j) bo[j] = *(const float4*)(b1 + 32 * wn + 8 * j + 4 * g32);
+    // A rows of this lane: row 32 wn + r32, f32 k = 16 kl + 8 g32 ..
+    const unsigned char* wrow = s32 + S32_W + (32 * wn + r32) * S32_WR + 32 * g32;
+    __syncthreads();
 
-    // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
-    const int oy = oy0 + py, ox = ox0 + px;
-    if (oy < Ho1 && ox < Wo1) {
-        float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
+    constexpr float inv255 = 1.0f / 255.0f;
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    for (int k = 1; t >= 0; ++k) {
+        const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+        const int oy0 = ty * S32_TH, ox0 = tx * S32_TW;
+        const int tn = fz::tile(ntiles, k);
+        if (tn >= 0) load_patch(tn);  // lands during this tile's model.0
+
+        // ---- model.0 on the 9 x 33 region: group g = 16 region pixels (the last group ragged); region pixel q <->
+        // model.0 (2 oy0 - 1 + q / 33, 2 ox0 - 1 + q % 33); its window starts at patch row 2 (q / 33), byte 6 (q % 33) + 7
+        for (int g = wid; g < (S32_MP + 15) / 16; g += S32_NT / 64) {
+            const int q = 16 * g + fr;
+            const int qi = q < S32_MP ? q / S32_MC : 0, qj = q < S32_MP ? q % S32_MC : 0;
+            const int base = S32_PATCH + 2 * qi * S32_PP + 6 * qj + 7;
+            bf16x8 bfr;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float4 bb = *(const float4*)(b1 + 32 * wn + 8 * j + 4 * g32);
-            *(f32x4*)(yp + 8 * j) = fz::act((f32x4){acc[4 * j] + bb.x, acc[4 * j + 1] + bb.y, acc[4 * j + 2] + bb.z,
-                                                     acc[4 * j + 3] + bb.w});
+            for (int e = 0; e < 8; ++e) bfr[e] = koff[e] >= 0 ? (__bf16)(float)s32[base + koff[e]] : (__bf16)0.0f;
+            f32x4 acc[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bfr, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bfr, acc[i], 0, 0, 0);
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bfr, acc[i], 0, 0, 0);
+            }
+            const int Y = 2 * oy0 - 1 + qi, X = 2 * ox0 - 1 + qj;
+            const bool in = (unsigned)Y < (unsigned)Ho0 && (unsigned)X < (unsigned)Wo0;
+            f32x4 lo = fz::act((f32x4){acc[0][0] * inv255 + bl.x, acc[0][1] * inv255 + bl.y, acc[0][2] * inv255 + bl.z,
+                                       acc[0][3] * inv255 + bl.w});
+            f32x4 hi = fz::act((f32x4){acc[1][0] * inv255 + bh.x, acc[1][1] * inv255 + bh.y, acc[1][2] * inv255 + bh.z,
+                                       acc[1][3] * inv255 + bh.w});
+            if (!in) lo = hi = (f32x4){0.f, 0.f, 0.f, 0.f};
+            bf16x8 tt3[3];
+            split3_bf16(__builtin_bit_cast(u32x4, lo), __builtin_bit_cast(u32x4, hi), tt3);
+            if (q < S32_MP) {
+                unsigned char* d = s32 + S32_M0 + q * S32_PS + (fq >> 1) * 96 + (fq & 1) * 16;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *(bf16x8*)(d + 32 * p) = tt3[p];
+            }
         }
+        __syncthreads();      // M0 complete; every wave is done with the patch
+        if (tn >= 0) store_patch();  // the next tile's patch (read after the barrier that ends this tile)
+
+        // ---- model.1: wave (wm, wn) = pixels 32 wm .. (tile rows 2 wm, 2 wm + 1) x channels 32 wn ..; K-step kl =
+        // tap * 2 + chunk, A from the resident weights, B from M0; two accumulator chains (products 0, 2, 4 / 1, 3, 5)
+        f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
+#pragma unroll 2
+        for (int kl = 0; kl < 18; ++kl) {
+            const int tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
+            bf16x8 ap[3], bp[3];
+            split3_bf16(*(const u32x4*)(wrow + 64 * kl), *(const u32x4*)(wrow + 64 * kl + 16), ap);
+            const unsigned char* bs = s32 + S32_M0 + ((2 * py + ky) * S32_MC + 2 * px + kx) * S32_PS + ch * 96 + 16 * g32;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bp[p] = *(const bf16x8*)(bs + 32 * p);
+#pragma unroll
+            for (int u = 0; u < 6; u += 2) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u]], bp[TB[u]], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u + 1]], bp[TB[u + 1]], acc1, 0, 0, 0);
+            }
+        }
+        // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
+        const int oy = oy0 + py, ox = ox0 + px;
+        if (oy < Ho1 && ox < Wo1) {
+            float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const f32x16 a2 = acc0 + acc1;
+                *(f32x4*)(yp + 8 * j) = fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
+                                                         a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w});
+            }
+        }
+        __syncthreads();  // M0 free for the next tile; its patch stored
+        t = tn;
     }
 }
 
@@ -3799,23 +3801,29 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a) {
     if (!a || !a->x || !a->w3 || !a->bias || !a->w || !a->b2 || !a->y || a->dtype != VA_DTYPE_F32 || a->Cin != 32 ||
         a->Cout != 64 || a->K != 288 || a->Kpad != 288 || a->Npad < 64 || a->N <= 0 || a->H <= 0 || a->W <= 0 ||
         (a->W * 3) % 16 || a->ldy < 64 || a->ldy % 4 || ((uintptr_t)a->y & 15) || ((uintptr_t)a->x & 15) ||
-        ((uintptr_t)a->bias & 15) || ((uintptr_t)a->b2 & 15) || (int64_t)a->H * a->W * 3 >= 0x80000000LL ||
-        (int64_t)a->Npad * a->Kpad * 4 >= 0x7ff00000LL)
+        ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15) || ((uintptr_t)a->b2 & 15) ||
+        (int64_t)a->H * a->W * 3 >= 0x80000000LL)
         return VA_ERR_ARG;
     const int Ho0 = (a->H + 1) / 2, Wo0 = (a->W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
     const int tiles_x = (Wo1 + S32_TW - 1) / S32_TW, tiles_y = (Ho1 + S32_TH - 1) / S32_TH;
     const int64_t nt = (int64_t)tiles_x * tiles_y * a->N;
     if (nt > INT32_MAX) return VA_ERR_ARG;
+    static DevVal<int> n_cu;  // per device: one persistent workgroup per CU
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)stem32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S32_LDS) !=
-            hipSuccess)
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
+            hipFuncSetAttribute((const void*)stem32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S32_LDS) !=
+                hipSuccess)
             return VA_ERR_HIP;
+        n_cu() = cus;
         attr() = true;
     }
-    hipLaunchKernelGGL(stem32_kernel, dim3((int)nt), dim3(S32_NT), S32_LDS, (hipStream_t)stream, (const uint8_t*)a->x,
-                       a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w, a->Npad * a->Kpad * 4,
-                       a->Kpad, a->b2, (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt);
+    const int grid = (int)(nt < n_cu() ? nt : n_cu());
+    hipLaunchKernelGGL(stem32_kernel, dim3(grid), dim3(S32_NT), S32_LDS, (hipStream_t)stream, (const uint8_t*)a->x,
+                       a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w, a->Kpad, a->b2,
+                       (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

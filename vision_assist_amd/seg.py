@@ -143,7 +143,9 @@ class SegOutputs:
 
 
 class SegNet:
-    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None):
+    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2f32: bool = False):
+        """c2f32: run model.2 on the fused f32 C2f kernel (va_seg_c2f_f32) in f32 plans -- off by default: it measured
+        slower than the block's four launches."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
@@ -207,9 +209,9 @@ class SegNet:
             for i, ci, co, n, shortcut in arch.c2f_plan():
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
-        # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32); VA_C2F=0 keeps it unfused (A/B)
+        # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32), on request (c2f32)
         self.c2f32 = {}
-        if dtype == "f32" and os.environ.get("VA_C2F", "1") != "0":
+        if dtype == "f32" and c2f32:
             for i, ci, co, n, shortcut in arch.c2f_plan():
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f32[i] = self._pack_c2f32(folded, i)
