@@ -46,7 +46,10 @@ PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0, "w8a16": 2500.0}
 # per-GPU batch (sweeps: DESIGN.md §5; fp8 / w8a16: C5's 64 / 8 GPUs)
 DEFAULT_BATCH = {"f32": 256, "bf16": 384, "fp8": 8, "w8a16": 8}
 PROF_KINDS = 8
-C5_REGIME = "dense_box"  # the regime extras.c5 runs in: the one its fp8 chain-parity test covers
+C5_REGIME = "dense_box"  # the regime extras.c5 runs in: the one its chain-parity tests cover
+# C5's kept form (the faster form that reaches chain agreement >= 0.75 in dense_box): w8a16 (e4m3
+# weights, bf16 activations) at chosen 0.75 / cells 0.875 / paths 0.875; w8a8 (e4m3 MFMA) at 0.25 / 0.75 / 0.75
+C5_FORM = "w8a16"
 
 
 def f32_split_terms() -> int:
@@ -73,7 +76,7 @@ def parse():
                    help="detection regime of the synthetic weights (regime_kwargs); the headline is 'sparse': 1-5 "
                         "compact detections per frame through decode / NMS / contours / mask choice, planted "
                         "navigation masks only on frames without a detection")
-    p.add_argument("--extras", default="c4,c2,dropin,dealer,bf16,dense,dense_box,c5,c5_w8a16",
+    p.add_argument("--extras", default="c4,c2,dropin,dealer,bf16,dense,dense_box,c5,c5_w8a8",
                    help="comma list of extra measurements in the same run: c4 (BASELINE configs[3]: one frame per GPU "
                         "per step, s-seg f32), c2 (configs[1]: n-seg bf16 batch-1 latency, seg-only and end to end), "
                         "dropin (FrameProcessor.__call__ per frame from host numpy frames, answers included), "
@@ -81,8 +84,8 @@ def parse():
                         "bf16 (the bf16 MFMA pipeline), "
                         "dense (300 detections per frame, the random weights' noise masks), dense_box (300 "
                         "detections per frame with solid box masks, one contour each, as a trained model's compact "
-                        "masks), c5 (YOLOv8m-seg 1280 on fp8 MFMA, batch 8), c5_w8a16 (the same with e4m3 weights "
-                        "dequantized into bf16 and bf16 activations); 'none' to skip")
+                        "masks), c5 (YOLOv8m-seg 1280, batch 8, C5's kept form: e4m3 weights dequantized into bf16, "
+                        "bf16 activations), c5_w8a8 (the same on the e4m3 MFMA with e4m3 activations); 'none' to skip")
     p.add_argument("--cpu-sample", type=int, default=256,
                    help="frames timed for the CPU baseline (0 = skip; 256 = ~10-20 s)")
     p.add_argument("--no-prof", action="store_true", help="skip the HIP-event timing of the isolated forwards")
@@ -631,27 +634,30 @@ def main():
             dt_, B_, reg_ = "bf16", args.batch or DEFAULT_BATCH["bf16"], args.regime
         elif ex in ("dense", "dense_box") and args.regime != ex:
             dt_, B_, reg_ = args.dtype, B, ex
-        elif ex == "c5" and not (args.scale == "m" and args.res == 1280 and args.dtype == "fp8"):
-            # C5 runs in the regime its parity test covers (tests/test_gpu_fp8.py::test_fp8_chain_1280_vs_fp32_oracle)
+        elif ex == "c5" and not (args.scale == "m" and args.res == 1280 and args.dtype == C5_FORM):
+            # C5 runs in the regime its parity tests cover (tests/test_gpu_fp8.py::test_*_chain_1280_vs_fp32_oracle)
+            dt_, B_, reg_ = C5_FORM, DEFAULT_BATCH[C5_FORM], C5_REGIME
+        elif ex == "c5_w8a8" and not (args.scale == "m" and args.res == 1280 and args.dtype == "fp8"):
             dt_, B_, reg_ = "fp8", DEFAULT_BATCH["fp8"], C5_REGIME
-        elif ex == "c5_w8a16" and not (args.scale == "m" and args.res == 1280 and args.dtype == "w8a16"):
-            dt_, B_, reg_ = "w8a16", DEFAULT_BATCH["w8a16"], C5_REGIME
         else:
             continue
-        sc_, rs_ = ("m", 1280) if ex in ("c5", "c5_w8a16") else (None, None)
+        sc_, rs_ = ("m", 1280) if ex in ("c5", "c5_w8a8") else (None, None)
         r = Run(args, dev, rank, dt_, B_, reg_, scale=sc_, res=rs_)
         m = r.measure(args.steps, min(args.warmup, 3), world, prof)
         ing = r.ingest(args.steps, world) if (ex == "bf16" and not args.no_ingest) else None
         r.release()
         e = {"value": round(m["value"], 2), "ms_per_step": round(m["ms_per_step"], 3), "dtype": dt_,
              "batch_per_gpu": B_, "regime": reg_}
-        if ex == "c5_w8a16":
-            e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU, weight-only form: YOLOv8m-seg 1280x1280, every conv's "
-                             "weights quantized to e4m3 (one scale per output channel) and dequantized into bf16, bf16 "
-                             "activations on the bf16 MFMA, batch 8, post-processing + grid / A* on GPU")
+        if ex == "c5":
+            e["form"] = ("w8a16: every conv's weights quantized to e4m3 (one scale per output channel) and dequantized "
+                         "into bf16, bf16 activations on the bf16 MFMA -- kept over the e4m3-MFMA form (c5_w8a8, faster) "
+                         "because only it reaches chain agreement >= 0.75 in dense_box (DESIGN.md §4.3)")
+            e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU: YOLOv8m-seg 1280x1280, e4m3 weights (w8a16), batch "
+                             "8 = 64 across 8 GPUs, post-processing + grid / A* on GPU")
             e["parity"] = ("tests/test_gpu_fp8.py::test_w8a16_chain_1280_vs_fp32_oracle: detections / chosen instance / "
                            f"cells / A* paths vs the fp32 oracle chain in the '{C5_REGIME}' regime this line runs")
-        if ex == "c5":
+        if ex == "c5_w8a8":
+            e["form"] = "w8a8: e4m3 weights and activations on the block-scaled e4m3 MFMA"
             e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU: YOLOv8m-seg 1280x1280, convs on e4m3 MFMA "
                              "(per-channel weight scales; activations stored as e4m3 with one calibrated power-of-two "
                              "scale per buffer), batch 8 = 64 across 8 GPUs, post-processing + grid / A* on GPU")

@@ -33,14 +33,14 @@ def test_bench_contract_line():
     # priced against the bf16 peak; the f32-MFMA view beside it
     assert d["dtype"] == "f32" and r["peak"] == 2500.0 and r["f32_equivalent"]["peak"] == 157.3
     assert abs(r["f32_equivalent"]["achieved"] * 6 - r["achieved"]) < 0.02 * r["achieved"]
-    assert set(d["extras"]) == {"bf16", "dense", "dense_box", "c5", "c5_w8a16", "c4", "c2", "dropin", "dealer"}
+    assert set(d["extras"]) == {"bf16", "dense", "dense_box", "c5", "c5_w8a8", "c4", "c2", "dropin", "dealer"}
     # C4's own shape (one frame per GPU per step), C2 latency, the drop-in FrameProcessor.__call__ rate
     assert d["extras"]["c4"]["batch_per_gpu"] == 1 and d["extras"]["c4"]["value"] > 0
     assert d["extras"]["c2"]["seg_only"]["median_ms"] > 0 and d["extras"]["c2"]["end_to_end"]["median_ms"] > 0
     assert d["extras"]["dropin"]["value"] > 0 and d["extras"]["dropin"]["calls_with_answer"] > 0
     assert d["extras"]["bf16"]["roofline"]["peak"] == 2500.0 and d["extras"]["dense"]["dtype"] == "f32"
-    assert d["extras"]["c5"]["dtype"] == "fp8" and d["extras"]["c5"]["roofline"]["peak"] == 5000.0
-    assert d["extras"]["c5_w8a16"]["dtype"] == "w8a16" and d["extras"]["c5_w8a16"]["roofline"]["peak"] == 2500.0
+    assert d["extras"]["c5"]["dtype"] == "w8a16" and d["extras"]["c5"]["roofline"]["peak"] == 2500.0
+    assert d["extras"]["c5_w8a8"]["dtype"] == "fp8" and d["extras"]["c5_w8a8"]["roofline"]["peak"] == 5000.0
     assert "grid_stage_ms_per_frame" in c and "path+analyser" in c["stage_ms_per_frame"]
 
 

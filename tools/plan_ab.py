@@ -1,6 +1,6 @@
 """Interleaved A/B of two segmentation plans that differ by a plan-time environment switch (e.g. VA_FUSE_UP,
 VA_STEM, VA_C2F): both plans are built in one process and their forwards alternate, timed with events.
-python tools/plan_ab.py NAME [--batch 64] [--rounds 20]"""
+python tools/plan_ab.py NAME [--batch 64] [--rounds 20] [--dtype bf16|f32]"""
 import argparse
 import os
 import sys
@@ -15,6 +15,7 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16")
     args = ap.parse_args()
     from vision_assist_amd.seg import SegNet
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
@@ -23,7 +24,7 @@ def main():
     nets, plans = {}, {}
     for v in ("0", "1"):
         os.environ[args.name] = v
-        nets[v] = SegNet(arch, fw, dtype="bf16")
+        nets[v] = SegNet(arch, fw, dtype=args.dtype)
         plans[v] = nets[v].plan(args.batch, 640, 640)
         plans[v]["frames"].copy_(torch.randint(0, 256, plans[v]["frames"].shape, dtype=torch.uint8, device="cuda"))
     times = {"0": [], "1": []}
