@@ -2628,15 +2628,18 @@ __global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restri
 // barely under the two unfused launches (~700 us, profiles/r05/stem/).
 // LDS: weights 64 rows x 1168 B (1152 used: an odd number of 16-byte slots per row, so 16 consecutive rows' reads
 // are conflict-free), model.0 planes 297 px x 208 B (chunk c, plane p, half g at 96 c + 32 p + 16 g: model.1's
-// stride-2 B reads at most 2-way bank conflicted), the frame patch 19 rows x 208 B.  4 waves: wave (wm, wn) computes
-// 32 pixels x 32 channels of model.1, the six term products in two independent accumulator chains.
-constexpr int S32_TH = 4, S32_TW = 16, S32_NT = 256;
+// stride-2 B reads at most 2-way bank conflicted), the frame patch 19 rows x 208 B, a 16 KiB buffer for the K-split's
+// partial sums.  8 waves (two per SIMD): wave w computes the 32 pixels x 32 channels block (wm, wn) = ((w & 3) >> 1,
+// w & 1) of model.1 over K-steps 9 (w >> 2) .. 9 (w >> 2) + 8, the six term products in two independent accumulator
+// chains; waves 4-7 hand their partial sums to waves 0-3 through LDS.  (One wave per SIMD, the whole K-loop per wave:
+// 775 us per 64 frames, profiles/r05/stem/.)
+constexpr int S32_TH = 4, S32_TW = 16, S32_NT = 512;
 constexpr int S32_MR = 2 * S32_TH + 1, S32_MC = 2 * S32_TW + 1, S32_MP = S32_MR * S32_MC;  // 9 x 33 = 297
 constexpr int S32_PS = 208;                           // LDS bytes per model.0 pixel
 constexpr int S32_PR = 2 * S32_MR + 1, S32_PP = 208;  // frame patch: 19 rows x 208 bytes (13 chunks of 16)
 constexpr int S32_WR = 1168;                          // LDS bytes per weight row (288 f32 + 16)
 constexpr int S32_W = 0, S32_M0 = S32_W + 64 * S32_WR, S32_PATCH = S32_M0 + S32_MP * S32_PS;
-constexpr int S32_LDS = S32_PATCH + S32_PR * S32_PP;
+constexpr int S32_PART = S32_PATCH + S32_PR * S32_PP, S32_LDS = S32_PART + 4 * 64 * 64;
 constexpr int S32_NPC = S32_PR * (S32_PP / 16);       // patch chunks (247 <= threads: one per thread)
 static_assert(S32_LDS <= 160 * 1024 && S32_NPC <= S32_NT, "LDS / patch chunks");
 
@@ -2689,7 +2692,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         koff[e] = k < 27 ? (tap / 3) * S32_PP + (tap % 3) * 3 + (2 - c) : -1;
     }
     const float4 bl = *(const float4*)(b0 + 8 * fq), bh = *(const float4*)(b0 + 8 * fq + 4);
-    const int wm = wid >> 1, wn = wid & 1, r32 = lane & 31, g32 = lane >> 5;
+    const int wm = (wid & 3) >> 1, wn = wid & 1, kh = wid >> 2, r32 = lane & 31, g32 = lane >> 5;
     const int py = 2 * wm + (r32 >> 4), px = r32 & 15;  // this lane's model.1 pixel in the tile
     float4 bo[4];
 #pragma unroll
@@ -2743,8 +2746,8 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         // ---- model.1: wave (wm, wn) = pixels 32 wm .. (tile rows 2 wm, 2 wm + 1) x channels 32 wn ..; K-step kl =
         // tap * 2 + chunk, A from the resident weights, B from M0; two accumulator chains (products 0, 2, 4 / 1, 3, 5)
         f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
-#pragma unroll 2
-        for (int kl = 0; kl < 18; ++kl) {
+#pragma unroll 3
+        for (int kl = 9 * kh; kl < 9 * kh + 9; ++kl) {
             const int tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
             bf16x8 ap[3], bp[3];
             split3_bf16(*(const u32x4*)(wrow + 64 * kl), *(const u32x4*)(wrow + 64 * kl + 16), ap);
@@ -2757,18 +2760,22 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u + 1]], bp[TB[u + 1]], acc1, 0, 0, 0);
             }
         }
+        // ---- K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 B per lane)
+        f32x16 a2 = acc0 + acc1;
+        f32x16* part = (f32x16*)(s32 + S32_PART + (wid & 3) * 4096) + lane;
+        if (kh) *part = a2;
+        __syncthreads();
         // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
         const int oy = oy0 + py, ox = ox0 + px;
-        if (oy < Ho1 && ox < Wo1) {
+        if (!kh && oy < Ho1 && ox < Wo1) {
+            a2 = a2 + *part;
             float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f32x16 a2 = acc0 + acc1;
+            for (int j = 0; j < 4; ++j)
                 *(f32x4*)(yp + 8 * j) = fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
                                                          a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w});
-            }
         }
-        __syncthreads();  // M0 free for the next tile; its patch stored
+        __syncthreads();  // M0 and the partial sums free for the next tile; its patch stored
         t = tn;
     }
 }
