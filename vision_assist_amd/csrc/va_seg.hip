@@ -2619,17 +2619,15 @@ __global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restri
 // three exact bf16 weight terms x the exact frame bytes on the MFMA, the sum x 1/255 + bias, SiLU) -> model.1 Conv(32,
 // 64, 3x3, s2) + SiLU (six exact bf16 term products per f32 product, the weights f32 split in registers) -> f32
 // NHWC.  Unfused, model.0's 320 x 320 x 32 f32 map (13 MB per 640 x 640 frame) is written and read back; here it
-// never leaves the chip.  Persistent: one workgroup per CU keeps model.1's whole weight matrix in LDS (64 rows x 288
-// f32, loaded once) and walks 4 x 16 tiles of the model.1 map (XCD-contiguous runs): per tile, model.0 on the 9 x 33
-// pixels the tile's taps read (zero outside model.0's map: model.1's padding) straight into LDS as three bf16 planes
-// (exact: h + m + l = the f32 value), then model.1's 18 K-steps (tap x 16-channel chunk) from there with no barrier
-// inside the K-loop; the next tile's frame patch is loaded into registers while this tile's model.0 runs.  A ring of
-// per-K-step weight stages with a barrier per step (6 MFMAs per wave between barriers) measured 675 us per 64 frames,
-// barely under the two unfused launches (~700 us, profiles/r05/stem/).
-// LDS: weights 64 rows x 1168 B (1152 used: an odd number of 16-byte slots per row, so 16 consecutive rows' reads
-// are conflict-free), model.0 planes 297 px x 208 B (chunk c, plane p, half g at 96 c + 32 p + 16 g: model.1's
-// stride-2 B reads at most 2-way bank conflicted), the frame patch 19 rows x 208 B, a 16 KiB buffer for the K-split's
-// partial sums.  8 waves (two per SIMD): wave w computes the 32 pixels x 32 channels block (wm, wn) = ((w & 3) >> 1,
+// never leaves the chip.  Persistent: one workgroup per CU walks 4 x 16 tiles of the model.1 map (XCD-contiguous
+// runs), each wave holding its share of model.1's weights in registers, split into the three bf16 terms once per
+// workgroup; per tile, model.0 on the 9 x 33 pixels the tile's taps read (zero outside model.0's map: model.1's
+// padding) straight into LDS as three bf16 planes (exact: h + m + l = the f32 value), then model.1's K-steps (tap x
+// 16-channel chunk) from there with no barrier inside the K-loop; the frame patches of the next two tiles are in
+// flight in registers while this tile runs.  (A ring of per-K-step weight stages with a barrier per step: 675 us per 64
+// frames; the weights in LDS split per K-step: 700-775 us; the two unfused launches ~750 us: profiles/r05/stem/.)
+// LDS: model.0 planes 297 px x 208 B (chunk c, plane p, half g at 96 c + 32 p + 16 g: model.1's stride-2 B reads at
+// most 2-way bank conflicted), the frame patch 19 rows x 208 B, a 16 KiB buffer for the K-split's partial sums.  8 waves (two per SIMD): wave w computes the 32 pixels x 32 channels block (wm, wn) = ((w & 3) >> 1,
 // w & 1) of model.1 over K-steps 9 (w >> 2) .. 9 (w >> 2) + 8, the six term products in two independent accumulator
 // chains; waves 4-7 hand their partial sums to waves 0-3 through LDS.  (One wave per SIMD, the whole K-loop per wave:
 // 775 us per 64 frames, profiles/r05/stem/.)
@@ -2637,8 +2635,7 @@ constexpr int S32_TH = 4, S32_TW = 16, S32_NT = 512;
 constexpr int S32_MR = 2 * S32_TH + 1, S32_MC = 2 * S32_TW + 1, S32_MP = S32_MR * S32_MC;  // 9 x 33 = 297
 constexpr int S32_PS = 208;                           // LDS bytes per model.0 pixel
 constexpr int S32_PR = 2 * S32_MR + 1, S32_PP = 208;  // frame patch: 19 rows x 208 bytes (13 chunks of 16)
-constexpr int S32_WR = 1168;                          // LDS bytes per weight row (288 f32 + 16)
-constexpr int S32_W = 0, S32_M0 = S32_W + 64 * S32_WR, S32_PATCH = S32_M0 + S32_MP * S32_PS;
+constexpr int S32_M0 = 0, S32_PATCH = S32_M0 + S32_MP * S32_PS;
 constexpr int S32_PART = S32_PATCH + S32_PR * S32_PP, S32_LDS = S32_PART + 4 * 64 * 64;
 constexpr int S32_NPC = S32_PR * (S32_PP / 16);       // patch chunks (247 <= threads: one per thread)
 static_assert(S32_LDS <= 160 * 1024 && S32_NPC <= S32_NT, "LDS / patch chunks");
@@ -2653,26 +2650,22 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     const int Ho0 = (H + 1) / 2, Wo0 = (W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
     int t = fz::tile(ntiles, 0);
     if (t < 0) return;
-    // model.1's weights, once: row r, f32 k at r * 1168 + 4 k
-    for (int i = tid; i < 64 * 72; i += S32_NT) {
-        const int r = i / 72, c = i - r * 72;
-        *(u32x4*)(s32 + S32_W + r * S32_WR + 16 * c) = *(const u32x4*)(w1 + (int64_t)r * Kpad + 4 * c);
-    }
     // the frame patch of tile tt: rows 4 oy0 - 3 .., bytes [12 ox0 - 16, 12 ox0 + 192) (16-byte aligned: W * 3 % 16 == 0)
-    u32x4 pf;
-    auto load_patch = [&](int tt) {
+    auto load_patch = [&](int tt) -> u32x4 {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (tt < 0) return v;
         const int tx = tt % tiles_x, t2 = tt / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
         const int r = tid / (S32_PP / 16), c = tid - r * (S32_PP / 16);
         const int iy = 4 * ty * S32_TH - 3 + r, rb = 12 * tx * S32_TW - 16 + 16 * c;
-        pf = (u32x4){0u, 0u, 0u, 0u};
         if (tid < S32_NPC && (unsigned)iy < (unsigned)H && rb >= 0 && rb < 3 * W)
-            pf = *(const u32x4*)(frames + (int64_t)n * H * W * 3 + (int64_t)iy * W * 3 + rb);
+            v = *(const u32x4*)(frames + (int64_t)n * H * W * 3 + (int64_t)iy * W * 3 + rb);
+        return v;
     };
-    auto store_patch = [&]() {
-        if (tid < S32_NPC) *(u32x4*)(s32 + S32_PATCH + 16 * tid) = pf;  // row r, chunk c at r * 208 + 16 c = 16 tid
+    auto store_patch = [&](const u32x4& v) {
+        if (tid < S32_NPC) *(u32x4*)(s32 + S32_PATCH + 16 * tid) = v;  // row r, chunk c at r * 208 + 16 c = 16 tid
     };
-    load_patch(t);
-    store_patch();
+    store_patch(load_patch(t));
+    u32x4 pf1 = load_patch(fz::tile(ntiles, 1));  // the next two tiles' patches in flight
 
     const int fr = lane & 15, fq = lane >> 4;
     // model.0 A fragments (conv0_f32m's permutation: fragment i, row r -> channel 8 (r / 4) + 4 i + r % 4, so lane
@@ -2697,8 +2690,13 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     float4 bo[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bo[j] = *(const float4*)(b1 + 32 * wn + 8 * j + 4 * g32);
-    // A rows of this lane: row 32 wn + r32, f32 k = 16 kl + 8 g32 ..
-    const unsigned char* wrow = s32 + S32_W + (32 * wn + r32) * S32_WR + 32 * g32;
+    // this wave's model.1 weights, split once: row 32 wn + r32, K-steps 9 kh .. 9 kh + 8, f32 k = 16 kl + 8 g32 ..
+    bf16x8 apr[9][3];
+    {
+        const float* wr = w1 + (int64_t)(32 * wn + r32) * Kpad + 8 * g32 + 16 * 9 * kh;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) split3_bf16(*(const u32x4*)(wr + 16 * i), *(const u32x4*)(wr + 16 * i + 4), apr[i]);
+    }
     __syncthreads();
 
     constexpr float inv255 = 1.0f / 255.0f;
@@ -2707,7 +2705,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
         const int oy0 = ty * S32_TH, ox0 = tx * S32_TW;
         const int tn = fz::tile(ntiles, k);
-        if (tn >= 0) load_patch(tn);  // lands during this tile's model.0
+        const u32x4 pf2 = load_patch(fz::tile(ntiles, k + 1));  // two tiles ahead
 
         // ---- model.0 on the 9 x 33 region: group g = 16 region pixels (the last group ragged); region pixel q <->
         // model.0 (2 oy0 - 1 + q / 33, 2 ox0 - 1 + q % 33); its window starts at patch row 2 (q / 33), byte 6 (q % 33) + 7
@@ -2740,24 +2738,23 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
                 for (int p = 0; p < 3; ++p) *(bf16x8*)(d + 32 * p) = tt3[p];
             }
         }
-        __syncthreads();      // M0 complete; every wave is done with the patch
-        if (tn >= 0) store_patch();  // the next tile's patch (read after the barrier that ends this tile)
+        __syncthreads();  // M0 complete; every wave is done with the patch
+        store_patch(pf1);  // the next tile's patch (read after the barrier that ends this tile)
 
         // ---- model.1: wave (wm, wn) = pixels 32 wm .. (tile rows 2 wm, 2 wm + 1) x channels 32 wn ..; K-step kl =
         // tap * 2 + chunk, A from the resident weights, B from M0; two accumulator chains (products 0, 2, 4 / 1, 3, 5)
         f32x16 acc0 = (f32x16){}, acc1 = (f32x16){};
-#pragma unroll 3
-        for (int kl = 9 * kh; kl < 9 * kh + 9; ++kl) {
-            const int tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
-            bf16x8 ap[3], bp[3];
-            split3_bf16(*(const u32x4*)(wrow + 64 * kl), *(const u32x4*)(wrow + 64 * kl + 16), ap);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int kl = 9 * kh + i, tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
+            bf16x8 bp[3];
             const unsigned char* bs = s32 + S32_M0 + ((2 * py + ky) * S32_MC + 2 * px + kx) * S32_PS + ch * 96 + 16 * g32;
 #pragma unroll
             for (int p = 0; p < 3; ++p) bp[p] = *(const bf16x8*)(bs + 32 * p);
 #pragma unroll
             for (int u = 0; u < 6; u += 2) {
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u]], bp[TB[u]], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u + 1]], bp[TB[u + 1]], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(apr[i][TA[u]], bp[TB[u]], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(apr[i][TA[u + 1]], bp[TB[u + 1]], acc1, 0, 0, 0);
             }
         }
         // ---- K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 B per lane)
@@ -2776,6 +2773,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
                                                          a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w});
         }
         __syncthreads();  // M0 and the partial sums free for the next tile; its patch stored
+        pf1 = pf2;
         t = tn;
     }
 }
