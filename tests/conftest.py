@@ -19,7 +19,7 @@ def goldens():
     return load_goldens()
 
 
-LIB_SWITCHES = ("VA_F32_SPLIT", "VA_CONV3H", "VA_CONV3T", "VA_SPLITK", "VA_CONV_PATCH", "VA_CONV4", "VA_PW",
+LIB_SWITCHES = ("VA_F32_SPLIT", "VA_CONV3H", "VA_CONV3T", "VA_CONV3Q", "VA_SPLITK", "VA_CONV_PATCH", "VA_CONV4", "VA_PW",
                 "VA_CT_RUNS", "VA_CT_WGP")
 
 

@@ -926,6 +926,45 @@ def test_conv3t_f32_a_stage_forward_bit_identical(B, switch):
         assert torch.equal(g, r), f"{name}: af vs planes max diff {(g - r).abs().max().item()}"
 
 
+@pytest.mark.parametrize("H,W,B,residual,slice_in", [
+    (160, 160, 3, False, 0),   # model.2's bottleneck map (100 tiles per frame)
+    (160, 160, 3, True, 4),    # + the shortcut, the input a channel slice
+    (37, 45, 32, True, 0),     # ragged tiles at the right / bottom edge, many frames
+    (20, 20, 70, False, 0),    # head level 2's map
+])
+def test_conv3q_op(H, W, B, residual, slice_in, switch):
+    """conv3q (the 32 -> 32 stride-1 3x3 f32 layers: weights split once into registers, each 18 x 18 input halo split
+    once into LDS planes, persistent over the tiles) on single ops: within f32 rounding of torch fp32, and of conv2's
+    three-term form (VA_CONV3Q=0) -- the same six term products per f32 product, summed in another order, so equal
+    in value but not in every bit (which also shows that the other kernel ran)."""
+    got, ref = _run_single_conv("f32", 32, 32, 3, 1, H, W, residual, slice_in=slice_in, B=B)
+    scale = max(1.0, ref.abs().max().item())
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+    switch("VA_CONV3Q", "0")
+    got_c2, _ = _run_single_conv("f32", 32, 32, 3, 1, H, W, residual, slice_in=slice_in, B=B)
+    assert (got - got_c2).abs().max().item() <= 2e-5 * scale
+    assert not torch.equal(got, got_c2)
+
+
+def test_conv3q_f32_forward(switch):
+    """The f32 forward with model.2's bottleneck convs on conv3q (B = 3: 300 tiles of the 160 x 160 map) against the
+    same forward with them on conv2 (VA_CONV3Q=0): f32-rounding close, and within the f32 bar of torch."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(3, seed=29)
+    switch("VA_CONV3Q", "0")
+    ref = _gpu_heads(net, frames)
+    switch("VA_CONV3Q", None)
+    got = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: conv3q vs conv2 max diff {d}"
+    torch.set_num_threads(8)
+    want = _ref_heads(arch, fw, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, want):
+        assert (g - r).abs().max().item() <= 1e-3, name
+
+
 @pytest.mark.parametrize("H,W,B", [(72, 112, 2), (640, 640, 1)])
 def test_stem_f32_op_vs_fp64(H, W, B):
     """va_seg_stem_f32 (uint8 frame -> model.0 -> model.1 in f32 as one kernel, model.0's map kept in LDS as three

@@ -3055,6 +3055,124 @@ __global__ __launch_bounds__(CF32_NT) void c2f32_kernel(const float* __restrict_
     }
 }
 
+// ----------------------------------------------------------------------------------------- f32 32-channel 3x3
+// The 32 -> 32 channel stride-1 3x3 f32 layers (model.2's bottleneck convs at 160 x 160 in YOLOv8s-seg, block.py
+// Bottleneck; the head's cv4.l.1, head.py Segment) with the stem's structure instead of conv2's im2col tiles, which
+// re-read every input pixel nine times through L2 and split both operands per K-step: the whole weight matrix
+// (32 x 288) is split into its three exact bf16 terms once per workgroup and held in registers, and per 16 x 16
+// output tile the 18 x 18 input halo is read once, split once into three bf16 planes in LDS (208 bytes per pixel:
+// [chunk 2][plane 3][16 channels], conflict-free 32-pixel reads) and every tap read from there -- no barrier inside
+// the K-loop.  Persistent: one 512-thread workgroup per CU walks the tiles (fz::tile, XCD-contiguous runs), the next
+// tile's halo in flight in registers during this one's MFMAs.  Wave w computes output rows 4 (w & 3) .. + 3 of the
+// tile (two 32-pixel blocks) x 32 channels over K-steps 9 (w >> 2) .. + 8 (tap x 16-channel chunk), the six term
+// products per K-step and block on v_mfma_f32_32x32x16_bf16 (the two blocks are the two accumulator chains); waves
+// 4-7 hand their partial sums to waves 0-3 through LDS, which add bias, SiLU and the residual (Bottleneck's
+// shortcut) and write f32.
+constexpr int Q3_T = 16, Q3_HW = Q3_T + 2, Q3_HP = Q3_HW * Q3_HW;  // 16 x 16 tile, 18 x 18 = 324-pixel halo
+constexpr int Q3_NT = 512, Q3_PS = 208;
+constexpr int Q3_NCH = Q3_HP * 8;                    // 16-byte input chunks (4 channels) per halo: 2592
+constexpr int Q3_LD = (Q3_NCH + Q3_NT - 1) / Q3_NT;  // per thread: 6
+constexpr int Q3_PART = Q3_HP * Q3_PS, Q3_LDS = Q3_PART + 4 * 2 * 64 * 64;  // planes 66 KiB + partial sums 32 KiB
+static_assert(Q3_LDS <= 160 * 1024, "one workgroup per CU");
+
+__global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntiles) {
+    extern __shared__ __align__(16) unsigned char q3[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const float* __restrict__ x = (const float*)a.x;
+    const int H = a.H, W = a.W, ldx = a.ldx;
+    int t = fz::tile(ntiles, 0);
+    if (t < 0) return;
+    // the 18 x 18 input pixels of tile tt (zero outside the image: the conv's padding), 8 chunks of 4 channels each;
+    // chunk c = 8 q + g <-> halo pixel q, channels 4 g .. 4 g + 3
+    auto load_halo = [&](int tt, u32x4 (&v)[Q3_LD]) {
+        int tx = 0, ty = 0, n = 0;
+        if (tt >= 0) {
+            tx = tt % tiles_x;
+            const int t2 = tt / tiles_x;
+            ty = t2 % tiles_y;
+            n = t2 / tiles_y;
+        }
+        const float* xn = x + (int64_t)n * H * W * ldx;
+#pragma unroll
+        for (int i = 0; i < Q3_LD; ++i) {
+            const int c = tid + Q3_NT * i, q = c >> 3, g = c & 7;
+            const int iy = ty * Q3_T - 1 + q / Q3_HW, ix = tx * Q3_T - 1 + q % Q3_HW;
+            v[i] = (u32x4){0u, 0u, 0u, 0u};
+            if (tt >= 0 && c < Q3_NCH && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                v[i] = *(const u32x4*)(xn + ((int64_t)iy * W + ix) * ldx + 4 * g);
+        }
+    };
+    u32x4 hv[Q3_LD];
+    load_halo(t, hv);
+
+    const int r32 = lane & 31, g32 = lane >> 5, kh = wid >> 2, pb = wid & 3;
+    // this wave's weights, split once: row (output channel) r32, K-steps 9 kh .. 9 kh + 8, f32 k = 16 kl + 8 g32 ..
+    bf16x8 apr[9][3];
+    {
+        const float* wr = (const float*)a.w + (int64_t)r32 * a.Kpad + 8 * g32 + 16 * 9 * kh;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) split3_bf16(*(const u32x4*)(wr + 16 * i), *(const u32x4*)(wr + 16 * i + 4), apr[i]);
+    }
+    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    for (int k = 1; t >= 0; ++k) {
+        const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
+#pragma unroll
+        for (int i = 0; i < Q3_LD; ++i) {
+            const int c = tid + Q3_NT * i;
+            if (c < Q3_NCH) cf32_put4(q3 + (c >> 3) * Q3_PS, c & 7, __builtin_bit_cast(f32x4, hv[i]));
+        }
+        const int tn = fz::tile(ntiles, k);
+        load_halo(tn, hv);  // the next tile's halo, in flight during this tile's K-loop
+        __syncthreads();    // planes complete
+
+        f32x16 acc[2] = {(f32x16){}, (f32x16){}};
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const int kl = 9 * kh + i, tap = kl >> 1, ch = kl & 1, ky = tap / 3, kx = tap % 3;
+            bf16x8 bp[2][3];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const unsigned char* bs =
+                    q3 + ((4 * pb + 2 * b + (r32 >> 4) + ky) * Q3_HW + (r32 & 15) + kx) * Q3_PS + ch * 96 + 16 * g32;
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bp[b][p] = *(const bf16x8*)(bs + 32 * p);
+            }
+#pragma unroll
+            for (int u = 0; u < 6; ++u)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(apr[i][TA[u]], bp[b][TB[u]], acc[b], 0, 0, 0);
+        }
+        // K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 bytes per lane and block)
+        f32x16* part = (f32x16*)(q3 + Q3_PART + pb * 8192) + lane;
+        if (kh) {
+            part[0] = acc[0];
+            part[64] = acc[1];
+        }
+        __syncthreads();  // partial sums complete; every wave is done with this tile's planes
+        if (!kh) {
+            // lane (r32, g32) holds channels 8 j + 4 g32 + (0..3), j = 0..3, of its block's pixel r32
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const f32x16 s = acc[b] + part[64 * b];
+                const int oy = ty * Q3_T + 4 * pb + 2 * b + (r32 >> 4), ox = tx * Q3_T + (r32 & 15);
+                if (oy >= H || ox >= W) continue;
+                const int64_t pix = ((int64_t)n * H + oy) * W + ox;
+                float* yp = (float*)a.y + pix * a.ldy + 4 * g32;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float4 bv = *(const float4*)(a.bias + 8 * j + 4 * g32);
+                    f32x4 v = {s[4 * j] + bv.x, s[4 * j + 1] + bv.y, s[4 * j + 2] + bv.z, s[4 * j + 3] + bv.w};
+                    if (a.act) v = fz::act(v);
+                    if (a.res) v = v + *(const f32x4*)((const float*)a.res + pix * a.ldr + 4 * g32 + 8 * j);
+                    *(f32x4*)(yp + 8 * j) = v;
+                }
+            }
+        }
+        t = tn;
+    }
+}
+
 // ----------------------------------------------------------------------------------------- SPPF pool
 // in: slice 0 of buf (c channels), writes slices 1..3 = MaxPool2d(5,1,2) applied 1, 2, 3 times (-inf padding).
 // With -inf padding and stride 1, k chained 5x5 pools equal one (4k+1)x(4k+1) pool clipped to the
@@ -3446,8 +3564,55 @@ hipError_t launch_conv3h_tail(const va_conv_args& a, hipStream_t st) {
     return a.Cout == 128 ? launch_conv3h_v<3, 3, 4, float, true>(a, st) : launch_conv3h_v<3, 3, 2, float, true>(a, st);
 }
 
+// the 32 -> 32 stride-1 3x3 f32 layers on conv3q_kernel (VA_CONV3Q=0: conv2's three-term form) when the launch has a
+// tile for every CU (below that conv2's split-K tiles fill the chip better)
+int conv3q_tiles(const va_conv_args& a, int* tx, int* ty) {
+    *tx = (a.W + Q3_T - 1) / Q3_T;
+    *ty = (a.H + Q3_T - 1) / Q3_T;
+    const int64_t nt = (int64_t)a.N * *tx * *ty;
+    return nt > INT32_MAX ? -1 : (int)nt;
+}
+int device_cus() {
+    static DevVal<int> n_cu;
+    if (!n_cu()) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return -1;
+        n_cu() = cus;
+    }
+    return n_cu();
+}
+bool use_conv3q(const va_conv_args& a) {
+    if (!va_sw().conv3q || a.mode != 0 || a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.H != a.Ho ||
+        a.W != a.Wo || a.Cin != 32 || a.Cout != 32 || a.K != 288 || a.Kpad != 288 || a.w2 || a.xu || a.ldx % 4 ||
+        a.ldy % 4 || ((uintptr_t)a.x & 15) || ((uintptr_t)a.y & 15) || ((uintptr_t)a.w & 15) ||
+        ((uintptr_t)a.bias & 15) || (a.res && (a.ldr % 4 || ((uintptr_t)a.res & 15))))
+        return false;
+    int tx, ty;
+    const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
+    return cus > 0 && nt >= cus;
+}
+hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)conv3q_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Q3_LDS) !=
+            hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    int tx, ty;
+    const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
+    if (nt <= 0 || cus <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(conv3q_kernel, dim3(nt < cus ? nt : cus), dim3(Q3_NT), Q3_LDS, st, a, tx, ty, nt);
+    return hipGetLastError();
+}
+
 template <int SPL, typename OutT>
 hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
+    if constexpr (SPL == 6 && sizeof(OutT) == 4) {
+        if (use_conv3q(a)) return launch_conv3q(a, st);
+    }
     if (SPL == 6 && use_conv3t(a)) return launch_conv3t<OutT>(a, st);
     if (SPL == 6 && use_conv3h_narrow(a)) return launch_conv3h_v<3, 3, 2, OutT>(a, st);
     if (a.mode == 2) return a.Cout > 64 ? launch_conv2<2, 2, 4, OutT, float, SPL>(a, st) : hipErrorInvalidValue;
