@@ -966,10 +966,12 @@ def test_conv3q_f32_forward(switch):
 
 
 @pytest.mark.parametrize("H,W,B", [(72, 112, 2), (640, 640, 1)])
-def test_stem_f32_op_vs_fp64(H, W, B):
+@pytest.mark.parametrize("tail", [False, True])
+def test_stem_f32_op_vs_fp64(H, W, B, tail):
     """va_seg_stem_f32 (uint8 frame -> model.0 -> model.1 in f32 as one kernel, model.0's map kept in LDS as three
     exact bf16 planes) on single ops against float64 torch of the two layers (x / 255, conv, SiLU, conv s2, SiLU):
-    within f32 rounding; ragged model.1 tiles at 72 x 112 (18 x 28: 4 x 16 tiles), frame edges, a full 640 frame."""
+    within f32 rounding; ragged model.1 tiles at 72 x 112 (18 x 28: 4 x 16 tiles), frame edges, a full 640 frame.
+    tail: + model.2.cv1 (1x1, 64 -> 64, SiLU) in the epilogue, model.1's map kept in LDS too."""
     import ctypes
 
     from vision_assist_amd import _lib
@@ -983,6 +985,9 @@ def test_stem_f32_op_vs_fp64(H, W, B):
     a = S.ConvArgs(x=frames.cuda().data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=net.w0_3.data_ptr(),
                    bias=net.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K, Kpad=p1.Kpad,
                    y=y.data_ptr(), ldy=72, dtype=S.VA_DTYPE_F32)
+    if tail:
+        assert net.stem32_b2 is not None
+        a.w2, a.b2, a.c2, a.act2 = net.w["model.2.cv1"].w.data_ptr(), net.stem32_b2.data_ptr(), 64, 1
     fd = frames.cuda()
     a.x = fd.data_ptr()
     _lib.check(lib.va_seg_stem_f32(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_stem_f32")
@@ -991,6 +996,9 @@ def test_stem_f32_op_vs_fp64(H, W, B):
     w1, b1 = fw["model.1"]
     x = (frames.flip(-1).double() / 255.0).permute(0, 3, 1, 2)
     ref = F.silu(F.conv2d(F.silu(F.conv2d(x, w0.double(), b0.double(), 2, 1)), w1.double(), b1.double(), 2, 1))
+    if tail:
+        wc, bc = fw["model.2.cv1"]
+        ref = F.silu(F.conv2d(ref, wc.double(), bc.double()))
     got = y[..., :64].cpu().permute(0, 3, 1, 2).double()
     assert torch.isfinite(y[..., :64]).all() and torch.isnan(y[..., 64:]).all()  # nothing past the slice
     scale = max(1.0, ref.abs().max().item())
@@ -1004,10 +1012,20 @@ def test_stem_f32_forward(monkeypatch):
     arch, fw, net = _net("f32", "s", seed=5)
     frames = _frames(2, seed=31)
     names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
-    assert "model.0+model.1 (fused f32 stem)" in names and "model.1" not in names
+    assert "model.0+model.1+model.2.cv1 (fused f32 stem)" in names and "model.1" not in names
+    assert "model.2.cv1" not in names
     got = _gpu_heads(net, frames)
-    monkeypatch.setenv("VA_STEM", "0")
+    monkeypatch.setenv("VA_STEM_TAIL", "0")  # cv1 a launch of its own
     from vision_assist_amd.seg import SegNet
+    net1 = SegNet(arch, fw, dtype="f32")
+    names1 = [m["name"] for m in net1.plan(2, 640, 640)["meta"]]
+    assert "model.0+model.1 (fused f32 stem)" in names1 and "model.2.cv1" in names1
+    ref1 = _gpu_heads(net1, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref1):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: stem with / without the cv1 tail max diff {d}"
+    monkeypatch.delenv("VA_STEM_TAIL")
+    monkeypatch.setenv("VA_STEM", "0")
     net2 = SegNet(arch, fw, dtype="f32")
     assert "model.1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
     ref = _gpu_heads(net2, frames)

@@ -673,6 +673,20 @@ __device__ __forceinline__ void split3_bf16(const u32x4& c0, const u32x4& c1, bf
 #pragma unroll
     for (int k = 0; k < 3; ++k) t[k] = __builtin_bit_cast(bf16x8, (u32x4){w[k][0], w[k][1], w[k][2], w[k][3]});
 }
+// four f32 -> three bf16 planes of 4 values each (split3_bf16's terms)
+__device__ __forceinline__ void split3_bf16x4(const f32x4& v, uint2 (&t)[3]) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const f32x2 x = {v[2 * e], v[2 * e + 1]};
+        const unsigned h = cvt_pk_bf16(x);
+        const f32x2 r = x - unpk_bf16(h);
+        const unsigned m = cvt_pk_bf16(r);
+        const unsigned l = cvt_pk_bf16(r - unpk_bf16(m));
+        (e ? t[0].y : t[0].x) = h;
+        (e ? t[1].y : t[1].x) = m;
+        (e ? t[2].y : t[2].x) = l;
+    }
+}
 
 // SPL (T = float only): 0 = exact f32 MFMA (v_mfma_f32_16x16x4_f32, 32 cycles per SIMD); 6 or 9 = the f32
 // operands split into three exact bf16 terms (split3_bf16) and multiplied on v_mfma_f32_16x16x32_bf16 (16 cycles
@@ -2639,12 +2653,19 @@ constexpr int S32_M0 = 0, S32_PATCH = S32_M0 + S32_MP * S32_PS;
 constexpr int S32_PART = S32_PATCH + S32_PR * S32_PP, S32_LDS = S32_PART + 4 * 64 * 64;
 constexpr int S32_NPC = S32_PR * (S32_PP / 16);       // patch chunks (247 <= threads: one per thread)
 static_assert(S32_LDS <= 160 * 1024 && S32_NPC <= S32_NT, "LDS / patch chunks");
+// TAIL (model.2.cv1, the C2f's 1x1 64 -> 64, fused): the tile's model.1 activations as three bf16 planes (64 pixels x
+// 400 bytes: [chunk 4][plane 3][16 channels] + 16 bytes, conflict-free 16-pixel reads) and cv1's weights pre-split
+// once per workgroup (64 rows x 400 bytes, the same layout over K)
+constexpr int S32_TP = 400, S32_T = S32_LDS, S32_W1 = S32_T + 64 * S32_TP, S32_LDS_T = S32_W1 + 64 * S32_TP;
+static_assert(S32_LDS_T <= 160 * 1024, "LDS with the tail");
 
+template <bool TAIL>
 __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                            const __bf16* __restrict__ w03, const float* __restrict__ b0,
                                                            const float* __restrict__ w1, int Kpad,
                                                            const float* __restrict__ b1, float* __restrict__ y, int ldy,
-                                                           int tiles_x, int tiles_y, int ntiles) {
+                                                           int tiles_x, int tiles_y, int ntiles,
+                                                           const float* __restrict__ wt, const float* __restrict__ bt) {
     extern __shared__ __align__(16) unsigned char s32[];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Ho0 = (H + 1) / 2, Wo0 = (W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
@@ -2696,6 +2717,15 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         const float* wr = w1 + (int64_t)(32 * wn + r32) * Kpad + 8 * g32 + 16 * 9 * kh;
 #pragma unroll
         for (int i = 0; i < 9; ++i) split3_bf16(*(const u32x4*)(wr + 16 * i), *(const u32x4*)(wr + 16 * i + 4), apr[i]);
+    }
+    if constexpr (TAIL) {  // cv1's [64][64] f32 weights: thread -> row tid / 8, K 8 (tid % 8) .. + 7
+        const int r = tid >> 3, q = tid & 7;
+        const float* src = wt + r * 64 + 8 * q;
+        bf16x8 tw[3];
+        split3_bf16(*(const u32x4*)src, *(const u32x4*)(src + 4), tw);
+        unsigned char* d = s32 + S32_W1 + r * S32_TP + (q >> 1) * 96 + 16 * (q & 1);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(bf16x8*)(d + 32 * p) = tw[p];
     }
     __syncthreads();
 
@@ -2764,15 +2794,66 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         __syncthreads();
         // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
         const int oy = oy0 + py, ox = ox0 + px;
-        if (!kh && oy < Ho1 && ox < Wo1) {
-            a2 = a2 + *part;
-            float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
+        if constexpr (TAIL) {
+            // model.1's activations -> the T planes (every pixel of the tile: an outside one is finite and unstored);
+            // channel c = 32 wn + 8 j + 4 g32 + e sits in chunk c / 16, at byte 2 (c % 16) of each plane's 32 bytes
+            if (!kh) {
+                a2 = a2 + *part;
+                unsigned char* tp = s32 + S32_T + (32 * wm + r32) * S32_TP + 8 * g32;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                *(f32x4*)(yp + 8 * j) = fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
-                                                         a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w});
+                for (int j = 0; j < 4; ++j) {
+                    uint2 tt3[3];
+                    split3_bf16x4(fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
+                                                  a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w}),
+                                  tt3);
+                    unsigned char* d = tp + (2 * wn + (j >> 1)) * 96 + 16 * (j & 1);
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) *(uint2*)(d + 32 * p) = tt3[p];
+                }
+            }
+            __syncthreads();  // T complete; M0 and the partial sums free for the next tile; its patch stored
+            if (!kh) {
+                // cv1 (1x1, 64 -> 64): wave (wm, wn) = pixels 32 wm .. x cv1 channels 32 wn ..; K-step j = model.1
+                // channels 16 j .. (four steps), A from the W1 planes, B from T; two accumulator chains
+                f32x16 c0 = (f32x16){}, c1 = (f32x16){};
+                const unsigned char* wa = s32 + S32_W1 + (32 * wn + r32) * S32_TP + 16 * g32;
+                const unsigned char* tb = s32 + S32_T + (32 * wm + r32) * S32_TP + 16 * g32;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    bf16x8 ap[3], bp[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        ap[p] = *(const bf16x8*)(wa + j * 96 + 32 * p);
+                        bp[p] = *(const bf16x8*)(tb + j * 96 + 32 * p);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 6; u += 2) {
+                        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u]], bp[TB[u]], c0, 0, 0, 0);
+                        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[u + 1]], bp[TB[u + 1]], c1, 0, 0, 0);
+                    }
+                }
+                if (oy < Ho1 && ox < Wo1) {
+                    const f32x16 cs = c0 + c1;
+                    float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float4 bv = *(const float4*)(bt + 32 * wn + 8 * j + 4 * g32);
+                        *(f32x4*)(yp + 8 * j) = fz::act((f32x4){cs[4 * j] + bv.x, cs[4 * j + 1] + bv.y,
+                                                                 cs[4 * j + 2] + bv.z, cs[4 * j + 3] + bv.w});
+                    }
+                }
+            }
+        } else {
+            if (!kh && oy < Ho1 && ox < Wo1) {
+                a2 = a2 + *part;
+                float* yp = y + (((int64_t)n * Ho1 + oy) * Wo1 + ox) * ldy + 32 * wn + 4 * g32;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    *(f32x4*)(yp + 8 * j) = fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
+                                                             a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w});
+            }
+            __syncthreads();  // M0 and the partial sums free for the next tile; its patch stored
         }
-        __syncthreads();  // M0 and the partial sums free for the next tile; its patch stored
         pf1 = pf2;
         t = tn;
     }
@@ -2812,20 +2893,6 @@ constexpr int CF32_W1 = 0, CF32_W2 = CF32_W1 + 64 * 64, CF32_W3 = CF32_W2 + 32 *
 constexpr int CF32_WN = CF32_W4 + 64 * 96;  // 28672 floats
 constexpr int CF32_NK = 4 + 18 + 18 + 6;    // K-steps per tile
 
-// four f32 -> three bf16 planes of 4 values each (split3_bf16's terms)
-__device__ __forceinline__ void split3_bf16x4(const f32x4& v, uint2 (&t)[3]) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        const f32x2 x = {v[2 * e], v[2 * e + 1]};
-        const unsigned h = cvt_pk_bf16(x);
-        const f32x2 r = x - unpk_bf16(h);
-        const unsigned m = cvt_pk_bf16(r);
-        const unsigned l = cvt_pk_bf16(r - unpk_bf16(m));
-        (e ? t[0].y : t[0].x) = h;
-        (e ? t[1].y : t[1].x) = m;
-        (e ? t[2].y : t[2].x) = l;
-    }
-}
 // channels 4 g .. 4 g + 3 (g = 0..7) of a 32-channel plane pixel at p: the three planes' 8-byte pieces
 __device__ __forceinline__ void cf32_put4(unsigned char* p, int g, const f32x4& v) {
     uint2 t[3];
@@ -3974,26 +4041,33 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a) {
         ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15) || ((uintptr_t)a->b2 & 15) ||
         (int64_t)a->H * a->W * 3 >= 0x80000000LL)
         return VA_ERR_ARG;
+    const bool tail = a->w2 != nullptr;
+    if (tail && (a->c2 != 64 || a->act2 != 1 || ((uintptr_t)a->w2 & 15))) return VA_ERR_ARG;
     const int Ho0 = (a->H + 1) / 2, Wo0 = (a->W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
     const int tiles_x = (Wo1 + S32_TW - 1) / S32_TW, tiles_y = (Ho1 + S32_TH - 1) / S32_TH;
     const int64_t nt = (int64_t)tiles_x * tiles_y * a->N;
     if (nt > INT32_MAX) return VA_ERR_ARG;
-    static DevVal<int> n_cu;  // per device: one persistent workgroup per CU
+    const int cus = device_cus();
     static DevFlag attr;
+    if (cus <= 0) return VA_ERR_HIP;
     if (!attr()) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0 ||
-            hipFuncSetAttribute((const void*)stem32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S32_LDS) !=
-                hipSuccess)
+        if (hipFuncSetAttribute((const void*)stem32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)stem32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS_T) != hipSuccess)
             return VA_ERR_HIP;
-        n_cu() = cus;
         attr() = true;
     }
-    const int grid = (int)(nt < n_cu() ? nt : n_cu());
-    hipLaunchKernelGGL(stem32_kernel, dim3(grid), dim3(S32_NT), S32_LDS, (hipStream_t)stream, (const uint8_t*)a->x,
-                       a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w, a->Kpad, a->b2,
-                       (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt);
+    const int grid = (int)(nt < cus ? nt : cus);
+    if (tail)
+        hipLaunchKernelGGL(stem32_kernel<true>, dim3(grid), dim3(S32_NT), S32_LDS_T, (hipStream_t)stream,
+                           (const uint8_t*)a->x, a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w,
+                           a->Kpad, a->b2, (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt, (const float*)a->w2,
+                           a->b2 + 64);
+    else
+        hipLaunchKernelGGL(stem32_kernel<false>, dim3(grid), dim3(S32_NT), S32_LDS, (hipStream_t)stream,
+                           (const uint8_t*)a->x, a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w,
+                           a->Kpad, a->b2, (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

@@ -203,6 +203,13 @@ class SegNet:
         # model.1's packed f32 weights; VA_STEM=0 keeps the two layers apart (A/B)
         self.stem32 = (dtype == "f32" and self.fuse_first and self.w0_3 is not None and w0.shape[0] == 32 and
                        tuple(folded["model.1"][0].shape) == (64, 32, 3, 3) and os.environ.get("VA_STEM", "1") != "0")
+        # ... with model.2.cv1 (the C2f's 1x1, 64 -> 64) in its epilogue, so model.1's map never reaches HBM either;
+        # VA_STEM_TAIL=0 keeps cv1 a launch of its own (A/B).  b2 = [model.1 bias | cv1 bias]
+        self.stem32_b2 = None
+        pc1 = self.w.get("model.2.cv1")
+        if (self.stem32 and not c2f32 and pc1 is not None and pc1.k == 1 and pc1.cin == 64 and pc1.cout == 64 and
+                pc1.Kpad == 64 and os.environ.get("VA_STEM_TAIL", "1") != "0"):
+            self.stem32_b2 = torch.cat([self.w["model.1"].b[:64], pc1.b[:64]]).contiguous()
         # C2f blocks the fused kernel covers (va355.h va_seg_c2f): n = 1, shortcut, 64 -> 64 (model.2 of 's')
         self.c2f_fused = {}
         if dtype == "bf16" and os.environ.get("VA_C2F", "1") != "0":
@@ -541,9 +548,13 @@ class SegNet:
                          "prefix": prefix, "src": src, "fp8": on_fp8})
             return ho, wo
 
-        def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None):
+        def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None, pre: Slice | None = None):
+            """pre: the block's concat buffer with cv1's output already in it (cv1 fused into the producer)"""
             _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
-            if i in self.c2f32 and src.c == 64 and src.ld % 4 == 0 and dst.ld % 4 == 0 and up is None:
+            if pre is not None:
+                c = co // 2
+                t = pre
+            elif i in self.c2f32 and src.c == 64 and src.ld % 4 == 0 and dst.ld % 4 == 0 and up is None:
                 blob, bias = self.c2f32[i]
                 ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
                                                              w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
@@ -553,7 +564,7 @@ class SegNet:
                              "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
                              "bytes": 4 * B * h * w * 128})
                 return
-            if i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
+            if pre is None and i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
                 ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld, w=blob.data_ptr(),
                                                              bias=bias.data_ptr(), Cout=64, y=dst.ptr, ldy=dst.ld,
@@ -563,9 +574,10 @@ class SegNet:
                              "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
                              "bytes": 2 * B * h * w * 128})
                 return
-            c = co // 2
-            t = new(h, w, (2 + n) * c)
-            conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w, up=up)
+            if pre is None:
+                c = co // 2
+                t = new(h, w, (2 + n) * c)
+                conv(f"model.{i}.cv1", src, t.sub(0, 2 * c), h, w, up=up)
             tmp = new(h, w, c)
             for j in range(n):
                 x_in = t.sub((1 + j) * c, c)
@@ -668,14 +680,25 @@ class SegNet:
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
                          "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
         elif self.stem32 and (W * 3) % 16 == 0:
-            a1 = new(h2, w2, a.c2)
             p1 = self.w["model.1"]
-            ops.append(SegOp(kind=VA_OP_STEM, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64,
-                                                          w3=self.w0_3.data_ptr(), bias=self.w0[1].data_ptr(),
-                                                          w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K,
-                                                          Kpad=p1.Kpad, y=a1.ptr, ldy=a1.ld, dtype=VA_DTYPE_F32)))
+            sa = ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=self.w0_3.data_ptr(),
+                          bias=self.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K,
+                          Kpad=p1.Kpad, dtype=VA_DTYPE_F32)
             macs = 27 * 32 * 4 + 288 * 64  # per model.1 output pixel: 4 model.0 pixels + model.1
-            meta.append({"name": "model.0+model.1 (fused f32 stem)", "kind": "conv", "M": B * h2 * w2, "N": 64,
+            name = "model.0+model.1 (fused f32 stem)"
+            if self.stem32_b2 is not None:  # + model.2.cv1: the stem writes cv1's output into model.2's concat buffer
+                n2 = next(p for p in a.c2f_plan() if p[0] == 2)[3]
+                t2 = new(h2, w2, (2 + n2) * 32)
+                a1 = t2.sub(0, 64)
+                sa.w2, sa.b2, sa.c2, sa.act2 = self.w["model.2.cv1"].w.data_ptr(), self.stem32_b2.data_ptr(), 64, 1
+                macs += 64 * 64
+                name = "model.0+model.1+model.2.cv1 (fused f32 stem)"
+            else:
+                t2 = None
+                a1 = new(h2, w2, a.c2)
+            sa.y, sa.ldy = a1.ptr, a1.ld
+            ops.append(SegOp(kind=VA_OP_STEM, a=sa))
+            meta.append({"name": name, "kind": "conv", "M": B * h2 * w2, "N": 64,
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
                          "flops_c0": 2 * B * h2 * w2 * 27 * 32 * 4,  # model.0's share (three term products, once)
                          "bytes": B * H * W * 3 + 4 * B * h2 * w2 * 64})
@@ -701,7 +724,7 @@ class SegNet:
             a1 = new(h2, w2, a.c2)
             conv("model.1", a0, a1, h1, w1, stride=2)
         p2 = new(h2, w2, a.c2)
-        c2f(2, a1, p2, h2, w2)
+        c2f(2, a1, p2, h2, w2, pre=t2 if self.stem32 and (W * 3) % 16 == 0 else None)
         a3 = new(h3, w3, a.c3)
         conv("model.3", p2, a3, h2, w2, stride=2)
         cat14 = new(h3, w3, a.c4 + a.c3)          # [up(h12) | P3]
