@@ -1088,7 +1088,8 @@ def test_c2f_f32_forward():
     assert "model.2 (fused f32 C2f)" in names and "model.2.cv1" not in names
     got = _gpu_heads(net, frames)
     net2 = SegNet(arch, fw, dtype="f32")
-    assert "model.2.cv1" in [m["name"] for m in net2.plan(2, 640, 640)["meta"]]
+    names2 = [m["name"] for m in net2.plan(2, 640, 640)["meta"]]  # cv1 in the stem's epilogue, the rest apart
+    assert "model.0+model.1+model.2.cv1 (fused f32 stem)" in names2 and "model.2.cv2" in names2
     ref = _gpu_heads(net2, frames)
     for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
         d = (g - r).abs().max().item()
