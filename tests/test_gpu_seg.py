@@ -947,6 +947,21 @@ def test_conv3q_op(H, W, B, residual, slice_in, switch):
     assert not torch.equal(got, got_c2)
 
 
+def test_conv3q_dynamic_schedule(switch):
+    """conv3q with a work counter (va_conv_args.wcnt: tiles claimed by the workgroups as they start, the schedule the
+    plans use) against the static schedule: bit-identical (the same per-tile arithmetic), twice in a row (the last
+    workgroup out zeroes the counters for the next launch), counters zero afterwards."""
+    ws = (torch.empty(1 << 20, dtype=torch.uint8, device="cuda"), torch.zeros(128, dtype=torch.int32, device="cuda"))
+    static, ref = _run_single_conv("f32", 32, 32, 3, 1, 160, 160, True, slice_in=4, B=5)
+    for _ in range(2):
+        dyn, _ = _run_single_conv("f32", 32, 32, 3, 1, 160, 160, True, slice_in=4, B=5, ws=ws)
+        assert torch.equal(dyn, static), (dyn - static).abs().max().item()
+        assert int(ws[1].abs().sum()) == 0
+    switch("VA_CONV3Q", "static")
+    st2, _ = _run_single_conv("f32", 32, 32, 3, 1, 160, 160, True, slice_in=4, B=5, ws=ws)
+    assert torch.equal(st2, static)
+
+
 def test_conv3q_f32_forward(switch):
     """The f32 forward with model.2's bottleneck convs on conv3q (B = 3: 300 tiles of the 160 x 160 map) against the
     same forward with them on conv2 (VA_CONV3Q=0): f32-rounding close, and within the f32 bar of torch."""
@@ -1003,6 +1018,39 @@ def test_stem_f32_op_vs_fp64(H, W, B, tail):
     assert torch.isfinite(y[..., :64]).all() and torch.isnan(y[..., 64:]).all()  # nothing past the slice
     scale = max(1.0, ref.abs().max().item())
     assert (got - ref).abs().max().item() <= 2e-5 * scale, (got - ref).abs().max().item()
+
+
+def test_stem_f32_dynamic_schedule():
+    """va_seg_stem_f32 with a work counter (va_conv_args.wcnt: the tiles claimed by the workgroups as they start, two
+    ahead; the schedule the plans use) against the static schedule (no counter): bit-identical, with and without the
+    cv1 tail, twice in a row (the counters are zeroed by the last workgroup out)."""
+    import ctypes
+
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    arch, fw, net = _net("f32", "s", seed=29)
+    lib = _lib.load()
+    B, H, W = 3, 640, 640
+    fd = _frames(B, H, W, seed=7).cuda()
+    wcnt = torch.zeros(128, dtype=torch.int32, device="cuda")
+    p1 = net.w["model.1"]
+    for tail in (False, True):
+        outs = []
+        for dyn in (False, True, True):
+            y = torch.full((B, H // 4, W // 4, 64), float("nan"), device="cuda")
+            a = S.ConvArgs(x=fd.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=net.w0_3.data_ptr(),
+                           bias=net.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K,
+                           Kpad=p1.Kpad, y=y.data_ptr(), ldy=64, dtype=S.VA_DTYPE_F32)
+            if tail:
+                a.w2, a.b2, a.c2, a.act2 = net.w["model.2.cv1"].w.data_ptr(), net.stem32_b2.data_ptr(), 64, 1
+            if dyn:
+                a.wcnt, a.ncnt = wcnt.data_ptr(), wcnt.numel()
+            _lib.check(lib.va_seg_stem_f32(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_stem_f32")
+            torch.cuda.synchronize()
+            outs.append(y)
+        assert torch.isfinite(outs[0]).all()
+        assert torch.equal(outs[1], outs[0]) and torch.equal(outs[2], outs[0]), tail
+        assert int(wcnt.abs().sum()) == 0
 
 
 def test_stem_f32_forward(monkeypatch):

@@ -1,12 +1,20 @@
 #!/bin/bash
-# same-box A/B of the headline: default vs the round-5 P2 forms off
+# Same-box A/B of the headline (bench.py, extras off): interleaved runs of the default and of each environment
+# setting given.   tools/ab_headline.sh <tag> <rounds> "VAR=V [VAR=V..]" ["VAR=V ..."] ...
 set -e -o pipefail
-OUT=gpurun_out/r05ab
-mkdir -p $OUT
+TAG=$1; ROUNDS=$2; shift 2
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
 B="python -u bench.py --steps 20 --extras none --cpu-sample 0 --no-prof --no-ingest"
-for r in 1 2; do
-  timeout -k 10 200 $B > $OUT/on_$r.json 2> $OUT/on_$r.err
-  VA_CONV3Q=0 VA_STEM_TAIL=0 timeout -k 10 200 $B > $OUT/off_$r.json 2> $OUT/off_$r.err
-  VA_CONV3Q=0 VA_STEM_TAIL=0 VA_STEM=0 timeout -k 10 200 $B > $OUT/nostem_$r.json 2> $OUT/nostem_$r.err
+for r in $(seq 1 "$ROUNDS"); do
+  timeout -k 10 200 $B > "$OUT/default_$r.json" 2> "$OUT/default_$r.err"
+  i=0
+  for e in "$@"; do
+    i=$((i + 1))
+    env $e timeout -k 10 200 $B > "$OUT/alt${i}_$r.json" 2> "$OUT/alt${i}_$r.err"
+  done
 done
-for f in $OUT/*.json; do echo "$f $(python -c "import json,sys;d=json.loads(open('$f').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'])")"; done
+i=0; for e in "$@"; do i=$((i + 1)); echo "alt$i = $e"; done
+for f in "$OUT"/*.json; do
+  echo "$f $(python -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'])")"
+done

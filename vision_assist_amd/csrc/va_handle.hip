@@ -47,7 +47,8 @@ void read_switches(VaSwitches& s) {
     s.conv3h = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
     e = getenv("VA_CONV3T");
     s.conv3t = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
-    s.conv3q = !env_off("VA_CONV3Q");
+    e = getenv("VA_CONV3Q");
+    s.conv3q = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "static") == 0 ? 2 : 1;
     s.splitk = !env_off("VA_SPLITK");
     s.patch = !env_off("VA_CONV_PATCH");
     e = getenv("VA_CONV4");

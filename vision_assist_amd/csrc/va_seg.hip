@@ -2628,6 +2628,23 @@ __global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restri
     }
 }
 
+// Work-queue schedule of the persistent kernels (conv3q, the f32 stem): tiles claimed from a counter of the plan
+// (va_conv_args.wcnt[0]) instead of fz::tile's static schedule, so that workgroups that start late (CUs held by a
+// kernel of another stream: the headline's two network streams overlap) take fewer tiles instead of stretching the
+// launch; the last workgroup out (wcnt[1]) zeroes both counters for the next launch of the plan (the split-K
+// counters' contract, va355.h).  Headline 4,951-4,969 (static) -> 5,018-5,045 frames/s with conv3q on it
+// (profiles/r05/workq/).
+__device__ __forceinline__ int wq_claim(int* cnt, int ntiles) {
+    const int v = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v < ntiles ? v : -1;
+}
+__device__ __forceinline__ void wq_release(int* cnt) {
+    if (__hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ----------------------------------------------------------------------------------------- f32 stem
 // The f32 stem as ONE launch: uint8 BGR frames -> model.0 Conv(3, 32, 3x3, s2) + SiLU (conv0_f32m's arithmetic: the
 // three exact bf16 weight terms x the exact frame bytes on the MFMA, the sum x 1/255 + bias, SiLU) -> model.1 Conv(32,
@@ -2659,18 +2676,41 @@ static_assert(S32_LDS <= 160 * 1024 && S32_NPC <= S32_NT, "LDS / patch chunks");
 constexpr int S32_TP = 400, S32_T = S32_LDS, S32_W1 = S32_T + 64 * S32_TP, S32_LDS_T = S32_W1 + 64 * S32_TP;
 static_assert(S32_LDS_T <= 160 * 1024, "LDS with the tail");
 
-template <bool TAIL>
+// DYN: the work-queue schedule (wq_claim; the tiles' frame patches are loaded two tiles ahead, so the claims run two
+// ahead too: tile j's index sits in LDS slot j % 3, written by thread 0 after the partial-sum barrier of the tile two
+// before it and read at the start of the tile before it)
+template <bool TAIL, bool DYN>
 __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                            const __bf16* __restrict__ w03, const float* __restrict__ b0,
                                                            const float* __restrict__ w1, int Kpad,
                                                            const float* __restrict__ b1, float* __restrict__ y, int ldy,
                                                            int tiles_x, int tiles_y, int ntiles,
-                                                           const float* __restrict__ wt, const float* __restrict__ bt) {
+                                                           const float* __restrict__ wt, const float* __restrict__ bt,
+                                                           int* __restrict__ wq) {
     extern __shared__ __align__(16) unsigned char s32[];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int Ho0 = (H + 1) / 2, Wo0 = (W + 1) / 2, Ho1 = (Ho0 + 1) / 2, Wo1 = (Wo0 + 1) / 2;
-    int t = fz::tile(ntiles, 0);
-    if (t < 0) return;
+    volatile int* slot = (volatile int*)(s32 + (TAIL ? S32_LDS_T : S32_LDS));
+    int t, nx;  // this tile, the next
+    if constexpr (DYN) {
+        if (tid == 0) {
+            slot[0] = wq_claim(wq, ntiles);
+            slot[1] = wq_claim(wq, ntiles);
+            slot[2] = wq_claim(wq, ntiles);
+        }
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(slot[0]);
+        nx = __builtin_amdgcn_readfirstlane(slot[1]);
+    } else {
+        t = fz::tile(ntiles, 0);
+        nx = fz::tile(ntiles, 1);
+    }
+    if (t < 0) {
+        if constexpr (DYN) {
+            if (tid == 0) wq_release(wq);
+        }
+        return;
+    }
     // the frame patch of tile tt: rows 4 oy0 - 3 .., bytes [12 ox0 - 16, 12 ox0 + 192) (16-byte aligned: W * 3 % 16 == 0)
     auto load_patch = [&](int tt) -> u32x4 {
         u32x4 v = {0u, 0u, 0u, 0u};
@@ -2686,7 +2726,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         if (tid < S32_NPC) *(u32x4*)(s32 + S32_PATCH + 16 * tid) = v;  // row r, chunk c at r * 208 + 16 c = 16 tid
     };
     store_patch(load_patch(t));
-    u32x4 pf1 = load_patch(fz::tile(ntiles, 1));  // the next two tiles' patches in flight
+    u32x4 pf1 = load_patch(nx);  // the next two tiles' patches in flight
 
     const int fr = lane & 15, fq = lane >> 4;
     // model.0 A fragments (conv0_f32m's permutation: fragment i, row r -> channel 8 (r / 4) + 4 i + r % 4, so lane
@@ -2734,8 +2774,9 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     for (int k = 1; t >= 0; ++k) {
         const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
         const int oy0 = ty * S32_TH, ox0 = tx * S32_TW;
-        const int tn = fz::tile(ntiles, k);
-        const u32x4 pf2 = load_patch(fz::tile(ntiles, k + 1));  // two tiles ahead
+        const int tn = nx;
+        const int tn2 = DYN ? __builtin_amdgcn_readfirstlane(slot[(k + 1) % 3]) : fz::tile(ntiles, k + 1);
+        const u32x4 pf2 = load_patch(tn2);  // two tiles ahead
 
         // ---- model.0 on the 9 x 33 region: group g = 16 region pixels (the last group ragged); region pixel q <->
         // model.0 (2 oy0 - 1 + q / 33, 2 ox0 - 1 + q % 33); its window starts at patch row 2 (q / 33), byte 6 (q % 33) + 7
@@ -2792,6 +2833,9 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         f32x16* part = (f32x16*)(s32 + S32_PART + (wid & 3) * 4096) + lane;
         if (kh) *part = a2;
         __syncthreads();
+        if constexpr (DYN) {
+            if (tid == 0) slot[(k + 2) % 3] = wq_claim(wq, ntiles);  // read after this tile's last barrier
+        }
         // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
         const int oy = oy0 + py, ox = ox0 + px;
         if constexpr (TAIL) {
@@ -2856,6 +2900,10 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         }
         pf1 = pf2;
         t = tn;
+        nx = tn2;
+    }
+    if constexpr (DYN) {
+        if (tid == 0) wq_release(wq);  // after this workgroup's last (failed) claim
     }
 }
 
@@ -3140,15 +3188,31 @@ constexpr int Q3_NT = 512, Q3_PS = 208;
 constexpr int Q3_NCH = Q3_HP * 8;                    // 16-byte input chunks (4 channels) per halo: 2592
 constexpr int Q3_LD = (Q3_NCH + Q3_NT - 1) / Q3_NT;  // per thread: 6
 constexpr int Q3_PART = Q3_HP * Q3_PS, Q3_LDS = Q3_PART + 4 * 2 * 64 * 64;  // planes 66 KiB + partial sums 32 KiB
-static_assert(Q3_LDS <= 160 * 1024, "one workgroup per CU");
+static_assert(Q3_LDS + 16 <= 160 * 1024, "one workgroup per CU");
 
+template <bool DYN>
 __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntiles) {
     extern __shared__ __align__(16) unsigned char q3[];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const float* __restrict__ x = (const float*)a.x;
     const int H = a.H, W = a.W, ldx = a.ldx;
-    int t = fz::tile(ntiles, 0);
-    if (t < 0) return;
+    // DYN: the claimed tiles, published by thread 0 in two alternating slots (iteration k writes slot k & 1, whose
+    // last readers read it before the barrier that ended iteration k - 1)
+    volatile int* slot = (volatile int*)(q3 + Q3_LDS);
+    int t;
+    if constexpr (DYN) {
+        if (tid == 0) slot[0] = wq_claim(a.wcnt, ntiles);
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(slot[0]);
+    } else {
+        t = fz::tile(ntiles, 0);
+    }
+    if (t < 0) {
+        if constexpr (DYN) {
+            if (tid == 0) wq_release(a.wcnt);
+        }
+        return;
+    }
     // the 18 x 18 input pixels of tile tt (zero outside the image: the conv's padding), 8 chunks of 4 channels each;
     // chunk c = 8 q + g <-> halo pixel q, channels 4 g .. 4 g + 3
     auto load_halo = [&](int tt, u32x4 (&v)[Q3_LD]) {
@@ -3188,9 +3252,17 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             const int c = tid + Q3_NT * i;
             if (c < Q3_NCH) cf32_put4(q3 + (c >> 3) * Q3_PS, c & 7, __builtin_bit_cast(f32x4, hv[i]));
         }
-        const int tn = fz::tile(ntiles, k);
-        load_halo(tn, hv);  // the next tile's halo, in flight during this tile's K-loop
-        __syncthreads();    // planes complete
+        int tn;
+        if constexpr (DYN) {
+            if (tid == 0) slot[k & 1] = wq_claim(a.wcnt, ntiles);
+            __syncthreads();  // planes complete; the next tile published
+            tn = __builtin_amdgcn_readfirstlane(slot[k & 1]);
+            load_halo(tn, hv);  // the next tile's halo, in flight during this tile's K-loop
+        } else {
+            tn = fz::tile(ntiles, k);
+            load_halo(tn, hv);
+            __syncthreads();  // planes complete
+        }
 
         f32x16 acc[2] = {(f32x16){}, (f32x16){}};
 #pragma unroll
@@ -3237,6 +3309,9 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             }
         }
         t = tn;
+    }
+    if constexpr (DYN) {
+        if (tid == 0) wq_release(a.wcnt);  // after this workgroup's last (failed) claim
     }
 }
 
@@ -3663,15 +3738,21 @@ bool use_conv3q(const va_conv_args& a) {
 hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3q_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, Q3_LDS) !=
-            hipSuccess)
+        if (hipFuncSetAttribute((const void*)conv3q_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Q3_LDS + 16) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv3q_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Q3_LDS + 16) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
     int tx, ty;
     const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
     if (nt <= 0 || cus <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(conv3q_kernel, dim3(nt < cus ? nt : cus), dim3(Q3_NT), Q3_LDS, st, a, tx, ty, nt);
+    const dim3 grid(nt < cus ? nt : cus);
+    if (a.wcnt && a.ncnt >= 2 && va_sw().conv3q != 2)  // a work counter of the plan: tiles claimed dynamically
+        hipLaunchKernelGGL(conv3q_kernel<true>, grid, dim3(Q3_NT), Q3_LDS + 16, st, a, tx, ty, nt);
+    else
+        hipLaunchKernelGGL(conv3q_kernel<false>, grid, dim3(Q3_NT), Q3_LDS + 16, st, a, tx, ty, nt);
     return hipGetLastError();
 }
 
@@ -4051,23 +4132,31 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a) {
     static DevFlag attr;
     if (cus <= 0) return VA_ERR_HIP;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)stem32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S32_LDS) != hipSuccess ||
-            hipFuncSetAttribute((const void*)stem32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                S32_LDS_T) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)stem32_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS + 16) != hipSuccess ||
+            hipFuncSetAttribute((const void*)stem32_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS + 16) != hipSuccess ||
+            hipFuncSetAttribute((const void*)stem32_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS_T + 16) != hipSuccess ||
+            hipFuncSetAttribute((const void*)stem32_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                S32_LDS_T + 16) != hipSuccess)
             return VA_ERR_HIP;
         attr() = true;
     }
     const int grid = (int)(nt < cus ? nt : cus);
+    const bool dyn = a->wcnt && a->ncnt >= 2 && va_sw().conv3q != 2;  // work-queue schedule (VA_CONV3Q=static: off)
+    const float* wt = tail ? (const float*)a->w2 : nullptr;
+    const float* bt = tail ? a->b2 + 64 : nullptr;
+    const size_t lds = (tail ? S32_LDS_T : S32_LDS) + 16;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(S32_NT), lds, (hipStream_t)stream, (const uint8_t*)a->x, a->N, a->H,
+                           a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w, a->Kpad, a->b2, (float*)a->y,
+                           a->ldy, tiles_x, tiles_y, (int)nt, wt, bt, a->wcnt);
+    };
     if (tail)
-        hipLaunchKernelGGL(stem32_kernel<true>, dim3(grid), dim3(S32_NT), S32_LDS_T, (hipStream_t)stream,
-                           (const uint8_t*)a->x, a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w,
-                           a->Kpad, a->b2, (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt, (const float*)a->w2,
-                           a->b2 + 64);
+        dyn ? go(stem32_kernel<true, true>) : go(stem32_kernel<true, false>);
     else
-        hipLaunchKernelGGL(stem32_kernel<false>, dim3(grid), dim3(S32_NT), S32_LDS, (hipStream_t)stream,
-                           (const uint8_t*)a->x, a->N, a->H, a->W, (const __bf16*)a->w3, a->bias, (const float*)a->w,
-                           a->Kpad, a->b2, (float*)a->y, a->ldy, tiles_x, tiles_y, (int)nt, nullptr, nullptr);
+        dyn ? go(stem32_kernel<false, true>) : go(stem32_kernel<false, false>);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 

@@ -681,9 +681,9 @@ class SegNet:
                          "bytes": B * H * W * 3 + 2 * B * h2 * w2 * 64})
         elif self.stem32 and (W * 3) % 16 == 0:
             p1 = self.w["model.1"]
-            sa = ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=self.w0_3.data_ptr(),
-                          bias=self.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad, K=p1.K,
-                          Kpad=p1.Kpad, dtype=VA_DTYPE_F32)
+            sa = with_ws(ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, Cout=64, w3=self.w0_3.data_ptr(),
+                                  bias=self.w0[1].data_ptr(), w=p1.w.data_ptr(), b2=p1.b.data_ptr(), Npad=p1.Npad,
+                                  K=p1.K, Kpad=p1.Kpad, dtype=VA_DTYPE_F32))  # wcnt: the work-queue schedule
             macs = 27 * 32 * 4 + 288 * 64  # per model.1 output pixel: 4 model.0 pixels + model.1
             name = "model.0+model.1 (fused f32 stem)"
             if self.stem32_b2 is not None:  # + model.2.cv1: the stem writes cv1's output into model.2's concat buffer
