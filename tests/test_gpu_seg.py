@@ -962,6 +962,24 @@ def test_conv3q_dynamic_schedule(switch):
     assert torch.equal(st2, static)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+def test_work_queue_forward_bit_identical(dtype, switch):
+    """The persistent kernels' work-queue schedule (the plan's counter: the bf16 stem and C2f, the f32 stem + cv1 tail
+    and conv3q) against their static schedule (VA_CONV3Q=static): the whole forward bit-identical, run twice (the
+    counters are zeroed by each launch's last workgroup)."""
+    arch, fw, net = _net(dtype, "s", seed=5)
+    frames = _frames(3, seed=37)
+    names = [m["name"] for m in net.plan(3, 640, 640)["meta"]]
+    assert any("fused" in n and "stem" in n for n in names)
+    switch("VA_CONV3Q", "static")
+    ref = _gpu_heads(net, frames)
+    switch("VA_CONV3Q", None)
+    for _ in range(2):
+        got = _gpu_heads(net, frames)
+        for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+            assert torch.equal(g, r), f"{name}: work queue vs static max diff {(g - r).abs().max().item()}"
+
+
 def test_conv3q_f32_forward(switch):
     """The f32 forward with model.2's bottleneck convs on conv3q (B = 3: 300 tiles of the 160 x 160 map) against the
     same forward with them on conv2 (VA_CONV3Q=0): f32-rounding close, and within the f32 bar of torch."""

@@ -33,6 +33,7 @@
 #include "../../include/va355.h"
 #include "va_dev.h"
 #include "va_fuse.h"
+#include "va_switch.h"
 
 namespace {
 
@@ -71,7 +72,7 @@ struct CfCfg {
     static constexpr int SINK = BIAS + 192 * 4;
     static constexpr int LDS = SINK + 64 * 16;
     static_assert(TH % NW == 0 && (TH * CF_T) % 16 == 0, "rows per wave");
-    static_assert(LDS * WPC <= 160 * 1024, "LDS per CU");
+    static_assert((LDS + 16) * WPC <= 160 * 1024, "LDS per CU (+ the work-queue slots)");
 };
 
 // 16-byte chunk c (0..3) of pixel p: pixels padded to 96 bytes, so a 3x3 tap is a constant offset
@@ -83,6 +84,7 @@ __device__ __forceinline__ int cf_addr(int p, int c) { return p * CF_PS + 16 * c
 struct CfGeom {
     int N, H, W, ldx, ldy, tx, tpf, ntiles;
     unsigned long long* trace;  // debug (va_c2f_trace): [grid][NW waves][CF_TR_TILES][CF_TR_PTS] clocks, or null
+    int* wq;                    // the plan's work counter (va_fuse.h fz::wq_claim), or null: fz::tile's static schedule
 };
 constexpr int CF_TR_TILES = 32, CF_TR_PTS = 6;
 
@@ -118,8 +120,25 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
     const float* b3 = b1 + 96;                              // m.0.cv2 [32]
     const float* b4 = b1 + 128;                             // cv2 [64]
 
-    int t = fz::tile(g.ntiles, 0);
-    if (t < 0) return;
+    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 before the stage-2 barrier of tile j - 1
+    volatile int* slot = (volatile int*)(cf_smem + C::LDS);
+    int t, nx;  // this tile, the next
+    if (g.wq) {
+        if (tid == 0) {
+            slot[0] = fz::wq_claim(g.wq, g.ntiles);
+            slot[1] = fz::wq_claim(g.wq, g.ntiles);
+        }
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(slot[0]);
+        nx = __builtin_amdgcn_readfirstlane(slot[1]);
+    } else {
+        t = fz::tile(g.ntiles, 0);
+        nx = fz::tile(g.ntiles, 1);
+    }
+    if (t < 0) {
+        if (g.wq && tid == 0) fz::wq_release(g.wq);
+        return;
+    }
     // weights and biases -> LDS (once per workgroup); with WREG the 1x1 weights -> registers
     {
         constexpr int nv = (C::WREG ? 36 : 48) * CF_FRAG / 8;
@@ -246,7 +265,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
             }
         }
         mark(k, 1);
-        const int tn = fz::tile(g.ntiles, k);
+        const int tn = nx;
         if (tn >= 0) load_tile(tn);  // lands during stages 2-4
         __syncthreads();
         mark(k, 2);
@@ -315,8 +334,10 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
         else
             stage2(std::integral_constant<int, NG2 - 1>{});
         mark(k, 3);
+        if (g.wq && tid == 0) slot[(k + 1) & 1] = fz::wq_claim(g.wq, g.ntiles);
         __syncthreads();
         mark(k, 4);
+        nx = g.wq ? __builtin_amdgcn_readfirstlane(slot[(k + 1) & 1]) : fz::tile(g.ntiles, k + 1);
 
         // ---- stage 3: m.0.cv2 (+ b) on the wave's centre rows; stage 4: cv2 -> HBM
         {
@@ -387,6 +408,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
         mark(k, 5);
         t = tn;
     }
+    if (g.wq && tid == 0) fz::wq_release(g.wq);  // after this workgroup's last (failed) claim
 }
 
 // the configuration: 8 x 16 tiles, 4 waves, two workgroups per CU (their phases drift apart, so one's SiLU
@@ -401,7 +423,7 @@ template <class C>
 hipError_t cf_launch(const va_conv_args* a, CfGeom g, int cus, hipStream_t st) {
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)c2f_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) !=
+        if (hipFuncSetAttribute((const void*)c2f_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS + 16) !=
             hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -413,7 +435,7 @@ hipError_t cf_launch(const va_conv_args* a, CfGeom g, int cus, hipStream_t st) {
     g.ntiles = (int)nt;
     int grid = C::WPC * (cus > 0 ? cus : 256);
     if (grid > g.ntiles) grid = g.ntiles;
-    hipLaunchKernelGGL(c2f_kernel<C>, dim3(grid), dim3(C::NW * 64), C::LDS, st, (const __bf16*)a->x,
+    hipLaunchKernelGGL(c2f_kernel<C>, dim3(grid), dim3(C::NW * 64), C::LDS + 16, st, (const __bf16*)a->x,
                        (const __bf16*)a->w, a->bias, (__bf16*)a->y, g);
     return hipGetLastError();
 }
@@ -440,6 +462,7 @@ extern "C" int va_seg_c2f(void* stream, const va_conv_args* a) {
     g.W = a->W;
     g.ldx = a->ldx;
     g.ldy = a->ldy;
+    g.wq = a->wcnt && a->ncnt >= 2 && va_sw().conv3q != 2 ? a->wcnt : nullptr;
     hipStream_t st = (hipStream_t)stream;
     const hipError_t rc = cf_launch<CfC>(a, g, g_cus, st);
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;

@@ -78,4 +78,17 @@ __device__ __forceinline__ int tile(int ntiles, int k) {
     return (t < ntiles && t < (x + 1) * run) ? t : -1;
 }
 
+// the work-queue schedule of the persistent kernels (va_seg.hip conv3q / stem32, va_stem.hip, va_c2f.hip): the next
+// tile from a counter of the plan (va_conv_args.wcnt[0]), or -1; the last workgroup out (counter [1]) zeroes both
+__device__ __forceinline__ int wq_claim(int* cnt, int ntiles) {
+    const int v = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v < ntiles ? v : -1;
+}
+__device__ __forceinline__ void wq_release(int* cnt) {
+    if (__hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace fz

@@ -2634,16 +2634,6 @@ __global__ __launch_bounds__(256) void conv0_f32m_kernel(const uint8_t* __restri
 // launch; the last workgroup out (wcnt[1]) zeroes both counters for the next launch of the plan (the split-K
 // counters' contract, va355.h).  Headline 4,951-4,969 (static) -> 5,018-5,045 frames/s with conv3q on it
 // (profiles/r05/workq/).
-__device__ __forceinline__ int wq_claim(int* cnt, int ntiles) {
-    const int v = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v < ntiles ? v : -1;
-}
-__device__ __forceinline__ void wq_release(int* cnt) {
-    if (__hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
 
 // ----------------------------------------------------------------------------------------- f32 stem
 // The f32 stem as ONE launch: uint8 BGR frames -> model.0 Conv(3, 32, 3x3, s2) + SiLU (conv0_f32m's arithmetic: the
@@ -2694,9 +2684,9 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     int t, nx;  // this tile, the next
     if constexpr (DYN) {
         if (tid == 0) {
-            slot[0] = wq_claim(wq, ntiles);
-            slot[1] = wq_claim(wq, ntiles);
-            slot[2] = wq_claim(wq, ntiles);
+            slot[0] = fz::wq_claim(wq, ntiles);
+            slot[1] = fz::wq_claim(wq, ntiles);
+            slot[2] = fz::wq_claim(wq, ntiles);
         }
         __syncthreads();
         t = __builtin_amdgcn_readfirstlane(slot[0]);
@@ -2707,7 +2697,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     }
     if (t < 0) {
         if constexpr (DYN) {
-            if (tid == 0) wq_release(wq);
+            if (tid == 0) fz::wq_release(wq);
         }
         return;
     }
@@ -2834,7 +2824,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         if (kh) *part = a2;
         __syncthreads();
         if constexpr (DYN) {
-            if (tid == 0) slot[(k + 2) % 3] = wq_claim(wq, ntiles);  // read after this tile's last barrier
+            if (tid == 0) slot[(k + 2) % 3] = fz::wq_claim(wq, ntiles);  // read after this tile's last barrier
         }
         // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
         const int oy = oy0 + py, ox = ox0 + px;
@@ -2903,7 +2893,7 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         nx = tn2;
     }
     if constexpr (DYN) {
-        if (tid == 0) wq_release(wq);  // after this workgroup's last (failed) claim
+        if (tid == 0) fz::wq_release(wq);  // after this workgroup's last (failed) claim
     }
 }
 
@@ -3201,7 +3191,7 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
     volatile int* slot = (volatile int*)(q3 + Q3_LDS);
     int t;
     if constexpr (DYN) {
-        if (tid == 0) slot[0] = wq_claim(a.wcnt, ntiles);
+        if (tid == 0) slot[0] = fz::wq_claim(a.wcnt, ntiles);
         __syncthreads();
         t = __builtin_amdgcn_readfirstlane(slot[0]);
     } else {
@@ -3209,7 +3199,7 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
     }
     if (t < 0) {
         if constexpr (DYN) {
-            if (tid == 0) wq_release(a.wcnt);
+            if (tid == 0) fz::wq_release(a.wcnt);
         }
         return;
     }
@@ -3254,7 +3244,7 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
         }
         int tn;
         if constexpr (DYN) {
-            if (tid == 0) slot[k & 1] = wq_claim(a.wcnt, ntiles);
+            if (tid == 0) slot[k & 1] = fz::wq_claim(a.wcnt, ntiles);
             __syncthreads();  // planes complete; the next tile published
             tn = __builtin_amdgcn_readfirstlane(slot[k & 1]);
             load_halo(tn, hv);  // the next tile's halo, in flight during this tile's K-loop
@@ -3311,7 +3301,7 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
         t = tn;
     }
     if constexpr (DYN) {
-        if (tid == 0) wq_release(a.wcnt);  // after this workgroup's last (failed) claim
+        if (tid == 0) fz::wq_release(a.wcnt);  // after this workgroup's last (failed) claim
     }
 }
 

@@ -27,6 +27,7 @@
 #include "../../include/va355.h"
 #include "va_dev.h"
 #include "va_fuse.h"
+#include "va_switch.h"
 
 namespace {
 
@@ -50,7 +51,7 @@ constexpr int ST_NG0 = (ST_G0 + ST_NW - 1) / ST_NW;
 constexpr int ST_ME = 0, ST_MO = ST_ME + ST_M * ST_EW * ST_PS, ST_P16 = ST_MO + ST_M * ST_OW * ST_PS;
 constexpr int ST_W1 = ST_P16 + ST_RR * ST_PW * 8, ST_BIAS = ST_W1 + 36 * 1024, ST_SINK = ST_BIAS + 96 * 4;
 constexpr int ST_LDS = ST_SINK + 64 * 16;
-static_assert(ST_LDS <= 160 * 1024, "LDS");
+static_assert(ST_LDS + 16 <= 160 * 1024, "LDS (+ the work-queue slots)");
 // weight blob (bf16, MFMA A-fragment order): W0 model.0 [2 channel groups][2 K-steps] (k = tap * 4 + c, c =
 // R, G, B, 0: 36 of 64; held in registers), W1 model.1 [9 taps][4 groups] (in LDS)
 constexpr int ST_FW0 = 0, ST_FW1 = 4 * fz::FRAG, ST_WBLOB = ST_FW1 + 36 * fz::FRAG;
@@ -62,6 +63,7 @@ __device__ __forceinline__ int st_addr(int p, int c) { return p * ST_PS + 16 * (
 struct StGeom {
     int N, H, W, Ho, Wo, Ho1, Wo1, ldy, tx, tpf, ntiles;
     unsigned long long* trace;  // debug (va_stem_trace): [grid][8 waves][32 tiles][5] real-time stamps, or null
+    int* wq;                    // the plan's work counter (va_fuse.h fz::wq_claim), or null: fz::tile's static schedule
 };
 
 __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __restrict__ frames,
@@ -73,8 +75,25 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
     const float* b0 = (const float*)(st_smem + ST_BIAS);  // model.0 [32]
     const float* b1 = b0 + 32;                              // model.1 [64]
 
-    int t = fz::tile(g.ntiles, 0);
-    if (t < 0) return;
+    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 before the last barrier of tile j - 2
+    volatile int* slot = (volatile int*)(st_smem + ST_LDS);
+    int t, nx;  // this tile, the next
+    if (g.wq) {
+        if (tid == 0) {
+            slot[0] = fz::wq_claim(g.wq, g.ntiles);
+            slot[1] = fz::wq_claim(g.wq, g.ntiles);
+        }
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(slot[0]);
+        nx = __builtin_amdgcn_readfirstlane(slot[1]);
+    } else {
+        t = fz::tile(g.ntiles, 0);
+        nx = fz::tile(g.ntiles, 1);
+    }
+    if (t < 0) {
+        if (g.wq && tid == 0) fz::wq_release(g.wq);
+        return;
+    }
     if (tid < 24) *(float4*)(st_smem + ST_BIAS + 16 * tid) = *(const float4*)(bias + 4 * tid);
     for (int i = tid; i < 36 * fz::FRAG / 8; i += ST_NW * 64)
         *(u32x4*)(st_smem + ST_W1 + 16 * i) = *(const u32x4*)(wf + ST_FW1 + 8 * i);
@@ -135,7 +154,7 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
         mark(k, 0);
         const int lane = fz::lane_id(), fr = lane & 15, fq = lane >> 4;
         const int n = t / g.tpf, rr = t % g.tpf, oy1 = (rr / g.tx) * ST_T, ox1 = (rr % g.tx) * ST_T;
-        const int tn = fz::tile(g.ntiles, k);
+        const int tn = nx;
         if (tn >= 0) load_span(tn);  // lands during this tile; converted into P16 after model.1
 
         // ---- model.0 on the 33 x 33 region (M0 row mr <-> model.0 row 2 oy1 - 1 + mr, column j likewise)
@@ -238,10 +257,13 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
         }
         mark(k, 3);
         if (tn >= 0) store_span();
+        if (g.wq && tid == 0) slot[(k + 1) & 1] = fz::wq_claim(g.wq, g.ntiles);
         __syncthreads();
         mark(k, 4);
+        nx = g.wq ? __builtin_amdgcn_readfirstlane(slot[(k + 1) & 1]) : fz::tile(g.ntiles, k + 1);
         t = tn;
     }
+    if (g.wq && tid == 0) fz::wq_release(g.wq);  // after this workgroup's last (failed) claim
 }
 
 int g_cus = 0;
@@ -269,6 +291,7 @@ extern "C" int va_seg_stem(void* stream, const va_conv_args* a) {
     g.Wo1 = (g.Wo + 1) / 2;
     g.ldy = a->ldy;
     g.trace = g_trace;
+    g.wq = a->wcnt && a->ncnt >= 2 && va_sw().conv3q != 2 ? a->wcnt : nullptr;
     // per-frame buffer descriptors: a frame's bytes (and the OOB sentinel above them) must fit 31 bits
     if ((int64_t)a->H * a->W * 3 >= 0x80000000LL || (int64_t)g.Ho1 * g.Wo1 * g.ldy * 2 >= 0x80000000LL)
         return VA_ERR_ARG;
@@ -282,14 +305,14 @@ extern "C" int va_seg_stem(void* stream, const va_conv_args* a) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ST_LDS) !=
+            hipFuncSetAttribute((const void*)stem_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ST_LDS + 16) !=
                 hipSuccess)
             return VA_ERR_HIP;
         ready() = true;
     }
     int grid = g_cus;
     if (grid > g.ntiles) grid = g.ntiles;
-    hipLaunchKernelGGL(stem_kernel, dim3(grid), dim3(ST_NW * 64), ST_LDS, (hipStream_t)stream,
+    hipLaunchKernelGGL(stem_kernel, dim3(grid), dim3(ST_NW * 64), ST_LDS + 16, (hipStream_t)stream,
                        (const uint8_t*)a->x, (const __bf16*)a->w, a->bias, (__bf16*)a->y, g);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }

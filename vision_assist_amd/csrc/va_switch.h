@@ -11,8 +11,8 @@ struct VaSwitches {
     int conv3t;      // VA_CONV3T: 0 = the wide f32 layers on conv2's three-term form; conv3t's A stage: 1 = the
                      // pre-split planes ("planes"), 2 = f32, split in registers ("af")
     int conv3q;      // VA_CONV3Q=0: the 32 -> 32 stride-1 3x3 f32 layers on conv2's three-term form instead of conv3q;
-                     // 2 = "static": conv3q and the f32 stem on fz::tile's static schedule instead of the plan's
-                     // work counter (va_seg.hip wq_claim)
+                     // 2 = "static": the persistent kernels (conv3q, the f32 and bf16 stems, the bf16 C2f) on
+                     // fz::tile's static schedule instead of the plan's work counter (va_fuse.h fz::wq_claim)
     bool splitk;     // VA_SPLITK=0: no split-K for launches of few tiles
     bool patch;      // VA_CONV_PATCH=0: the narrow bf16 3x3 layers on conv_dn instead of the patch kernel
     int conv4_min;   // VA_CONV4: 0 = conv4 off (-1 here), "all" = every eligible layer (1), default 256 tiles

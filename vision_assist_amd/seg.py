@@ -566,9 +566,9 @@ class SegNet:
                 return
             if pre is None and i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
-                ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld, w=blob.data_ptr(),
-                                                             bias=bias.data_ptr(), Cout=64, y=dst.ptr, ldy=dst.ld,
-                                                             dtype=self.va_dtype)))
+                ops.append(SegOp(kind=VA_OP_C2F, a=with_ws(ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
+                                                                     w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                                                                     y=dst.ptr, ldy=dst.ld, dtype=self.va_dtype))))
                 macs = 64 * 64 + 2 * 32 * 288 + 64 * 96  # per pixel, the four convs
                 meta.append({"name": f"model.{i} (fused C2f)", "kind": "conv", "M": B * h * w, "N": 64,
                              "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
@@ -672,9 +672,9 @@ class SegNet:
         if self.stem is not None and W % 16 == 0:
             a1 = new(h2, w2, a.c2)
             blob, bias = self.stem
-            ops.append(SegOp(kind=VA_OP_STEM, a=ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32, w=blob.data_ptr(),
-                                                          bias=bias.data_ptr(), Cout=64, y=a1.ptr, ldy=a1.ld,
-                                                          dtype=self.va_dtype)))
+            ops.append(SegOp(kind=VA_OP_STEM, a=with_ws(ConvArgs(x=frames.data_ptr(), N=B, H=H, W=W, Cin=32,
+                                                                  w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
+                                                                  y=a1.ptr, ldy=a1.ld, dtype=self.va_dtype))))
             macs = 27 * 32 * 4 + 288 * 64  # per model.1 output pixel: 4 model.0 pixels + model.1
             meta.append({"name": "model.0+model.1 (fused stem)", "kind": "conv", "M": B * h2 * w2, "N": 64,
                          "K": macs // 64, "k": 3, "stride": 2, "flops": 2 * B * h2 * w2 * macs,
