@@ -244,7 +244,10 @@ typedef struct va_conv_args {
      * epilogue -- same operands, same per-split f32 accumulation, then one f32 sum of the partials.  The
      * dispatcher only splits when tiles * splits * 64 KiB <= ws_bytes and tiles <= ncnt.  wcnt must be zero
      * before the first call; every split launch leaves it zero again.  A plan's ops run in order on one
-     * stream, so one workspace serves them all; two streams need two. */
+     * stream, so one workspace serves them all; two streams need two.  The persistent kernels (the f32 32-channel
+     * 3x3 conv3q, va_seg_stem / va_seg_stem_f32, va_seg_c2f) use wcnt[0..1] (ncnt >= 2) as a work counter when it
+     * is given: tiles claimed as workgroups start, not a static schedule, and both counters zero again when the
+     * launch ends (VA_CONV3Q=static: the static schedule). */
     void* ws;
     int64_t ws_bytes;
     int32_t* wcnt;
@@ -285,7 +288,10 @@ int va_seg_c2f_f32(void* stream, const va_conv_args* a);
  *   a.w3   model.0's K-padded weights as three exact bf16 terms [32][4][3][8] (va_seg_conv0_f32m's w3)
  *   a.bias model.0's bias float [32]
  *   a.w    model.1's packed f32 weights [Npad][Kpad], K = Kpad = 288 ordered (ky, kx, ci)
- *   a.b2   model.1's bias float [64] */
+ *   a.b2   model.1's bias float [64]
+ * Optional tail (a.w2 != NULL): model.2.cv1, the C2f's 1x1 Conv(64, 64) + SiLU, in the epilogue -- model.1's map
+ * stays on the chip too and a.y receives cv1's output: a.w2 = its f32 weights [>= 64][64], a.b2 = [model.1 bias 64 |
+ * cv1 bias 64], a.c2 = 64, a.act2 = 1.  Replaces the model.2.cv1 va_seg_conv as well. */
 int va_seg_stem_f32(void* stream, const va_conv_args* a);
 /* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
  * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
