@@ -385,11 +385,14 @@ def test_conv3h_op(monkeypatch, cin, cout, H, W, B, residual, switch):
     (64, 64, 64, False, 40, 40, 2),    # the box branch: narrow main conv (64-channel tile), 64 float outputs
     (128, 128, 80, False, 23, 21, 3),  # the cls branch: 80 outputs (a ragged third 32-row block), image seams
     (128, 128, 32, True, 20, 20, 3),   # proto.cv3's shape: 32 outputs with SiLU
+    (32, 32, 32, False, 80, 80, 3),    # the cv4 branch (cv4.l.1 -> cv4.l.2) on conv3q's tail form
+    (32, 32, 20, True, 37, 45, 5),     # conv3q's tail: ragged tiles, fewer outputs, SiLU
 ])
 def test_conv3h_fused_tail_op(cin, cout, c2, act2, H, W, B):
-    """The f32 fused 1x1 tail (va_seg.hip conv_tail32): a stride-1 3x3 conv on conv3h whose whole channel set is one
-    tile, + bias + SiLU, contracted in the epilogue with the tail's pre-split weights (six exact term products per
-    f32 product) + b2 (+ SiLU): within f32 rounding of torch fp32 of the two layers in sequence."""
+    """The f32 fused 1x1 tail (va_seg.hip conv_tail32; 32-channel main convs: conv3q's TAIL form): a stride-1 3x3
+    conv whose whole channel set is one tile, + bias + SiLU, contracted in the epilogue with the tail's pre-split
+    weights (six exact term products per f32 product) + b2 (+ SiLU): within f32 rounding of torch fp32 of the two
+    layers in sequence."""
     import ctypes
 
     from vision_assist_amd import _lib
@@ -415,7 +418,8 @@ def test_conv3h_fused_tail_op(cin, cout, c2, act2, H, W, B):
     args = S.ConvArgs(x=xin.data_ptr(), N=B, H=H, W=W, Cin=p.cin, ldx=ld_in, kh=3, kw=3, stride=1, pad=1, Ho=H,
                       Wo=W, w=p.w.data_ptr(), bias=p.b.data_ptr(), Cout=cout, Npad=p.Npad, K=p.K, Kpad=p.Kpad,
                       y=y.data_ptr() + 4 * 4, ldy=ld_out, act=1, mode=0, M=B * H * W, dtype=S.VA_DTYPE_F32,
-                      w3=p.w3.data_ptr(), w2=planes.data_ptr(), b2=p2.b.data_ptr(), c2=c2, act2=1 if act2 else 0)
+                      w3=p.w3.data_ptr() if p.w3 is not None else None, w2=planes.data_ptr(), b2=p2.b.data_ptr(),
+                      c2=c2, act2=1 if act2 else 0)
     _lib.check(net.lib.va_seg_conv(_lib.stream_ptr(), ctypes.byref(args)), "va_seg_conv")
     torch.cuda.synchronize()
     got = y[..., 4:4 + c2].cpu().permute(0, 3, 1, 2)
@@ -425,6 +429,23 @@ def test_conv3h_fused_tail_op(cin, cout, c2, act2, H, W, B):
         ref = F.silu(ref)
     scale = max(1.0, ref.abs().max().item())
     assert (got.double() - ref).abs().max().item() <= 2e-5 * scale, (got.double() - ref).abs().max().item()
+
+
+def test_conv3q_tail_forward(monkeypatch):
+    """B = 12: the head's cv4.0.1 -> cv4.0.2 fused on conv3q (300 tiles of the 80 x 80 map); heads against the same
+    forward with the tails unfused (VA_FUSE_TAIL=0): f32-rounding close."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(12, seed=43)
+    names = [m["name"] for m in net.plan(12, 640, 640)["meta"]]
+    assert "model.22.cv4.0.1+model.22.cv4.0.2" in names and "model.22.cv4.1.1" in names  # level 1: 75 tiles
+    got = _gpu_heads(net, frames)
+    monkeypatch.setenv("VA_FUSE_TAIL", "0")
+    net._plans.clear()
+    assert "model.22.cv4.0.2" in [m["name"] for m in net.plan(12, 640, 640)["meta"]]
+    ref = _gpu_heads(net, frames)
+    for name, g, r in zip(("box", "cls", "coef", "proto"), got, ref):
+        d = (g - r).abs().max().item()
+        assert d <= 1e-4 * max(1.0, r.abs().max().item()), f"{name}: fused vs unfused max diff {d}"
 
 
 def test_fused_tails_f32_forward(monkeypatch):

@@ -3178,9 +3178,15 @@ constexpr int Q3_NT = 512, Q3_PS = 208;
 constexpr int Q3_NCH = Q3_HP * 8;                    // 16-byte input chunks (4 channels) per halo: 2592
 constexpr int Q3_LD = (Q3_NCH + Q3_NT - 1) / Q3_NT;  // per thread: 6
 constexpr int Q3_PART = Q3_HP * Q3_PS, Q3_LDS = Q3_PART + 4 * 2 * 64 * 64;  // planes 66 KiB + partial sums 32 KiB
-static_assert(Q3_LDS + 16 <= 160 * 1024, "one workgroup per CU");
+// TAIL: a fused 1x1 tail (the head's cv4.l.2, 32 -> c2 <= 32, after cv4.l.1: va_conv_args.w2 as conv3h's tail
+// planes [32][4][3][8]) in the epilogue; its weights re-laid in LDS once per workgroup so that lane (r, g) reads, for
+// tail K-step s, the 8 channels 16 s + 4 g + (0..3) and 16 s + 8 + 4 g + (0..3) -- exactly the 8 channels of the
+// main conv's accumulator registers j = 2 s, 2 s + 1 of lane (pixel, g): the B operand is the lane's own split
+// activations, no exchange between lanes
+constexpr int Q3_W2 = Q3_LDS + 16, Q3_LDS_T = Q3_W2 + 32 * 2 * 3 * 32;
+static_assert(Q3_LDS_T <= 160 * 1024, "one workgroup per CU");
 
-template <bool DYN>
+template <bool DYN, bool TAIL = false>
 __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntiles) {
     extern __shared__ __align__(16) unsigned char q3[];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -3234,6 +3240,14 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
 #pragma unroll
         for (int i = 0; i < 9; ++i) split3_bf16(*(const u32x4*)(wr + 16 * i), *(const u32x4*)(wr + 16 * i + 4), apr[i]);
     }
+    if constexpr (TAIL) {  // piece (row r, K-step s, plane p, half g): two 8-byte runs of the host planes
+        if (tid < 32 * 2 * 3 * 2) {
+            const int g = tid & 1, p = (tid >> 1) % 3, s = (tid / 6) & 1, r = tid / 12;
+            const unsigned char* src = (const unsigned char*)a.w2 + ((r * 4 + 2 * s) * 3 + p) * 16 + 8 * g;
+            const uint2 lo = *(const uint2*)src, hi = *(const uint2*)(src + 48);  // group 2 s, group 2 s + 1
+            *(u32x4*)(q3 + Q3_W2 + ((r * 2 + s) * 3 + p) * 32 + 16 * g) = (u32x4){lo.x, lo.y, hi.x, hi.y};
+        }
+    }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
     for (int k = 1; t >= 0; ++k) {
         const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
@@ -3285,16 +3299,50 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             for (int b = 0; b < 2; ++b) {
                 const f32x16 s = acc[b] + part[64 * b];
                 const int oy = ty * Q3_T + 4 * pb + 2 * b + (r32 >> 4), ox = tx * Q3_T + (r32 & 15);
-                if (oy >= H || ox >= W) continue;
+                const bool inside = oy < H && ox < W;
+                // (the tail's MFMAs take every lane's operands -- its A rows from lanes of pixels outside the map
+                // too -- so only its stores are predicated)
+                if (!TAIL && !inside) continue;
                 const int64_t pix = ((int64_t)n * H + oy) * W + ox;
                 float* yp = (float*)a.y + pix * a.ldy + 4 * g32;
+                if constexpr (TAIL) {
+                    f32x4 v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float4 bv = *(const float4*)(a.bias + 8 * j + 4 * g32);
-                    f32x4 v = {s[4 * j] + bv.x, s[4 * j + 1] + bv.y, s[4 * j + 2] + bv.z, s[4 * j + 3] + bv.w};
-                    if (a.act) v = fz::act(v);
-                    if (a.res) v = v + *(const f32x4*)((const float*)a.res + pix * a.ldr + 4 * g32 + 8 * j);
-                    *(f32x4*)(yp + 8 * j) = v;
+                    for (int j = 0; j < 4; ++j) {
+                        const float4 bv = *(const float4*)(a.bias + 8 * j + 4 * g32);
+                        v[j] = (f32x4){s[4 * j] + bv.x, s[4 * j + 1] + bv.y, s[4 * j + 2] + bv.z, s[4 * j + 3] + bv.w};
+                        if (a.act) v[j] = fz::act(v[j]);
+                    }
+                    f32x16 o = (f32x16){};
+#pragma unroll
+                    for (int st = 0; st < 2; ++st) {
+                        bf16x8 bq[3], aq[3];
+                        split3_bf16(__builtin_bit_cast(u32x4, v[2 * st]), __builtin_bit_cast(u32x4, v[2 * st + 1]), bq);
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            aq[p] = *(const bf16x8*)(q3 + Q3_W2 + ((r32 * 2 + st) * 3 + p) * 32 + 16 * g32);
+#pragma unroll
+                        for (int u = 0; u < 6; ++u)
+                            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[TA[u]], bq[TB[u]], o, 0, 0, 0);
+                    }
+                    // lane (r32, g32) holds tail channels 8 j + 4 g32 + (0..3) of its pixel
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (!inside || 8 * j + 4 * g32 >= a.c2) continue;
+                        const float4 bv = *(const float4*)(a.b2 + 8 * j + 4 * g32);
+                        f32x4 w = {o[4 * j] + bv.x, o[4 * j + 1] + bv.y, o[4 * j + 2] + bv.z, o[4 * j + 3] + bv.w};
+                        if (a.act2) w = fz::act(w);
+                        *(f32x4*)(yp + 8 * j) = w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float4 bv = *(const float4*)(a.bias + 8 * j + 4 * g32);
+                        f32x4 v = {s[4 * j] + bv.x, s[4 * j + 1] + bv.y, s[4 * j + 2] + bv.z, s[4 * j + 3] + bv.w};
+                        if (a.act) v = fz::act(v);
+                        if (a.res) v = v + *(const f32x4*)((const float*)a.res + pix * a.ldr + 4 * g32 + 8 * j);
+                        *(f32x4*)(yp + 8 * j) = v;
+                    }
                 }
             }
         }
@@ -3715,23 +3763,35 @@ int device_cus() {
     }
     return n_cu();
 }
+bool conv3q_shape_ok(const va_conv_args& a) {
+    return a.mode == 0 && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.H == a.Ho && a.W == a.Wo &&
+           a.Cin == 32 && a.Cout == 32 && a.K == 288 && a.Kpad == 288 && !a.xu && a.ldx % 4 == 0 && a.ldy % 4 == 0 &&
+           ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.y & 15) == 0 && ((uintptr_t)a.w & 15) == 0 &&
+           ((uintptr_t)a.bias & 15) == 0 && (!a.res || (a.ldr % 4 == 0 && ((uintptr_t)a.res & 15) == 0));
+}
 bool use_conv3q(const va_conv_args& a) {
-    if (!va_sw().conv3q || a.mode != 0 || a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.H != a.Ho ||
-        a.W != a.Wo || a.Cin != 32 || a.Cout != 32 || a.K != 288 || a.Kpad != 288 || a.w2 || a.xu || a.ldx % 4 ||
-        a.ldy % 4 || ((uintptr_t)a.x & 15) || ((uintptr_t)a.y & 15) || ((uintptr_t)a.w & 15) ||
-        ((uintptr_t)a.bias & 15) || (a.res && (a.ldr % 4 || ((uintptr_t)a.res & 15))))
-        return false;
+    if (!va_sw().conv3q || a.w2 || !conv3q_shape_ok(a)) return false;
     int tx, ty;
     const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
     return cus > 0 && nt >= cus;
 }
+// f32 fused 1x1 tail on a 32-channel 3x3 (the head's cv4.l.1 -> cv4.l.2): conv3q's TAIL form, whatever VA_CONV3Q
+// says or the tile count (a planned fused op has no other form; the planner fuses where conv3q has a tile per CU)
+bool conv3q_tail_ok(const va_conv_args& a) {
+    return a.w2 && a.b2 && !a.res && a.c2 > 0 && a.c2 <= 32 && a.c2 % 4 == 0 && ((uintptr_t)a.w2 & 15) == 0 &&
+           ((uintptr_t)a.b2 & 15) == 0 && conv3q_shape_ok(a);
+}
 hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3q_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)conv3q_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 Q3_LDS + 16) != hipSuccess ||
-            hipFuncSetAttribute((const void*)conv3q_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Q3_LDS + 16) != hipSuccess)
+            hipFuncSetAttribute((const void*)conv3q_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Q3_LDS + 16) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv3q_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Q3_LDS_T) != hipSuccess ||
+            hipFuncSetAttribute((const void*)conv3q_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                Q3_LDS_T) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
@@ -3739,10 +3799,12 @@ hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
     if (nt <= 0 || cus <= 0) return hipErrorInvalidValue;
     const dim3 grid(nt < cus ? nt : cus);
-    if (a.wcnt && a.ncnt >= 2 && va_sw().conv3q != 2)  // a work counter of the plan: tiles claimed dynamically
-        hipLaunchKernelGGL(conv3q_kernel<true>, grid, dim3(Q3_NT), Q3_LDS + 16, st, a, tx, ty, nt);
+    const bool dyn = a.wcnt && a.ncnt >= 2 && va_sw().conv3q != 2;  // a work counter of the plan: tiles claimed
+    auto go = [&](auto kern, int lds) { hipLaunchKernelGGL(kern, grid, dim3(Q3_NT), lds, st, a, tx, ty, nt); };
+    if (a.w2)
+        dyn ? go(conv3q_kernel<true, true>, Q3_LDS_T) : go(conv3q_kernel<false, true>, Q3_LDS_T);
     else
-        hipLaunchKernelGGL(conv3q_kernel<false>, grid, dim3(Q3_NT), Q3_LDS + 16, st, a, tx, ty, nt);
+        dyn ? go(conv3q_kernel<true, false>, Q3_LDS + 16) : go(conv3q_kernel<false, false>, Q3_LDS + 16);
     return hipGetLastError();
 }
 
@@ -3778,7 +3840,10 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
                 return launch_conv2<2, 2, 4, OutT>(a, st);
             }
         }
-        if constexpr (sizeof(T) == 4) return launch_conv3h_tail(a, st);
+        if constexpr (sizeof(T) == 4) {
+            if (a.Cout == 32) return conv3q_tail_ok(a) ? launch_conv3q(a, st) : hipErrorInvalidValue;
+            return launch_conv3h_tail(a, st);
+        }
         return hipErrorInvalidValue;
     }
     if constexpr (sizeof(T) == 2) {
@@ -3890,7 +3955,8 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     // bias4: mode 2 only -- bf16 through conv2's fused-tail path, f32 through the plain epilogue
     if (a->bias4 && (a->mode != 2 || (bf && (!a->w2 || a->Cout != 128)))) return VA_ERR_ARG;
     // f32 fused tail: conv3h's conditions (launch_conv3h_tail) are checked at dispatch
-    if (a->w2 && a->dtype == VA_DTYPE_F32 &&
+    if (a->w2 && a->dtype == VA_DTYPE_F32 && a->Cout == 32 && !conv3q_tail_ok(*a)) return VA_ERR_ARG;
+    if (a->w2 && a->dtype == VA_DTYPE_F32 && a->Cout != 32 &&
         (!a->w3 || a->res || !a->b2 || a->c2 <= 0 || a->c2 > T3_TAIL_C2 || a->c2 % 4 || a->mode == 1 ||
          (a->Cout != 64 && a->Cout != 128)))
         return VA_ERR_ARG;
