@@ -3744,8 +3744,11 @@ hipError_t launch_conv3h_tail(const va_conv_args& a, hipStream_t st) {
     return a.Cout == 128 ? launch_conv3h_v<3, 3, 4, float, true>(a, st) : launch_conv3h_v<3, 3, 2, float, true>(a, st);
 }
 
-// the 32 -> 32 stride-1 3x3 f32 layers on conv3q_kernel (VA_CONV3Q=0: conv2's three-term form) when the launch has a
-// tile for every CU (below that conv2's split-K tiles fill the chip better)
+// the 32 -> 32 stride-1 3x3 f32 layers on conv3q_kernel (VA_CONV3Q=0: conv2's three-term form) when the launch has
+// four tiles per CU or more: a workgroup's first tile carries the weight split and an exposed halo load (~19 us per
+// tile when a workgroup runs one or two: batch 4's 400 tiles took 38 us against conv2's 28, batch 1 21 vs 20;
+// profiles/r05/conv3q/ab_b1.log, ab_b4.log), at 25 per CU a tile costs ~9 us (batch 64: 220 vs 293 us)
+constexpr int Q3_MIN_TILES_PER_CU = 4;
 int conv3q_tiles(const va_conv_args& a, int* tx, int* ty) {
     *tx = (a.W + Q3_T - 1) / Q3_T;
     *ty = (a.H + Q3_T - 1) / Q3_T;
@@ -3773,7 +3776,7 @@ bool use_conv3q(const va_conv_args& a) {
     if (!va_sw().conv3q || a.w2 || !conv3q_shape_ok(a)) return false;
     int tx, ty;
     const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
-    return cus > 0 && nt >= cus;
+    return cus > 0 && nt >= Q3_MIN_TILES_PER_CU * cus;
 }
 // f32 fused 1x1 tail on a 32-channel 3x3 (the head's cv4.l.1 -> cv4.l.2): conv3q's TAIL form, whatever VA_CONV3Q
 // says or the tile count (a planned fused op has no other form; the planner fuses where conv3q has a tile per CU)

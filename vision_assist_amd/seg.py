@@ -893,12 +893,12 @@ class SegNet:
         p, p2 = self.w[prefix], self.w[tail]
         if self.dtype == "f32" and p.cin == 32 and p.cout == 32:
             # the 32-channel 3x3 (the head's cv4.l.1) on conv3q with the tail in its epilogue, where the launch has
-            # a 16 x 16 tile per CU (M / 256 is a lower bound of its tiles)
+            # four 16 x 16 tiles per CU (va_seg.hip Q3_MIN_TILES_PER_CU; M / 256 is a lower bound of its tiles)
             if os.environ.get("VA_FUSE_TAIL", "1") == "0" or os.environ.get("VA_CONV3Q", "1") == "0":
                 return False
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
             return (p.k == 3 and not p.deconv and p2.k == 1 and p2.cin == 32 and p2.cout <= 32 and p2.cout % 4 == 0
-                    and M // 256 >= cus)
+                    and M // 256 >= 4 * cus)
         if self.dtype == "f32":
             return p.k == 3 and not p.deconv and p.w3 is not None and self._fuse_tail_f32(p.cout, p2, M)
         if self.dtype != "bf16" or os.environ.get("VA_FUSE_TAIL", "1") == "0":
