@@ -435,6 +435,7 @@ hipError_t cf_launch(const va_conv_args* a, CfGeom g, int cus, hipStream_t st) {
     g.ntiles = (int)nt;
     int grid = C::WPC * (cus > 0 ? cus : 256);
     if (grid > g.ntiles) grid = g.ntiles;
+    if (g.ntiles < fz::WQ_MIN_TILES_PER_WG * grid) g.wq = nullptr;  // one or two tiles per workgroup: static
     hipLaunchKernelGGL(c2f_kernel<C>, dim3(grid), dim3(C::NW * 64), C::LDS + 16, st, (const __bf16*)a->x,
                        (const __bf16*)a->w, a->bias, (__bf16*)a->y, g);
     return hipGetLastError();

@@ -80,6 +80,10 @@ __device__ __forceinline__ int tile(int ntiles, int k) {
 
 // the work-queue schedule of the persistent kernels (va_seg.hip conv3q / stem32, va_stem.hip, va_c2f.hip): the next
 // tile from a counter of the plan (va_conv_args.wcnt[0]), or -1; the last workgroup out (counter [1]) zeroes both
+// the launchers use it from this many tiles per workgroup: below that (batch-1 shapes) every workgroup runs one or two
+// tiles, a late one cannot be helped, and the claims' extra barrier costs (the drop-in call 543-548 calls/s on the
+// static schedule against 534-537 with claims, profiles/r05/workq/dropin/)
+constexpr int WQ_MIN_TILES_PER_WG = 4;
 __device__ __forceinline__ int wq_claim(int* cnt, int ntiles) {
     const int v = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v < ntiles ? v : -1;

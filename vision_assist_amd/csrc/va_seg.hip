@@ -3802,7 +3802,8 @@ hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     const int nt = conv3q_tiles(a, &tx, &ty), cus = device_cus();
     if (nt <= 0 || cus <= 0) return hipErrorInvalidValue;
     const dim3 grid(nt < cus ? nt : cus);
-    const bool dyn = a.wcnt && a.ncnt >= 2 && va_sw().conv3q != 2;  // a work counter of the plan: tiles claimed
+    const bool dyn = a.wcnt && a.ncnt >= 2 && va_sw().conv3q != 2 &&  // a work counter of the plan: tiles claimed
+                     nt >= fz::WQ_MIN_TILES_PER_WG * (int)grid.x;
     auto go = [&](auto kern, int lds) { hipLaunchKernelGGL(kern, grid, dim3(Q3_NT), lds, st, a, tx, ty, nt); };
     if (a.w2)
         dyn ? go(conv3q_kernel<true, true>, Q3_LDS_T) : go(conv3q_kernel<false, true>, Q3_LDS_T);
@@ -4203,7 +4204,8 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a) {
         attr() = true;
     }
     const int grid = (int)(nt < cus ? nt : cus);
-    const bool dyn = a->wcnt && a->ncnt >= 2 && va_sw().conv3q != 2;  // work-queue schedule (VA_CONV3Q=static: off)
+    const bool dyn = a->wcnt && a->ncnt >= 2 && va_sw().conv3q != 2 &&  // work-queue schedule (VA_CONV3Q=static: off)
+                     nt >= (int64_t)fz::WQ_MIN_TILES_PER_WG * grid;
     const float* wt = tail ? (const float*)a->w2 : nullptr;
     const float* bt = tail ? a->b2 + 64 : nullptr;
     const size_t lds = (tail ? S32_LDS_T : S32_LDS) + 16;

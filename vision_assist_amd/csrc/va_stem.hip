@@ -312,6 +312,7 @@ extern "C" int va_seg_stem(void* stream, const va_conv_args* a) {
     }
     int grid = g_cus;
     if (grid > g.ntiles) grid = g.ntiles;
+    if (g.ntiles < fz::WQ_MIN_TILES_PER_WG * grid) g.wq = nullptr;  // one or two tiles per workgroup: static
     hipLaunchKernelGGL(stem_kernel, dim3(grid), dim3(ST_NW * 64), ST_LDS + 16, (hipStream_t)stream,
                        (const uint8_t*)a->x, (const __bf16*)a->w, a->bias, (__bf16*)a->y, g);
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
