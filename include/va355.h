@@ -273,6 +273,27 @@ int va_seg_c2f(void* stream, const va_conv_args* a);
  *   a.w    bf16 weight blob in MFMA fragment order (20480 values; layout: seg.py SegNet._pack_stem)
  *   a.bias float [96] = model.0 [32] | model.1 [64] */
 int va_seg_stem(void* stream, const va_conv_args* a);
+/* Any C2f block of YOLOv8n/s-seg as ONE launch for small batches (bf16; the batch-1 latency path, C2):
+ * cv1 (1x1, ci -> 2c) -> chunk -> n Bottlenecks (3x3 c -> c, 3x3 c -> c, + shortcut when set) -> cat -> cv2 (1x1,
+ * (2 + n) c -> co), every conv with folded BN bias + SiLU, each intermediate rounded to bf16 as a stored layer
+ * would be.  A workgroup owns a T x T output tile and recomputes the 2n-pixel halo its 3x3s need; nothing but the
+ * block's output leaves the chip.  Fields: a.x / a.ldx / a.Cin = ci (input, ci % 8 == 0; with a.xu / a.ldu /
+ * a.cu the first cu channels are the nearest-x2 upsample of a half-resolution slice, read in place as for
+ * va_seg_conv), a.y / a.ldy / a.Cout = co (co % 16 == 0), a.N / H / W, a.dtype = VA_DTYPE_BF16, a.mode = 3, and
+ *   a.Npad   hidden width c (16, 32, 64 or 128)
+ *   a.kh     n, Bottlenecks (1 or 2);  a.kw  shortcut (1 / 0)
+ *   a.stride tile side T (the LDS layout must fit: va_c2fb_layout)
+ *   a.w      bf16 A fragments (seg.py SegNet._pack_c2fb): per conv (cv1, m.0.cv1, m.0.cv2, .., cv2) the packed
+ *            [Cout][K] weights (K ordered (ky, kx, ci)) zero padded to 16-row x 32-column tiles, in tile order
+ *            [Cout / 16][K / 32], each tile as 64 lanes x 8 (lane 16 q + r: row r, columns 8 q .. 8 q + 7)
+ *   a.bias   float, per conv its biases zero padded to a multiple of 16, in the same order
+ * ldx, ldy, ldu % 8 == 0; x, xu, y, w, bias 16-byte aligned.  Replaces the block's 2n + 2 va_seg_conv calls
+ * (block.py C2f, Bottleneck) inside YOLO.predict (FrameProcessor.py:322).  VA_OP_C2F with a.mode == 3. */
+int va_seg_c2fb(void* stream, const va_conv_args* a);
+/* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels and tile side T: out[0] = LDS bytes per
+ * workgroup, out[1] = A fragments of the weight blob, out[2] = floats of the bias blob.  VA_ERR_ARG when the
+ * shape is not covered or the layout exceeds the 160 KiB of LDS (out[1], out[2] still set for a covered shape). */
+int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int64_t* out);
 /* The same C2f block in f32 (the headline's precision) as ONE launch, every intermediate on the chip as three exact
  * bf16 planes, the convs as six exact term products: a.x / a.ldx (float, 64 channels, ldx % 4 == 0), a.y / a.ldy
  * (float, ldy % 4 == 0), a.N / H / W, a.Cin = a.Cout = 64, a.dtype = VA_DTYPE_F32, and
@@ -348,7 +369,7 @@ int va_seg_upsample2x(void* stream, const void* src, int32_t ld_s, void* dst, in
 #define VA_OP_CONV0 5       /* preprocess fused into model.0: a.x = uint8 frames, a.N/H/W (input), a.w, a.bias,
                                a.Cout, a.y, a.ldy, a.dtype (FP8: e4m3 output with a.yscale; F32 with a.w3: the
                                MFMA form) -- see va_seg_conv0 / va_seg_conv0_f32(m) / va_seg_conv0_e4m3 */
-#define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f */
+#define VA_OP_C2F 6         /* fused C2f block: see va_seg_c2f (a.mode == 3: va_seg_c2fb) */
 #define VA_OP_STEM 7        /* fused preprocess + model.0 + model.1: va_seg_stem (bf16), va_seg_stem_f32 (f32) */
 /* Branch-parallel lists (small batches, where one layer does not fill the 256 CUs): an op with lane L > 0
  * is issued on auxiliary stream L of the calling stream (VA_LANES - 1 of them, created on first use per

@@ -56,6 +56,8 @@ SIGNATURES = [
     ("va_astar_run", I32, [P, P, P, I32, I32, P, P, I32, P, P, ctypes.POINTER(I32)]),
     ("va_seg_conv", I32, [P, P]),
     ("va_seg_c2f", I32, [P, P]),
+    ("va_seg_c2fb", I32, [P, P]),
+    ("va_c2fb_layout", I32, [I32, I32, I32, I32, I32, ctypes.POINTER(I64)]),
     ("va_seg_stem", I32, [P, P]),
     ("va_seg_stem_f32", I32, [P, P]),
     ("va_seg_c2f_f32", I32, [P, P]),

@@ -1,0 +1,331 @@
+// va_c2fb.hip -- a whole YOLOv8 C2f block of any width as ONE launch for small batches (bf16): block.py C2f
+// (cv1 -> chunk -> n Bottlenecks -> cat -> cv2), every intermediate in LDS, for the batch-1 forward that
+// FrameProcessor.py:322's model.predict runs per frame (C2, BASELINE.json configs[1]).
+//
+// At batch 1 a C2f block is 4 (n = 1) or 6 (n = 2) dependent launches of a few us each whose MFMA work is tiny
+// (model.6 of YOLOv8n-seg at 40 x 40: 0.5 GFLOP), so the block's time is launch boundaries, prologues and store
+// tails (DESIGN.md §5's phase clocks).  Here a workgroup owns a T x T output tile and recomputes what the tile needs:
+//
+//   region IN  (T + 4n)^2 pixels of the block's input (ci channels, zero outside the frame; an FPN upsample prefix
+//              is read in place from its half-resolution source, va355.h va_conv_args.xu)
+//   cv1        1x1 ci -> 2c over all of IN -> R0 (zero outside the frame: the 3x3s' padding)
+//   m.j.cv1    3x3 c -> c: R(2j) -> R(2j+1), one pixel smaller on every side; R(0) means R0's second half (b)
+//   m.j.cv2    3x3 c -> c: R(2j+1) -> R(2j+2), + R(2j) at the same pixel (shortcut)
+//   cv2        1x1 over [R0 (a | b) | R2 | R4 ...] at the tile's pixels (the concat, read in place) -> y
+//
+// Each conv is an implicit GEMM over its output region in 16-pixel x 16-channel blocks on
+// v_mfma_f32_16x16x32_bf16: the activations (B) from LDS, the weights (A) straight from global memory in
+// fragment order (seg.py SegNet._pack_c2fb; L2-resident, eight K-steps loaded ahead), eight waves sharing the
+// blocks.  Every intermediate is bias + SiLU (+ shortcut) in f32 rounded to bf16 -- the rounding a stored layer
+// gets -- so the block equals the unfused layers up to the f32 summation order inside each conv.  The halo
+// recompute (a T = 4 tile of an n = 1 block computes cv1 on 8 x 8 pixels) costs MFMA time the batch-1 forward
+// has to spare: a layer there fills a few dozen of the 256 CUs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/va355.h"
+#include "va_dev.h"
+#include "va_fuse.h"
+
+namespace {
+
+using fz::mma;
+
+constexpr int XB_NW = 8, XB_NT = 64 * XB_NW;
+constexpr int XB_G = 4;       // 16-pixel blocks per work item (one A fragment feeds XB_G MFMAs)
+constexpr int XB_KC = 8;      // K-steps of A fragments loaded ahead
+constexpr int XB_LDS_MAX = 160 * 1024;
+
+struct XbGeom {
+    const __bf16* x;
+    const __bf16* xu;
+    __bf16* y;
+    const bf16x8* w;  // fragments: conv q at w + 64 * wf[q], [ncb][ks][64 lanes]
+    const float* b;   // biases: conv q at b + bo[q], [16 ncb]
+    int N, H, W, ci, cu, ldx, ldu, co, ldy;
+    int T, tx, tpf;   // tile side, tiles per row, tiles per frame
+    int sc;           // Bottleneck shortcut
+    int psi;          // LDS bytes per pixel of the input region
+    int in_off;       // LDS offset of the input region (R1 .. R2n alias it once cv1 has read it)
+    int off_r[5];     // LDS offsets of R0 .. R2n
+    int wf[6], bo[6]; // per conv (cv1, m.0.cv1, m.0.cv2, [m.1.cv1, m.1.cv2,] cv2)
+};
+
+// conv q's shape: output channels, K (elements), K-steps of 32
+template <int C, int NB>
+struct XbConvShape {
+    static __host__ __device__ int nout(int q, int co) { return q == 0 ? 2 * C : q == 2 * NB + 1 ? co : C; }
+    static __host__ __device__ int k(int q, int ci) { return q == 0 ? ci : q == 2 * NB + 1 ? (2 + NB) * C : 9 * C; }
+};
+
+// LDS pixel strides: 16 bytes past the channels (rows of 16 pixels then spread over the banks)
+template <int C>
+constexpr int ps0() { return 4 * C + 16; }
+template <int C>
+constexpr int psc() { return 2 * C + 16; }
+
+
+// an LDS region: byte offset, width in pixels (regions are square), pixel stride, first channel; off < 0 = none
+struct XbIo {
+    int off, w, ps, c0;
+};
+
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+
+// One conv of the block over an ow x ow output region whose pixel 0 sits at image (oy, ox) of frame n.
+// KIND 0: 1x1 over the input region (cv1; src = IN, the same geometry as the output);
+// KIND 1: 3x3 from src (one pixel larger on every side), + res at the same pixel (two larger) when res.off >= 0;
+// KIND 2: 1x1 over the concat [R0 | R2 | R4 ...] at the tile's pixels (cv2), written to g.y.
+// Pixels outside the frame are stored as zero (the next 3x3's padding); KIND 2 skips them.
+template <int C, int NB, int KIND>
+__device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, int q, int nout, int kel, int ow, int oy,
+                                        int ox, int n, XbIo src, XbIo dst, XbIo res, int lane, int wid) {
+    constexpr int H2 = 2 * NB;
+    const int ks = (kel + 31) >> 5, ncb = (nout + 15) >> 4;
+    const int P = ow * ow, npb = (P + 15) >> 4, ngr = (npb + XB_G - 1) / XB_G;
+    const int items = ngr * ncb;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int S0 = g.T + 2 * H2;
+    for (int it = wid; it < items; it += XB_NW) {
+        const int cb = it % ncb, gr = it / ncb;
+        const int nb = min(XB_G, npb - gr * XB_G);  // live pixel blocks of this item (wave-uniform)
+        int base[XB_G], pr[XB_G], pc[XB_G];
+#pragma unroll
+        for (int j = 0; j < XB_G; ++j) {
+            int p = ((gr * XB_G + j) << 4) + fr;
+            p = p < P ? p : P - 1;  // a block's tail lanes read a real pixel; their results are dropped
+            const int r = p / ow, c = p - r * ow;
+            pr[j] = r;
+            pc[j] = c;
+            if constexpr (KIND == 0) base[j] = src.off + p * src.ps;
+            else if constexpr (KIND == 1) base[j] = src.off + (r * src.w + c) * src.ps + src.c0 * 2;
+            else base[j] = 0;
+        }
+        f32x4 acc[XB_G];
+#pragma unroll
+        for (int j = 0; j < XB_G; ++j) acc[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        const bf16x8* wb = g.w + (int64_t)64 * (g.wf[q] + cb * ks) + lane;
+        auto step = [&](int k, bf16x8 a) {
+            const int kk = min((k << 5) + (fq << 3), kel - 8);  // past K: the last group (its weights are zero)
+#pragma unroll
+            for (int j = 0; j < XB_G; ++j) {
+                if (j < nb) {
+                    int addr;
+                    if constexpr (KIND == 0) {
+                        addr = base[j] + kk * 2;
+                    } else if constexpr (KIND == 1) {
+                        const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
+                        addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
+                    } else if (kk < 2 * C) {
+                        addr = g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * ps0<C>() + kk * 2;
+                    } else {
+                        const int s = (kk - 2 * C) / C + 1, ch = kk - (s + 1) * C;
+                        const int hs = H2 - 2 * s, ws = g.T + 2 * hs;  // R(2s): halo hs
+                        addr = g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * psc<C>() + ch * 2;
+                    }
+                    acc[j] = mma(a, *(const bf16x8*)(smem + addr), acc[j]);
+                }
+            }
+        };
+        bf16x8 a0[XB_KC], a1[XB_KC];
+#pragma unroll
+        for (int i = 0; i < XB_KC; ++i)
+            if (i < ks) a0[i] = wb[64 * i];
+        for (int k0 = 0; k0 < ks; k0 += 2 * XB_KC) {
+#pragma unroll
+            for (int i = 0; i < XB_KC; ++i)
+                if (k0 + XB_KC + i < ks) a1[i] = wb[64 * (k0 + XB_KC + i)];
+#pragma unroll
+            for (int i = 0; i < XB_KC; ++i)
+                if (k0 + i < ks) step(k0 + i, a0[i]);
+#pragma unroll
+            for (int i = 0; i < XB_KC; ++i)
+                if (k0 + 2 * XB_KC + i < ks) a0[i] = wb[64 * (k0 + 2 * XB_KC + i)];
+#pragma unroll
+            for (int i = 0; i < XB_KC; ++i)
+                if (k0 + XB_KC + i < ks) step(k0 + XB_KC + i, a1[i]);
+        }
+        // epilogue: the lane holds channels 4 fq .. 4 fq + 3 of block cb for its pixel of each block
+        const int co = (cb << 4) + (fq << 2);
+        if (co >= nout) continue;
+        const f32x4 bias = *(const f32x4*)(g.b + g.bo[q] + co);
+#pragma unroll
+        for (int j = 0; j < XB_G; ++j) {
+            const int p = ((gr * XB_G + j) << 4) + fr;
+            if (j >= nb || p >= P) continue;
+            const int r = pr[j], c = pc[j], iy = oy + r, ix = ox + c;
+            const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+            f32x4 v = fz::act(acc[j] + bias);
+            if (KIND == 1 && res.off >= 0) {  // Bottleneck shortcut, added after the activation (va_seg.hip epilogue)
+                const uint2 rr = *(const uint2*)(smem + res.off + ((r + 2) * res.w + c + 2) * res.ps + (res.c0 + co) * 2);
+                v += (f32x4){bf_lo(rr.x), bf_hi(rr.x), bf_lo(rr.y), bf_hi(rr.y)};
+            }
+            bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            if constexpr (KIND == 2) {
+                if (in) *(bf16x4*)(g.y + ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldy + co) = o;
+            } else {
+                if (!in) o = (bf16x4){(__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f, (__bf16)0.0f};
+                *(bf16x4*)(smem + dst.off + p * dst.ps + (dst.c0 + co) * 2) = o;
+            }
+        }
+    }
+}
+
+template <int C, int NB>
+__global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int H2 = 2 * NB;
+    const int T = g.T, S0 = T + 2 * H2;
+    const int t = blockIdx.x, n = t / g.tpf, tt = t - n * g.tpf, ty = tt / g.tx, tx = tt - ty * g.tx;
+    const int y0 = ty * T, x0 = tx * T;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // the input region, eight 16-byte loads in flight per thread before their LDS stores
+    const int cg = g.ci >> 3, total = S0 * S0 * cg;
+    for (int q0 = tid; q0 < total; q0 += 8 * XB_NT) {
+        u32x4 v[8];
+        int dst[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int qq = q0 + i * XB_NT;
+            v[i] = (u32x4){0u, 0u, 0u, 0u};
+            dst[i] = -1;
+            if (qq < total) {
+                const int px = qq / cg, ch = (qq - px * cg) << 3;
+                const int ry = px / S0, rx = px - ry * S0, iy = y0 - H2 + ry, ix = x0 - H2 + rx;
+                dst[i] = g.in_off + px * g.psi + ch * 2;
+                if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) {
+                    if (ch < g.cu)
+                        v[i] = *(const u32x4*)(g.xu + ((int64_t)(n * (g.H >> 1) + (iy >> 1)) * (g.W >> 1) + (ix >> 1)) *
+                                                          g.ldu + ch);
+                    else
+                        v[i] = *(const u32x4*)(g.x + ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldx + ch);
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (dst[i] >= 0) *(u32x4*)(smem + dst[i]) = v[i];
+    }
+    __syncthreads();
+    const XbIo none = {-1, 0, 0, 0};
+    const XbIo r0 = {g.off_r[0], S0, ps0<C>(), 0};
+    xb_conv<C, NB, 0>(g, smem, 0, 2 * C, g.ci, S0, y0 - H2, x0 - H2, n, XbIo{g.in_off, S0, g.psi, 0}, r0, none, lane,
+                      wid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int hs = H2 - 2 * j, ws = T + 2 * hs;  // R(2j): halo hs
+        const XbIo rin = j == 0 ? XbIo{g.off_r[0], S0, ps0<C>(), C} : XbIo{g.off_r[2 * j], ws, psc<C>(), 0};
+        const XbIo rmid = {g.off_r[2 * j + 1], ws - 2, psc<C>(), 0}, rout = {g.off_r[2 * j + 2], ws - 4, psc<C>(), 0};
+        xb_conv<C, NB, 1>(g, smem, 1 + 2 * j, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane, wid);
+        __syncthreads();
+        xb_conv<C, NB, 1>(g, smem, 2 + 2 * j, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
+                          g.sc ? rin : none, lane, wid);
+        __syncthreads();
+    }
+    xb_conv<C, NB, 2>(g, smem, 2 * NB + 1, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
+}
+
+// LDS layout of one configuration: [R0][IN, later R1 .. R2n]; returns the bytes (or -1)
+int xb_layout(int C, int NB, int ci, int T, int* off_r, int* in_off, int* psi) {
+    if (T < 1 || T > 64) return -1;
+    const int S0 = T + 4 * NB;
+    const int64_t r0 = (int64_t)S0 * S0 * (4 * C + 16), in = (int64_t)S0 * S0 * (2 * ci + 16);
+    int64_t rs = 0;
+    off_r[0] = 0;
+    for (int j = 1; j <= 2 * NB; ++j) {
+        const int s = T + 2 * (2 * NB - j);
+        off_r[j] = (int)(r0 + rs);
+        rs += (int64_t)s * s * (2 * C + 16);
+    }
+    *in_off = (int)r0;
+    *psi = 2 * ci + 16;
+    const int64_t tot = r0 + (in > rs ? in : rs);
+    return tot > XB_LDS_MAX ? -1 : (int)tot;
+}
+
+// fragment / bias offsets of the blob (seg.py SegNet._pack_c2fb): conv q = cv1, m.0.cv1, m.0.cv2, .., cv2, each
+// [ceil(nout / 16)][ceil(K / 32)] fragments and 16 ceil(nout / 16) biases; returns the totals
+void xb_blob(int C, int NB, int ci, int co, int* wf, int* bo, int64_t* frags, int64_t* biases) {
+    int64_t f = 0, b = 0;
+    for (int q = 0; q < 2 * NB + 2; ++q) {
+        const int nout = q == 0 ? 2 * C : q == 2 * NB + 1 ? co : C;
+        const int k = q == 0 ? ci : q == 2 * NB + 1 ? (2 + NB) * C : 9 * C;
+        wf[q] = (int)f;
+        bo[q] = (int)b;
+        f += (int64_t)((nout + 15) / 16) * ((k + 31) / 32);
+        b += 16 * ((nout + 15) / 16);
+    }
+    *frags = f;
+    *biases = b;
+}
+
+template <int C, int NB>
+hipError_t xb_launch(const XbGeom& g, int lds, int ntiles, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)c2fb_kernel<C, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                XB_LDS_MAX) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    hipLaunchKernelGGL((c2fb_kernel<C, NB>), dim3(ntiles), dim3(XB_NT), lds, st, g);
+    return hipGetLastError();
+}
+
+bool xb_shape_ok(int C, int NB) { return (C == 16 || C == 32 || C == 64 || C == 128) && (NB == 1 || NB == 2); }
+
+}  // namespace
+
+extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int64_t* out3) {
+    if (!out3 || !xb_shape_ok(c, n) || ci <= 0 || co <= 0) return VA_ERR_ARG;
+    int off_r[5], in_off, psi, wf[6], bo[6];
+    const int lds = xb_layout(c, n, ci, T, off_r, &in_off, &psi);
+    xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2]);
+    out3[0] = lds;
+    return lds < 0 ? VA_ERR_ARG : VA_OK;
+}
+
+extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
+    if (!a || !a->x || !a->w || !a->bias || !a->y || a->dtype != VA_DTYPE_BF16) return VA_ERR_ARG;
+    const int C = a->Npad, NB = a->kh, T = a->stride, ci = a->Cin, co = a->Cout;
+    if (!xb_shape_ok(C, NB) || a->N <= 0 || a->H <= 0 || a->W <= 0 || ci % 8 || co % 16 || ci <= 0 || co <= 0 ||
+        a->ldx % 8 || a->ldy % 8 || a->ldx < ci || a->ldy < co || ((uintptr_t)a->x & 15) || ((uintptr_t)a->y & 15) ||
+        ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15))
+        return VA_ERR_ARG;
+    if (a->xu && (a->cu <= 0 || a->cu % 8 || a->cu >= ci || a->ldu % 8 || a->ldu < a->cu || a->H % 2 || a->W % 2 ||
+                  ((uintptr_t)a->xu & 15)))
+        return VA_ERR_ARG;
+    XbGeom g;
+    const int lds = xb_layout(C, NB, ci, T, g.off_r, &g.in_off, &g.psi);
+    if (lds < 0) return VA_ERR_ARG;
+    int64_t frags, biases;
+    xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases);
+    g.x = (const __bf16*)a->x;
+    g.xu = (const __bf16*)a->xu;
+    g.y = (__bf16*)a->y;
+    g.w = (const bf16x8*)a->w;
+    g.b = a->bias;
+    g.N = a->N, g.H = a->H, g.W = a->W, g.ci = ci, g.cu = a->xu ? a->cu : 0, g.ldx = a->ldx, g.ldu = a->ldu;
+    g.co = co, g.ldy = a->ldy, g.T = T, g.sc = a->kw ? 1 : 0;
+    g.tx = (a->W + T - 1) / T;
+    const int64_t tpf = (int64_t)g.tx * ((a->H + T - 1) / T), nt = tpf * a->N;
+    if (nt > INT32_MAX) return VA_ERR_ARG;
+    g.tpf = (int)tpf;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t rc;
+    switch (C * 4 + NB) {
+        case 16 * 4 + 1: rc = xb_launch<16, 1>(g, lds, (int)nt, st); break;
+        case 16 * 4 + 2: rc = xb_launch<16, 2>(g, lds, (int)nt, st); break;
+        case 32 * 4 + 1: rc = xb_launch<32, 1>(g, lds, (int)nt, st); break;
+        case 32 * 4 + 2: rc = xb_launch<32, 2>(g, lds, (int)nt, st); break;
+        case 64 * 4 + 1: rc = xb_launch<64, 1>(g, lds, (int)nt, st); break;
+        case 64 * 4 + 2: rc = xb_launch<64, 2>(g, lds, (int)nt, st); break;
+        case 128 * 4 + 1: rc = xb_launch<128, 1>(g, lds, (int)nt, st); break;
+        default: rc = xb_launch<128, 2>(g, lds, (int)nt, st); break;
+    }
+    return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
+}

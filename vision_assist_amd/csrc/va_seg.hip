@@ -4345,7 +4345,9 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                          : va_seg_conv0(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             case VA_OP_C2F:
-                rc = a.dtype == VA_DTYPE_F32 ? va_seg_c2f_f32(st, &a) : va_seg_c2f(st, &a);
+                rc = a.mode == 3                ? va_seg_c2fb(st, &a)
+                     : a.dtype == VA_DTYPE_F32 ? va_seg_c2f_f32(st, &a)
+                                               : va_seg_c2f(st, &a);
                 break;
             case VA_OP_STEM:
                 rc = a.dtype == VA_DTYPE_F32 ? va_seg_stem_f32(st, &a) : va_seg_stem(st, &a);

@@ -29,6 +29,8 @@ F8_MAX = 448.0     # largest OCP e4m3 value
 FP8_HEADROOM = 8.0  # calibration amax x this x the buffer scale lands in [224, 448] (SegNet.calibrate_fp8)
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 VA_OP_FORK, VA_OP_JOIN = 8, 9  # lanes of a branch-parallel list (va355.h)
+C2FB_MAX_B = 1      # va_seg_c2fb for batches up to this (SegNet.c2fb_max_b)
+C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may leave
 SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -65,6 +67,10 @@ class SegOp(ctypes.Structure):
 
 def _ceil(a, b):
     return (a + b - 1) // b * b
+
+
+def _cdiv(a, b):
+    return (a + b - 1) // b
 
 
 @dataclass
@@ -216,6 +222,12 @@ class SegNet:
             for i, ci, co, n, shortcut in arch.c2f_plan():
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
+        # small batches (bf16): every C2f block as one launch, intermediates on the chip and the 3x3s' halo recomputed
+        # per tile (va355.h va_seg_c2fb), for B <= c2fb_max_b; VA_C2FB=0 keeps the blocks' layers apart (A/B).
+        # c2fb_tile: per block index a tile side overriding _c2fb_tile's choice (tools / tests)
+        self.c2fb_max_b = C2FB_MAX_B if (dtype == "bf16" and os.environ.get("VA_C2FB", "1") != "0") else 0
+        self.c2fb = {}
+        self.c2fb_tile = {}
         # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32), on request (c2f32)
         self.c2f32 = {}
         if dtype == "f32" and c2f32:
@@ -238,6 +250,45 @@ class SegNet:
             for prefix, p in self.w.items():
                 if p.cin % 16 == 0:
                     self.w8[prefix] = self._pack_fp8(p)
+
+    def _pack_c2fb(self, i: int, n: int):
+        """(weight blob, bias blob) of va_seg_c2fb for C2f block ``model.{i}`` with n Bottlenecks: per conv (cv1,
+        m.j.cv1 / m.j.cv2, cv2) the packed bf16 rows [Cout][K] (the unfused layers' own weights, K ordered (ky, kx,
+        ci)) zero padded to 16 x 32 tiles, tile order [Cout / 16][K / 32], each tile as MFMA A fragment lanes
+        (lane 16 q + r: row r, columns 8 q .. 8 q + 7); biases zero padded to 16 per conv."""
+        if i in self.c2fb:
+            return self.c2fb[i]
+        names = [f"model.{i}.cv1"] + [f"model.{i}.m.{j}.cv{k}" for j in range(n) for k in (1, 2)] + [f"model.{i}.cv2"]
+        frags, biases = [], []
+        for nm in names:
+            p = self.w[nm]
+            ncb, ks = _cdiv(p.cout, 16), _cdiv(p.K, 32)
+            wm = torch.zeros(16 * ncb, 32 * ks, dtype=p.w.dtype, device=p.w.device)
+            wm[:p.cout, :p.K] = p.w[:p.cout, :p.K]
+            frags.append(wm.reshape(ncb, 16, ks, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1))
+            b = torch.zeros(16 * ncb, dtype=torch.float32, device=p.b.device)
+            b[:p.cout] = p.b[:p.cout].float()
+            biases.append(b)
+        self.c2fb[i] = (torch.cat(frags).contiguous(), torch.cat(biases).contiguous())
+        return self.c2fb[i]
+
+    def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int):
+        """(LDS bytes or -1, A fragments, bias floats) of va_seg_c2fb's layout (va355.h va_c2fb_layout)."""
+        out = (ctypes.c_int64 * 3)()
+        rc = self.lib.va_c2fb_layout(c, n, ci, co, T, out)
+        return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]))
+
+    def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int) -> int:
+        """va_seg_c2fb's tile side for block i at B x h x w: the largest of 16 / 8 / 4 / 2 whose launch has at
+        least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
+        larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits."""
+        if i in self.c2fb_tile:
+            return self.c2fb_tile[i]
+        fits = [T for T in (16, 8, 4, 2) if self.c2fb_layout(co // 2, n, ci, co, T)[0] > 0]
+        for T in fits:
+            if B * _cdiv(h, T) * _cdiv(w, T) >= C2FB_MIN_TILES:
+                return T
+        return fits[-1] if fits else 0
 
     def _pack_c2f32(self, folded: dict, i: int):
         """(weight blob, bias blob) of va_seg_c2f_f32: the four convs' f32 weights row-major [Cout][K] with K ordered
@@ -564,6 +615,24 @@ class SegNet:
                              "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
                              "bytes": 4 * B * h * w * 128})
                 return
+            c = co // 2
+            if (pre is None and B <= self.c2fb_max_b and c in (16, 32, 64, 128) and n in (1, 2) and ci % 8 == 0 and
+                    co % 16 == 0 and src.ld % 8 == 0 and dst.ld % 8 == 0 and (up is None or up.ld % 8 == 0) and
+                    src.c == ci):
+                T = self._c2fb_tile(i, B, h, w, ci, co, n)
+                if T:
+                    blob, bias = self._pack_c2fb(i, n)
+                    args = ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=ci, ldx=src.ld, w=blob.data_ptr(),
+                                    bias=bias.data_ptr(), Cout=co, y=dst.ptr, ldy=dst.ld, dtype=VA_DTYPE_BF16, mode=3,
+                                    kh=n, kw=1 if shortcut else 0, Npad=c, stride=T)
+                    if up is not None:
+                        args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
+                    ops.append(SegOp(kind=VA_OP_C2F, a=args))
+                    macs = ci * 2 * c + n * 2 * 9 * c * c + (2 + n) * c * co  # per output pixel, without the halo
+                    meta.append({"name": f"model.{i} (fused C2f, T={T})", "kind": "conv", "M": B * h * w, "N": co,
+                                 "K": macs // co, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
+                                 "bytes": 2 * B * h * w * (ci + co)})
+                    return
             if pre is None and i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
                 ops.append(SegOp(kind=VA_OP_C2F, a=with_ws(ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
