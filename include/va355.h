@@ -288,12 +288,16 @@ int va_seg_stem(void* stream, const va_conv_args* a);
  *            [Cout / 16][K / 32], each tile as 64 lanes x 8 (lane 16 q + r: row r, columns 8 q .. 8 q + 7)
  *   a.bias   float, per conv its biases zero padded to a multiple of 16, in the same order
  * ldx, ldy, ldu % 8 == 0; x, xu, y, w, bias 16-byte aligned.  Replaces the block's 2n + 2 va_seg_conv calls
- * (block.py C2f, Bottleneck) inside YOLO.predict (FrameProcessor.py:322).  VA_OP_C2F with a.mode == 3. */
+ * (block.py C2f, Bottleneck) inside YOLO.predict (FrameProcessor.py:322).  VA_OP_C2F with a.mode == 3.
+ * a.dtype = VA_DTYPE_F32 (the reference's precision; c up to 256): float activations (ldx, ldy, ldu % 4 == 0), every
+ * product as six exact bf16 term products (va_seg_conv's f32 arithmetic), a.w = the same tiles as three fragments
+ * each (h, m, l: the exact three-term bf16 split of the f32 weights, [tile][3][64 lanes][8]). */
 int va_seg_c2fb(void* stream, const va_conv_args* a);
-/* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels and tile side T: out[0] = LDS bytes per
- * workgroup, out[1] = A fragments of the weight blob, out[2] = floats of the bias blob.  VA_ERR_ARG when the
- * shape is not covered or the layout exceeds the 160 KiB of LDS (out[1], out[2] still set for a covered shape). */
-int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int64_t* out);
+/* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels, tile side T and dtype: out[0] = LDS bytes
+ * per workgroup, out[1] = A fragments (64 lanes x 8 bf16) of the weight blob, out[2] = floats of the bias blob.
+ * VA_ERR_ARG when the shape is not covered or the layout exceeds the 160 KiB of LDS (out[1], out[2] still set for a
+ * covered shape). */
+int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int64_t* out);
 /* The same C2f block in f32 (the headline's precision) as ONE launch, every intermediate on the chip as three exact
  * bf16 planes, the convs as six exact term products: a.x / a.ldx (float, 64 channels, ldx % 4 == 0), a.y / a.ldy
  * (float, ldy % 4 == 0), a.N / H / W, a.Cin = a.Cout = 64, a.dtype = VA_DTYPE_F32, and

@@ -36,34 +36,43 @@ def _block_ref(x, fw, i, n, shortcut):
     return bf(conv(f"model.{i}.cv2", torch.cat(ys, 1)))
 
 
-def _net():
+# the same blocks of YOLOv8s-seg (the f32 form: the drop-in call's batch-1 network)
+S_BLOCKS = [(2, 64, 64, 1, True, 0, 160, 160), (4, 128, 128, 2, True, 0, 80, 80), (6, 256, 256, 2, True, 0, 40, 40),
+            (8, 512, 512, 1, True, 0, 20, 20), (12, 768, 256, 1, False, 512, 40, 40),
+            (15, 384, 128, 1, False, 256, 80, 80), (18, 384, 256, 1, False, 0, 40, 40),
+            (21, 768, 512, 1, False, 0, 20, 20)]
+
+
+def _net(scale="n", dtype="bf16"):
     from vision_assist_amd.seg import SegNet
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
-    arch = Arch("n")
+    arch = Arch(scale)
     fw = fold(arch, synthetic_state_dict(arch, seed=3))
-    return arch, fw, SegNet(arch, fw, dtype="bf16")
+    return arch, fw, SegNet(arch, fw, dtype=dtype, c2fb_f32=dtype == "f32")
 
 
 def _run_block(net, i, ci, co, n, shortcut, cu, B, H, W, T, pad_x=8, pad_y=16, seed=0):
     from vision_assist_amd import _lib
     from vision_assist_amd import seg as S
+    f32 = net.store == "f32"
+    dt = torch.float32 if f32 else torch.bfloat16
     g = torch.Generator().manual_seed(seed * 7919 + i)
     ldx, ldy = ci + pad_x, co + pad_y
-    x = (torch.randn(B, H, W, ci, generator=g) * 1.5).to(torch.bfloat16)
-    xin = torch.full((B, H, W, ldx), float("nan"), dtype=torch.bfloat16)  # channels never read stay NaN
+    x = (torch.randn(B, H, W, ci, generator=g) * 1.5).to(dt)
+    xin = torch.full((B, H, W, ldx), float("nan"), dtype=dt)  # channels never read stay NaN
     xin[..., cu:ci] = x[..., cu:]
     xu = None
     if cu:
-        half = (torch.randn(B, H // 2, W // 2, cu, generator=g) * 1.5).to(torch.bfloat16)
+        half = (torch.randn(B, H // 2, W // 2, cu, generator=g) * 1.5).to(dt)
         x[..., :cu] = half.repeat_interleave(2, 1).repeat_interleave(2, 2)
-        xu = torch.zeros(B, H // 2, W // 2, cu + 8, dtype=torch.bfloat16)
+        xu = torch.zeros(B, H // 2, W // 2, cu + 8, dtype=dt)
         xu[..., :cu] = half
         xu = xu.cuda()
     xd = xin.cuda()
-    y = torch.full((B, H, W, ldy), 7.0, dtype=torch.bfloat16, device="cuda")
+    y = torch.full((B, H, W, ldy), 7.0, dtype=dt, device="cuda")
     blob, bias = net._pack_c2fb(i, n)
     a = S.ConvArgs(x=xd.data_ptr(), N=B, H=H, W=W, Cin=ci, ldx=ldx, w=blob.data_ptr(), bias=bias.data_ptr(), Cout=co,
-                   y=y.data_ptr(), ldy=ldy, dtype=S.VA_DTYPE_BF16, mode=3, kh=n, kw=1 if shortcut else 0, Npad=co // 2,
+                   y=y.data_ptr(), ldy=ldy, dtype=net.va_dtype, mode=3, kh=n, kw=1 if shortcut else 0, Npad=co // 2,
                    stride=T)
     if cu:
         a.xu, a.ldu, a.cu = xu.data_ptr(), cu + 8, cu
@@ -131,3 +140,75 @@ def test_c2fb_forward_vs_unfused(monkeypatch):
     for k, (g_, r) in enumerate(zip(fused, plain)):
         err = ((g_ - r).norm() / r.norm()).item()
         assert err < 2e-2, f"output {k}: fused vs unfused C2f blocks {err}"
+
+
+def _block_ref64(x, fw, i, n, shortcut):
+    """block.py C2f in float64 (x: NCHW float64), the f32 weights as given."""
+    silu = F.silu
+
+    def conv(name, t, pad=0):
+        w, b = fw[name]
+        return silu(F.conv2d(t, w.double(), b.double(), padding=pad))
+
+    t = conv(f"model.{i}.cv1", x)
+    c = t.shape[1] // 2
+    ys = [t[:, :c], t[:, c:]]
+    for j in range(n):
+        o = conv(f"model.{i}.m.{j}.cv2", conv(f"model.{i}.m.{j}.cv1", ys[-1], 1), 1)
+        ys.append(o + ys[-1] if shortcut else o)
+    return conv(f"model.{i}.cv2", torch.cat(ys, 1))
+
+
+@pytest.mark.parametrize("blk", S_BLOCKS, ids=[f"model.{b[0]}" for b in S_BLOCKS])
+def test_c2fb_f32_block_batch1(blk):
+    """The f32 form on every C2f block of s-seg at its 640 x 640 size, batch 1 (the planner's tile side) against the
+    block in float64: every product as six exact bf16 term products, f32 accumulation, so f32 rounding level."""
+    i, ci, co, n, sc, cu, H, W = blk
+    arch, fw, net = _net("s", "f32")
+    T = net._c2fb_tile(i, 1, H, W, ci, co, n)
+    assert T > 0
+    x, got = _run_block(net, i, ci, co, n, sc, cu, 1, H, W, T)
+    ref = _block_ref64(x.double().permute(0, 3, 1, 2), fw, i, n, sc).permute(0, 2, 3, 1)
+    err = (got.double() - ref).abs()
+    assert err.max().item() <= 2e-5 * max(1.0, ref.abs().max().item()), (err.max().item(), ref.abs().max().item())
+    assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("i,T,B,H,W", [(4, 2, 2, 20, 28), (6, 2, 1, 7, 9), (21, 2, 2, 6, 10), (2, 8, 1, 24, 40)])
+def test_c2fb_f32_tiles_ragged(i, T, B, H, W):
+    blk = next(b for b in S_BLOCKS if b[0] == i)
+    _, ci, co, n, sc, cu, _, _ = blk
+    arch, fw, net = _net("s", "f32")
+    x, got = _run_block(net, i, ci, co, n, sc, cu, B, H, W, T, seed=B + H)
+    ref = _block_ref64(x.double().permute(0, 3, 1, 2), fw, i, n, sc).permute(0, 2, 3, 1)
+    err = (got.double() - ref).abs()
+    assert err.max().item() <= 2e-5 * max(1.0, ref.abs().max().item()), err.max().item()
+
+
+def test_c2fb_f32_forward_vs_unfused():
+    """The batch-1 s-seg f32 plan (the drop-in call's network) with its C2f blocks as va_seg_c2fb ops (opt-in:
+    SegNet(c2fb_f32=True)): heads equal to the unfused plan's at f32 rounding level, and within the 1e-3 bar of the
+    float32 torch reference."""
+    from oracle import yolo_ref as Y
+    from vision_assist_amd.seg import SegNet
+    arch, fw, net = _net("s", "f32")
+    names = [m["name"] for m in net.plan(1, 640, 640)["meta"]]
+    assert sum("fused C2f, T=" in nm for nm in names) >= 7, names
+    frames = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(4), dtype=torch.uint8)
+
+    def heads(nt):
+        out = nt.forward(frames.cuda())
+        torch.cuda.synchronize()
+        return [t.float().cpu() for t in out.levels] + [out.proto.float().cpu()]
+
+    fused = heads(net)
+    plain_net = SegNet(arch, fw, dtype="f32")  # the default: f32 blocks unfused
+    assert not any("fused C2f, T=" in m["name"] for m in plain_net.plan(1, 640, 640)["meta"])
+    plain = heads(plain_net)
+    for k, (g_, r) in enumerate(zip(fused, plain)):
+        assert (g_ - r).abs().max().item() <= 1e-4, f"output {k}: {(g_ - r).abs().max().item()}"
+    box, cls, coef, proto = Y.forward(arch, fw, Y.preprocess(frames))
+    lv = torch.cat([t.flatten(1, 2) for t in fused[:3]], 1).permute(0, 2, 1)
+    ref = torch.cat([box, cls, coef], 1)
+    assert (lv - ref).abs().max().item() <= 1e-3
+    assert (fused[3].permute(0, 3, 1, 2) - proto).abs().max().item() <= 1e-3

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--scale", default="n")
+    ap.add_argument("--dtype", default="bf16", help="bf16 (C2) or f32 (the drop-in call's network)")
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--min-tiles", default="32,96,256", help="C2FB_MIN_TILES values to compare")
@@ -34,12 +35,12 @@ def main():
     frames = torch.randint(0, 256, (B, 640, 640, 3), generator=torch.Generator().manual_seed(1),
                            dtype=torch.uint8).cuda()
     variants = {}
-    off = S.SegNet(arch, fw, dtype="bf16")
+    off = S.SegNet(arch, fw, dtype=a.dtype)
     off.c2fb_max_b = 0
     variants["unfused"] = off
     for mt in [int(v) for v in a.min_tiles.split(",") if v]:
         S.C2FB_MIN_TILES = mt
-        net = S.SegNet(arch, fw, dtype="bf16")
+        net = S.SegNet(arch, fw, dtype=a.dtype, c2fb_f32=True)
         net.c2fb_max_b = B
         plan = net.plan(B, 640, 640)  # tile sides are chosen at planning time
         variants[f"c2fb_min{mt}"] = net
@@ -88,7 +89,7 @@ def main():
         for nm, us in ops[k]:
             if "C2f" in nm or k == "unfused":
                 print(f"   {nm:50s} {us:8.2f}")
-    out = {"batch": B, "scale": a.scale, "seg_only": summary, "ops_us": ops}
+    out = {"batch": B, "scale": a.scale, "dtype": a.dtype, "seg_only": summary, "ops_us": ops}
     print(json.dumps(summary))
     if a.json:
         with open(a.json, "w") as f:

@@ -229,6 +229,247 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
     xb_conv<C, NB, 2>(g, smem, 2 * NB + 1, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
 }
 
+// ---- the f32 form (the reference's precision: the drop-in call's batch-1 network, FrameProcessor.py:322) ----
+// The same block with every value an f32: the regions hold f32 in LDS, each operand is split on read into three exact
+// bf16 terms (x = h + m + l, va_seg.hip split3_bf16) and a product is the six term products h.h, h.m, m.h, h.l, m.m,
+// l.h accumulated in f32 on the bf16 MFMA -- the arithmetic of the unfused f32 layers (va_seg.hip §f32), in another
+// summation order.  The weights come pre-split (three fragments per 16 x 32 tile).  cv1 reads its operand straight
+// from global memory (an f32 input region of the wide blocks would not fit beside R0), computing the b half on all
+// of R0's pixels and the a half only at the tile's own pixels (R0a).
+constexpr int XF_G = 2;   // 16-pixel blocks per work item
+constexpr int XF_KC = 4;  // K-steps loaded ahead
+
+struct XfGeom {
+    const float* x;
+    const float* xu;
+    float* y;
+    const bf16x8* w;  // three-term fragments: conv q's tile (cb, k) at w + 192 * (wf[q] + cb * ks + k), [3][64]
+    const float* b;
+    int N, H, W, ci, cu, ldx, ldu, co, ldy;
+    int T, tx, tpf, sc;
+    int off_r0a;      // LDS offset of R0a (the a half at the tile's T x T pixels)
+    int off_r[5];     // R0b (the b half on all of R0), R1 .. R2n
+    int wf[6], bo[6];
+};
+
+template <int C>
+constexpr int pf() { return 4 * C + 16; }
+
+__device__ __forceinline__ unsigned xf_pk(f32x2 v) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+__device__ __forceinline__ f32x2 xf_unpk(unsigned p) {
+    return (f32x2){__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
+}
+// eight f32 -> three bf16x8 terms, round to nearest even each (va_seg.hip split3_bf16: the same terms)
+__device__ __forceinline__ void xf_split3(const f32x4& lo, const f32x4& hi, bf16x8 (&t)[3]) {
+    unsigned w[3][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const f32x4& c = e < 2 ? lo : hi;
+        const f32x2 x = {c[2 * (e & 1)], c[2 * (e & 1) + 1]};
+        w[0][e] = xf_pk(x);
+        const f32x2 r = x - xf_unpk(w[0][e]);
+        w[1][e] = xf_pk(r);
+        w[2][e] = xf_pk(r - xf_unpk(w[1][e]));
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = __builtin_bit_cast(bf16x8, (u32x4){w[k][0], w[k][1], w[k][2], w[k][3]});
+}
+__device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
+    c = mma(a[0], b[0], c);
+    c = mma(a[0], b[1], c);
+    c = mma(a[1], b[0], c);
+    c = mma(a[0], b[2], c);
+    c = mma(a[1], b[1], c);
+    return mma(a[2], b[0], c);
+}
+
+// One f32 conv of the block (xb_conv's roles): KIND 0 = cv1 rows cb0 * 16 .. from global memory onto dst; 1 = 3x3
+// from src (+ res); 2 = cv2 over [R0a | R0b | R2 | R4 ..] at the tile's pixels, to g.y.
+template <int C, int NB, int KIND>
+__device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, int q, int cb0, int nout, int kel, int ow,
+                                        int oy, int ox, int n, XbIo src, XbIo dst, XbIo res, int lane, int wid) {
+    constexpr int H2 = 2 * NB;
+    const int ks = (kel + 31) >> 5, ncb = (nout + 15) >> 4;
+    const int P = ow * ow, npb = (P + 15) >> 4, ngr = (npb + XF_G - 1) / XF_G;
+    const int items = ngr * ncb;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int S0 = g.T + 2 * H2;
+    for (int it = wid; it < items; it += XB_NW) {
+        const int cb = it % ncb, gr = it / ncb;
+        const int nb = min(XF_G, npb - gr * XF_G);
+        int pr[XF_G], pc[XF_G], base[XF_G];
+        int64_t gx[XF_G], gu[XF_G];  // KIND 0: element offsets of the pixel in x / xu (-1: outside the frame)
+#pragma unroll
+        for (int j = 0; j < XF_G; ++j) {
+            int p = ((gr * XF_G + j) << 4) + fr;
+            p = p < P ? p : P - 1;
+            const int r = p / ow, c = p - r * ow;
+            pr[j] = r;
+            pc[j] = c;
+            base[j] = KIND == 1 ? src.off + (r * src.w + c) * src.ps : 0;
+            if constexpr (KIND == 0) {
+                const int iy = oy + r, ix = ox + c;
+                const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+                gx[j] = in ? ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldx : -1;
+                gu[j] = in ? ((int64_t)(n * (g.H >> 1) + (iy >> 1)) * (g.W >> 1) + (ix >> 1)) * g.ldu : -1;
+            }
+        }
+        f32x4 acc[XF_G];
+#pragma unroll
+        for (int j = 0; j < XF_G; ++j) acc[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+        const bf16x8* wb = g.w + (int64_t)192 * (g.wf[q] + (cb0 + cb) * ks) + lane;
+        // the lane's B element offset for K-step k of block j (LDS byte offset; KIND 0: handled in load_b)
+        auto lds_addr = [&](int k, int j) {
+            const int kk = min((k << 5) + (fq << 3), kel - 8);
+            if constexpr (KIND == 1) {
+                const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
+                return base[j] + (ky * src.w + kx) * src.ps + ch * 4;
+            } else {
+                if (kk < C) return g.off_r0a + (pr[j] * g.T + pc[j]) * pf<C>() + kk * 4;
+                if (kk < 2 * C) return g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * pf<C>() + (kk - C) * 4;
+                const int s = (kk - 2 * C) / C + 1, ch = kk - (s + 1) * C;
+                const int hs = H2 - 2 * s, ws = g.T + 2 * hs;
+                return g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * pf<C>() + ch * 4;
+            }
+        };
+        // K-steps in chunks of KC, double-buffered: the next chunk's A fragments (and, for cv1, its B operands from
+        // global memory) are in flight while this chunk's MFMAs run; B from LDS is read as it is used
+        constexpr int KC = KIND == 0 ? 2 : XF_KC;
+        bf16x8 a0[KC][3], a1[KC][3];
+        f32x4 b0[KC][XF_G][2], b1[KC][XF_G][2];
+        auto load = [&](bf16x8 (&a)[KC][3], f32x4 (&bv)[KC][XF_G][2], int k0) {
+#pragma unroll
+            for (int i = 0; i < KC; ++i) {
+                if (k0 + i < ks) {
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) a[i][t] = wb[192 * (k0 + i) + 64 * t];
+                    if constexpr (KIND == 0) {
+                        const int kk = min(((k0 + i) << 5) + (fq << 3), kel - 8);
+                        const bool up = kk < g.cu;
+#pragma unroll
+                        for (int j = 0; j < XF_G; ++j) {
+                            const int64_t o = up ? gu[j] : gx[j];
+                            if (j < nb && o >= 0) {
+                                const float* p = (up ? g.xu : g.x) + o + kk;
+                                bv[i][j][0] = *(const f32x4*)p;
+                                bv[i][j][1] = *(const f32x4*)(p + 4);
+                            } else {
+                                bv[i][j][0] = bv[i][j][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                            }
+                        }
+                    }
+                }
+            }
+        };
+        auto compute = [&](const bf16x8 (&a)[KC][3], const f32x4 (&bv)[KC][XF_G][2], int k0) {
+#pragma unroll
+            for (int i = 0; i < KC; ++i) {
+                if (k0 + i < ks) {
+#pragma unroll
+                    for (int j = 0; j < XF_G; ++j) {
+                        if (j < nb) {
+                            bf16x8 bt[3];
+                            if constexpr (KIND == 0) {
+                                xf_split3(bv[i][j][0], bv[i][j][1], bt);
+                            } else {
+                                const unsigned char* p = smem + lds_addr(k0 + i, j);
+                                xf_split3(*(const f32x4*)p, *(const f32x4*)(p + 16), bt);
+                            }
+                            acc[j] = mma6(a[i], bt, acc[j]);
+                        }
+                    }
+                }
+            }
+        };
+        load(a0, b0, 0);
+        for (int k0 = 0; k0 < ks; k0 += 2 * KC) {
+            load(a1, b1, k0 + KC);
+            compute(a0, b0, k0);
+            load(a0, b0, k0 + 2 * KC);
+            compute(a1, b1, k0 + KC);
+        }
+        const int co = (cb << 4) + (fq << 2);
+        if (co >= nout) continue;
+        const f32x4 bias = *(const f32x4*)(g.b + g.bo[q] + 16 * cb0 + co);
+#pragma unroll
+        for (int j = 0; j < XF_G; ++j) {
+            const int p = ((gr * XF_G + j) << 4) + fr;
+            if (j >= nb || p >= P) continue;
+            const int r = pr[j], c = pc[j], iy = oy + r, ix = ox + c;
+            const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+            f32x4 v = fz::act(acc[j] + bias);
+            if (KIND == 1 && res.off >= 0)
+                v += *(const f32x4*)(smem + res.off + ((r + 2) * res.w + c + 2) * res.ps + (res.c0 + co) * 4);
+            if constexpr (KIND == 2) {
+                if (in) *(f32x4*)(g.y + ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldy + co) = v;
+            } else {
+                if (!in) v = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+                *(f32x4*)(smem + dst.off + p * dst.ps + (dst.c0 + co) * 4) = v;
+            }
+        }
+    }
+}
+
+template <int C, int NB>
+__global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int H2 = 2 * NB;
+    const int T = g.T, S0 = T + 2 * H2;
+    const int t = blockIdx.x, n = t / g.tpf, tt = t - n * g.tpf, ty = tt / g.tx, tx = tt - ty * g.tx;
+    const int y0 = ty * T, x0 = tx * T;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const XbIo none = {-1, 0, 0, 0};
+    const XbIo r0b = {g.off_r[0], S0, pf<C>(), 0}, r0a = {g.off_r0a, T, pf<C>(), 0};
+    xf_conv<C, NB, 0>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
+    xf_conv<C, NB, 0>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int hs = H2 - 2 * j, ws = T + 2 * hs;
+        const XbIo rin = j == 0 ? r0b : XbIo{g.off_r[2 * j], ws, pf<C>(), 0};
+        const XbIo rmid = {g.off_r[2 * j + 1], ws - 2, pf<C>(), 0}, rout = {g.off_r[2 * j + 2], ws - 4, pf<C>(), 0};
+        xf_conv<C, NB, 1>(g, smem, 1 + 2 * j, 0, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane,
+                          wid);
+        __syncthreads();
+        xf_conv<C, NB, 1>(g, smem, 2 + 2 * j, 0, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
+                          g.sc ? rin : none, lane, wid);
+        __syncthreads();
+    }
+    xf_conv<C, NB, 2>(g, smem, 2 * NB + 1, 0, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
+}
+
+// f32 LDS layout: [R0b][R0a][R1] .. [R2n]; returns the bytes (or -1)
+int xf_layout(int C, int NB, int T, int* off_r0a, int* off_r) {
+    if (T < 1 || T > 64) return -1;
+    const int S0 = T + 4 * NB, ps = 4 * C + 16;
+    int64_t o = (int64_t)S0 * S0 * ps;
+    off_r[0] = 0;
+    *off_r0a = (int)o;
+    o += (int64_t)T * T * ps;
+    for (int j = 1; j <= 2 * NB; ++j) {
+        const int s = T + 2 * (2 * NB - j);
+        off_r[j] = (int)o;
+        o += (int64_t)s * s * ps;
+    }
+    return o > XB_LDS_MAX ? -1 : (int)o;
+}
+
+template <int C, int NB>
+hipError_t xf_launch(const XfGeom& g, int lds, int ntiles, hipStream_t st) {
+    static DevFlag attr;
+    if (!attr()) {
+        if (hipFuncSetAttribute((const void*)c2fbf_kernel<C, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                XB_LDS_MAX) != hipSuccess)
+            return hipErrorInvalidValue;
+        attr() = true;
+    }
+    hipLaunchKernelGGL((c2fbf_kernel<C, NB>), dim3(ntiles), dim3(XB_NT), lds, st, g);
+    return hipGetLastError();
+}
+
 // LDS layout of one configuration: [R0][IN, later R1 .. R2n]; returns the bytes (or -1)
 int xb_layout(int C, int NB, int ci, int T, int* off_r, int* in_off, int* psi) {
     if (T < 1 || T > 64) return -1;
@@ -276,21 +517,29 @@ hipError_t xb_launch(const XbGeom& g, int lds, int ntiles, hipStream_t st) {
     return hipGetLastError();
 }
 
-bool xb_shape_ok(int C, int NB) { return (C == 16 || C == 32 || C == 64 || C == 128) && (NB == 1 || NB == 2); }
+bool xb_shape_ok(int C, int NB, bool f32 = false) {
+    return (C == 16 || C == 32 || C == 64 || C == 128 || (f32 && C == 256)) && (NB == 1 || NB == 2);
+}
 
 }  // namespace
 
-extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int64_t* out3) {
-    if (!out3 || !xb_shape_ok(c, n) || ci <= 0 || co <= 0) return VA_ERR_ARG;
+extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int64_t* out3) {
+    const bool f32 = dtype == VA_DTYPE_F32;
+    if (!out3 || !xb_shape_ok(c, n, f32) || ci <= 0 || co <= 0 || (!f32 && dtype != VA_DTYPE_BF16)) return VA_ERR_ARG;
     int off_r[5], in_off, psi, wf[6], bo[6];
-    const int lds = xb_layout(c, n, ci, T, off_r, &in_off, &psi);
+    const int lds = f32 ? xf_layout(c, n, T, &in_off, off_r) : xb_layout(c, n, ci, T, off_r, &in_off, &psi);
     xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2]);
+    if (f32) out3[1] *= 3;  // three term fragments per tile
     out3[0] = lds;
     return lds < 0 ? VA_ERR_ARG : VA_OK;
 }
 
+static int c2fb_f32(const va_conv_args* a, hipStream_t st);
+
 extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
-    if (!a || !a->x || !a->w || !a->bias || !a->y || a->dtype != VA_DTYPE_BF16) return VA_ERR_ARG;
+    if (!a || !a->x || !a->w || !a->bias || !a->y || (a->dtype != VA_DTYPE_BF16 && a->dtype != VA_DTYPE_F32))
+        return VA_ERR_ARG;
+    if (a->dtype == VA_DTYPE_F32) return c2fb_f32(a, (hipStream_t)stream);
     const int C = a->Npad, NB = a->kh, T = a->stride, ci = a->Cin, co = a->Cout;
     if (!xb_shape_ok(C, NB) || a->N <= 0 || a->H <= 0 || a->W <= 0 || ci % 8 || co % 16 || ci <= 0 || co <= 0 ||
         a->ldx % 8 || a->ldy % 8 || a->ldx < ci || a->ldy < co || ((uintptr_t)a->x & 15) || ((uintptr_t)a->y & 15) ||
@@ -326,6 +575,47 @@ extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
         case 64 * 4 + 2: rc = xb_launch<64, 2>(g, lds, (int)nt, st); break;
         case 128 * 4 + 1: rc = xb_launch<128, 1>(g, lds, (int)nt, st); break;
         default: rc = xb_launch<128, 2>(g, lds, (int)nt, st); break;
+    }
+    return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
+    const int C = a->Npad, NB = a->kh, T = a->stride, ci = a->Cin, co = a->Cout;
+    if (!xb_shape_ok(C, NB, true) || a->N <= 0 || a->H <= 0 || a->W <= 0 || ci % 8 || co % 16 || ci <= 0 || co <= 0 ||
+        a->ldx % 4 || a->ldy % 4 || a->ldx < ci || a->ldy < co || ((uintptr_t)a->x & 15) || ((uintptr_t)a->y & 15) ||
+        ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15))
+        return VA_ERR_ARG;
+    if (a->xu && (a->cu <= 0 || a->cu % 8 || a->cu >= ci || a->ldu % 4 || a->ldu < a->cu || a->H % 2 || a->W % 2 ||
+                  ((uintptr_t)a->xu & 15)))
+        return VA_ERR_ARG;
+    XfGeom g;
+    const int lds = xf_layout(C, NB, T, &g.off_r0a, g.off_r);
+    if (lds < 0) return VA_ERR_ARG;
+    int64_t frags, biases;
+    xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases);
+    g.x = (const float*)a->x;
+    g.xu = (const float*)a->xu;
+    g.y = (float*)a->y;
+    g.w = (const bf16x8*)a->w;
+    g.b = a->bias;
+    g.N = a->N, g.H = a->H, g.W = a->W, g.ci = ci, g.cu = a->xu ? a->cu : 0, g.ldx = a->ldx, g.ldu = a->ldu;
+    g.co = co, g.ldy = a->ldy, g.T = T, g.sc = a->kw ? 1 : 0;
+    g.tx = (a->W + T - 1) / T;
+    const int64_t tpf = (int64_t)g.tx * ((a->H + T - 1) / T), nt = tpf * a->N;
+    if (nt > INT32_MAX) return VA_ERR_ARG;
+    g.tpf = (int)tpf;
+    hipError_t rc;
+    switch (C * 4 + NB) {
+        case 16 * 4 + 1: rc = xf_launch<16, 1>(g, lds, (int)nt, st); break;
+        case 16 * 4 + 2: rc = xf_launch<16, 2>(g, lds, (int)nt, st); break;
+        case 32 * 4 + 1: rc = xf_launch<32, 1>(g, lds, (int)nt, st); break;
+        case 32 * 4 + 2: rc = xf_launch<32, 2>(g, lds, (int)nt, st); break;
+        case 64 * 4 + 1: rc = xf_launch<64, 1>(g, lds, (int)nt, st); break;
+        case 64 * 4 + 2: rc = xf_launch<64, 2>(g, lds, (int)nt, st); break;
+        case 128 * 4 + 1: rc = xf_launch<128, 1>(g, lds, (int)nt, st); break;
+        case 128 * 4 + 2: rc = xf_launch<128, 2>(g, lds, (int)nt, st); break;
+        case 256 * 4 + 1: rc = xf_launch<256, 1>(g, lds, (int)nt, st); break;
+        default: rc = xf_launch<256, 2>(g, lds, (int)nt, st); break;
     }
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
 }

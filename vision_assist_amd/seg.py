@@ -149,9 +149,11 @@ class SegOutputs:
 
 
 class SegNet:
-    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2f32: bool = False):
+    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2f32: bool = False,
+                 c2fb_f32: bool = False):
         """c2f32: run model.2 on the fused f32 C2f kernel (va_seg_c2f_f32) in f32 plans -- off by default: it measured
-        slower than the block's four launches."""
+        slower than the block's four launches.  c2fb_f32: the batch-1 C2f blocks of f32 plans on
+        va_seg_c2fb's f32 form -- off by default, measured slower."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
@@ -223,9 +225,13 @@ class SegNet:
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
         # small batches (bf16): every C2f block as one launch, intermediates on the chip and the 3x3s' halo recomputed
-        # per tile (va355.h va_seg_c2fb), for B <= c2fb_max_b; VA_C2FB=0 keeps the blocks' layers apart (A/B).
-        # c2fb_tile: per block index a tile side overriding _c2fb_tile's choice (tools / tests)
-        self.c2fb_max_b = C2FB_MAX_B if (dtype == "bf16" and os.environ.get("VA_C2FB", "1") != "0") else 0
+        # per tile (va355.h va_seg_c2fb), for B <= c2fb_max_b; VA_C2FB=0 keeps the blocks' layers apart (A/B).  The
+        # f32 form of the same kernel is opt-in (c2fb_f32=True): its six term products per product put 6x the MFMA
+        # work of the halo recompute on the few dozen workgroups a batch-1 block has, and the s-seg batch-1 forward
+        # measured 1.28 -> 1.67 ms with it.  c2fb_tile: per block index a tile side overriding
+        # _c2fb_tile's choice (tools / tests)
+        on = os.environ.get("VA_C2FB", "1") != "0" and (dtype == "bf16" or (dtype == "f32" and c2fb_f32))
+        self.c2fb_max_b = C2FB_MAX_B if on else 0
         self.c2fb = {}
         self.c2fb_tile = {}
         # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32), on request (c2f32)
@@ -253,9 +259,10 @@ class SegNet:
 
     def _pack_c2fb(self, i: int, n: int):
         """(weight blob, bias blob) of va_seg_c2fb for C2f block ``model.{i}`` with n Bottlenecks: per conv (cv1,
-        m.j.cv1 / m.j.cv2, cv2) the packed bf16 rows [Cout][K] (the unfused layers' own weights, K ordered (ky, kx,
+        m.j.cv1 / m.j.cv2, cv2) the packed rows [Cout][K] (the unfused layers' own weights, K ordered (ky, kx,
         ci)) zero padded to 16 x 32 tiles, tile order [Cout / 16][K / 32], each tile as MFMA A fragment lanes
-        (lane 16 q + r: row r, columns 8 q .. 8 q + 7); biases zero padded to 16 per conv."""
+        (lane 16 q + r: row r, columns 8 q .. 8 q + 7) -- bf16, or in f32 mode three fragments per tile, the exact
+        bf16 terms h, m, l of the f32 weights (split3_bf16's split); biases zero padded to 16 per conv."""
         if i in self.c2fb:
             return self.c2fb[i]
         names = [f"model.{i}.cv1"] + [f"model.{i}.m.{j}.cv{k}" for j in range(n) for k in (1, 2)] + [f"model.{i}.cv2"]
@@ -265,7 +272,14 @@ class SegNet:
             ncb, ks = _cdiv(p.cout, 16), _cdiv(p.K, 32)
             wm = torch.zeros(16 * ncb, 32 * ks, dtype=p.w.dtype, device=p.w.device)
             wm[:p.cout, :p.K] = p.w[:p.cout, :p.K]
-            frags.append(wm.reshape(ncb, 16, ks, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1))
+            if self.store == "f32":
+                h = wm.to(torch.bfloat16)
+                r = wm - h.float()
+                m = r.to(torch.bfloat16)
+                t3 = torch.stack([h, m, (r - m.float()).to(torch.bfloat16)])  # [3][16 ncb][32 ks]
+                frags.append(t3.reshape(3, ncb, 16, ks, 4, 8).permute(1, 3, 0, 4, 2, 5).reshape(-1))
+            else:
+                frags.append(wm.reshape(ncb, 16, ks, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1))
             b = torch.zeros(16 * ncb, dtype=torch.float32, device=p.b.device)
             b[:p.cout] = p.b[:p.cout].float()
             biases.append(b)
@@ -275,7 +289,7 @@ class SegNet:
     def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int):
         """(LDS bytes or -1, A fragments, bias floats) of va_seg_c2fb's layout (va355.h va_c2fb_layout)."""
         out = (ctypes.c_int64 * 3)()
-        rc = self.lib.va_c2fb_layout(c, n, ci, co, T, out)
+        rc = self.lib.va_c2fb_layout(c, n, ci, co, T, self.va_dtype, out)
         return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]))
 
     def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int) -> int:
@@ -616,14 +630,14 @@ class SegNet:
                              "bytes": 4 * B * h * w * 128})
                 return
             c = co // 2
-            if (pre is None and B <= self.c2fb_max_b and c in (16, 32, 64, 128) and n in (1, 2) and ci % 8 == 0 and
+            if (pre is None and B <= self.c2fb_max_b and c in (16, 32, 64, 128, 256) and n in (1, 2) and ci % 8 == 0 and
                     co % 16 == 0 and src.ld % 8 == 0 and dst.ld % 8 == 0 and (up is None or up.ld % 8 == 0) and
                     src.c == ci):
                 T = self._c2fb_tile(i, B, h, w, ci, co, n)
                 if T:
                     blob, bias = self._pack_c2fb(i, n)
                     args = ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=ci, ldx=src.ld, w=blob.data_ptr(),
-                                    bias=bias.data_ptr(), Cout=co, y=dst.ptr, ldy=dst.ld, dtype=VA_DTYPE_BF16, mode=3,
+                                    bias=bias.data_ptr(), Cout=co, y=dst.ptr, ldy=dst.ld, dtype=self.va_dtype, mode=3,
                                     kh=n, kw=1 if shortcut else 0, Npad=c, stride=T)
                     if up is not None:
                         args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
@@ -631,7 +645,7 @@ class SegNet:
                     macs = ci * 2 * c + n * 2 * 9 * c * c + (2 + n) * c * co  # per output pixel, without the halo
                     meta.append({"name": f"model.{i} (fused C2f, T={T})", "kind": "conv", "M": B * h * w, "N": co,
                                  "K": macs // co, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
-                                 "bytes": 2 * B * h * w * (ci + co)})
+                                 "bytes": (2 if self.store == "bf16" else 4) * B * h * w * (ci + co)})
                     return
             if pre is None and i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
