@@ -287,17 +287,23 @@ int va_seg_stem(void* stream, const va_conv_args* a);
  *            [Cout][K] weights (K ordered (ky, kx, ci)) zero padded to 16-row x 32-column tiles, in tile order
  *            [Cout / 16][K / 32], each tile as 64 lanes x 8 (lane 16 q + r: row r, columns 8 q .. 8 q + 7)
  *   a.bias   float, per conv its biases zero padded to a multiple of 16, in the same order
+ * Optional stride-2 prologue (bf16; a.res != NULL): the block's input channels [0, cs) are Conv(cis -> cs, 3x3,
+ * stride 2, pad 1) + bias + SiLU of a.res ([N][2H][2W], channel stride a.ldr), computed per tile from its (2(T + 4n)
+ * + 1)^2 source pixels -- the backbone's / PAN's stride-2 convs (model.3 / 5 / 7 / 16 / 19) whose only consumer is
+ * the block; a.c2 = cs (% 16 == 0, <= ci), a.K = cis (a power of two, 8 .. 512), the conv's tiles and biases after
+ * cv2's in a.w / a.bias; x's first cs channels are not read; no xu.
  * ldx, ldy, ldu % 8 == 0; x, xu, y, w, bias 16-byte aligned.  Replaces the block's 2n + 2 va_seg_conv calls
  * (block.py C2f, Bottleneck) inside YOLO.predict (FrameProcessor.py:322).  VA_OP_C2F with a.mode == 3.
  * a.dtype = VA_DTYPE_F32 (the reference's precision; c up to 256): float activations (ldx, ldy, ldu % 4 == 0), every
  * product as six exact bf16 term products (va_seg_conv's f32 arithmetic), a.w = the same tiles as three fragments
  * each (h, m, l: the exact three-term bf16 split of the f32 weights, [tile][3][64 lanes][8]). */
 int va_seg_c2fb(void* stream, const va_conv_args* a);
-/* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels, tile side T and dtype: out[0] = LDS bytes
- * per workgroup, out[1] = A fragments (64 lanes x 8 bf16) of the weight blob, out[2] = floats of the bias blob.
- * VA_ERR_ARG when the shape is not covered or the layout exceeds the 160 KiB of LDS (out[1], out[2] still set for a
- * covered shape). */
-int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int64_t* out);
+/* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels, tile side T, dtype and the stride-2
+ * prologue's cs / cis channels (0, 0: none): out[0] = LDS bytes per workgroup, out[1] = A fragments (64 lanes x 8
+ * bf16) of the weight blob, out[2] = floats of the bias blob.  VA_ERR_ARG when the shape is not covered or the layout
+ * exceeds the 160 KiB of LDS (out[1], out[2] still set for a covered shape). */
+int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int32_t cs, int32_t cis,
+                   int64_t* out);
 /* The same C2f block in f32 (the headline's precision) as ONE launch, every intermediate on the chip as three exact
  * bf16 planes, the convs as six exact term products: a.x / a.ldx (float, 64 channels, ldx % 4 == 0), a.y / a.ldy
  * (float, ldy % 4 == 0), a.N / H / W, a.Cin = a.Cout = 64, a.dtype = VA_DTYPE_F32, and

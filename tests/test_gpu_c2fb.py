@@ -125,6 +125,9 @@ def test_c2fb_forward_vs_unfused(monkeypatch):
     arch, fw, net = _net()
     names = [m["name"] for m in net.plan(1, 640, 640)["meta"]]
     assert sum("fused C2f, T=" in nm for nm in names) == 8, names
+    # the stride-2 prologues where they leave the block its tile side (model.5 stays a launch of its own)
+    assert [nm.split("+")[0] for nm in names if "+model." in nm and "C2f" in nm] == \
+        ["model.3", "model.7", "model.16", "model.19"], names
     frames = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(4), dtype=torch.uint8)
 
     def heads(nt):
@@ -212,3 +215,48 @@ def test_c2fb_f32_forward_vs_unfused():
     ref = torch.cat([box, cls, coef], 1)
     assert (lv - ref).abs().max().item() <= 1e-3
     assert (fused[3].permute(0, 3, 1, 2) - proto).abs().max().item() <= 1e-3
+
+
+S2_CASES = [(4, "model.3", 1, 80, 80, 0), (6, "model.5", 1, 40, 40, 0), (8, "model.7", 1, 20, 20, 0),
+            (18, "model.16", 1, 40, 40, 0), (21, "model.19", 1, 20, 20, 0), (4, "model.3", 2, 10, 14, 4),
+            (21, "model.19", 2, 6, 10, 2)]
+
+
+@pytest.mark.parametrize("i,s2,B,H,W,T", S2_CASES)
+def test_c2fb_stride2_prologue(i, s2, B, H, W, T):
+    """The stride-2 conv that feeds a block (model.3 / 5 / 7 / 16 / 19 of n-seg) as va_seg_c2fb's prologue: the block's
+    first cs input channels computed per tile from the 2x-resolution source (x's first cs channels are NaN, never
+    read; for model.18 / .21 the rest of the concat comes from x), against the conv + block in fp32 with the unfused
+    layers' bf16 rounding; T = 0: the planner's tile side."""
+    from vision_assist_amd import _lib
+    from vision_assist_amd import seg as S
+    blk = next(b for b in N_BLOCKS if b[0] == i)
+    _, ci, co, n, sc, cu, _, _ = blk
+    arch, fw, net = _net()
+    ps2 = net.w[s2]
+    cs, cis = ps2.cout, ps2.cin
+    T = T or net._c2fb_tile(i, B, H, W, ci, co, n, cs, cis)
+    assert T > 0
+    g = torch.Generator().manual_seed(i * 31 + B)
+    xs = (torch.randn(B, 2 * H, 2 * W, cis, generator=g) * 1.5).to(torch.bfloat16)
+    xsd = torch.zeros(B, 2 * H, 2 * W, cis + 8, dtype=torch.bfloat16)
+    xsd[..., :cis] = xs
+    rest = (torch.randn(B, H, W, ci - cs, generator=g) * 1.5).to(torch.bfloat16)
+    xin = torch.full((B, H, W, ci + 8), float("nan"), dtype=torch.bfloat16)
+    xin[..., cs:ci] = rest
+    xd, xsdd = xin.cuda(), xsd.cuda()
+    y = torch.full((B, H, W, co + 16), 7.0, dtype=torch.bfloat16, device="cuda")
+    blob, bias = net._pack_c2fb(i, n, s2)
+    a = S.ConvArgs(x=xd.data_ptr(), N=B, H=H, W=W, Cin=ci, ldx=ci + 8, w=blob.data_ptr(), bias=bias.data_ptr(),
+                   Cout=co, y=y.data_ptr(), ldy=co + 16, dtype=S.VA_DTYPE_BF16, mode=3, kh=n, kw=1 if sc else 0,
+                   Npad=co // 2, stride=T, res=xsdd.data_ptr(), ldr=cis + 8, c2=cs, K=cis)
+    _lib.check(_lib.load().va_seg_c2fb(_lib.stream_ptr(), ctypes.byref(a)), "va_seg_c2fb")
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert (got[..., co:] == 7.0).all(), "wrote outside its channel slice"
+    bf = lambda t: t.to(torch.bfloat16).float()
+    w2, b2 = fw[s2]
+    head = bf(F.silu(F.conv2d(xs.float().permute(0, 3, 1, 2), bf(w2.float()), b2.float(), stride=2, padding=1)))
+    x = torch.cat([head, rest.float().permute(0, 3, 1, 2)], 1)
+    ref = _block_ref(x, fw, i, n, sc).permute(0, 2, 3, 1)
+    _check(got[..., :co], ref)

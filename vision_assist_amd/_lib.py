@@ -57,7 +57,7 @@ SIGNATURES = [
     ("va_seg_conv", I32, [P, P]),
     ("va_seg_c2f", I32, [P, P]),
     ("va_seg_c2fb", I32, [P, P]),
-    ("va_c2fb_layout", I32, [I32, I32, I32, I32, I32, I32, ctypes.POINTER(I64)]),
+    ("va_c2fb_layout", I32, [I32, I32, I32, I32, I32, I32, I32, I32, ctypes.POINTER(I64)]),
     ("va_seg_stem", I32, [P, P]),
     ("va_seg_stem_f32", I32, [P, P]),
     ("va_seg_c2f_f32", I32, [P, P]),

@@ -48,7 +48,11 @@ struct XbGeom {
     int psi;          // LDS bytes per pixel of the input region
     int in_off;       // LDS offset of the input region (R1 .. R2n alias it once cv1 has read it)
     int off_r[5];     // LDS offsets of R0 .. R2n
-    int wf[6], bo[6]; // per conv (cv1, m.0.cv1, m.0.cv2, [m.1.cv1, m.1.cv2,] cv2)
+    int wf[7], bo[7]; // per conv (cv1, m.0.cv1, m.0.cv2, [m.1.cv1, m.1.cv2,] cv2[, the stride-2 prologue])
+    // optional stride-2 prologue: input channels [0, cs) are Conv(cis -> cs, 3x3, s2, p1) + SiLU of xs ([N][2H][2W],
+    // channel stride ldxs), computed per tile from the source region SR ((2 S0 + 1)^2 pixels) staged at off_sr
+    const __bf16* xs;
+    int ldxs, cs, cis, lgcis, off_sr, pss;
 };
 
 // conv q's shape: output channels, K (elements), K-steps of 32
@@ -102,6 +106,7 @@ __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, in
             pc[j] = c;
             if constexpr (KIND == 0) base[j] = src.off + p * src.ps;
             else if constexpr (KIND == 1) base[j] = src.off + (r * src.w + c) * src.ps + src.c0 * 2;
+            else if constexpr (KIND == 3) base[j] = src.off + (2 * r * src.w + 2 * c) * src.ps;
             else base[j] = 0;
         }
         f32x4 acc[XB_G];
@@ -118,6 +123,9 @@ __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, in
                         addr = base[j] + kk * 2;
                     } else if constexpr (KIND == 1) {
                         const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
+                        addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
+                    } else if constexpr (KIND == 3) {  // stride 2 from SR: output (r, c) reads SR (2r + ky, 2c + kx)
+                        const int tap = kk >> g.lgcis, ch = kk - (tap << g.lgcis), ky = tap / 3, kx = tap - 3 * ky;
                         addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
                     } else if (kk < 2 * C) {
                         addr = g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * ps0<C>() + kk * 2;
@@ -183,7 +191,30 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
     const int y0 = ty * T, x0 = tx * T;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // the input region, eight 16-byte loads in flight per thread before their LDS stores
-    const int cg = g.ci >> 3, total = S0 * S0 * cg;
+    if (g.cs > 0) {  // the stride-2 prologue's source region, zero outside the source frame
+        const int S2 = 2 * S0 + 1, sg = g.cis >> 3, stot = S2 * S2 * sg, sy0 = 2 * (y0 - H2) - 1, sx0 = 2 * (x0 - H2) - 1;
+        for (int q0 = tid; q0 < stot; q0 += 8 * XB_NT) {
+            u32x4 v[8];
+            int dst[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int qq = q0 + i * XB_NT;
+                v[i] = (u32x4){0u, 0u, 0u, 0u};
+                dst[i] = -1;
+                if (qq < stot) {
+                    const int px = qq / sg, ch = (qq - px * sg) << 3;
+                    const int ry = px / S2, rx = px - ry * S2, iy = sy0 + ry, ix = sx0 + rx;
+                    dst[i] = g.off_sr + px * g.pss + ch * 2;
+                    if (iy >= 0 && iy < 2 * g.H && ix >= 0 && ix < 2 * g.W)
+                        v[i] = *(const u32x4*)(g.xs + ((int64_t)(n * 2 * g.H + iy) * 2 * g.W + ix) * g.ldxs + ch);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (dst[i] >= 0) *(u32x4*)(smem + dst[i]) = v[i];
+        }
+    }
+    const int cg = (g.ci - g.cs) >> 3, total = S0 * S0 * cg;  // the channels not produced by the prologue
     for (int q0 = tid; q0 < total; q0 += 8 * XB_NT) {
         u32x4 v[8];
         int dst[8];
@@ -193,7 +224,7 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
             v[i] = (u32x4){0u, 0u, 0u, 0u};
             dst[i] = -1;
             if (qq < total) {
-                const int px = qq / cg, ch = (qq - px * cg) << 3;
+                const int px = qq / cg, ch = g.cs + ((qq - px * cg) << 3);
                 const int ry = px / S0, rx = px - ry * S0, iy = y0 - H2 + ry, ix = x0 - H2 + rx;
                 dst[i] = g.in_off + px * g.psi + ch * 2;
                 if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) {
@@ -211,9 +242,13 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
     }
     __syncthreads();
     const XbIo none = {-1, 0, 0, 0};
-    const XbIo r0 = {g.off_r[0], S0, ps0<C>(), 0};
-    xb_conv<C, NB, 0>(g, smem, 0, 2 * C, g.ci, S0, y0 - H2, x0 - H2, n, XbIo{g.in_off, S0, g.psi, 0}, r0, none, lane,
-                      wid);
+    const XbIo r0 = {g.off_r[0], S0, ps0<C>(), 0}, rin = {g.in_off, S0, g.psi, 0};
+    if (g.cs > 0) {  // IN channels [0, cs) = the stride-2 conv of SR (zero outside the frame)
+        xb_conv<C, NB, 3>(g, smem, 2 * NB + 2, g.cs, 9 * g.cis, S0, y0 - H2, x0 - H2, n,
+                          XbIo{g.off_sr, 2 * S0 + 1, g.pss, 0}, rin, none, lane, wid);
+        __syncthreads();
+    }
+    xb_conv<C, NB, 0>(g, smem, 0, 2 * C, g.ci, S0, y0 - H2, x0 - H2, n, rin, r0, none, lane, wid);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -471,10 +506,17 @@ hipError_t xf_launch(const XfGeom& g, int lds, int ntiles, hipStream_t st) {
 }
 
 // LDS layout of one configuration: [R0][IN, later R1 .. R2n]; returns the bytes (or -1)
-int xb_layout(int C, int NB, int ci, int T, int* off_r, int* in_off, int* psi) {
+int xb_layout(int C, int NB, int ci, int T, int* off_r, int* in_off, int* psi, int cis = 0, int* off_sr = nullptr,
+              int* pss = nullptr) {
     if (T < 1 || T > 64) return -1;
-    const int S0 = T + 4 * NB;
-    const int64_t r0 = (int64_t)S0 * S0 * (4 * C + 16), in = (int64_t)S0 * S0 * (2 * ci + 16);
+    const int S0 = T + 4 * NB, S2 = 2 * S0 + 1;
+    const int64_t r0 = (int64_t)S0 * S0 * (4 * C + 16);
+    int64_t in = (int64_t)S0 * S0 * (2 * ci + 16);
+    if (cis > 0) {  // the prologue's source region after IN (both dead once cv1 has run)
+        *off_sr = (int)(r0 + in);
+        *pss = 2 * cis + 16;
+        in += (int64_t)S2 * S2 * (2 * cis + 16);
+    }
     int64_t rs = 0;
     off_r[0] = 0;
     for (int j = 1; j <= 2 * NB; ++j) {
@@ -490,11 +532,12 @@ int xb_layout(int C, int NB, int ci, int T, int* off_r, int* in_off, int* psi) {
 
 // fragment / bias offsets of the blob (seg.py SegNet._pack_c2fb): conv q = cv1, m.0.cv1, m.0.cv2, .., cv2, each
 // [ceil(nout / 16)][ceil(K / 32)] fragments and 16 ceil(nout / 16) biases; returns the totals
-void xb_blob(int C, int NB, int ci, int co, int* wf, int* bo, int64_t* frags, int64_t* biases) {
+void xb_blob(int C, int NB, int ci, int co, int* wf, int* bo, int64_t* frags, int64_t* biases, int cs = 0,
+             int cis = 0) {
     int64_t f = 0, b = 0;
-    for (int q = 0; q < 2 * NB + 2; ++q) {
-        const int nout = q == 0 ? 2 * C : q == 2 * NB + 1 ? co : C;
-        const int k = q == 0 ? ci : q == 2 * NB + 1 ? (2 + NB) * C : 9 * C;
+    for (int q = 0; q < 2 * NB + 2 + (cs > 0); ++q) {
+        const int nout = q == 0 ? 2 * C : q == 2 * NB + 1 ? co : q == 2 * NB + 2 ? cs : C;
+        const int k = q == 0 ? ci : q == 2 * NB + 1 ? (2 + NB) * C : q == 2 * NB + 2 ? 9 * cis : 9 * C;
         wf[q] = (int)f;
         bo[q] = (int)b;
         f += (int64_t)((nout + 15) / 16) * ((k + 31) / 32);
@@ -517,18 +560,27 @@ hipError_t xb_launch(const XbGeom& g, int lds, int ntiles, hipStream_t st) {
     return hipGetLastError();
 }
 
+// the stride-2 prologue: cs output channels (a multiple of 16, at most ci), cis input channels (a power of two >= 8)
+bool xb_s2_ok(int ci, int cs, int cis) {
+    return cs > 0 && cs % 16 == 0 && cs <= ci && cis >= 8 && cis <= 512 && (cis & (cis - 1)) == 0;
+}
+
 bool xb_shape_ok(int C, int NB, bool f32 = false) {
     return (C == 16 || C == 32 || C == 64 || C == 128 || (f32 && C == 256)) && (NB == 1 || NB == 2);
 }
 
 }  // namespace
 
-extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int64_t* out3) {
+extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int32_t cs,
+                              int32_t cis, int64_t* out3) {
     const bool f32 = dtype == VA_DTYPE_F32;
-    if (!out3 || !xb_shape_ok(c, n, f32) || ci <= 0 || co <= 0 || (!f32 && dtype != VA_DTYPE_BF16)) return VA_ERR_ARG;
-    int off_r[5], in_off, psi, wf[6], bo[6];
-    const int lds = f32 ? xf_layout(c, n, T, &in_off, off_r) : xb_layout(c, n, ci, T, off_r, &in_off, &psi);
-    xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2]);
+    if (!out3 || !xb_shape_ok(c, n, f32) || ci <= 0 || co <= 0 || (!f32 && dtype != VA_DTYPE_BF16) ||
+        (cs && (f32 || !xb_s2_ok(ci, cs, cis))))
+        return VA_ERR_ARG;
+    int off_r[5], in_off, psi, wf[7], bo[7], off_sr, pss;
+    const int lds = f32 ? xf_layout(c, n, T, &in_off, off_r)
+                        : xb_layout(c, n, ci, T, off_r, &in_off, &psi, cs ? cis : 0, &off_sr, &pss);
+    xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2], cs, cis);
     if (f32) out3[1] *= 3;  // three term fragments per tile
     out3[0] = lds;
     return lds < 0 ? VA_ERR_ARG : VA_OK;
@@ -548,11 +600,17 @@ extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
     if (a->xu && (a->cu <= 0 || a->cu % 8 || a->cu >= ci || a->ldu % 8 || a->ldu < a->cu || a->H % 2 || a->W % 2 ||
                   ((uintptr_t)a->xu & 15)))
         return VA_ERR_ARG;
+    // the stride-2 prologue (a.res = its source xs, a.ldr = ldxs, a.c2 = cs, a.K = cis)
+    const int cs = a->res ? a->c2 : 0, cis = a->res ? a->K : 0;
+    if (cs && (!xb_s2_ok(ci, cs, cis) || a->xu || a->ldr % 8 || a->ldr < cis || ((uintptr_t)a->res & 15)))
+        return VA_ERR_ARG;
     XbGeom g;
-    const int lds = xb_layout(C, NB, ci, T, g.off_r, &g.in_off, &g.psi);
+    const int lds = xb_layout(C, NB, ci, T, g.off_r, &g.in_off, &g.psi, cis, &g.off_sr, &g.pss);
     if (lds < 0) return VA_ERR_ARG;
     int64_t frags, biases;
-    xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases);
+    xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases, cs, cis);
+    g.xs = (const __bf16*)a->res;
+    g.ldxs = a->ldr, g.cs = cs, g.cis = cis, g.lgcis = cs ? 31 - __builtin_clz(cis) : 0;
     g.x = (const __bf16*)a->x;
     g.xu = (const __bf16*)a->xu;
     g.y = (__bf16*)a->y;

@@ -257,15 +257,17 @@ class SegNet:
                 if p.cin % 16 == 0:
                     self.w8[prefix] = self._pack_fp8(p)
 
-    def _pack_c2fb(self, i: int, n: int):
+    def _pack_c2fb(self, i: int, n: int, s2: str | None = None):
         """(weight blob, bias blob) of va_seg_c2fb for C2f block ``model.{i}`` with n Bottlenecks: per conv (cv1,
         m.j.cv1 / m.j.cv2, cv2) the packed rows [Cout][K] (the unfused layers' own weights, K ordered (ky, kx,
         ci)) zero padded to 16 x 32 tiles, tile order [Cout / 16][K / 32], each tile as MFMA A fragment lanes
         (lane 16 q + r: row r, columns 8 q .. 8 q + 7) -- bf16, or in f32 mode three fragments per tile, the exact
-        bf16 terms h, m, l of the f32 weights (split3_bf16's split); biases zero padded to 16 per conv."""
-        if i in self.c2fb:
-            return self.c2fb[i]
+        bf16 terms h, m, l of the f32 weights (split3_bf16's split); biases zero padded to 16 per conv.  s2: the
+        stride-2 conv fused as the block's prologue (va355.h va_seg_c2fb), its tiles and biases last."""
+        if (i, s2) in self.c2fb:
+            return self.c2fb[(i, s2)]
         names = [f"model.{i}.cv1"] + [f"model.{i}.m.{j}.cv{k}" for j in range(n) for k in (1, 2)] + [f"model.{i}.cv2"]
+        names += [s2] if s2 else []
         frags, biases = [], []
         for nm in names:
             p = self.w[nm]
@@ -283,22 +285,23 @@ class SegNet:
             b = torch.zeros(16 * ncb, dtype=torch.float32, device=p.b.device)
             b[:p.cout] = p.b[:p.cout].float()
             biases.append(b)
-        self.c2fb[i] = (torch.cat(frags).contiguous(), torch.cat(biases).contiguous())
-        return self.c2fb[i]
+        self.c2fb[(i, s2)] = (torch.cat(frags).contiguous(), torch.cat(biases).contiguous())
+        return self.c2fb[(i, s2)]
 
-    def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int):
-        """(LDS bytes or -1, A fragments, bias floats) of va_seg_c2fb's layout (va355.h va_c2fb_layout)."""
+    def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int, cs: int = 0, cis: int = 0):
+        """(LDS bytes or -1, A fragments, bias floats) of va_seg_c2fb's layout (va355.h va_c2fb_layout); cs / cis:
+        the stride-2 prologue's output / input channels (0: none)."""
         out = (ctypes.c_int64 * 3)()
-        rc = self.lib.va_c2fb_layout(c, n, ci, co, T, self.va_dtype, out)
+        rc = self.lib.va_c2fb_layout(c, n, ci, co, T, self.va_dtype, cs, cis, out)
         return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]))
 
-    def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int) -> int:
+    def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int, cs: int = 0, cis: int = 0) -> int:
         """va_seg_c2fb's tile side for block i at B x h x w: the largest of 16 / 8 / 4 / 2 whose launch has at
         least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
         larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits."""
         if i in self.c2fb_tile:
             return self.c2fb_tile[i]
-        fits = [T for T in (16, 8, 4, 2) if self.c2fb_layout(co // 2, n, ci, co, T)[0] > 0]
+        fits = [T for T in (16, 8, 4, 2) if self.c2fb_layout(co // 2, n, ci, co, T, cs, cis)[0] > 0]
         for T in fits:
             if B * _cdiv(h, T) * _cdiv(w, T) >= C2FB_MIN_TILES:
                 return T
@@ -613,9 +616,16 @@ class SegNet:
                          "prefix": prefix, "src": src, "fp8": on_fp8})
             return ho, wo
 
-        def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None, pre: Slice | None = None):
-            """pre: the block's concat buffer with cv1's output already in it (cv1 fused into the producer)"""
+        def c2f(i, src: Slice, dst: Slice, h, w, up: Slice | None = None, pre: Slice | None = None,
+                s2: tuple | None = None):
+            """pre: the block's concat buffer with cv1's output already in it (cv1 fused into the producer).
+            s2 = (prefix, source slice): the stride-2 conv that writes the block's first input channels (src's first
+            cs), run as the fused block's prologue where va_seg_c2fb takes the block, else as its own op first."""
             _, ci, co, n, shortcut = next(p for p in a.c2f_plan() if p[0] == i)
+            cs = cis = 0
+            if s2 is not None:
+                ps2 = self.w[s2[0]]
+                cs, cis = ps2.cout, ps2.cin
             if pre is not None:
                 c = co // 2
                 t = pre
@@ -634,19 +644,36 @@ class SegNet:
                     co % 16 == 0 and src.ld % 8 == 0 and dst.ld % 8 == 0 and (up is None or up.ld % 8 == 0) and
                     src.c == ci):
                 T = self._c2fb_tile(i, B, h, w, ci, co, n)
+                # the stride-2 prologue where its source region still leaves the block its tile side (a smaller tile
+                # recomputes more of the block than the prologue saves: model.5 + model.6 of n-seg at T = 2 took 74 us
+                # against 15 + 30 apart, profiles/r05/c2fb/ab_b1_s2.log)
+                if s2 is not None and not (self.store == "bf16" and up is None and s2[1].ld % 8 == 0 and
+                                           s2[1].c == cis and cis >= 8 and cis & (cis - 1) == 0 and cs % 16 == 0 and
+                                           T and self._c2fb_tile(i, B, h, w, ci, co, n, cs, cis) == T):
+                    conv(s2[0], s2[1], src.sub(0, cs), 2 * h, 2 * w, stride=2)
+                    s2 = None
                 if T:
-                    blob, bias = self._pack_c2fb(i, n)
+                    blob, bias = self._pack_c2fb(i, n, s2[0] if s2 else None)
                     args = ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=ci, ldx=src.ld, w=blob.data_ptr(),
                                     bias=bias.data_ptr(), Cout=co, y=dst.ptr, ldy=dst.ld, dtype=self.va_dtype, mode=3,
                                     kh=n, kw=1 if shortcut else 0, Npad=c, stride=T)
                     if up is not None:
                         args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
-                    ops.append(SegOp(kind=VA_OP_C2F, a=args))
                     macs = ci * 2 * c + n * 2 * 9 * c * c + (2 + n) * c * co  # per output pixel, without the halo
-                    meta.append({"name": f"model.{i} (fused C2f, T={T})", "kind": "conv", "M": B * h * w, "N": co,
-                                 "K": macs // co, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
-                                 "bytes": (2 if self.store == "bf16" else 4) * B * h * w * (ci + co)})
+                    name = f"model.{i} (fused C2f, T={T})"
+                    es = 2 if self.store == "bf16" else 4
+                    nbytes = es * B * h * w * (ci + co)
+                    if s2 is not None:  # va355.h va_seg_c2fb: a.res / ldr = the prologue's source, c2 = cs, K = cis
+                        args.res, args.ldr, args.c2, args.K = s2[1].ptr, s2[1].ld, cs, cis
+                        macs += 9 * cis * cs
+                        name = f"{s2[0]}+model.{i} (fused C2f, T={T})"
+                        nbytes += es * B * 4 * h * w * cis - es * B * h * w * cs
+                    ops.append(SegOp(kind=VA_OP_C2F, a=args))
+                    meta.append({"name": name, "kind": "conv", "M": B * h * w, "N": co, "K": macs // co, "k": 1,
+                                 "stride": 1, "flops": 2 * B * h * w * macs, "bytes": nbytes})
                     return
+            if s2 is not None:
+                conv(s2[0], s2[1], src.sub(0, cs), 2 * h, 2 * w, stride=2)
             if pre is None and i in self.c2f_fused and src.c == 64 and src.ld % 8 == 0 and dst.ld % 8 == 0:
                 blob, bias = self.c2f_fused[i]
                 ops.append(SegOp(kind=VA_OP_C2F, a=with_ws(ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
@@ -808,20 +835,18 @@ class SegNet:
             conv("model.1", a0, a1, h1, w1, stride=2)
         p2 = new(h2, w2, a.c2)
         c2f(2, a1, p2, h2, w2, pre=t2 if self.stem32 and (W * 3) % 16 == 0 else None)
+        # each stride-2 conv feeds only the C2f block after it: c2f() runs it first, or as the fused block's prologue
         a3 = new(h3, w3, a.c3)
-        conv("model.3", p2, a3, h2, w2, stride=2)
         cat14 = new(h3, w3, a.c4 + a.c3)          # [up(h12) | P3]
         P3 = cat14.sub(a.c4, a.c3)
-        c2f(4, a3, P3, h3, w3)
+        c2f(4, a3, P3, h3, w3, s2=("model.3", p2))
         a5 = new(h4, w4, a.c4)
-        conv("model.5", P3, a5, h3, w3, stride=2)
         cat11 = new(h4, w4, a.c5 + a.c4)          # [up(P5) | P4]
         P4 = cat11.sub(a.c5, a.c4)
-        c2f(6, a5, P4, h4, w4)
+        c2f(6, a5, P4, h4, w4, s2=("model.5", P3))
         a7 = new(h5, w5, a.c5)
-        conv("model.7", P4, a7, h4, w4, stride=2)
         b8 = new(h5, w5, a.c5)
-        c2f(8, a7, b8, h5, w5)
+        c2f(8, a7, b8, h5, w5, s2=("model.7", P4))
         cs = a.c5 // 2
         sp = new(h5, w5, 4 * cs)
         conv("model.9.cv1", b8, sp.sub(0, cs), h5, w5)
@@ -845,13 +870,11 @@ class SegNet:
         o3 = new(h3, w3, a.c3)
         c2f(15, cat14, o3, h3, w3, up=h12 if fuse_up else None)
         marks = {"A": len(ops)}  # op index ranges of the branches finish() may put on lanes
-        conv("model.16", o3, cat17.sub(0, a.c3), h3, w3, stride=2)
         o4 = new(h4, w4, a.c4)
-        c2f(18, cat17, o4, h4, w4)
+        c2f(18, cat17, o4, h4, w4, s2=("model.16", o3))
         marks["B"] = len(ops)
-        conv("model.19", o4, cat20.sub(0, a.c4), h4, w4, stride=2)
         o5 = new(h5, w5, a.c5)
-        c2f(21, cat20, o5, h5, w5)
+        c2f(21, cat20, o5, h5, w5, s2=("model.19", o4))
         marks["C"] = len(ops)
         # Segment head: per level [box 64 | cls nc | coef 32] float32
         cb, cc, cm = a.head_c2, a.head_c3, a.head_c4
