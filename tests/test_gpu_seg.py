@@ -248,14 +248,16 @@ def test_fused_tail_matches_unfused(monkeypatch):
         assert err < 1e-3, f"{name}: fused vs unfused {err}"
 
 
-def test_proto_subpixel_fold(monkeypatch):
-    """bf16 proto via the sub-pixel fold (upsample + cv2 + cv3 as one mode-2 op) vs the unfolded
-    deconv -> 3x3 -> 1x1 chain and vs the fp32 torch reference: the fold drops the bf16 rounding of
-    the 160x160 intermediate, so it must be at least about as close to fp32 as the unfolded path."""
-    arch, fw, net = _net("bf16", "s")
-    names = [m["name"] for m in net.plan(2, 640, 640)["meta"]]
+@pytest.mark.parametrize("scale,res", [("s", 640), ("m", 320)])
+def test_proto_subpixel_fold(monkeypatch, scale, res):
+    """bf16 proto via the sub-pixel fold (upsample + cv2 [+ cv3 as its tail] as one mode-2 op; m's 192-channel proto
+    folds without the tail, cv3 a 1x1 of its own) vs the unfolded deconv -> 3x3 -> 1x1 chain and vs the fp32 torch
+    reference: the fold drops the bf16 rounding of the 4x intermediate (s), so it must be at least about as close to
+    fp32 as the unfolded path."""
+    arch, fw, net = _net("bf16", scale)
+    names = [m["name"] for m in net.plan(2, res, res)["meta"]]
     assert any("sub-pixel fold" in n for n in names)
-    frames = _frames(2, seed=6)
+    frames = _frames(2, res, res, seed=6)
     ref = _ref_heads(arch, fw, frames)[3]
     folded = _gpu_heads(net, frames)[3]
     monkeypatch.setenv("VA_FOLD_PROTO", "0")

@@ -3956,8 +3956,9 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
     if (a->mode == 2 && (a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res || a->Cout <= 64 || a->Kpad % ks))
         return VA_ERR_ARG;
-    // bias4: mode 2 only -- bf16 through conv2's fused-tail path, f32 through the plain epilogue
-    if (a->bias4 && (a->mode != 2 || (bf && (!a->w2 || a->Cout != 128)))) return VA_ERR_ARG;
+    // bias4: mode 2 only -- bf16 through conv2's fused-tail path (Cout 128) or its plain epilogue (the wider protos of
+    // m / l / x, no tail), f32 through the plain epilogue
+    if (a->bias4 && (a->mode != 2 || (bf && a->w2 && a->Cout != 128))) return VA_ERR_ARG;
     // f32 fused tail: conv3h's conditions (launch_conv3h_tail) are checked at dispatch
     if (a->w2 && a->dtype == VA_DTYPE_F32 && a->Cout == 32 && !conv3q_tail_ok(*a)) return VA_ERR_ARG;
     if (a->w2 && a->dtype == VA_DTYPE_F32 && a->Cout != 32 &&

@@ -198,7 +198,8 @@ class SegNet:
             if os.environ.get("VA_CONV0_F32M", "1") != "0":
                 self.w0_3 = split3_bf16(w0p).to(self.device).contiguous()
         # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
-        fold_ok = arch.npr == 128 if dtype == "bf16" else (arch.npr >= 128 and dtype == "f32")
+        # (bf16 wider protos -- m's 192 -- fold without the tail: conv2's plain mode-2 epilogue, then cv3 as a 1x1)
+        fold_ok = arch.npr >= 128 and arch.npr % 64 == 0 and dtype in ("bf16", "f32")
         self.proto_fold = self._fold_proto(folded) if (fold_ok and os.environ.get("VA_FOLD_PROTO", "1") != "0") \
             else None
         # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
@@ -930,6 +931,24 @@ class SegNet:
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
                          "bytes": 4 * B * h3 * w3 * pf.cin + 4 * pf.w.numel() + 4 * B * h2 * w2 * pf.cout})
+            proto = new(h2, w2, NM, torch.float32)
+            conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
+            return finish(proto)
+        if self.proto_fold is not None and self.proto_fold.cout != 128:
+            # bf16, a wider proto (m: 192 channels): the fold alone into the 4x map, then cv3 as its own 1x1 -- 40 % of
+            # the unfolded pair's MACs (the ConvTranspose GEMM + the 3x3 on the 4x map)
+            pf = self.proto_fold
+            pr1 = new(h3, w3, a.npr)
+            conv("model.22.proto.cv1", o3, pr1, h3, w3)
+            pr3 = new(h2, w2, a.npr)
+            ops.append(SegOp(kind=VA_OP_CONV, a=with_ws(ConvArgs(
+                x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
+                w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
+                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1))))
+            meta.append({"name": "model.22.proto.upsample+cv2 (sub-pixel fold)", "kind": "conv",
+                         "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
+                         "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
+                         "bytes": 2 * B * h3 * w3 * pf.cin + 2 * pf.w.numel() + 2 * B * h2 * w2 * pf.cout})
             proto = new(h2, w2, NM, torch.float32)
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
             return finish(proto)
