@@ -102,11 +102,13 @@ def parse():
                    help="frames in flight per GPU in the c4 extra (batch 1: more concurrent forwards fill the chip)")
     p.add_argument("--c4-seg-streams", type=int, default=3, choices=[1, 2, 3, 4],
                    help="network streams of the c4 extra (3 + the grid stage's stream: one hardware queue each)")
-    p.add_argument("--dealer-workers-per-gpu", type=int, default=1,
+    # dealer defaults from the round-5 sweep (profiles/r05/dealer/): 2 workers x 16 frames x 128 slots 3,858-4,031
+    # frames/s per GPU; 1 x 32 x 64 2,670; 3 x 16 3,984; 4 x 16 3,637; 2 x 8 3,341
+    p.add_argument("--dealer-workers-per-gpu", type=int, default=2,
                    help="FrameProcessor worker processes per GPU in the dealer extra (each its own PathFinder shard)")
-    p.add_argument("--dealer-batch", type=int, default=32,
+    p.add_argument("--dealer-batch", type=int, default=16,
                    help="frames a dealer worker runs as one device batch (up to; what waits in its ring)")
-    p.add_argument("--dealer-slots", type=int, default=64, help="ring slots per dealer worker")
+    p.add_argument("--dealer-slots", type=int, default=128, help="ring slots per dealer worker")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -506,8 +508,9 @@ def dealer_rate(args, dev, frames_n: int = 1024) -> dict:
     return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "gpus": ngpu, "frames": frames_n,
             "frames_with_answer": answers, "dtype": "f32", "regime": args.regime, "worker_batch": args.dealer_batch,
             "slots": args.dealer_slots,
-            "workload": "one reader dealing host 640x640 frames round-robin to one FrameProcessor worker process per "
-                        "GPU (vision_assist_amd.shard.FrameDealer), answers back in frame order; each worker runs "
+            "workload": f"one reader dealing host 640x640 frames round-robin to {args.dealer_workers_per_gpu} "
+                        "FrameProcessor worker process(es) per GPU (vision_assist_amd.shard.FrameDealer: shared-memory "
+                        "frame ring with shared head / tail counters), answers back in frame order; each worker runs "
                         f"up to {args.dealer_batch} waiting frames as one device batch, two batches in flight "
                         "(pipeline.StreamBatches), answers built frame by frame in order"}
 

@@ -78,7 +78,9 @@ class FrameDealer:
     PathFinder singletons (the reference's process-global state, PathFinder.py:32: a shard's answers equal the
     reference run over that shard's frames in order), and results come back in frame order.  No collective and no
     torch.distributed: pixels travel through a shared-memory ring of ``slots`` frames per worker (a memcpy, no
-    pickling), the small results through one queue.
+    pickling) whose head / tail counters sit in shared memory too (the reader publishes a frame by bumping the head
+    after its copy, the worker frees slots by bumping the tail once it has copied frames out; frame i is worker
+    i % G's (i // G)-th frame, so no index travels), the small results through one queue, one message per batch.
 
     worker_factory: a picklable callable run once inside each worker, ``worker_factory(device_index) -> fn`` with
     ``fn(frame: np.ndarray uint8 [H, W, 3]) -> picklable result`` (default: dropin_worker -- YOLO + FrameProcessor
@@ -104,14 +106,13 @@ class FrameDealer:
         ctx = tmp.get_context("spawn")
         self.ring = torch.zeros((self.G, slots, H, W, 3), dtype=torch.uint8).share_memory_()
         self._ring_np = self.ring.numpy()  # frames are copied in by numpy (one thread; see submit)
-        self.inq = [ctx.Queue() for _ in range(self.G)]
-        self.free = [ctx.Queue() for _ in range(self.G)]
+        # per worker: [head = frames published, tail = frames copied out of the ring, stop]; head is written by the
+        # reader only, tail by the worker only (aligned int64 stores; x86 keeps the frame's stores ahead of the head's)
+        self.ctl = torch.zeros((self.G, 3), dtype=torch.int64).share_memory_()
+        self._ctl = self.ctl.numpy()
         self.outq = ctx.Queue()
-        for w in range(self.G):
-            for s in range(slots):
-                self.free[w].put(s)
         self.procs = [ctx.Process(target=_dealer_worker, daemon=True,
-                                  args=(w, devices[w], worker_factory, self.ring, self.inq[w], self.free[w], self.outq))
+                                  args=(w, self.G, devices[w], worker_factory, self.ring, self.ctl, self.outq))
                       for w in range(self.G)]
         for p in self.procs:
             p.start()
@@ -151,23 +152,26 @@ class FrameDealer:
     def submit(self, frame) -> int:
         """Deal one frame (np.ndarray / tensor uint8 [H, W, 3]) to worker n % G; blocks while that worker's ring is
         full.  -> the frame's index in the stream."""
-        import queue
         if self.broken:
             raise RuntimeError(self.broken)
         idx, w = self.n, self.n % self.G
         t = torch.as_tensor(frame)
         if tuple(t.shape) != (self.H, self.W, 3) or t.dtype != torch.uint8:
             raise ValueError(f"frame must be uint8 [{self.H}, {self.W}, 3], got {tuple(t.shape)} {t.dtype}")
-        while True:
-            try:
-                slot = self.free[w].get(timeout=self.poll)
-                break
-            except queue.Empty:
-                self._check_workers()
+        ctl = self._ctl[w]
+        head = int(ctl[0])
+        if head - int(ctl[1]) >= self.slots:  # the ring is full: wait for the worker to copy frames out
+            nap, t0 = 2e-5, time.monotonic()
+            while head - int(ctl[1]) >= self.slots:
+                time.sleep(nap)
+                nap = min(nap * 2, 1e-3)
+                if time.monotonic() - t0 > self.poll:
+                    self._check_workers()
+                    t0 = time.monotonic()
         # numpy's copy, not torch's: torch's CPU copy of a frame wakes its OpenMP pool, whose workers then spin
         # between frames and exhaust the box's CPU quota for every process of it (pipeline.FramePipeline._pinned)
-        np.copyto(self._ring_np[w, slot], t.numpy() if t.device.type == "cpu" else t.cpu().numpy())
-        self.inq[w].put((idx, slot))
+        np.copyto(self._ring_np[w, head % self.slots], t.numpy() if t.device.type == "cpu" else t.cpu().numpy())
+        ctl[0] = head + 1  # publish: the worker may read the slot from now on
         self.n += 1
         return idx
 
@@ -221,8 +225,8 @@ class FrameDealer:
                 self.discard()
 
     def close(self) -> None:
-        for q in self.inq:
-            q.put(None)
+        """The workers finish the frames already dealt, then exit."""
+        self._ctl[:, 2] = 1
         for p in self.procs:
             p.join(timeout=60)
             if p.is_alive():
@@ -242,11 +246,12 @@ class _Failed:
         self.tb = tb
 
 
-def _dealer_worker(w, device, factory, ring, inq, free, outq):
-    """Worker process: frames from its ring slots, in submission order.  A plain ``fn`` runs frame by frame; a
-    batching one (``max_batch`` / ``begin`` / ``end``, see FrameDealer) gets every frame waiting in the queue, up to
-    max_batch, as one batch, with the next batch begun before the previous one is ended."""
-    import queue
+def _dealer_worker(w, G, device, factory, ring, ctl, outq):
+    """Worker process: frames from its ring slots, in submission order (its j-th frame is the stream's w + j G).  A
+    plain ``fn`` runs frame by frame; a batching one (``max_batch`` / ``begin`` / ``end``, see FrameDealer) gets every
+    published frame not yet taken, up to max_batch, as one batch, with the next batch begun before the previous one
+    is ended.  Idle, it polls the ring's head with a backoff (20 us doubling to 1 ms); it exits once the reader has
+    set stop and every published frame is done."""
     import traceback
     try:
         if device is not None and torch.cuda.is_available():
@@ -258,7 +263,9 @@ def _dealer_worker(w, device, factory, ring, inq, free, outq):
     outq.put(("ready", w, None))
     begin = getattr(fn, "begin", None)
     k = max(1, int(getattr(fn, "max_batch", 1))) if begin is not None else 1
-    pend, stop = None, False
+    c = ctl.numpy()[w]
+    S = ring.shape[1]
+    pend, taken, nap = None, 0, 2e-5
 
     def emit(idxs, tok):
         if tok[0] == "error":
@@ -279,38 +286,38 @@ def _dealer_worker(w, device, factory, ring, inq, free, outq):
                 outq.put(("error", [i], "".join(traceback.format_exception(type(r), r, r.__traceback__))))
 
     while True:
-        items = []
-        while not stop and len(items) < k:
-            try:  # block only when nothing else is to be done
-                item = inq.get(block=pend is None and not items)
-            except queue.Empty:
-                break
-            if item is None:
-                stop = True
-                break
-            items.append(item)
-        tok = None
-        if items:
-            idxs = [i for i, _ in items]
+        n = min(int(c[0]) - taken, k)
+        if n == 0:
+            if pend is not None:  # nothing new to overlap with: finish the batch in flight
+                emit(*pend)
+                pend = None
+                continue
+            if c[2] and int(c[0]) == taken:
+                return
+            time.sleep(nap)
+            nap = min(nap * 2, 1e-3)
+            continue
+        nap = 2e-5
+        idxs = [w + (taken + j) * G for j in range(n)]
+        views = [ring[w, (taken + j) % S].numpy() for j in range(n)]
+        frames = None
+        try:
+            if begin is not None:
+                tok = ("ok", begin(views))
+            else:
+                frames = [v.copy() for v in views]
+        except Exception:
+            tok = ("error", traceback.format_exc())
+        taken += n
+        c[1] = taken  # the slots are reusable as soon as the pixels are copied out
+        if frames is not None:  # frame by frame: run them once their slots are free
             try:
-                if begin is not None:
-                    tok = ("ok", begin([ring[w, s].numpy() for _, s in items]))
-                    for _, s in items:
-                        free.put(s)
-                else:
-                    frames = [ring[w, s].numpy().copy() for _, s in items]
-                    for _, s in items:
-                        free.put(s)  # the slot is reusable as soon as the pixels are copied out
-                    tok = ("ok", [fn(f) for f in frames])
+                tok = ("ok", [fn(f) for f in frames])
             except Exception:
                 tok = ("error", traceback.format_exc())
-                for _, s in items:
-                    free.put(s)
         if pend is not None:
             emit(*pend)
-        pend = (idxs, tok) if items else None
-        if stop and pend is None:
-            return
+        pend = (idxs, tok)
 
 
 class dropin_worker:
