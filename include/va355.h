@@ -327,6 +327,10 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a);
 /* Debug: record per-wave stage clocks (s_memtime) of the first 32 tiles of every workgroup of the next
  * va_seg_c2f launches into device memory buf ([grid][8][32][6] uint64), or stop (buf = NULL). */
 int va_c2f_trace(void* buf);
+/* Debug: per-workgroup stage clocks of the next va_seg_c2fb launches into device memory buf ([grid][10] uint64: thread
+ * 0's s_memtime at the start, after each stage's barrier and at the end; unused points keep their contents), or stop
+ * (buf = NULL). */
+int va_c2fb_trace(void* buf);
 /* Debug: the same for va_seg_stem ([grid][8][32][5] uint64 of the 100 MHz real-time counter). */
 int va_stem_trace(void* buf);
 

@@ -62,6 +62,7 @@ SIGNATURES = [
     ("va_seg_stem_f32", I32, [P, P]),
     ("va_seg_c2f_f32", I32, [P, P]),
     ("va_c2f_trace", I32, [P]),
+    ("va_c2fb_trace", I32, [P]),
     ("va_stem_trace", I32, [P]),
     ("va_seg_preprocess", I32, [P, P, I32, I32, I32, I32, P]),
     ("va_seg_conv0", I32, [P, P, I32, I32, I32, P, P, I32, P, I32]),

@@ -35,6 +35,10 @@ constexpr int XB_NW = 8, XB_NT = 64 * XB_NW;
 constexpr int XB_G = 4;       // 16-pixel blocks per work item (one A fragment feeds XB_G MFMAs)
 constexpr int XB_KC = 8;      // K-steps of A fragments loaded ahead
 constexpr int XB_LDS_MAX = 160 * 1024;
+constexpr int XB_TR = 10;     // stage clocks per workgroup in the debug trace: start, after each stage, end
+// debug trace: thread 0 stamps the shader clock (s_memtime) at point pt after the workgroup's barrier
+#define XB_MARK(g, pt) \
+    if ((g).trace && threadIdx.x == 0) (g).trace[blockIdx.x * XB_TR + (pt)] = __builtin_amdgcn_s_memtime()
 
 struct XbGeom {
     const __bf16* x;
@@ -53,6 +57,8 @@ struct XbGeom {
     // channel stride ldxs), computed per tile from the source region SR ((2 S0 + 1)^2 pixels) staged at off_sr
     const __bf16* xs;
     int ldxs, cs, cis, lgcis, off_sr, pss;
+    unsigned long long* trace;  // debug (va_c2fb_trace): [grid][XB_TR] stage clocks of wave 0, or null
+    int off_b, nbias;           // the biases' copy in LDS (off_b) and their count
 };
 
 // conv q's shape: output channels, K (elements), K-steps of 32
@@ -84,9 +90,31 @@ __device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(f
 // KIND 1: 3x3 from src (one pixel larger on every side), + res at the same pixel (two larger) when res.off >= 0;
 // KIND 2: 1x1 over the concat [R0 | R2 | R4 ...] at the tile's pixels (cv2), written to g.y.
 // Pixels outside the frame are stored as zero (the next 3x3's padding); KIND 2 skips them.
+// every conv's biases into LDS at off_b (issued beside the first stage's loads; read after its barrier)
+__device__ __forceinline__ void xb_bias_to_lds(const float* b, int nbias, unsigned char* smem, int off_b) {
+    for (int i = 4 * (int)threadIdx.x; i < nbias; i += 4 * XB_NT)
+        *(f32x4*)(smem + off_b + 4 * i) = *(const f32x4*)(b + i);
+}
+
+// the first XB_KC A fragments of conv q's 16-channel block cb (ks K-steps): what an item's K loop starts on
+__device__ __forceinline__ void xb_first(const XbGeom& g, int q, int cb, int ks, int lane, bf16x8 (&a0)[XB_KC]) {
+    const bf16x8* wb = g.w + (int64_t)64 * (g.wf[q] + cb * ks) + lane;
+#pragma unroll
+    for (int i = 0; i < XB_KC; ++i) a0[i] = wb[64 * min(i, ks - 1)];
+}
+
+// a conv's shape as its successor's prefetch needs it: index, 16-channel blocks, K-steps (q < 0: none)
+struct XbNext {
+    int q, ncb, ks;
+};
+
+// a0 holds the first chunk of this conv's first item for the wave (issued before the barrier that precedes the
+// conv, or by the previous item); the item loop issues the next item's first chunk before its epilogue, and the
+// last item the successor conv's (nx) -- so no item and no stage starts on an exposed L2 round trip
 template <int C, int NB, int KIND>
 __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, int q, int nout, int kel, int ow, int oy,
-                                        int ox, int n, XbIo src, XbIo dst, XbIo res, int lane, int wid) {
+                                        int ox, int n, XbIo src, XbIo dst, XbIo res, int lane, int wid,
+                                        bf16x8 (&a0)[XB_KC], XbNext nx) {
     constexpr int H2 = 2 * NB;
     const int ks = (kel + 31) >> 5, ncb = (nout + 15) >> 4;
     const int P = ow * ow, npb = (P + 15) >> 4, ngr = (npb + XB_G - 1) / XB_G;
@@ -113,53 +141,59 @@ __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, in
 #pragma unroll
         for (int j = 0; j < XB_G; ++j) acc[j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
         const bf16x8* wb = g.w + (int64_t)64 * (g.wf[q] + cb * ks) + lane;
+        // one K-step: the four blocks' B fragments read together (a block past the item's live ones reads a clamped
+        // real pixel), then the live blocks' MFMAs.  (MFMAs on the dead blocks too -- no guard at all -- gave
+        // non-finite outputs on the live ones, profiles/r05/c2fb/bisect.log; the guard stays.)
         auto step = [&](int k, bf16x8 a) {
             const int kk = min((k << 5) + (fq << 3), kel - 8);  // past K: the last group (its weights are zero)
+            bf16x8 b[XB_G];
 #pragma unroll
             for (int j = 0; j < XB_G; ++j) {
-                if (j < nb) {
-                    int addr;
-                    if constexpr (KIND == 0) {
-                        addr = base[j] + kk * 2;
-                    } else if constexpr (KIND == 1) {
-                        const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
-                        addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
-                    } else if constexpr (KIND == 3) {  // stride 2 from SR: output (r, c) reads SR (2r + ky, 2c + kx)
-                        const int tap = kk >> g.lgcis, ch = kk - (tap << g.lgcis), ky = tap / 3, kx = tap - 3 * ky;
-                        addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
-                    } else if (kk < 2 * C) {
-                        addr = g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * ps0<C>() + kk * 2;
-                    } else {
-                        const int s = (kk - 2 * C) / C + 1, ch = kk - (s + 1) * C;
-                        const int hs = H2 - 2 * s, ws = g.T + 2 * hs;  // R(2s): halo hs
-                        addr = g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * psc<C>() + ch * 2;
-                    }
-                    acc[j] = mma(a, *(const bf16x8*)(smem + addr), acc[j]);
+                int addr;
+                if constexpr (KIND == 0) {
+                    addr = base[j] + kk * 2;
+                } else if constexpr (KIND == 1) {
+                    const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
+                    addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
+                } else if constexpr (KIND == 3) {  // stride 2 from SR: output (r, c) reads SR (2r + ky, 2c + kx)
+                    const int tap = kk >> g.lgcis, ch = kk - (tap << g.lgcis), ky = tap / 3, kx = tap - 3 * ky;
+                    addr = base[j] + (ky * src.w + kx) * src.ps + ch * 2;
+                } else if (kk < 2 * C) {
+                    addr = g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * ps0<C>() + kk * 2;
+                } else {
+                    const int s = (kk - 2 * C) / C + 1, ch = kk - (s + 1) * C;
+                    const int hs = H2 - 2 * s, ws = g.T + 2 * hs;  // R(2s): halo hs
+                    addr = g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * psc<C>() + ch * 2;
                 }
+                b[j] = *(const bf16x8*)(smem + addr);
             }
-        };
-        bf16x8 a0[XB_KC], a1[XB_KC];
 #pragma unroll
-        for (int i = 0; i < XB_KC; ++i)
-            if (i < ks) a0[i] = wb[64 * i];
+            for (int j = 0; j < XB_G; ++j)
+                if (j < nb) acc[j] = mma(a, b[j], acc[j]);
+        };
+        // A loads unconditional (a chunk past ks re-reads the last step, unused): a fixed count in flight, so the
+        // waits before each step count loads instead of draining them all (vmcnt(0))
+        bf16x8 a1[XB_KC];
         for (int k0 = 0; k0 < ks; k0 += 2 * XB_KC) {
 #pragma unroll
-            for (int i = 0; i < XB_KC; ++i)
-                if (k0 + XB_KC + i < ks) a1[i] = wb[64 * (k0 + XB_KC + i)];
+            for (int i = 0; i < XB_KC; ++i) a1[i] = wb[64 * min(k0 + XB_KC + i, ks - 1)];
 #pragma unroll
             for (int i = 0; i < XB_KC; ++i)
                 if (k0 + i < ks) step(k0 + i, a0[i]);
 #pragma unroll
-            for (int i = 0; i < XB_KC; ++i)
-                if (k0 + 2 * XB_KC + i < ks) a0[i] = wb[64 * (k0 + 2 * XB_KC + i)];
+            for (int i = 0; i < XB_KC; ++i) a0[i] = wb[64 * min(k0 + 2 * XB_KC + i, ks - 1)];
 #pragma unroll
             for (int i = 0; i < XB_KC; ++i)
                 if (k0 + XB_KC + i < ks) step(k0 + XB_KC + i, a1[i]);
         }
+        // the next item's first chunk (this conv's, or the successor's first item) in flight under the epilogue
+        if (it + XB_NW < items) xb_first(g, q, (it + XB_NW) % ncb, ks, lane, a0);
+        else if (nx.q >= 0) xb_first(g, nx.q, wid % nx.ncb, nx.ks, lane, a0);
         // epilogue: the lane holds channels 4 fq .. 4 fq + 3 of block cb for its pixel of each block
         const int co = (cb << 4) + (fq << 2);
         if (co >= nout) continue;
-        const f32x4 bias = *(const f32x4*)(g.b + g.bo[q] + co);
+        const f32x4 bias = *(const f32x4*)(smem + g.off_b + (g.bo[q] + co) * 4);  // (a global load here stalled
+                                                                                     //  every item's epilogue)
 #pragma unroll
         for (int j = 0; j < XB_G; ++j) {
             const int p = ((gr * XB_G + j) << 4) + fr;
@@ -180,6 +214,7 @@ __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, in
             }
         }
     }
+    if (wid >= items && nx.q >= 0) xb_first(g, nx.q, wid % nx.ncb, nx.ks, lane, a0);  // idle here: prefetch only
 }
 
 template <int C, int NB>
@@ -189,7 +224,10 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
     const int T = g.T, S0 = T + 2 * H2;
     const int t = blockIdx.x, n = t / g.tpf, tt = t - n * g.tpf, ty = tt / g.tx, tx = tt - ty * g.tx;
     const int y0 = ty * T, x0 = tx * T;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // the wave index as a scalar: item / block / guard arithmetic derived from it stays wave-uniform (scalar branches)
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    XB_MARK(g, 0);
+    xb_bias_to_lds(g.b, g.nbias, smem, g.off_b);
     // the input region, eight 16-byte loads in flight per thread before their LDS stores
     if (g.cs > 0) {  // the stride-2 prologue's source region, zero outside the source frame
         const int S2 = 2 * S0 + 1, sg = g.cis >> 3, stot = S2 * S2 * sg, sy0 = 2 * (y0 - H2) - 1, sx0 = 2 * (x0 - H2) - 1;
@@ -241,27 +279,44 @@ __global__ __launch_bounds__(XB_NT) void c2fb_kernel(XbGeom g) {
             if (dst[i] >= 0) *(u32x4*)(smem + dst[i]) = v[i];
     }
     __syncthreads();
+    XB_MARK(g, 1);
     const XbIo none = {-1, 0, 0, 0};
     const XbIo r0 = {g.off_r[0], S0, ps0<C>(), 0}, rin = {g.in_off, S0, g.psi, 0};
+    // the convs' shapes for the prefetch chain: cv1 (q 0), m.j.cv1 / cv2 (1 .. 2n), cv2 (2n + 1)
+    const XbNext n_cv1 = {0, (2 * C) >> 4, (g.ci + 31) >> 5}, n_m = {1, C >> 4, (9 * C + 31) >> 5};
+    const XbNext n_cv2 = {2 * NB + 1, (g.co + 15) >> 4, ((2 + NB) * C + 31) >> 5}, n_end = {-1, 1, 0};
+    bf16x8 a0[XB_KC];  // the first chunk of the wave's next item (see xb_conv)
     if (g.cs > 0) {  // IN channels [0, cs) = the stride-2 conv of SR (zero outside the frame)
+        xb_first(g, 2 * NB + 2, wid % ((g.cs + 15) >> 4), (9 * g.cis + 31) >> 5, lane, a0);
         xb_conv<C, NB, 3>(g, smem, 2 * NB + 2, g.cs, 9 * g.cis, S0, y0 - H2, x0 - H2, n,
-                          XbIo{g.off_sr, 2 * S0 + 1, g.pss, 0}, rin, none, lane, wid);
+                          XbIo{g.off_sr, 2 * S0 + 1, g.pss, 0}, rin, none, lane, wid, a0, n_cv1);
         __syncthreads();
+    } else {
+        xb_first(g, 0, wid % n_cv1.ncb, n_cv1.ks, lane, a0);
     }
-    xb_conv<C, NB, 0>(g, smem, 0, 2 * C, g.ci, S0, y0 - H2, x0 - H2, n, rin, r0, none, lane, wid);
+    XB_MARK(g, 2);
+    xb_conv<C, NB, 0>(g, smem, 0, 2 * C, g.ci, S0, y0 - H2, x0 - H2, n, rin, r0, none, lane, wid, a0, n_m);
     __syncthreads();
+    XB_MARK(g, 3);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int hs = H2 - 2 * j, ws = T + 2 * hs;  // R(2j): halo hs
         const XbIo rin = j == 0 ? XbIo{g.off_r[0], S0, ps0<C>(), C} : XbIo{g.off_r[2 * j], ws, psc<C>(), 0};
         const XbIo rmid = {g.off_r[2 * j + 1], ws - 2, psc<C>(), 0}, rout = {g.off_r[2 * j + 2], ws - 4, psc<C>(), 0};
-        xb_conv<C, NB, 1>(g, smem, 1 + 2 * j, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane, wid);
+        xb_conv<C, NB, 1>(g, smem, 1 + 2 * j, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane, wid,
+                          a0, XbNext{2 + 2 * j, n_m.ncb, n_m.ks});
         __syncthreads();
+        XB_MARK(g, 4 + 2 * j);
         xb_conv<C, NB, 1>(g, smem, 2 + 2 * j, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
-                          g.sc ? rin : none, lane, wid);
+                          g.sc ? rin : none, lane, wid, a0, j + 1 < NB ? XbNext{3 + 2 * j, n_m.ncb, n_m.ks} : n_cv2);
         __syncthreads();
+        XB_MARK(g, 5 + 2 * j);
     }
-    xb_conv<C, NB, 2>(g, smem, 2 * NB + 1, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
+    xb_conv<C, NB, 2>(g, smem, 2 * NB + 1, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid, a0, n_end);
+    if (g.trace) {
+        __syncthreads();
+        XB_MARK(g, XB_TR - 1);
+    }
 }
 
 // ---- the f32 form (the reference's precision: the drop-in call's batch-1 network, FrameProcessor.py:322) ----
@@ -285,6 +340,8 @@ struct XfGeom {
     int off_r0a;      // LDS offset of R0a (the a half at the tile's T x T pixels)
     int off_r[5];     // R0b (the b half on all of R0), R1 .. R2n
     int wf[6], bo[6];
+    unsigned long long* trace;  // debug (va_c2fb_trace), as XbGeom's
+    int off_b, nbias;           // the biases' copy in LDS (off_b) and their count
 };
 
 template <int C>
@@ -375,26 +432,24 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
         constexpr int KC = KIND == 0 ? 2 : XF_KC;
         bf16x8 a0[KC][3], a1[KC][3];
         f32x4 b0[KC][XF_G][2], b1[KC][XF_G][2];
+        // loads unconditional (clamped to the last step / a real pixel, zeros selected after): a fixed count in
+        // flight for counted waits
         auto load = [&](bf16x8 (&a)[KC][3], f32x4 (&bv)[KC][XF_G][2], int k0) {
 #pragma unroll
             for (int i = 0; i < KC; ++i) {
-                if (k0 + i < ks) {
+                const int kc = min(k0 + i, ks - 1);
 #pragma unroll
-                    for (int t = 0; t < 3; ++t) a[i][t] = wb[192 * (k0 + i) + 64 * t];
-                    if constexpr (KIND == 0) {
-                        const int kk = min(((k0 + i) << 5) + (fq << 3), kel - 8);
-                        const bool up = kk < g.cu;
+                for (int t = 0; t < 3; ++t) a[i][t] = wb[192 * kc + 64 * t];
+                if constexpr (KIND == 0) {
+                    const int kk = min((kc << 5) + (fq << 3), kel - 8);
+                    const bool up = kk < g.cu;
 #pragma unroll
-                        for (int j = 0; j < XF_G; ++j) {
-                            const int64_t o = up ? gu[j] : gx[j];
-                            if (j < nb && o >= 0) {
-                                const float* p = (up ? g.xu : g.x) + o + kk;
-                                bv[i][j][0] = *(const f32x4*)p;
-                                bv[i][j][1] = *(const f32x4*)(p + 4);
-                            } else {
-                                bv[i][j][0] = bv[i][j][1] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-                            }
-                        }
+                    for (int j = 0; j < XF_G; ++j) {
+                        const int64_t o = up ? gu[j] : gx[j];
+                        const float* p = (up ? g.xu : g.x) + (o >= 0 ? o : 0) + kk;
+                        const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f}, v0 = *(const f32x4*)p, v1 = *(const f32x4*)(p + 4);
+                        bv[i][j][0] = o >= 0 ? v0 : z;
+                        bv[i][j][1] = o >= 0 ? v1 : z;
                     }
                 }
             }
@@ -403,16 +458,21 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
 #pragma unroll
             for (int i = 0; i < KC; ++i) {
                 if (k0 + i < ks) {
+                    f32x4 lv[XF_G][2];
+                    if constexpr (KIND != 0) {  // the blocks' LDS reads together, then their splits and MFMAs
+#pragma unroll
+                        for (int j = 0; j < XF_G; ++j) {
+                            const unsigned char* p = smem + lds_addr(k0 + i, j);
+                            lv[j][0] = *(const f32x4*)p;
+                            lv[j][1] = *(const f32x4*)(p + 16);
+                        }
+                    }
 #pragma unroll
                     for (int j = 0; j < XF_G; ++j) {
-                        if (j < nb) {
+                        if (j < nb) {  // (unguarded, the bf16 form's live blocks went non-finite: kept guarded)
                             bf16x8 bt[3];
-                            if constexpr (KIND == 0) {
-                                xf_split3(bv[i][j][0], bv[i][j][1], bt);
-                            } else {
-                                const unsigned char* p = smem + lds_addr(k0 + i, j);
-                                xf_split3(*(const f32x4*)p, *(const f32x4*)(p + 16), bt);
-                            }
+                            if constexpr (KIND == 0) xf_split3(bv[i][j][0], bv[i][j][1], bt);
+                            else xf_split3(lv[j][0], lv[j][1], bt);
                             acc[j] = mma6(a[i], bt, acc[j]);
                         }
                     }
@@ -428,7 +488,7 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
         }
         const int co = (cb << 4) + (fq << 2);
         if (co >= nout) continue;
-        const f32x4 bias = *(const f32x4*)(g.b + g.bo[q] + 16 * cb0 + co);
+        const f32x4 bias = *(const f32x4*)(smem + g.off_b + (g.bo[q] + 16 * cb0 + co) * 4);
 #pragma unroll
         for (int j = 0; j < XF_G; ++j) {
             const int p = ((gr * XF_G + j) << 4) + fr;
@@ -455,12 +515,21 @@ __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
     const int T = g.T, S0 = T + 2 * H2;
     const int t = blockIdx.x, n = t / g.tpf, tt = t - n * g.tpf, ty = tt / g.tx, tx = tt - ty * g.tx;
     const int y0 = ty * T, x0 = tx * T;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // the wave index as a scalar: item / block / guard arithmetic derived from it stays wave-uniform (scalar branches)
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const XbIo none = {-1, 0, 0, 0};
     const XbIo r0b = {g.off_r[0], S0, pf<C>(), 0}, r0a = {g.off_r0a, T, pf<C>(), 0};
+    XB_MARK(g, 0);
+    xb_bias_to_lds(g.b, g.nbias, smem, g.off_b);
+    __syncthreads();
     xf_conv<C, NB, 0>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
+    if (g.trace) {
+        __syncthreads();
+        XB_MARK(g, 1);
+    }
     xf_conv<C, NB, 0>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
     __syncthreads();
+    XB_MARK(g, 3);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int hs = H2 - 2 * j, ws = T + 2 * hs;
@@ -469,11 +538,17 @@ __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
         xf_conv<C, NB, 1>(g, smem, 1 + 2 * j, 0, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane,
                           wid);
         __syncthreads();
+        XB_MARK(g, 4 + 2 * j);
         xf_conv<C, NB, 1>(g, smem, 2 + 2 * j, 0, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
                           g.sc ? rin : none, lane, wid);
         __syncthreads();
+        XB_MARK(g, 5 + 2 * j);
     }
     xf_conv<C, NB, 2>(g, smem, 2 * NB + 1, 0, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
+    if (g.trace) {
+        __syncthreads();
+        XB_MARK(g, XB_TR - 1);
+    }
 }
 
 // f32 LDS layout: [R0b][R0a][R1] .. [R2n]; returns the bytes (or -1)
@@ -565,6 +640,8 @@ bool xb_s2_ok(int ci, int cs, int cis) {
     return cs > 0 && cs % 16 == 0 && cs <= ci && cis >= 8 && cis <= 512 && (cis & (cis - 1)) == 0;
 }
 
+unsigned long long* g_xb_trace = nullptr;  // va_c2fb_trace
+
 bool xb_shape_ok(int C, int NB, bool f32 = false) {
     return (C == 16 || C == 32 || C == 64 || C == 128 || (f32 && C == 256)) && (NB == 1 || NB == 2);
 }
@@ -582,8 +659,8 @@ extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int3
                         : xb_layout(c, n, ci, T, off_r, &in_off, &psi, cs ? cis : 0, &off_sr, &pss);
     xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2], cs, cis);
     if (f32) out3[1] *= 3;  // three term fragments per tile
-    out3[0] = lds;
-    return lds < 0 ? VA_ERR_ARG : VA_OK;
+    out3[0] = lds < 0 ? -1 : lds + 4 * out3[2];  // + the biases' LDS copy
+    return lds < 0 || out3[0] > XB_LDS_MAX ? VA_ERR_ARG : VA_OK;
 }
 
 static int c2fb_f32(const va_conv_args* a, hipStream_t st);
@@ -609,6 +686,10 @@ extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
     if (lds < 0) return VA_ERR_ARG;
     int64_t frags, biases;
     xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases, cs, cis);
+    g.off_b = lds, g.nbias = (int)biases;  // the biases' LDS copy after the layout (16-byte multiples: biases % 16 == 0)
+    const int lds_b = lds + (int)biases * 4;
+    if (lds_b > XB_LDS_MAX) return VA_ERR_ARG;
+    g.trace = g_xb_trace;
     g.xs = (const __bf16*)a->res;
     g.ldxs = a->ldr, g.cs = cs, g.cis = cis, g.lgcis = cs ? 31 - __builtin_clz(cis) : 0;
     g.x = (const __bf16*)a->x;
@@ -625,14 +706,14 @@ extern "C" int va_seg_c2fb(void* stream, const va_conv_args* a) {
     hipStream_t st = (hipStream_t)stream;
     hipError_t rc;
     switch (C * 4 + NB) {
-        case 16 * 4 + 1: rc = xb_launch<16, 1>(g, lds, (int)nt, st); break;
-        case 16 * 4 + 2: rc = xb_launch<16, 2>(g, lds, (int)nt, st); break;
-        case 32 * 4 + 1: rc = xb_launch<32, 1>(g, lds, (int)nt, st); break;
-        case 32 * 4 + 2: rc = xb_launch<32, 2>(g, lds, (int)nt, st); break;
-        case 64 * 4 + 1: rc = xb_launch<64, 1>(g, lds, (int)nt, st); break;
-        case 64 * 4 + 2: rc = xb_launch<64, 2>(g, lds, (int)nt, st); break;
-        case 128 * 4 + 1: rc = xb_launch<128, 1>(g, lds, (int)nt, st); break;
-        default: rc = xb_launch<128, 2>(g, lds, (int)nt, st); break;
+        case 16 * 4 + 1: rc = xb_launch<16, 1>(g, lds_b, (int)nt, st); break;
+        case 16 * 4 + 2: rc = xb_launch<16, 2>(g, lds_b, (int)nt, st); break;
+        case 32 * 4 + 1: rc = xb_launch<32, 1>(g, lds_b, (int)nt, st); break;
+        case 32 * 4 + 2: rc = xb_launch<32, 2>(g, lds_b, (int)nt, st); break;
+        case 64 * 4 + 1: rc = xb_launch<64, 1>(g, lds_b, (int)nt, st); break;
+        case 64 * 4 + 2: rc = xb_launch<64, 2>(g, lds_b, (int)nt, st); break;
+        case 128 * 4 + 1: rc = xb_launch<128, 1>(g, lds_b, (int)nt, st); break;
+        default: rc = xb_launch<128, 2>(g, lds_b, (int)nt, st); break;
     }
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
@@ -651,6 +732,10 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
     if (lds < 0) return VA_ERR_ARG;
     int64_t frags, biases;
     xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases);
+    g.off_b = lds, g.nbias = (int)biases;
+    const int lds_b = lds + (int)biases * 4;
+    if (lds_b > XB_LDS_MAX) return VA_ERR_ARG;
+    g.trace = g_xb_trace;
     g.x = (const float*)a->x;
     g.xu = (const float*)a->xu;
     g.y = (float*)a->y;
@@ -664,16 +749,23 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
     g.tpf = (int)tpf;
     hipError_t rc;
     switch (C * 4 + NB) {
-        case 16 * 4 + 1: rc = xf_launch<16, 1>(g, lds, (int)nt, st); break;
-        case 16 * 4 + 2: rc = xf_launch<16, 2>(g, lds, (int)nt, st); break;
-        case 32 * 4 + 1: rc = xf_launch<32, 1>(g, lds, (int)nt, st); break;
-        case 32 * 4 + 2: rc = xf_launch<32, 2>(g, lds, (int)nt, st); break;
-        case 64 * 4 + 1: rc = xf_launch<64, 1>(g, lds, (int)nt, st); break;
-        case 64 * 4 + 2: rc = xf_launch<64, 2>(g, lds, (int)nt, st); break;
-        case 128 * 4 + 1: rc = xf_launch<128, 1>(g, lds, (int)nt, st); break;
-        case 128 * 4 + 2: rc = xf_launch<128, 2>(g, lds, (int)nt, st); break;
-        case 256 * 4 + 1: rc = xf_launch<256, 1>(g, lds, (int)nt, st); break;
-        default: rc = xf_launch<256, 2>(g, lds, (int)nt, st); break;
+        case 16 * 4 + 1: rc = xf_launch<16, 1>(g, lds_b, (int)nt, st); break;
+        case 16 * 4 + 2: rc = xf_launch<16, 2>(g, lds_b, (int)nt, st); break;
+        case 32 * 4 + 1: rc = xf_launch<32, 1>(g, lds_b, (int)nt, st); break;
+        case 32 * 4 + 2: rc = xf_launch<32, 2>(g, lds_b, (int)nt, st); break;
+        case 64 * 4 + 1: rc = xf_launch<64, 1>(g, lds_b, (int)nt, st); break;
+        case 64 * 4 + 2: rc = xf_launch<64, 2>(g, lds_b, (int)nt, st); break;
+        case 128 * 4 + 1: rc = xf_launch<128, 1>(g, lds_b, (int)nt, st); break;
+        case 128 * 4 + 2: rc = xf_launch<128, 2>(g, lds_b, (int)nt, st); break;
+        case 256 * 4 + 1: rc = xf_launch<256, 1>(g, lds_b, (int)nt, st); break;
+        default: rc = xf_launch<256, 2>(g, lds_b, (int)nt, st); break;
     }
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
+}
+
+// Debug: stage clocks of the next va_seg_c2fb launches into device memory buf ([grid][10] uint64: s_memtime of thread 0
+// at the start, after each stage's barrier, and at the end), or stop (NULL)
+extern "C" int va_c2fb_trace(void* buf) {
+    g_xb_trace = (unsigned long long*)buf;
+    return VA_OK;
 }
