@@ -167,6 +167,10 @@ __device__ __forceinline__ void xb_conv(const XbGeom& g, unsigned char* smem, in
                 }
                 b[j] = *(const bf16x8*)(smem + addr);
             }
+            // the reads are used here, ahead of the guards: the compiler cannot sink them into the guarded blocks
+            // (where each got a wait of its own); one wait covers the four
+#pragma unroll
+            for (int j = 0; j < XB_G; ++j) asm volatile("" ::"v"(b[j]));
 #pragma unroll
             for (int j = 0; j < XB_G; ++j)
                 if (j < nb) acc[j] = mma(a, b[j], acc[j]);
@@ -466,6 +470,8 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
                             lv[j][0] = *(const f32x4*)p;
                             lv[j][1] = *(const f32x4*)(p + 16);
                         }
+#pragma unroll
+                        for (int j = 0; j < XF_G; ++j) asm volatile("" ::"v"(lv[j][0]), "v"(lv[j][1]));  // (as xb_conv)
                     }
 #pragma unroll
                     for (int j = 0; j < XF_G; ++j) {
