@@ -296,12 +296,15 @@ int va_seg_stem(void* stream, const va_conv_args* a);
  * (block.py C2f, Bottleneck) inside YOLO.predict (FrameProcessor.py:322).  VA_OP_C2F with a.mode == 3.
  * a.dtype = VA_DTYPE_F32 (the reference's precision; c up to 256): float activations (ldx, ldy, ldu % 4 == 0), every
  * product as six exact bf16 term products (va_seg_conv's f32 arithmetic), a.w = the same tiles as three fragments
- * each (h, m, l: the exact three-term bf16 split of the f32 weights, [tile][3][64 lanes][8]). */
+ * each (h, m, l: the exact three-term bf16 split of the f32 weights, [tile][3][64 lanes][8]).  Its intermediates sit in
+ * LDS as their three bf16 terms (split once by the producing conv's epilogue) where that layout fits, else as f32
+ * split per read (va_c2fb_layout out[3]). */
 int va_seg_c2fb(void* stream, const va_conv_args* a);
 /* va_seg_c2fb's sizes for hidden width c, n Bottlenecks, ci / co channels, tile side T, dtype and the stride-2
  * prologue's cs / cis channels (0, 0: none): out[0] = LDS bytes per workgroup, out[1] = A fragments (64 lanes x 8
- * bf16) of the weight blob, out[2] = floats of the bias blob.  VA_ERR_ARG when the shape is not covered or the layout
- * exceeds the 160 KiB of LDS (out[1], out[2] still set for a covered shape). */
+ * bf16) of the weight blob, out[2] = floats of the bias blob, out[3] = 1 when the f32 form keeps its intermediates as
+ * bf16 term planes (else 0).  VA_ERR_ARG when the shape is not covered or the layout exceeds the 160 KiB of LDS
+ * (out[1], out[2] still set for a covered shape).  out holds 4 values. */
 int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int32_t cs, int32_t cis,
                    int64_t* out);
 /* The same C2f block in f32 (the headline's precision) as ONE launch, every intermediate on the chip as three exact

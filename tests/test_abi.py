@@ -111,25 +111,29 @@ def _c2fb_expect(c, n, ci, co, cs=0, cis=0, f32=False):
     return tiles * (3 if f32 else 1), sum(16 * -(-o // 16) for o, _ in convs)
 
 
-@pytest.mark.parametrize("c,n,ci,co,T,cs,cis,f32", [
-    (16, 1, 32, 32, 16, 0, 0, False), (32, 2, 64, 64, 8, 64, 32, False), (64, 2, 128, 128, 4, 0, 0, False),
-    (128, 1, 256, 256, 2, 256, 128, False), (64, 1, 384, 128, 4, 0, 0, False), (64, 1, 192, 128, 4, 64, 64, False),
-    (128, 1, 384, 256, 2, 128, 128, False), (256, 1, 512, 512, 2, 0, 0, True), (64, 2, 128, 128, 4, 0, 0, True)])
-def test_c2fb_layout_matches_packing(c, n, ci, co, T, cs, cis, f32):
+@pytest.mark.parametrize("c,n,ci,co,T,cs,cis,f32,planes", [
+    (16, 1, 32, 32, 16, 0, 0, False, 0), (32, 2, 64, 64, 8, 64, 32, False, 0), (64, 2, 128, 128, 4, 0, 0, False, 0),
+    (128, 1, 256, 256, 2, 256, 128, False, 0), (64, 1, 384, 128, 4, 0, 0, False, 0),
+    (64, 1, 192, 128, 4, 64, 64, False, 0), (128, 1, 384, 256, 2, 128, 128, False, 0),
+    (256, 1, 512, 512, 2, 0, 0, True, 1), (64, 2, 128, 128, 4, 0, 0, True, 1), (128, 2, 256, 256, 2, 0, 0, True, 0),
+    (64, 1, 192, 128, 8, 0, 0, True, 1)])
+def test_c2fb_layout_matches_packing(c, n, ci, co, T, cs, cis, f32, planes):
     """va_c2fb_layout (host side of va_seg_c2fb): the LDS of the planner's tile sides for YOLOv8n's blocks (bf16, with
-    the stride-2 prologues it fuses) and s's (f32) fits 160 KiB, and the blob sizes equal the packing's."""
+    the stride-2 prologues it fuses) and s's (f32) fits 160 KiB, the blob sizes equal the packing's, and the f32 form
+    keeps its intermediates as bf16 term planes where they fit (s's model.6, c 128 with two Bottlenecks, stays f32)."""
     from vision_assist_amd import _lib
     lib = _lib.load()
-    out = (ctypes.c_int64 * 3)()
+    out = (ctypes.c_int64 * 4)()
     rc = lib.va_c2fb_layout(c, n, ci, co, T, 2 if f32 else 1, cs, cis, out)  # va355.h VA_DTYPE_F32 / _BF16
     assert rc == 0 and 0 < out[0] <= 160 * 1024, (rc, out[0])
     assert (out[1], out[2]) == _c2fb_expect(c, n, ci, co, cs, cis, f32)
+    assert out[3] == planes
 
 
 def test_c2fb_layout_rejects_what_the_kernel_does_not_cover():
     from vision_assist_amd import _lib
     lib = _lib.load()
-    out = (ctypes.c_int64 * 3)()
+    out = (ctypes.c_int64 * 4)()
     assert lib.va_c2fb_layout(48, 1, 96, 96, 4, 1, 0, 0, out) != 0        # hidden width 48
     assert lib.va_c2fb_layout(64, 3, 128, 128, 4, 1, 0, 0, out) != 0      # three Bottlenecks
     assert lib.va_c2fb_layout(128, 2, 256, 256, 16, 1, 0, 0, out) != 0    # past the LDS

@@ -350,6 +350,9 @@ struct XfGeom {
 
 template <int C>
 constexpr int pf() { return 4 * C + 16; }
+// the f32 form's LDS pixel stride: f32 values, or (PL) the three bf16 term planes h | m | l of C channels each
+template <int C, bool PL>
+constexpr int xps() { return PL ? 6 * C + 16 : 4 * C + 16; }
 
 __device__ __forceinline__ unsigned xf_pk(f32x2 v) {
     typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
@@ -373,6 +376,21 @@ __device__ __forceinline__ void xf_split3(const f32x4& lo, const f32x4& hi, bf16
 #pragma unroll
     for (int k = 0; k < 3; ++k) t[k] = __builtin_bit_cast(bf16x8, (u32x4){w[k][0], w[k][1], w[k][2], w[k][3]});
 }
+// four f32 -> their three bf16 terms, four of each (xf_split3's split)
+__device__ __forceinline__ void xf_split3x4(const f32x4& v, uint2 (&t)[3]) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const f32x2 x = {v[2 * e], v[2 * e + 1]};
+        const unsigned h = xf_pk(x);
+        const f32x2 r = x - xf_unpk(h);
+        const unsigned m = xf_pk(r);
+        const unsigned l = xf_pk(r - xf_unpk(m));
+        (e ? t[0].y : t[0].x) = h;
+        (e ? t[1].y : t[1].x) = m;
+        (e ? t[2].y : t[2].x) = l;
+    }
+}
+
 __device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 c) {
     c = mma(a[0], b[0], c);
     c = mma(a[0], b[1], c);
@@ -384,9 +402,12 @@ __device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3]
 
 // One f32 conv of the block (xb_conv's roles): KIND 0 = cv1 rows cb0 * 16 .. from global memory onto dst; 1 = 3x3
 // from src (+ res); 2 = cv2 over [R0a | R0b | R2 | R4 ..] at the tile's pixels, to g.y.
-template <int C, int NB, int KIND>
+// PL: the regions hold each value as its three bf16 terms (planes h | m | l per pixel, split once by the producing
+// epilogue) instead of f32 -- B fragments read as they are, no split per read (72 per element of a 128-channel 3x3)
+template <int C, int NB, int KIND, bool PL>
 __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, int q, int cb0, int nout, int kel, int ow,
                                         int oy, int ox, int n, XbIo src, XbIo dst, XbIo res, int lane, int wid) {
+    constexpr int EB = PL ? 2 : 4;  // LDS bytes per channel of a plane / per f32
     constexpr int H2 = 2 * NB;
     const int ks = (kel + 31) >> 5, ncb = (nout + 15) >> 4;
     const int P = ow * ow, npb = (P + 15) >> 4, ngr = (npb + XF_G - 1) / XF_G;
@@ -422,13 +443,13 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
             const int kk = min((k << 5) + (fq << 3), kel - 8);
             if constexpr (KIND == 1) {
                 const int tap = kk / C, ch = kk - tap * C, ky = tap / 3, kx = tap - 3 * ky;
-                return base[j] + (ky * src.w + kx) * src.ps + ch * 4;
+                return base[j] + (ky * src.w + kx) * src.ps + ch * EB;
             } else {
-                if (kk < C) return g.off_r0a + (pr[j] * g.T + pc[j]) * pf<C>() + kk * 4;
-                if (kk < 2 * C) return g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * pf<C>() + (kk - C) * 4;
+                if (kk < C) return g.off_r0a + (pr[j] * g.T + pc[j]) * xps<C, PL>() + kk * EB;
+                if (kk < 2 * C) return g.off_r[0] + ((pr[j] + H2) * S0 + pc[j] + H2) * xps<C, PL>() + (kk - C) * EB;
                 const int s = (kk - 2 * C) / C + 1, ch = kk - (s + 1) * C;
                 const int hs = H2 - 2 * s, ws = g.T + 2 * hs;
-                return g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * pf<C>() + ch * 4;
+                return g.off_r[2 * s] + ((pr[j] + hs) * ws + pc[j] + hs) * xps<C, PL>() + ch * EB;
             }
         };
         // K-steps in chunks of KC, double-buffered: the next chunk's A fragments (and, for cv1, its B operands from
@@ -463,7 +484,17 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
             for (int i = 0; i < KC; ++i) {
                 if (k0 + i < ks) {
                     f32x4 lv[XF_G][2];
-                    if constexpr (KIND != 0) {  // the blocks' LDS reads together, then their splits and MFMAs
+                    bf16x8 pv[XF_G][3];
+                    if constexpr (KIND != 0 && PL) {  // the blocks' three term fragments, read as they are
+#pragma unroll
+                        for (int j = 0; j < XF_G; ++j) {
+                            const unsigned char* p = smem + lds_addr(k0 + i, j);
+#pragma unroll
+                            for (int t = 0; t < 3; ++t) pv[j][t] = *(const bf16x8*)(p + 2 * C * t);
+                        }
+#pragma unroll
+                        for (int j = 0; j < XF_G; ++j) asm volatile("" ::"v"(pv[j][0]), "v"(pv[j][1]), "v"(pv[j][2]));
+                    } else if constexpr (KIND != 0) {  // the blocks' LDS reads together, then their splits and MFMAs
 #pragma unroll
                         for (int j = 0; j < XF_G; ++j) {
                             const unsigned char* p = smem + lds_addr(k0 + i, j);
@@ -476,10 +507,14 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
 #pragma unroll
                     for (int j = 0; j < XF_G; ++j) {
                         if (j < nb) {  // (unguarded, the bf16 form's live blocks went non-finite: kept guarded)
-                            bf16x8 bt[3];
-                            if constexpr (KIND == 0) xf_split3(bv[i][j][0], bv[i][j][1], bt);
-                            else xf_split3(lv[j][0], lv[j][1], bt);
-                            acc[j] = mma6(a[i], bt, acc[j]);
+                            if constexpr (KIND != 0 && PL) {
+                                acc[j] = mma6(a[i], pv[j], acc[j]);
+                            } else {
+                                bf16x8 bt[3];
+                                if constexpr (KIND == 0) xf_split3(bv[i][j][0], bv[i][j][1], bt);
+                                else xf_split3(lv[j][0], lv[j][1], bt);
+                                acc[j] = mma6(a[i], bt, acc[j]);
+                            }
                         }
                     }
                 }
@@ -502,19 +537,37 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
             const int r = pr[j], c = pc[j], iy = oy + r, ix = ox + c;
             const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
             f32x4 v = fz::act(acc[j] + bias);
-            if (KIND == 1 && res.off >= 0)
-                v += *(const f32x4*)(smem + res.off + ((r + 2) * res.w + c + 2) * res.ps + (res.c0 + co) * 4);
+            if (KIND == 1 && res.off >= 0) {
+                const unsigned char* rp = smem + res.off + ((r + 2) * res.w + c + 2) * res.ps + (res.c0 + co) * EB;
+                if constexpr (PL) {  // (h + m) + l: exact (the split's terms sum back to the value)
+                    const uint2 h = *(const uint2*)rp, m = *(const uint2*)(rp + 2 * C), l = *(const uint2*)(rp + 4 * C);
+                    const f32x2 h0 = xf_unpk(h.x), h1 = xf_unpk(h.y), m0 = xf_unpk(m.x), m1 = xf_unpk(m.y);
+                    const f32x2 l0 = xf_unpk(l.x), l1 = xf_unpk(l.y);
+                    v += (f32x4){(h0[0] + m0[0]) + l0[0], (h0[1] + m0[1]) + l0[1], (h1[0] + m1[0]) + l1[0],
+                                 (h1[1] + m1[1]) + l1[1]};
+                } else {
+                    v += *(const f32x4*)rp;
+                }
+            }
             if constexpr (KIND == 2) {
                 if (in) *(f32x4*)(g.y + ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldy + co) = v;
             } else {
                 if (!in) v = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-                *(f32x4*)(smem + dst.off + p * dst.ps + (dst.c0 + co) * 4) = v;
+                unsigned char* dp = smem + dst.off + p * dst.ps + (dst.c0 + co) * EB;
+                if constexpr (PL) {  // split once here for every later read
+                    uint2 t3[3];
+                    xf_split3x4(v, t3);
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) *(uint2*)(dp + 2 * C * t) = t3[t];
+                } else {
+                    *(f32x4*)dp = v;
+                }
             }
         }
     }
 }
 
-template <int C, int NB>
+template <int C, int NB, bool PL>
 __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int H2 = 2 * NB;
@@ -524,33 +577,34 @@ __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
     // the wave index as a scalar: item / block / guard arithmetic derived from it stays wave-uniform (scalar branches)
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const XbIo none = {-1, 0, 0, 0};
-    const XbIo r0b = {g.off_r[0], S0, pf<C>(), 0}, r0a = {g.off_r0a, T, pf<C>(), 0};
+    const XbIo r0b = {g.off_r[0], S0, xps<C, PL>(), 0}, r0a = {g.off_r0a, T, xps<C, PL>(), 0};
     XB_MARK(g, 0);
     xb_bias_to_lds(g.b, g.nbias, smem, g.off_b);
     __syncthreads();
-    xf_conv<C, NB, 0>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
+    xf_conv<C, NB, 0, PL>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
     if (g.trace) {
         __syncthreads();
         XB_MARK(g, 1);
     }
-    xf_conv<C, NB, 0>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
+    xf_conv<C, NB, 0, PL>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
     __syncthreads();
     XB_MARK(g, 3);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int hs = H2 - 2 * j, ws = T + 2 * hs;
-        const XbIo rin = j == 0 ? r0b : XbIo{g.off_r[2 * j], ws, pf<C>(), 0};
-        const XbIo rmid = {g.off_r[2 * j + 1], ws - 2, pf<C>(), 0}, rout = {g.off_r[2 * j + 2], ws - 4, pf<C>(), 0};
-        xf_conv<C, NB, 1>(g, smem, 1 + 2 * j, 0, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane,
+        const XbIo rin = j == 0 ? r0b : XbIo{g.off_r[2 * j], ws, xps<C, PL>(), 0};
+        const XbIo rmid = {g.off_r[2 * j + 1], ws - 2, xps<C, PL>(), 0};
+        const XbIo rout = {g.off_r[2 * j + 2], ws - 4, xps<C, PL>(), 0};
+        xf_conv<C, NB, 1, PL>(g, smem, 1 + 2 * j, 0, C, 9 * C, ws - 2, y0 - hs + 1, x0 - hs + 1, n, rin, rmid, none, lane,
                           wid);
         __syncthreads();
         XB_MARK(g, 4 + 2 * j);
-        xf_conv<C, NB, 1>(g, smem, 2 + 2 * j, 0, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
+        xf_conv<C, NB, 1, PL>(g, smem, 2 + 2 * j, 0, C, 9 * C, ws - 4, y0 - hs + 2, x0 - hs + 2, n, rmid, rout,
                           g.sc ? rin : none, lane, wid);
         __syncthreads();
         XB_MARK(g, 5 + 2 * j);
     }
-    xf_conv<C, NB, 2>(g, smem, 2 * NB + 1, 0, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
+    xf_conv<C, NB, 2, PL>(g, smem, 2 * NB + 1, 0, g.co, (2 + NB) * C, T, y0, x0, n, none, none, none, lane, wid);
     if (g.trace) {
         __syncthreads();
         XB_MARK(g, XB_TR - 1);
@@ -558,9 +612,9 @@ __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
 }
 
 // f32 LDS layout: [R0b][R0a][R1] .. [R2n]; returns the bytes (or -1)
-int xf_layout(int C, int NB, int T, int* off_r0a, int* off_r) {
+int xf_layout(int C, int NB, int T, int* off_r0a, int* off_r, bool pl = false) {
     if (T < 1 || T > 64) return -1;
-    const int S0 = T + 4 * NB, ps = 4 * C + 16;
+    const int S0 = T + 4 * NB, ps = pl ? 6 * C + 16 : 4 * C + 16;
     int64_t o = (int64_t)S0 * S0 * ps;
     off_r[0] = 0;
     *off_r0a = (int)o;
@@ -574,16 +628,29 @@ int xf_layout(int C, int NB, int T, int* off_r0a, int* off_r) {
 }
 
 template <int C, int NB>
-hipError_t xf_launch(const XfGeom& g, int lds, int ntiles, hipStream_t st) {
+hipError_t xf_launch(const XfGeom& g, int lds, int ntiles, hipStream_t st, bool pl) {
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)c2fbf_kernel<C, NB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)c2fbf_kernel<C, NB, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                XB_LDS_MAX) != hipSuccess ||
+            hipFuncSetAttribute((const void*)c2fbf_kernel<C, NB, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 XB_LDS_MAX) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
-    hipLaunchKernelGGL((c2fbf_kernel<C, NB>), dim3(ntiles), dim3(XB_NT), lds, st, g);
+    if (pl)
+        hipLaunchKernelGGL((c2fbf_kernel<C, NB, true>), dim3(ntiles), dim3(XB_NT), lds, st, g);
+    else
+        hipLaunchKernelGGL((c2fbf_kernel<C, NB, false>), dim3(ntiles), dim3(XB_NT), lds, st, g);
     return hipGetLastError();
+}
+
+// the f32 form's layout: the term planes where they fit the LDS with the biases, else f32 (*pl says which)
+int xf_choose(int C, int NB, int T, int nbias, int* off_r0a, int* off_r, bool* pl) {
+    int lds = xf_layout(C, NB, T, off_r0a, off_r, true);
+    *pl = lds >= 0 && lds + 4 * nbias <= XB_LDS_MAX;
+    if (!*pl) lds = xf_layout(C, NB, T, off_r0a, off_r, false);
+    return lds;
 }
 
 // LDS layout of one configuration: [R0][IN, later R1 .. R2n]; returns the bytes (or -1)
@@ -661,11 +728,15 @@ extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int3
         (cs && (f32 || !xb_s2_ok(ci, cs, cis))))
         return VA_ERR_ARG;
     int off_r[5], in_off, psi, wf[7], bo[7], off_sr, pss;
-    const int lds = f32 ? xf_layout(c, n, T, &in_off, off_r)
+    int64_t fr, nbias;
+    xb_blob(c, n, ci, co, wf, bo, &fr, &nbias, cs, cis);
+    bool pl;
+    const int lds = f32 ? xf_choose(c, n, T, (int)nbias, &in_off, off_r, &pl)
                         : xb_layout(c, n, ci, T, off_r, &in_off, &psi, cs ? cis : 0, &off_sr, &pss);
     xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2], cs, cis);
     if (f32) out3[1] *= 3;  // three term fragments per tile
     out3[0] = lds < 0 ? -1 : lds + 4 * out3[2];  // + the biases' LDS copy
+    out3[3] = f32 && pl;
     return lds < 0 || out3[0] > XB_LDS_MAX ? VA_ERR_ARG : VA_OK;
 }
 
@@ -734,10 +805,11 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
                   ((uintptr_t)a->xu & 15)))
         return VA_ERR_ARG;
     XfGeom g;
-    const int lds = xf_layout(C, NB, T, &g.off_r0a, g.off_r);
-    if (lds < 0) return VA_ERR_ARG;
     int64_t frags, biases;
     xb_blob(C, NB, ci, co, g.wf, g.bo, &frags, &biases);
+    bool pl;
+    const int lds = xf_choose(C, NB, T, (int)biases, &g.off_r0a, g.off_r, &pl);
+    if (lds < 0) return VA_ERR_ARG;
     g.off_b = lds, g.nbias = (int)biases;
     const int lds_b = lds + (int)biases * 4;
     if (lds_b > XB_LDS_MAX) return VA_ERR_ARG;
@@ -755,16 +827,16 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
     g.tpf = (int)tpf;
     hipError_t rc;
     switch (C * 4 + NB) {
-        case 16 * 4 + 1: rc = xf_launch<16, 1>(g, lds_b, (int)nt, st); break;
-        case 16 * 4 + 2: rc = xf_launch<16, 2>(g, lds_b, (int)nt, st); break;
-        case 32 * 4 + 1: rc = xf_launch<32, 1>(g, lds_b, (int)nt, st); break;
-        case 32 * 4 + 2: rc = xf_launch<32, 2>(g, lds_b, (int)nt, st); break;
-        case 64 * 4 + 1: rc = xf_launch<64, 1>(g, lds_b, (int)nt, st); break;
-        case 64 * 4 + 2: rc = xf_launch<64, 2>(g, lds_b, (int)nt, st); break;
-        case 128 * 4 + 1: rc = xf_launch<128, 1>(g, lds_b, (int)nt, st); break;
-        case 128 * 4 + 2: rc = xf_launch<128, 2>(g, lds_b, (int)nt, st); break;
-        case 256 * 4 + 1: rc = xf_launch<256, 1>(g, lds_b, (int)nt, st); break;
-        default: rc = xf_launch<256, 2>(g, lds_b, (int)nt, st); break;
+        case 16 * 4 + 1: rc = xf_launch<16, 1>(g, lds_b, (int)nt, st, pl); break;
+        case 16 * 4 + 2: rc = xf_launch<16, 2>(g, lds_b, (int)nt, st, pl); break;
+        case 32 * 4 + 1: rc = xf_launch<32, 1>(g, lds_b, (int)nt, st, pl); break;
+        case 32 * 4 + 2: rc = xf_launch<32, 2>(g, lds_b, (int)nt, st, pl); break;
+        case 64 * 4 + 1: rc = xf_launch<64, 1>(g, lds_b, (int)nt, st, pl); break;
+        case 64 * 4 + 2: rc = xf_launch<64, 2>(g, lds_b, (int)nt, st, pl); break;
+        case 128 * 4 + 1: rc = xf_launch<128, 1>(g, lds_b, (int)nt, st, pl); break;
+        case 128 * 4 + 2: rc = xf_launch<128, 2>(g, lds_b, (int)nt, st, pl); break;
+        case 256 * 4 + 1: rc = xf_launch<256, 1>(g, lds_b, (int)nt, st, pl); break;
+        default: rc = xf_launch<256, 2>(g, lds_b, (int)nt, st, pl); break;
     }
     return rc == hipSuccess ? VA_OK : VA_ERR_HIP;
 }

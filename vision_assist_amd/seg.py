@@ -150,10 +150,11 @@ class SegOutputs:
 
 class SegNet:
     def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2f32: bool = False,
-                 c2fb_f32: bool = False):
+                 c2fb_f32: bool = True):
         """c2f32: run model.2 on the fused f32 C2f kernel (va_seg_c2f_f32) in f32 plans -- off by default: it measured
         slower than the block's four launches.  c2fb_f32: the batch-1 C2f blocks of f32 plans on
-        va_seg_c2fb's f32 form -- off by default, measured slower."""
+        va_seg_c2fb's f32 form where its layout keeps the intermediates as term planes (_c2fb_tile); False keeps
+        them apart (A/B)."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
@@ -226,11 +227,10 @@ class SegNet:
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
         # small batches (bf16): every C2f block as one launch, intermediates on the chip and the 3x3s' halo recomputed
-        # per tile (va355.h va_seg_c2fb), for B <= c2fb_max_b; VA_C2FB=0 keeps the blocks' layers apart (A/B).  The
-        # f32 form of the same kernel is opt-in (c2fb_f32=True): its six term products per product put 6x the MFMA
-        # work of the halo recompute on the few dozen workgroups a batch-1 block has, and the s-seg batch-1 forward
-        # measured 1.28 -> 1.67 ms with it.  c2fb_tile: per block index a tile side overriding
-        # _c2fb_tile's choice (tools / tests)
+        # per tile (va355.h va_seg_c2fb), for B <= c2fb_max_b; VA_C2FB=0 keeps the blocks' layers apart (A/B).  f32
+        # plans take the f32 form of the same kernel for the blocks whose intermediates fit the LDS as bf16 term
+        # planes (split once per value, not per read): s-seg's batch-1 forward 1.28 -> 1.21 ms, n-seg's 1.05 ->
+        # 0.70.  c2fb_tile: per block index a tile side overriding _c2fb_tile's choice (tools / tests)
         on = os.environ.get("VA_C2FB", "1") != "0" and (dtype == "bf16" or (dtype == "f32" and c2fb_f32))
         self.c2fb_max_b = C2FB_MAX_B if on else 0
         self.c2fb = {}
@@ -290,19 +290,23 @@ class SegNet:
         return self.c2fb[(i, s2)]
 
     def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int, cs: int = 0, cis: int = 0):
-        """(LDS bytes or -1, A fragments, bias floats) of va_seg_c2fb's layout (va355.h va_c2fb_layout); cs / cis:
-        the stride-2 prologue's output / input channels (0: none)."""
-        out = (ctypes.c_int64 * 3)()
+        """(LDS bytes or -1, A fragments, bias floats, f32 term planes 1 / 0) of va_seg_c2fb's layout (va355.h
+        va_c2fb_layout); cs / cis: the stride-2 prologue's output / input channels (0: none)."""
+        out = (ctypes.c_int64 * 4)()
         rc = self.lib.va_c2fb_layout(c, n, ci, co, T, self.va_dtype, cs, cis, out)
-        return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]))
+        return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]), int(out[3]))
 
     def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int, cs: int = 0, cis: int = 0) -> int:
         """va_seg_c2fb's tile side for block i at B x h x w: the largest of 16 / 8 / 4 / 2 whose launch has at
         least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
-        larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits."""
+        larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits.  f32: only layouts
+        with the intermediates as term planes and hidden widths up to 128 -- the f32-region form (a split per read)
+        and s's 256-wide blocks at T = 2 measured slower than the blocks' layers apart."""
         if i in self.c2fb_tile:
             return self.c2fb_tile[i]
-        fits = [T for T in (16, 8, 4, 2) if self.c2fb_layout(co // 2, n, ci, co, T, cs, cis)[0] > 0]
+        c = co // 2
+        lay = {T: self.c2fb_layout(c, n, ci, co, T, cs, cis) for T in (16, 8, 4, 2)}
+        fits = [T for T, l in lay.items() if l[0] > 0 and (self.store == "bf16" or (l[3] and c <= 128))]
         for T in fits:
             if B * _cdiv(h, T) * _cdiv(w, T) >= C2FB_MIN_TILES:
                 return T
