@@ -346,7 +346,12 @@ struct XfGeom {
     int wf[6], bo[6];
     unsigned long long* trace;  // debug (va_c2fb_trace), as XbGeom's
     int off_b, nbias;           // the biases' copy in LDS (off_b) and their count
+    int off_stg;                // >= 0: cv1's operand staged in LDS from here (xf_cv1_staged), else read per item
 };
+
+// cv1's staged operand (PL): K-chunks of XF_SK input channels of the tile's S0 x S0 pixels, as three bf16 planes per
+// pixel (stride XF_SPS); XF_UMAX (pixel, 8-channel) units per thread stage a chunk, XF_IMAX items per wave
+constexpr int XF_SK = 64, XF_SPS = 6 * XF_SK + 16, XF_UMAX = 4, XF_IMAX = 4;
 
 template <int C>
 constexpr int pf() { return 4 * C + 16; }
@@ -567,6 +572,142 @@ __device__ __forceinline__ void xf_conv(const XfGeom& g, unsigned char* smem, in
     }
 }
 
+// cv1 (both halves: b on all S0 x S0 pixels -> R0b, a on the T x T centre -> R0a) with its operand staged: per K-chunk
+// of XF_SK channels the tile's input pixels are loaded from global memory once (the next chunk's in flight under this
+// chunk's MFMAs), split once into their three bf16 terms and stored as planes past R0a (R1 .. are not written yet);
+// every output-channel item then reads its B fragments from there as they are.  The per-item form (xf_conv KIND 0)
+// loads and splits each input element once per 16 output channels: 2C / 16 times.  Items (half, 16 output channels,
+// XF_G pixel blocks) as xf_conv's, at most XF_IMAX per wave (the host's condition), their accumulators held across
+// the chunks; the same K order, so the same sums.
+template <int C, int NB>
+__device__ __forceinline__ void xf_cv1_staged(const XfGeom& g, unsigned char* smem, int y0, int x0, int n, XbIo r0b,
+                                              XbIo r0a, int lane, int wid) {
+    constexpr int H2 = 2 * NB, NCB = C / 16, SKS = XF_SK / 32;
+    const int T = g.T, S0 = T + 2 * H2, PB = S0 * S0, PA = T * T;
+    const int ngrB = (((PB + 15) >> 4) + XF_G - 1) / XF_G, ngrA = (((PA + 15) >> 4) + XF_G - 1) / XF_G;
+    const int itB = ngrB * NCB, items = itB + ngrA * NCB;
+    const int fr = lane & 15, fq = lane >> 4, tid = threadIdx.x;
+    const int ks = (g.ci + 31) >> 5, nch = (g.ci + XF_SK - 1) / XF_SK;
+    unsigned char* stg = smem + g.off_stg;
+    f32x4 acc[XF_IMAX][XF_G];
+    int sp[XF_IMAX][XF_G];  // the lane's staged pixel per block (its row of the block)
+    int nbk[XF_IMAX];       // live blocks of the item (0: no item)
+    const bf16x8* wb[XF_IMAX];
+#pragma unroll
+    for (int i = 0; i < XF_IMAX; ++i) {
+        const int it = wid + XB_NW * i;
+        const bool hb = it < itB;
+        const int loc = hb ? it : it - itB, cb = loc % NCB, gr = loc / NCB;
+        const int ow = hb ? S0 : T, P = hb ? PB : PA;
+        nbk[i] = it < items ? min(XF_G, ((P + 15) >> 4) - gr * XF_G) : 0;
+        wb[i] = g.w + (int64_t)192 * (g.wf[0] + ((hb ? NCB : 0) + cb) * ks) + lane;
+#pragma unroll
+        for (int j = 0; j < XF_G; ++j) {
+            acc[i][j] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            const int p = min(((gr * XF_G + j) << 4) + fr, P - 1), r = p / ow, c = p - r * ow;
+            sp[i][j] = hb ? p : (r + H2) * S0 + c + H2;
+        }
+    }
+    // staging units u = tid + XB_NT m: pixel u / 8, channels 8 (u % 8) .. of the chunk
+    f32x4 rv[XF_UMAX][2];
+    auto load_units = [&](int ch) {
+#pragma unroll
+        for (int m = 0; m < XF_UMAX; ++m) {
+            const int u = tid + XB_NT * m, px = u >> 3, k = ch * XF_SK + ((u & 7) << 3);
+            const int r = px / S0, c = px - r * S0, iy = y0 - H2 + r, ix = x0 - H2 + c;
+            const bool live = px < PB && k < g.ci && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+            const bool up = k < g.cu;
+            const int64_t o = live ? (up ? ((int64_t)(n * (g.H >> 1) + (iy >> 1)) * (g.W >> 1) + (ix >> 1)) * g.ldu
+                                         : ((int64_t)(n * g.H + iy) * g.W + ix) * g.ldx) + k : 0;
+            const float* p = (live && up ? g.xu : g.x) + o;
+            const f32x4 z = {0.0f, 0.0f, 0.0f, 0.0f}, v0 = *(const f32x4*)p, v1 = *(const f32x4*)(p + 4);
+            rv[m][0] = live ? v0 : z;
+            rv[m][1] = live ? v1 : z;
+        }
+    };
+    auto store_units = [&]() {
+#pragma unroll
+        for (int m = 0; m < XF_UMAX; ++m) {
+            const int u = tid + XB_NT * m, px = u >> 3;
+            if (px < PB) {
+                bf16x8 t3[3];
+                xf_split3(rv[m][0], rv[m][1], t3);
+                unsigned char* d = stg + px * XF_SPS + ((u & 7) << 4);
+#pragma unroll
+                for (int t = 0; t < 3; ++t) *(bf16x8*)(d + 2 * XF_SK * t) = t3[t];
+            }
+        }
+    };
+    // item i's A fragments of chunk ch (both K-steps; clamped to the last step: a fixed count in flight)
+    bf16x8 a[XF_IMAX][SKS][3];
+    auto load_a = [&](int i, int ch) {
+#pragma unroll
+        for (int s = 0; s < SKS; ++s) {
+            const int k = min(ch * SKS + s, ks - 1);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) a[i][s][t] = wb[i][192 * k + 64 * t];
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < XF_IMAX; ++i) load_a(i, 0);
+    load_units(0);
+    for (int ch = 0; ch < nch; ++ch) {
+        // the staged operand, then the next chunk's loads in flight under this chunk's MFMAs: its input pixels, and
+        // each item's A fragments as soon as the item is done with this chunk's
+        store_units();
+        __syncthreads();
+        if (ch + 1 < nch) load_units(ch + 1);
+#pragma unroll
+        for (int i = 0; i < XF_IMAX; ++i) {
+            if (nbk[i] == 0) continue;  // wave-uniform
+#pragma unroll
+            for (int s = 0; s < SKS; ++s) {
+                if (ch * SKS + s >= ks) continue;
+                bf16x8 pv[XF_G][3];
+#pragma unroll
+                for (int j = 0; j < XF_G; ++j) {
+                    const unsigned char* p = stg + sp[i][j] * XF_SPS + ((s * 32 + 8 * fq) << 1);
+#pragma unroll
+                    for (int t = 0; t < 3; ++t) pv[j][t] = *(const bf16x8*)(p + 2 * XF_SK * t);
+                }
+#pragma unroll
+                for (int j = 0; j < XF_G; ++j) asm volatile("" ::"v"(pv[j][0]), "v"(pv[j][1]), "v"(pv[j][2]));
+#pragma unroll
+                for (int j = 0; j < XF_G; ++j)
+                    if (j < nbk[i]) acc[i][j] = mma6(a[i][s], pv[j], acc[i][j]);
+            }
+            load_a(i, ch + 1);
+        }
+        __syncthreads();  // the chunk read by every item before the next one is stored
+    }
+    // epilogue (xf_conv's, KIND 0): bias + SiLU, zero outside the frame, split once into the region's planes
+#pragma unroll
+    for (int i = 0; i < XF_IMAX; ++i) {
+        if (nbk[i] == 0) continue;
+        const int it = wid + XB_NW * i;
+        const bool hb = it < itB;
+        const int loc = hb ? it : it - itB, cb = loc % NCB, gr = loc / NCB;
+        const int ow = hb ? S0 : T, P = hb ? PB : PA, oy = hb ? y0 - H2 : y0, ox = hb ? x0 - H2 : x0;
+        const XbIo dst = hb ? r0b : r0a;
+        const int co = (cb << 4) + (fq << 2);
+        const f32x4 bias = *(const f32x4*)(smem + g.off_b + (g.bo[0] + (hb ? C : 0) + co) * 4);
+#pragma unroll
+        for (int j = 0; j < XF_G; ++j) {
+            const int p = ((gr * XF_G + j) << 4) + fr;
+            if (j >= nbk[i] || p >= P) continue;
+            const int r = p / ow, c = p - r * ow, iy = oy + r, ix = ox + c;
+            const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+            f32x4 v = fz::act(acc[i][j] + bias);
+            if (!in) v = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+            uint2 t3[3];
+            xf_split3x4(v, t3);
+            unsigned char* dp = smem + dst.off + p * dst.ps + (dst.c0 + co) * 2;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) *(uint2*)(dp + 2 * C * t) = t3[t];
+        }
+    }
+}
+
 template <int C, int NB, bool PL>
 __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -581,12 +722,16 @@ __global__ __launch_bounds__(XB_NT) void c2fbf_kernel(XfGeom g) {
     XB_MARK(g, 0);
     xb_bias_to_lds(g.b, g.nbias, smem, g.off_b);
     __syncthreads();
-    xf_conv<C, NB, 0, PL>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
-    if (g.trace) {
-        __syncthreads();
-        XB_MARK(g, 1);
+    if (PL && g.off_stg >= 0) {  // kernel-uniform
+        xf_cv1_staged<C, NB>(g, smem, y0, x0, n, r0b, r0a, lane, wid);
+    } else {
+        xf_conv<C, NB, 0, PL>(g, smem, 0, C / 16, C, g.ci, S0, y0 - H2, x0 - H2, n, none, r0b, none, lane, wid);
+        if (g.trace) {
+            __syncthreads();
+            XB_MARK(g, 1);
+        }
+        xf_conv<C, NB, 0, PL>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
     }
-    xf_conv<C, NB, 0, PL>(g, smem, 0, 0, C, g.ci, T, y0, x0, n, none, r0a, none, lane, wid);
     __syncthreads();
     XB_MARK(g, 3);
 #pragma unroll
@@ -643,6 +788,20 @@ hipError_t xf_launch(const XfGeom& g, int lds, int ntiles, hipStream_t st, bool 
     else
         hipLaunchKernelGGL((c2fbf_kernel<C, NB, false>), dim3(ntiles), dim3(XB_NT), lds, st, g);
     return hipGetLastError();
+}
+
+// cv1's operand staged (xf_cv1_staged, term-plane layouts) where its chunk fits from R1 on (moving the biases up if it
+// reaches past the regions), its units fit XF_UMAX per thread and its items XF_IMAX per wave: *off_stg (else -1);
+// returns the biases' LDS offset
+int xf_stage(int C, int NB, int T, bool pl, int lds, int nbias, int off_r1, int* off_stg) {
+    const int S0 = T + 4 * NB, pb = S0 * S0;
+    auto groups = [](int p) { return ((p + 15) / 16 + XF_G - 1) / XF_G; };
+    const int items = (C / 16) * (groups(pb) + groups(T * T));
+    const int end = off_r1 + pb * XF_SPS, ob = end > lds ? (end + 15) & ~15 : lds;
+    *off_stg = -1;
+    if (!pl || pb * 8 > XB_NT * XF_UMAX || items > XB_NW * XF_IMAX || ob + 4 * nbias > XB_LDS_MAX) return lds;
+    *off_stg = off_r1;
+    return ob;
 }
 
 // the f32 form's layout: the term planes where they fit the LDS with the biases, else f32 (*pl says which)
@@ -735,7 +894,9 @@ extern "C" int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int3
                         : xb_layout(c, n, ci, T, off_r, &in_off, &psi, cs ? cis : 0, &off_sr, &pss);
     xb_blob(c, n, ci, co, wf, bo, &out3[1], &out3[2], cs, cis);
     if (f32) out3[1] *= 3;  // three term fragments per tile
-    out3[0] = lds < 0 ? -1 : lds + 4 * out3[2];  // + the biases' LDS copy
+    int off_stg;
+    const int ob = f32 && lds >= 0 ? xf_stage(c, n, T, pl, lds, (int)nbias, off_r[1], &off_stg) : lds;
+    out3[0] = lds < 0 ? -1 : ob + 4 * out3[2];  // + the biases' LDS copy
     out3[3] = f32 && pl;
     return lds < 0 || out3[0] > XB_LDS_MAX ? VA_ERR_ARG : VA_OK;
 }
@@ -810,8 +971,9 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
     bool pl;
     const int lds = xf_choose(C, NB, T, (int)biases, &g.off_r0a, g.off_r, &pl);
     if (lds < 0) return VA_ERR_ARG;
-    g.off_b = lds, g.nbias = (int)biases;
-    const int lds_b = lds + (int)biases * 4;
+    g.nbias = (int)biases;
+    g.off_b = xf_stage(C, NB, T, pl, lds, (int)biases, g.off_r[1], &g.off_stg);
+    const int lds_b = g.off_b + (int)biases * 4;
     if (lds_b > XB_LDS_MAX) return VA_ERR_ARG;
     g.trace = g_xb_trace;
     g.x = (const float*)a->x;
