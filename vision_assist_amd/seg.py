@@ -30,9 +30,7 @@ FP8_HEADROOM = 8.0  # calibration amax x this x the buffer scale lands in [224, 
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 VA_OP_FORK, VA_OP_JOIN = 8, 9  # lanes of a branch-parallel list (va355.h)
 C2FB_MAX_B = 1      # va_seg_c2fb for batches up to this (SegNet.c2fb_max_b)
-C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may leave (bf16)
-C2FB_CUS = 256       # SegNet._c2fb_tile_f32: workgroups per round (one per CU)
-C2FB_F32_FIXED = 16_000_000  # SegNet._c2fb_tile_f32: a tile's fixed latency in MACs
+C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may leave
 SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -291,27 +289,6 @@ class SegNet:
         self.c2fb[(i, s2)] = (torch.cat(frags).contiguous(), torch.cat(biases).contiguous())
         return self.c2fb[(i, s2)]
 
-    def _c2fb_tile_f32(self, B: int, h: int, w: int, ci: int, co: int, n: int, c: int) -> int:
-        """The f32 form's tile side: any T <= 16 whose layout keeps the intermediates as term planes (hidden width
-        <= 128), at the least (workgroup rounds) x (per-tile MACs with the halos + C2FB_F32_FIXED): one 8-wave
-        workgroup per CU (its registers), so tiles past a multiple of C2FB_CUS cost a whole round, and a tile's fixed
-        latency is worth C2FB_F32_FIXED MACs (fitted to the batch-1 s-seg blocks: model.12 / 18 at T = 3, 78 / 59 us,
-        against 87 / 67 at T = 4; model.15 at T = 5, 41 us, against 55 at T = 8, profiles/r05/c2fb_tiles/)."""
-        if c > 128:
-            return 0
-        best, bcost = 0, None
-        for T in range(16, 1, -1):  # (T = 1: a 1 + 4n square of halo per output pixel)
-            lay = self.c2fb_layout(c, n, ci, co, T)
-            if lay[0] <= 0 or not lay[3]:
-                continue
-            S0 = T + 4 * n
-            macs = (S0 * S0 + T * T) * ci * c + T * T * (2 + n) * c * co
-            macs += sum(((S0 - 4 * j - 2) ** 2 + (S0 - 4 * j - 4) ** 2) * 9 * c * c for j in range(n))
-            cost = _cdiv(B * _cdiv(h, T) * _cdiv(w, T), C2FB_CUS) * (macs + C2FB_F32_FIXED)
-            if bcost is None or cost < bcost:
-                best, bcost = T, cost
-        return best
-
     def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int, cs: int = 0, cis: int = 0):
         """(LDS bytes or -1, A fragments, bias floats, f32 term planes 1 / 0) of va_seg_c2fb's layout (va355.h
         va_c2fb_layout); cs / cis: the stride-2 prologue's output / input channels (0: none)."""
@@ -322,17 +299,14 @@ class SegNet:
     def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int, cs: int = 0, cis: int = 0) -> int:
         """va_seg_c2fb's tile side for block i at B x h x w: the largest of 16 / 8 / 4 / 2 whose launch has at
         least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
-        larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits.  f32:
-        _c2fb_tile_f32 -- only layouts with the intermediates as term planes and hidden widths up to 128: the
-        f32-region form (a split per read) and s's 256-wide blocks at T = 2 measured slower than the blocks' layers
-        apart."""
+        larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits.  f32: only layouts
+        with the intermediates as term planes and hidden widths up to 128 -- the f32-region form (a split per read)
+        and s's 256-wide blocks at T = 2 measured slower than the blocks' layers apart."""
         if i in self.c2fb_tile:
             return self.c2fb_tile[i]
         c = co // 2
-        if self.store == "f32":
-            return self._c2fb_tile_f32(B, h, w, ci, co, n, c)
         lay = {T: self.c2fb_layout(c, n, ci, co, T, cs, cis) for T in (16, 8, 4, 2)}
-        fits = [T for T, l in lay.items() if l[0] > 0]
+        fits = [T for T, l in lay.items() if l[0] > 0 and (self.store == "bf16" or (l[3] and c <= 128))]
         for T in fits:
             if B * _cdiv(h, T) * _cdiv(w, T) >= C2FB_MIN_TILES:
                 return T
