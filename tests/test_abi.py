@@ -130,6 +130,25 @@ def test_c2fb_layout_matches_packing(c, n, ci, co, T, cs, cis, f32, planes):
     assert out[3] == planes
 
 
+@pytest.mark.parametrize("c,n,ci,co,T,lds", [
+    (64, 1, 384, 128, 8, 150336),   # s's model.15: cv1's staged chunk inside the regions (R1 on), biases after them
+    (64, 1, 192, 128, 4, 59136),    # the staged chunk past the regions: the biases move up behind it
+    (128, 1, 768, 256, 4, 106560)])
+def test_c2fb_f32_layout_with_cv1_staging(c, n, ci, co, T, lds):
+    """va_c2fb_layout's f32 LDS with cv1's operand staged (va_c2fb.hip xf_stage: 64-channel chunks of the tile's
+    S0 x S0 pixels as three bf16 planes, 400 bytes a pixel, from R1's offset): the regions R0b | R0a | R1 .. at 6C + 16
+    bytes a pixel, then the chunk where it reaches past them, then the biases."""
+    from vision_assist_amd import _lib
+    lib = _lib.load()
+    out = (ctypes.c_int64 * 4)()
+    assert lib.va_c2fb_layout(c, n, ci, co, T, 2, 0, 0, out) == 0 and out[3] == 1
+    S0, ps = T + 4 * n, 6 * c + 16
+    regions = [S0 * S0, T * T] + [(T + 2 * (2 * n - j)) ** 2 for j in range(1, 2 * n + 1)]
+    off_r1 = (regions[0] + regions[1]) * ps
+    end = max(sum(regions) * ps, off_r1 + S0 * S0 * 400)
+    assert out[0] == end + 4 * out[2] == lds
+
+
 def test_c2fb_layout_rejects_what_the_kernel_does_not_cover():
     from vision_assist_amd import _lib
     lib = _lib.load()
