@@ -2,7 +2,8 @@
 """va_seg_c2fb at large batches: the f32 (or bf16) forward with chosen C2f blocks as one launch each (tile sides given
 per block) against the default plan, rounds interleaved in one process (HIP events around whole forwards), then
 per-op event times of the fused blocks.  The fused variants run with the stem's cv1 tail off (VA_STEM_TAIL=0: the
-block's cv1 is part of the fused launch).  Run on the GPU box:
+block's cv1 is part of the fused launch; --rest planner: the unlisted blocks as the planner takes them).  Run on
+the GPU box:
     python tools/c2fb_big.py --batch 64 --blocks 2:8 --blocks 2:4"""
 import argparse
 import ctypes
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--scale", default="s")
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--blocks", action="append", default=[], help="variant: i:T[,i:T..] (fused blocks, tile sides)")
+    ap.add_argument("--rest", default="off", choices=["off", "planner"],
+                    help="blocks a variant does not list: unfused (off) or the planner's choice")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--json", default="")
@@ -43,7 +46,7 @@ def main():
         net = S.SegNet(arch, fw, dtype=a.dtype, c2fb_f32=True)
         del os.environ["VA_STEM_TAIL"]
         net.c2fb_max_b = B
-        net.c2fb_tile = {i: tiles.get(i, 0) for i in BLOCKS}
+        net.c2fb_tile = dict(tiles) if a.rest == "planner" else {i: tiles.get(i, 0) for i in BLOCKS}
         nets["fused " + v] = net
     plans = {}
     for k, net in nets.items():
