@@ -125,9 +125,9 @@ def test_c2fb_forward_vs_unfused(monkeypatch):
     arch, fw, net = _net()
     names = [m["name"] for m in net.plan(1, 640, 640)["meta"]]
     assert sum("fused C2f, T=" in nm for nm in names) == 8, names
-    # the stride-2 prologues where they leave the block its tile side (model.5 stays a launch of its own)
+    # the stride-2 prologues where they leave the block its tile side (all five at the cost model's sides)
     assert [nm.split("+")[0] for nm in names if "+model." in nm and "C2f" in nm] == \
-        ["model.3", "model.7", "model.16", "model.19"], names
+        ["model.3", "model.5", "model.7", "model.16", "model.19"], names
     frames = torch.randint(0, 256, (1, 640, 640, 3), generator=torch.Generator().manual_seed(4), dtype=torch.uint8)
 
     def heads(nt):

@@ -30,7 +30,9 @@ FP8_HEADROOM = 8.0  # calibration amax x this x the buffer scale lands in [224, 
 VA_OP_CONV, VA_OP_SPPF, VA_OP_UPSAMPLE, VA_OP_PREPROCESS, VA_OP_CONV0, VA_OP_C2F, VA_OP_STEM = 1, 2, 3, 4, 5, 6, 7
 VA_OP_FORK, VA_OP_JOIN = 8, 9  # lanes of a branch-parallel list (va355.h)
 C2FB_MAX_B = 1      # va_seg_c2fb for batches up to this (SegNet.c2fb_max_b)
-C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may leave
+C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may leave (f32)
+C2FB_CUS = 256       # SegNet._c2fb_tile_bf16: workgroups per round (one per CU)
+C2FB_FIXED = 16_000_000  # SegNet._c2fb_tile_bf16: a tile's fixed latency, in MACs
 SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
@@ -289,6 +291,26 @@ class SegNet:
         self.c2fb[(i, s2)] = (torch.cat(frags).contiguous(), torch.cat(biases).contiguous())
         return self.c2fb[(i, s2)]
 
+    def _c2fb_tile_bf16(self, B: int, h: int, w: int, ci: int, co: int, n: int, c: int, cs: int, cis: int) -> int:
+        """bf16 (C2's latency plan): any side 2 .. 16 whose layout fits (with the stride-2 prologue's source region
+        when cs), at the least (workgroup rounds of C2FB_CUS) x (per-tile MACs with the halos + C2FB_FIXED): a tile
+        count just past a multiple of the CUs costs a whole round, and 100 tiles leave most CUs idle.  n-seg batch 1:
+        model.2 / 4 / 6 / 12 / 15 / 18 at T = 10 / 5 / 3 / 3 / 5 / 3 instead of 16 / 8 / 4 / 4 / 8 / 4 (all five
+        stride-2 prologues fused), C2 seg-only 0.362 -> 0.346 ms (profiles/r05/c2fb_tiles/bf16_n/).  (The f32 form
+        keeps the 96-tile rule: with several frames in flight on other streams its full-chip launches cost C4 5 %,
+        DESIGN.md §4.1.)"""
+        best, bcost = 0, None
+        for T in range(16, 1, -1):
+            if self.c2fb_layout(c, n, ci, co, T, cs, cis)[0] <= 0:
+                continue
+            S0 = T + 4 * n
+            macs = (S0 * S0 + T * T) * ci * c + T * T * (2 + n) * c * co + S0 * S0 * 9 * cis * cs
+            macs += sum(((S0 - 4 * j - 2) ** 2 + (S0 - 4 * j - 4) ** 2) * 9 * c * c for j in range(n))
+            cost = _cdiv(B * _cdiv(h, T) * _cdiv(w, T), C2FB_CUS) * (macs + C2FB_FIXED)
+            if bcost is None or cost < bcost:
+                best, bcost = T, cost
+        return best
+
     def c2fb_layout(self, c: int, n: int, ci: int, co: int, T: int, cs: int = 0, cis: int = 0):
         """(LDS bytes or -1, A fragments, bias floats, f32 term planes 1 / 0) of va_seg_c2fb's layout (va355.h
         va_c2fb_layout); cs / cis: the stride-2 prologue's output / input channels (0: none)."""
@@ -297,14 +319,16 @@ class SegNet:
         return (int(out[0]) if rc == 0 else -1, int(out[1]), int(out[2]), int(out[3]))
 
     def _c2fb_tile(self, i: int, B: int, h: int, w: int, ci: int, co: int, n: int, cs: int = 0, cis: int = 0) -> int:
-        """va_seg_c2fb's tile side for block i at B x h x w: the largest of 16 / 8 / 4 / 2 whose launch has at
-        least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
+        """va_seg_c2fb's tile side for block i at B x h x w (bf16: _c2fb_tile_bf16): the largest of 16 / 8 / 4 / 2
+        whose launch has at least C2FB_MIN_TILES workgroups (a batch-1 layer fills a few dozen of the 256 CUs, so a smaller tile's
         larger halo share costs less than idle CUs) and whose LDS layout fits; 0 when none fits.  f32: only layouts
         with the intermediates as term planes and hidden widths up to 128 -- the f32-region form (a split per read)
         and s's 256-wide blocks at T = 2 measured slower than the blocks' layers apart."""
         if i in self.c2fb_tile:
             return self.c2fb_tile[i]
         c = co // 2
+        if self.store == "bf16":
+            return self._c2fb_tile_bf16(B, h, w, ci, co, n, c, cs, cis)
         lay = {T: self.c2fb_layout(c, n, ci, co, T, cs, cis) for T in (16, 8, 4, 2)}
         fits = [T for T, l in lay.items() if l[0] > 0 and (self.store == "bf16" or (l[3] and c <= 128))]
         for T in fits:
@@ -651,7 +675,7 @@ class SegNet:
                 T = self._c2fb_tile(i, B, h, w, ci, co, n)
                 # the stride-2 prologue where its source region still leaves the block its tile side (a smaller tile
                 # recomputes more of the block than the prologue saves: model.5 + model.6 of n-seg at T = 2 took 74 us
-                # against 15 + 30 apart, profiles/r05/c2fb/ab_b1_s2.log)
+                # against 15 + 30 apart, profiles/r05/c2fb/ab_b1_s2.log; at T = 3, 38 against 15 + 27)
                 if s2 is not None and not (self.store == "bf16" and up is None and s2[1].ld % 8 == 0 and
                                            s2[1].c == cis and cis >= 8 and cis & (cis - 1) == 0 and cs % 16 == 0 and
                                            T and self._c2fb_tile(i, B, h, w, ci, co, n, cs, cis) == T):
