@@ -351,7 +351,7 @@ struct XfGeom {
 
 // cv1's staged operand (PL): K-chunks of XF_SK input channels of the tile's S0 x S0 pixels, as three bf16 planes per
 // pixel (stride XF_SPS); XF_UMAX (pixel, 8-channel) units per thread stage a chunk, XF_IMAX items per wave
-constexpr int XF_SK = 64, XF_SPS = 6 * XF_SK + 16, XF_UMAX = 4, XF_IMAX = 4;
+constexpr int XF_SK = 64, XF_UPP = XF_SK / 8, XF_SPS = 6 * XF_SK + 16, XF_UMAX = 4, XF_IMAX = 4;
 
 template <int C>
 constexpr int pf() { return 4 * C + 16; }
@@ -608,12 +608,12 @@ __device__ __forceinline__ void xf_cv1_staged(const XfGeom& g, unsigned char* sm
             sp[i][j] = hb ? p : (r + H2) * S0 + c + H2;
         }
     }
-    // staging units u = tid + XB_NT m: pixel u / 8, channels 8 (u % 8) .. of the chunk
+    // staging units u = tid + XB_NT m: pixel u / XF_UPP, channels 8 (u % XF_UPP) .. of the chunk
     f32x4 rv[XF_UMAX][2];
     auto load_units = [&](int ch) {
 #pragma unroll
         for (int m = 0; m < XF_UMAX; ++m) {
-            const int u = tid + XB_NT * m, px = u >> 3, k = ch * XF_SK + ((u & 7) << 3);
+            const int u = tid + XB_NT * m, px = u / XF_UPP, k = ch * XF_SK + ((u % XF_UPP) << 3);
             const int r = px / S0, c = px - r * S0, iy = y0 - H2 + r, ix = x0 - H2 + c;
             const bool live = px < PB && k < g.ci && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
             const bool up = k < g.cu;
@@ -628,11 +628,11 @@ __device__ __forceinline__ void xf_cv1_staged(const XfGeom& g, unsigned char* sm
     auto store_units = [&]() {
 #pragma unroll
         for (int m = 0; m < XF_UMAX; ++m) {
-            const int u = tid + XB_NT * m, px = u >> 3;
+            const int u = tid + XB_NT * m, px = u / XF_UPP;
             if (px < PB) {
                 bf16x8 t3[3];
                 xf_split3(rv[m][0], rv[m][1], t3);
-                unsigned char* d = stg + px * XF_SPS + ((u & 7) << 4);
+                unsigned char* d = stg + px * XF_SPS + ((u % XF_UPP) << 4);
 #pragma unroll
                 for (int t = 0; t < 3; ++t) *(bf16x8*)(d + 2 * XF_SK * t) = t3[t];
             }
@@ -799,7 +799,7 @@ int xf_stage(int C, int NB, int T, bool pl, int lds, int nbias, int off_r1, int*
     const int items = (C / 16) * (groups(pb) + groups(T * T));
     const int end = off_r1 + pb * XF_SPS, ob = end > lds ? (end + 15) & ~15 : lds;
     *off_stg = -1;
-    if (!pl || pb * 8 > XB_NT * XF_UMAX || items > XB_NW * XF_IMAX || ob + 4 * nbias > XB_LDS_MAX) return lds;
+    if (!pl || pb * XF_UPP > XB_NT * XF_UMAX || items > XB_NW * XF_IMAX || ob + 4 * nbias > XB_LDS_MAX) return lds;
     *off_stg = off_r1;
     return ob;
 }
