@@ -307,13 +307,6 @@ int va_seg_c2fb(void* stream, const va_conv_args* a);
  * (out[1], out[2] still set for a covered shape).  out holds 4 values. */
 int va_c2fb_layout(int32_t c, int32_t n, int32_t ci, int32_t co, int32_t T, int32_t dtype, int32_t cs, int32_t cis,
                    int64_t* out);
-/* The same C2f block in f32 (the headline's precision) as ONE launch, every intermediate on the chip as three exact
- * bf16 planes, the convs as six exact term products: a.x / a.ldx (float, 64 channels, ldx % 4 == 0), a.y / a.ldy
- * (float, ldy % 4 == 0), a.N / H / W, a.Cin = a.Cout = 64, a.dtype = VA_DTYPE_F32, and
- *   a.w    float blob [cv1 64 x 64 | m.0.cv1 32 x 288 | m.0.cv2 32 x 288 | cv2 64 x 96], rows [Cout][K], K ordered
- *          (ky, kx, ci) (layout: seg.py SegNet._pack_c2f32)
- *   a.bias float [64 | 32 | 32 | 64] */
-int va_seg_c2f_f32(void* stream, const va_conv_args* a);
 /* The stem in f32 (the headline's precision) as ONE launch: uint8 BGR frames [N][H][W][3] -> model.0 (the
  * three exact bf16 terms of its weights x the frame bytes, x 1/255, + bias, SiLU) -> model.1 Conv(32, 64, 3x3, s2)
  * + SiLU as six exact bf16 term products -> float a.y [N][ceil(H/4)][ceil(W/4)] (channel stride a.ldy % 4 == 0);

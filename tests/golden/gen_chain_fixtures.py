@@ -12,6 +12,8 @@ Sets:
                   per shard, frames in shard order (SURVEY.md §8e per-shard replay); regimes sparse / dense_box.
   c5/<regime>:    YOLOv8m-seg at 1280 x 1280 (BASELINE configs[4]), frames frame_batch(8000, 8, 1280), one
                   PathFinder state; regimes sparse / dense_box (the fp8 chain test's reference).
+  c2/<regime>:    YOLOv8n-seg 640 (BASELINE configs[1]), frames frame_batch(9000 + i, 1), i < 16, one at a time
+                  with one PathFinder state (C2's batch-1 plan, tests/test_gpu_chain.py); regime sparse.
 
 Per frame: det float32 [k, 6] (x1 y1 x2 y2 score cls, base64), chosen index, rect, cells uint8 [32, 32]
 (base64), A* paths and float64 costs (hex).  Re-run:  python tests/golden/gen_chain_fixtures.py  (~5 min, 8 CPUs)
@@ -31,7 +33,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 OUT = os.path.join(HERE, "chain_oracle.json.gz")
-CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES = 32, 8, 2, 8
+CHAIN_FRAMES, C4_FRAMES, C4_WORLD, C5_FRAMES, C2_FRAMES = 32, 8, 2, 8, 16
 
 
 def _enc(rec: dict) -> dict:
@@ -59,6 +61,10 @@ def _job(args):
         arch, fw = weights(regime, scale="m")
         torch.set_num_threads(4)
         return f"c5/{regime}", [_enc(r) for r in oracle_sequence(arch, fw, frame_batch(8000, C5_FRAMES, 1280))]
+    if kind == "c2":
+        arch, fw = weights(regime, scale="n")
+        pf = onav.PathFinderOracle()
+        return f"c2/{regime}", [_enc(oracle_frame(arch, fw, frame_batch(9000 + i, 1), pf)) for i in range(C2_FRAMES)]
     recs = [None] * C4_FRAMES
     for r in range(C4_WORLD):
         pf = onav.PathFinderOracle()
@@ -70,7 +76,7 @@ def _job(args):
 def main():
     only = sys.argv[1:]  # optional set names to (re)generate, the rest kept from the existing file
     jobs = [("chain", r) for r in ("sparse", "dense", "dense_box")] + [("c4", r) for r in ("sparse", "dense_box")] + \
-        [("c5", r) for r in ("sparse", "dense_box")]
+        [("c5", r) for r in ("sparse", "dense_box")] + [("c2", "sparse")]
     old = {}
     if only and os.path.exists(OUT):
         with gzip.open(OUT, "rt") as f:

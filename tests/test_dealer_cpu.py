@@ -150,3 +150,32 @@ def test_dealer_dead_worker_raises_instead_of_hanging():
         assert d.broken
         with pytest.raises(RuntimeError):
             d.submit(np.full((4, 4, 3), 2, np.uint8))
+
+
+@pytest.mark.parametrize("readers", [1, 2, 3])
+def test_dealer_reader_threads_in_order(readers):
+    """Frames copied into the rings by reader threads (FrameDealer readers > 0: thread r fills the rings of workers
+    w % R == r): the same in-order answers as the calling-thread copies, batching and frame-by-frame workers, rings
+    small enough that every reader waits for free slots."""
+    from vision_assist_amd.shard import FrameDealer
+    vals = list(range(1, 7)) + list(range(8, 40))
+    with FrameDealer(BatchingWorker(), [None, None, None], 4, 4, slots=2, readers=readers) as d:
+        got = list(d.map(np.full((4, 4, 3), v, np.uint8) for v in vals))
+        assert [g[0] for g in got] == vals
+    with FrameDealer(FailingWorker(), [None, None], 4, 4, slots=1, readers=readers) as d:
+        assert list(d.map(np.full((4, 4, 3), v, np.uint8) for v in vals)) == vals
+
+
+def test_dealer_refuses_a_ring_larger_than_dev_shm(monkeypatch):
+    """the ring lives in /dev/shm; a ring that does not fit is refused up front with its size named, not
+    left to fail (or SIGBUS) inside torch's shared-memory allocation."""
+    import os
+
+    from vision_assist_amd.shard import FrameDealer
+
+    class St:
+        f_bavail, f_frsize = 10, 4096  # 40 KiB free
+
+    monkeypatch.setattr(os, "statvfs", lambda p: St())
+    with pytest.raises(ValueError, match="MiB of /dev/shm"):
+        FrameDealer(FailingWorker(), [None, None], 64, 64, slots=8)

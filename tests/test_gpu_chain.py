@@ -93,6 +93,52 @@ def test_chain_vs_fp32_oracle(dtype, regime):
             assert rr[k] >= floor, (k, rr[k], floor)
 
 
+# C2's own plan (BASELINE configs[1]: YOLOv8n-seg bf16, batch 1): every C2f block one va_seg_c2fb launch with the
+# stride-2 convs as their prologues, head levels and proto on lanes -- frame by frame through post-processing,
+# contours, the mask choice and grid / A* against the fp32 oracle chain (chain_oracle.json.gz["c2/sparse"], one
+# PathFinder state across the 16 frames).  Floors one frame under the rates measured on the GPU (bf16 moves scores and
+# mask values by more than f32 rounding, so per-frame identity is not expected; tests/test_gpu_seg.py holds the
+# plan's head tensors to the bf16 bar)
+C2_FLOOR = {"chosen": 0.875, "cells": 0.8125, "paths": 0.8125}
+
+
+def test_c2_batch1_plan_chain_vs_fp32_oracle():
+    from vision_assist_amd.pipeline import FramePipeline
+    from vision_assist_amd.post import PLANT_NEVER
+    arch, fw = weights("sparse", scale="n")
+    want = load_fixture("c2/sparse")
+    pipe = FramePipeline(arch, fw, 1, 640, 640, dtype="bf16")
+    names = [m["name"] for m in pipe.plan["meta"]]
+    # the plan under test is C2's: fused C2f blocks (with stride-2 prologues) and lanes
+    assert sum("fused C2f" in n for n in names) == 8, names
+    assert sum(n.startswith("model.") and "+model." in n and "fused C2f" in n for n in names) >= 4, names
+    assert any(n.startswith("fork lane") for n in names), names
+    cmps = []
+    for i, w in enumerate(want):
+        res = pipe.run(frame_batch(9000 + i, 1).cuda(), plant_mode=PLANT_NEVER)
+        torch.cuda.synchronize()
+        det, _ = pipe.post.det_tensor(0)
+        nf = res.frame(0)
+        chosen = int(pipe.post.chosen[0])
+        ok = nf.status == 0
+        got = {"det": det, "chosen": chosen,
+               "rect": tuple(int(v) for v in pipe.post.rects[0].cpu()) if chosen >= 0 else None,
+               "cells": pipe.post.cells[0].cpu().numpy() if chosen >= 0 else None,
+               "paths": [q["path"] for q in nf.queries] if ok else None,
+               "costs": [float(q["cost"]).hex() if q["path"] else None for q in nf.queries] if ok else None}
+        cmps.append(compare(got, w, f32=False))
+    rr = rates(cmps)
+    _RESULTS["c2_bf16_batch1/sparse"] = rr
+    out = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "chain_agreement.json"), "w") as f:
+            json.dump(_RESULTS, f, indent=1)
+    print("c2 bf16 batch 1 sparse", json.dumps(rr))
+    assert rr["frames_with_mask"] >= len(want) // 2
+    for k, floor in C2_FLOOR.items():
+        assert rr[k] >= floor, (k, rr[k], floor)
+
+
 def test_call_matches_oracle_chain_answers():
     """FrameProcessor.__call__ (f32 YOLO surface, the reference's precision) on 16 frames of the sparse regime
     (1-5 compact detections, as a trained model's frames): the answer strings equal the oracle chain's (predict

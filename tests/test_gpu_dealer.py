@@ -72,9 +72,9 @@ class C4BatchRecordWorker(C4RecordWorker):
         return Fn()
 
 
-@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("batched,readers", [(False, 0), (True, 0), (True, 2)])
 @pytest.mark.parametrize("regime", ["sparse", "dense_box"])
-def test_dealer_two_workers_vs_per_shard_oracle_replay(regime, batched):
+def test_dealer_two_workers_vs_per_shard_oracle_replay(regime, batched, readers):
     import torch
 
     from tests.chain_util import compare, frame_batch, load_fixture
@@ -82,7 +82,7 @@ def test_dealer_two_workers_vs_per_shard_oracle_replay(regime, batched):
     frames = [frame_batch(7000 + i, 1)[0].numpy() for i in range(N_FRAMES)]
     want = load_fixture(f"c4/{regime}")
     worker = C4BatchRecordWorker(regime) if batched else C4RecordWorker(regime)
-    with FrameDealer(worker, [0, 0], 640, 640, slots=4 if batched else 2) as d:
+    with FrameDealer(worker, [0, 0], 640, 640, slots=4 if batched else 2, readers=readers) as d:
         got = list(d.map(frames))
     bad = []
     for i, (g, w) in enumerate(zip(got, want)):
@@ -118,3 +118,46 @@ def test_frameprocessor_map_answers_in_order():
     assert len(answers) == len(frames)
     assert all(isinstance(a, (str, list)) for a in answers)
     assert any(a != [] for a in answers)
+
+
+def test_stream_batches_failed_end_loses_only_its_batch():
+    """a grid stage that raises in StreamBatches.end spends that batch's token -- the next batches begin
+    and end in order, with the answers of the same frames run through a fresh StreamBatches."""
+    import torch
+
+    from tests.chain_util import frame_batch, weights
+    from vision_assist_amd.pipeline import StreamBatches
+    arch, fw = weights("sparse")
+    frames = [frame_batch(7200 + i, 1)[0].numpy() for i in range(6)]
+
+    def answers(sb, batches, fail_first=False):
+        out = []
+        toks = [sb.begin(frames[a:b]) for a, b in batches[:2]]
+        if fail_first:
+            real = sb.pipes[0].nav_run
+
+            def boom(*a, **k):
+                sb.pipes[0].nav_run = real
+                raise RuntimeError("injected grid-stage failure")
+            sb.pipes[0].nav_run = boom
+            with pytest.raises(RuntimeError, match="injected"):
+                sb.end(toks[0])
+        else:
+            res = sb.end(toks[0])
+            out += [[q["path"] for q in res.frame(i).queries] for i in range(toks[0][1])]
+        for k, (a, b) in enumerate(batches[1:]):
+            if k + 2 < len(batches):
+                toks.append(sb.begin(frames[batches[k + 2][0]:batches[k + 2][1]]))
+            res = sb.end(toks[k + 1])
+            out += [[q["path"] for q in res.frame(i).queries] for i in range(toks[k + 1][1])]
+        return out
+
+    batches = [(0, 2), (2, 4), (4, 6)]
+    sb = StreamBatches(arch, fw, 2, 640, 640, dtype="f32", device=torch.device("cuda", 0))
+    got = answers(sb, batches, fail_first=True)
+    assert sb.done == sb.k == 3
+    # the same later frames through a fresh object whose first batch ends normally: the angle cache then holds that
+    # batch's keys, which the failed run never added -- so compare the frames of batches 2 and 3 run alone
+    ref = StreamBatches(arch, fw, 2, 640, 640, dtype="f32", device=torch.device("cuda", 0))
+    want = answers(ref, [(2, 4), (4, 6)])
+    assert got == want

@@ -1,10 +1,15 @@
-"""The frame dealer's transport alone (vision_assist_amd.shard.FrameDealer): one reader dealing 640x640 frames to 1 or 2
-worker processes whose batching workers do no work ("triv") or copy the frames out ("copy") -- the host-side ceiling
-of the dealer extra, CPU only:  python tools/dealer_ceiling.py  (DESIGN.md §5)."""
-import sys, time
+"""The frame dealer's transport alone (vision_assist_amd.shard.FrameDealer): one frame source dealt to G worker
+processes whose batching workers do no work ("triv") or copy the frames out ("copy"), with the frame copies into the
+rings on the calling thread (readers 0) or on R reader threads -- the host-side ceiling of the dealer, CPU only:
+python tools/dealer_ceiling.py [G ...]  (DESIGN.md §5-6)."""
+import os
+import sys
+import time
+
 import numpy as np
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
-from vision_assist_amd.shard import FrameDealer
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vision_assist_amd.shard import FrameDealer  # noqa: E402
 
 
 class Triv:
@@ -33,17 +38,23 @@ def factory_copy(dev):
     return TrivCopy()
 
 
+def ceiling(fac, G: int, readers: int, n: int = 2048, slots: int = 32, frames=None) -> float:
+    """frames/s through a dealer of G workers built by fac, n frames after a warm-up."""
+    if frames is None:
+        rng = np.random.default_rng(0)
+        frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
+    with FrameDealer(fac, [None] * G, 640, 640, slots=slots, readers=readers) as d:
+        for _ in d.map(frames[i % 16] for i in range(128)):
+            pass
+        t0 = time.perf_counter()
+        for _ in d.map(frames[i % 16] for i in range(n)):
+            pass
+        return n / (time.perf_counter() - t0)
+
+
 if __name__ == "__main__":
-    rng = np.random.default_rng(0)
-    frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
+    Gs = [int(a) for a in sys.argv[1:]] or [1, 2, 4]
     for name, fac in (("triv", factory_triv), ("copy", factory_copy)):
-        for G in (1, 2):
-            with FrameDealer(fac, [None] * G, 640, 640, slots=64) as d:
-                for _ in d.map(frames[i % 16] for i in range(256)):
-                    pass
-                t0 = time.perf_counter()
-                n = 2048
-                for _ in d.map(frames[i % 16] for i in range(n)):
-                    pass
-                dt = time.perf_counter() - t0
-            print(name, G, round(n / dt, 1), "frames/s", flush=True)
+        for G in Gs:
+            for readers in sorted({0, 1, G}):
+                print(name, "workers", G, "readers", readers, round(ceiling(fac, G, readers), 1), "frames/s", flush=True)

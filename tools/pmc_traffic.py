@@ -23,7 +23,7 @@ import os
 import re
 import sys
 
-CONV_RE = re.compile(r"(conv(0|2|3|4|8|3h|3t|3q|_dn|_patch|0_f32|0_f32m)?|c2f|c2f32|stem|stem32|pw)_kernel")
+CONV_RE = re.compile(r"(conv(0|2|3|4|8|3h|3t|3q|_dn|_patch|0_f32|0_f32m)?|c2f|stem|stem32|pw)_kernel")
 
 
 def family(name: str) -> str:

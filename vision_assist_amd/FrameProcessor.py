@@ -476,18 +476,23 @@ class FrameProcessor:
             raise TypeError("FrameProcessor needs a vision_assist_amd.yolo.YOLO model (the device pipeline)")
         H, W = int(frames[0].shape[0]), int(frames[0].shape[1])
         sb = self.model.stream_batches(H, W, max_batch, seen=path_finder.seen)
-        return sb, sb.begin(frames), list(frames), H, W
+        # the token keeps the batch's size, not the frames: they are views of ring slots that the dealer reuses as
+        # soon as begin returns, so a later read of their pixels would see another frame's
+        return sb, sb.begin(frames), len(frames), H, W
 
     def _end_batch(self, token) -> list:
         """The answers of a begun batch, frame by frame in stream order -- __call__'s on each frame (the grid
         stage ran the frames in order against the one angle cache); an IndexError object in the place of a frame
         whose __call__ would raise it."""
-        sb, tok, frames, H, W = token
+        sb, tok, n, H, W = token
         res = sb.end(tok)
         dims = sb.pipes[0].nav.dims
         out = []
-        for i, fr in enumerate(frames):
-            self.frame = fr
+        # debug drawing is per call (_begin_batch refuses debug), so no pixels are read here; self.frame keeps only
+        # the frame's shape for the reference methods that read it (a zero-stride read-only array, no memory)
+        blank = np.broadcast_to(np.zeros((), np.uint8), (H, W, 3))
+        for i in range(n):
+            self.frame = blank
             try:
                 out.append(self._answer(dims, res.frame(i), H, W))
             except IndexError as e:
@@ -495,14 +500,19 @@ class FrameProcessor:
         return out
 
     # ------- multi-GPU stream -------
-    def map(self, frames, devices=None, slots: int = 128, batch: int = 16, workers_per_gpu: int = 2):
+    def map(self, frames, devices=None, slots: int | None = None, batch: int = 16, workers_per_gpu: int = 2,
+            readers: int = 0):
         """Answers of a frame stream in frame order, the frames dealt round-robin to worker processes on the GPUs
         (vision_assist_amd.shard.FrameDealer): frame i goes to worker i % G on devices[i % G], each worker running
         this model in its own FrameProcessor with its own PathFinder angle cache -- per shard the answers of
         __call__ over that shard's frames in order.  devices: one GPU index per worker (default: every visible GPU,
         ``workers_per_gpu`` workers on each -- two keep a GPU busy while the other builds its answers on the host:
         3,858-4,031 frames/s per GPU against 2,670 with one); batch: frames a worker runs as one
-        device batch (up to; what is waiting in its ring of ``slots`` frames).  The first frame fixes the
+        device batch (up to; what is waiting in its ring of ``slots`` frames, default 4 x batch: the ring lives in
+        /dev/shm, G x slots frames, and the dealer refuses a ring larger than the free space there; the bench's 128
+        slots measured 1-3 % above 64).  readers: reader threads that copy frames into the rings (FrameDealer; 0 = the
+        calling thread, whose copies cap a node near one GPU's rate; with readers a frame must stay unmodified until its
+        answer is back).  The first frame fixes the
         frame size; the dealer is kept for later calls with the same devices, size and model settings (close_map
         ends it); a consumer that stops early leaves nothing behind for the next call (FrameDealer.map), and a
         dealer whose worker died is dropped."""
@@ -519,12 +529,14 @@ class FrameProcessor:
         if not hasattr(self.model, "spec"):
             raise TypeError("FrameProcessor.map needs a vision_assist_amd.yolo.YOLO model")
         calib = getattr(self.model, "fp8_calib", None)  # set after construction: travels with the worker spec
-        key = (tuple(devices), H, W, slots, batch, id(calib))
+        if slots is None:
+            slots = 4 * batch
+        key = (tuple(devices), H, W, slots, batch, readers, id(calib))
         dealers = self.__dict__.setdefault("_dealers", {})
         if key not in dealers:
             model, kw = self.model.spec
             dealers[key] = FrameDealer(dropin_worker(model, batch=batch, fp8_calib=calib, **kw), devices, H, W,
-                                       slots=slots)
+                                       slots=slots, readers=readers)
         d = dealers[key]
 
         def chain():

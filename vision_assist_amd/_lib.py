@@ -60,7 +60,6 @@ SIGNATURES = [
     ("va_c2fb_layout", I32, [I32, I32, I32, I32, I32, I32, I32, I32, ctypes.POINTER(I64)]),
     ("va_seg_stem", I32, [P, P]),
     ("va_seg_stem_f32", I32, [P, P]),
-    ("va_seg_c2f_f32", I32, [P, P]),
     ("va_c2f_trace", I32, [P]),
     ("va_c2fb_trace", I32, [P]),
     ("va_stem_trace", I32, [P]),

@@ -962,6 +962,9 @@ static int c2fb_f32(const va_conv_args* a, hipStream_t st) {
         a->ldx % 4 || a->ldy % 4 || a->ldx < ci || a->ldy < co || ((uintptr_t)a->x & 15) || ((uintptr_t)a->y & 15) ||
         ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15))
         return VA_ERR_ARG;
+    // the stride-2 prologue (a->res / c2 / K) is a bf16 form only (va_c2fb_layout rejects cs for f32 as well): an f32
+    // call that names one would compute the block from x's first cs channels, which nobody wrote
+    if (a->res || a->c2 || a->K) return VA_ERR_ARG;
     if (a->xu && (a->cu <= 0 || a->cu % 8 || a->cu >= ci || a->ldu % 4 || a->ldu < a->cu || a->H % 2 || a->W % 2 ||
                   ((uintptr_t)a->xu & 15)))
         return VA_ERR_ARG;

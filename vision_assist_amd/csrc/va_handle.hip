@@ -44,9 +44,9 @@ void read_switches(VaSwitches& s) {
     const char* e = getenv("VA_F32_SPLIT");
     s.f32_split = !e ? 6 : e[0] == '9' ? 9 : e[0] == '6' ? 6 : 0;
     e = getenv("VA_CONV3H");
-    s.conv3h = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
+    s.conv3h = !e ? 1 : e[0] == '0' ? 0 : 1;
     e = getenv("VA_CONV3T");
-    s.conv3t = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "af") == 0 ? 2 : 1;
+    s.conv3t = !e ? 1 : e[0] == '0' ? 0 : 1;
     e = getenv("VA_CONV3Q");
     s.conv3q = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "static") == 0 ? 2 : 1;
     s.splitk = !env_off("VA_SPLITK");

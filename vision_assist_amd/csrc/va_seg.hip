@@ -1129,14 +1129,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 // LDS row: 128 bytes = 8 slots of 16 B; chunk c = 3 g + p (c < 6) sits in slot c ^ (r & 7) ^ ((r >> 4) & 1) -- the
 // 32-row fragment reads are conflict-free, slots 6-7 of a chunk are DMA'd from the zero page.
 constexpr int T3_BN = 128, T3_KS = 16, T3_ROW = 128;
-// AF: the A rows as f32 (64 bytes: 16 channels, DMA'd from va_conv_args.w; conv3h's AF), split into the three
-// terms in registers -- 8 instead of 16 KiB of A DMA per K-step (12 of them weight bytes, 4 the zero page's)
-template <int WM, int NSTAGE, bool AF = false>
+template <int WM, int NSTAGE>
 struct T3Cfg {
     static constexpr int BM = 64 * WM, NT = 128 * WM, STAGE = (BM + T3_BN) * T3_ROW;
     static constexpr int EPI = BM * (T3_BN + 4) * 4;
     static constexpr int LDS = NSTAGE * STAGE > EPI ? NSTAGE * STAGE : EPI;
-    static constexpr int NA = (AF ? 8 : 16) / (2 * WM);  // A-DMA instructions per wave per K-step (16 / 8 KiB of A)
+    static constexpr int NA = 16 / (2 * WM);  // A-DMA instructions per wave per K-step (16 KiB of A)
     static_assert(LDS <= 160 * 1024, "LDS");
 };
 
@@ -1156,9 +1154,9 @@ __device__ __forceinline__ void t3_waitvm() {
 // WM = 4, NSTAGE = 3: 256-pixel tiles, 8 waves, one workgroup per CU, A DMA'd two K-steps ahead;
 // WM = 2, NSTAGE = 2: 128-pixel tiles, 4 waves, two workgroups per CU, A one K-step ahead.  B registers always
 // two K-steps ahead.
-template <int WM, int NSTAGE, typename OutT, bool AF = false>
+template <int WM, int NSTAGE, typename OutT>
 __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int ntn, int ntiles) {
-    using Cfg = T3Cfg<WM, NSTAGE, AF>;
+    using Cfg = T3Cfg<WM, NSTAGE>;
     extern __shared__ __align__(16) unsigned char smt[];
     constexpr int BM = Cfg::BM, BN = T3_BN, NT = Cfg::NT, WN = 2, TNS = 4, NA = Cfg::NA;
     int bid = blockIdx.x;
@@ -1173,8 +1171,7 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     const int wm = wid / WN, wn = wid % WN;
     const int m0 = tm * BM, n0 = tn * BN;
     const float* __restrict__ X = (const float*)a.x;
-    const void* WA = AF ? (const void*)((const float*)a.w + (int64_t)cls * a.Npad * a.Kpad)
-                        : (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
+    const void* WA = (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     auto stA = [&](int s) { return smt + s * Cfg::STAGE; };
     auto stB = [&](int s) { return smt + s * Cfg::STAGE + BN * T3_ROW; };
@@ -1200,26 +1197,19 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     // buffer_load ... lds, not global_load_lds: the compiler's wait pass takes a pending FLAT-encoded LDS DMA as
     // "VM and LGKM out of order" and answers the next register dependency with vmcnt(0), draining the B loads two
     // steps ahead.  Chunks 6-7 (and K-steps past the last) use an offset past the descriptor's range: zeros.
-    // AF: instruction i = wid + 2 WM j holds rows 16 i .. 16 i + 15 as 64-byte f32 rows; lane l: row 16 i + (l >> 2),
-    // slot l & 3 -> f32 quarter slot ^ ((row >> 2) & 3)
     const void* zpage = (const void*)g_zero_page;
-    const int wa_bytes = AF ? a.Npad * a.Kpad * 4 : a.Npad * a.Kpad * 3 * 2;
+    const int wa_bytes = a.Npad * a.Kpad * 3 * 2;
     constexpr int T3_OOR = 0x7ff00000;
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-        if constexpr (AF) {
-            const int row = 16 * (wid + 2 * WM * j) + (lane >> 2), q = (lane & 3) ^ ((row >> 2) & 3);
-            aoff[j] = ((n0 + row) * a.Kpad + 4 * q) * 4;
-        } else {
-            const int row = 8 * (wid + 2 * WM * j) + (lane >> 3);
-            const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
-            aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
-        }
+        const int row = 8 * (wid + 2 * WM * j) + (lane >> 3);
+        const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
+        aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
     }
     auto dmaA = [&](int k, int s, bool live) {  // K-step k (channels 16 k ..) into stage s; !live: zeros
         unsigned char* base = stA(s);
-        const int soff = live ? k * (AF ? 64 : 96) : T3_OOR;
+        const int soff = live ? k * 96 : T3_OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j)
             t3_dma16(WA, wa_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
@@ -1290,16 +1280,8 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib) {
             const int row = wn * 64 + 32 * ib + r32;
-            if constexpr (AF) {
-                const int sw = (row >> 2) & 3;
-                const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
-                const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
-                split3_bf16(lo, hi, ap[ib]);
-            } else {
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
-            }
+            for (int p = 0; p < 3; ++p) ap[ib][p] = *(const bf16x8*)(as_ + row * T3_ROW + 16 * t3_slot(3 * g32 + p, row));
         }
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
@@ -1366,19 +1348,16 @@ static_assert(T3H_NU * T3H_NT >= 2 * T3H_HMAX, "halo units");
 // (the narrow layers: waves 2 x 2, each 64 pixels x 32 channels).  TPS = taps per K-step: a stage holds TPS taps'
 // weights of the chunk, one BN x 96-byte block per tap.  (TPS = 2 on the narrow tiles -- the wide tiles' 24 MFMAs per
 // wave and barrier -- measured neutral, 14.10 vs 14.11 ms per 64-frame forward, profiles/r04/conv3h_tps/; the
-// library instantiates TPS = 1 only)
-// AF: the A stage holds the weights as f32 (64-byte rows of 16 channels, DMA'd from va_conv_args.w) and every wave
-// splits its A fragments into the three bf16 terms in registers (split3_bf16: the same terms the host's split3_bf16
-// pre-splits, so the same products) -- 4 instead of 6 L2 -> LDS bytes per weight, the stream that fills the L2 on
-// the 128-channel layers
-template <int TNS, int TPS = 1, bool AF = false>
+// library instantiates TPS = 1 only).  (The A stage as f32 weights split in registers per wave -- 4 instead of 6
+// L2 -> LDS bytes per weight -- measured 4-10 % slower and was removed in round 6)
+template <int TNS, int TPS = 1>
 struct T3HCfg {
     static constexpr int BN = 32 * TNS;
-    static constexpr int AROW = AF ? 64 : T3H_ROW;                // LDS bytes per weight row of a (tap, chunk)
-    static constexpr int ABLK = BN * AROW;                        // one tap's weights of a chunk: 12 / 6 KiB (AF 8 / 4)
+    static constexpr int AROW = T3H_ROW;                          // LDS bytes per weight row of a (tap, chunk)
+    static constexpr int ABLK = BN * AROW;                        // one tap's weights of a chunk: 12 / 6 KiB
     static constexpr int ASTAGE = TPS * ABLK;
-    static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6; AF 8 / 4)
-    static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2; AF 2 / 1)
+    static constexpr int NP = ASTAGE / 1024;                      // A-DMA pieces per K-step (12 / 6)
+    static constexpr int NAW = (NP + 3) / 4;                      // pieces of the busiest wave (3 / 2)
     static constexpr int ZROW = T3H_NSA * ASTAGE + 2 * T3H_HALO;  // the zero row
     static constexpr int SINK = ZROW + 128;                       // 1 KiB the idle pieces' zero DMAs land in
     static constexpr int LDS0 = NP % 4 ? SINK + 1024 : ZROW + T3H_ROW;
@@ -1403,10 +1382,10 @@ __device__ __forceinline__ void t3h_unroll(F&& f) {
     }
 }
 
-template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1, bool AF = false>
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
 __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn, int ntiles, int lgw, int tiles_x) {
     extern __shared__ __align__(16) unsigned char smh[];
-    using Cfg = T3HCfg<TNS, TPS, AF>;
+    using Cfg = T3HCfg<TNS, TPS>;
     constexpr int BM = T3H_BM, BN = Cfg::BN, NT = T3H_NT, WN = 2, CB = TNS / 2, T = KH * KW;
     constexpr int S = (T + TPS - 1) / TPS;  // K-steps per chunk
     static_assert(S >= 2, "the halo is stored at a chunk's second step");
@@ -1429,37 +1408,30 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
     const int n0 = tn * BN;
     const int nch = a.Cin / T3_KS;
     const float* __restrict__ X = (const float*)a.x;
-    // A source: the pre-split planes (w3), or with AF the f32 weights (w); mode 2: the sub-pixel class's matrix
-    const void* WA = AF ? (const void*)((const float*)a.w + (int64_t)cls * a.Npad * a.Kpad)
-                        : (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
+    // A source: the pre-split planes (w3); mode 2: the sub-pixel class's matrix
+    const void* WA = (const void*)((const __bf16*)a.w3 + (int64_t)cls * a.Npad * a.Kpad * 3);
     auto stA = [&](int s) { return smh + s * Cfg::ASTAGE; };
     auto halo = [&](int b) { return smh + T3H_NSA * Cfg::ASTAGE + b * T3H_HALO; };
 
     // ---- A DMA: piece P = wid + 4 j of a stage (1 KiB, linear in LDS); lane l writes bytes 16 l of it: row o / 96,
-    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run (AF: row o / 64,
-    // slot (o % 64) / 16 -> f32 quarter slot ^ ((row >> 2) & 3)).  Every wave issues NA pieces per K-step (12 over 4
-    // waves; 64-channel tiles: 6, so waves 2-3 send their second piece's zeros to a sink; AF: 8 / 4, even): a fixed
-    // count, no branch, so the counted waits and the compiler's own stay exact
-    const int wa_bytes = AF ? a.Npad * a.Kpad * 4 : a.Npad * a.Kpad * 3 * 2;
+    // slot (o % 96) / 16 -> chunk slot ^ ((row >> 3) & 1) of that weight row's (tap, chunk) run.  Every wave issues
+    // NA pieces per K-step (12 over 4 waves; 64-channel tiles: 6, so waves 2-3 send their second piece's zeros to a
+    // sink): a fixed count, no branch, so the counted waits and the compiler's own stay exact
+    const int wa_bytes = a.Npad * a.Kpad * 3 * 2;
     constexpr int OOR = 0x7ff00000;
     constexpr int NA = Cfg::NAW;
     int aoff[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
         const int o = (1024 * (wid + (NT / 64) * j)) % Cfg::ABLK + 16 * lane;  // offset in the piece's tap block
-        if constexpr (AF) {
-            const int row = o / 64, q = ((o - row * 64) >> 4) ^ ((row >> 2) & 3);
-            aoff[j] = ((n0 + row) * a.Kpad + 4 * q) * 4;
-        } else {
-            const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
-            aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
-        }
+        const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
+        aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
     }
     // stage s <- the weights of taps TPS t .. of chunk c (kl_h = tap * nch + chunk, or -1: zeros); a piece's tap
     // block is wave-uniform, so the per-tap source offset is a scalar select
     auto dmaA = [&](int kl0, int kl1, int s) {
         unsigned char* base = stA(s);
-        constexpr int KLB = AF ? 64 : 96;  // source bytes of one (tap, chunk) run of a row
+        constexpr int KLB = 96;  // source bytes of one (tap, chunk) run of a row
         const int so0 = kl0 >= 0 ? kl0 * KLB : OOR, so1 = kl1 >= 0 ? kl1 * KLB : OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
@@ -1567,17 +1539,10 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
 #pragma unroll
                 for (int ib = 0; ib < CB; ++ib) {
                     const int row = wn * 32 * CB + 32 * ib + r32;
-                    if constexpr (AF) {  // this lane's 8 f32 weights (two 16-byte quarters), split here
-                        const int sw = (row >> 2) & 3;
-                        const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
-                        const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
-                        split3_bf16(lo, hi, ap[ib]);
-                    } else {
-                        const int sw = (row >> 3) & 1;
+                    const int sw = (row >> 3) & 1;
 #pragma unroll
-                        for (int p = 0; p < 3; ++p)
-                            ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
-                    }
+                    for (int p = 0; p < 3; ++p)
+                        ap[ib][p] = *(const bf16x8*)(as_ + row * T3H_ROW + 16 * ((3 * g32 + p) ^ sw));
                 }
 #pragma unroll
                 for (int jb = 0; jb < 2; ++jb) {
@@ -2897,267 +2862,14 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
     }
 }
 
-// ----------------------------------------------------------------------------------------- f32 fused C2f
-// One YOLOv8 C2f block (n = 1, shortcut, 64 -> 64 channels, hidden 32: model.2 of YOLOv8s-seg; block.py C2f.forward)
-// in f32 as ONE launch, the bf16 c2f_kernel's dataflow with the f32 convs' arithmetic (six exact bf16 term products
-// per f32 product, f32 accumulation): unfused the block is four launches moving ~2.9 GB per 64 frames of 640 x 640
-// through HBM (the 96-channel concat buffer written, re-read in slices and whole); here every intermediate stays in
-// LDS as three exact bf16 planes.  A workgroup owns an 8 x 16 output tile, 8 waves:
-//   stage 1  cv1 (1x1, 64 -> 64) on the 12 x 20 tile + halo 2 (4 K-steps of 16 input channels; each chunk of the
-//            input staged once, split once, double-buffered, the next chunk loaded while this one's MFMAs run):
-//            b = channels 32..63 of every pixel -> S1 (zero outside the image: m.0.cv1's padding), a = channels
-//            0..31 of the centre -> A;
-//   stage 2  m.0.cv1 (3x3, 32 -> 32) on the 10 x 18 tile + halo 1 from S1 -> S2 (zero outside the image);
-//   stage 3  m.0.cv2 (3x3, 32 -> 32) on the centre from S2, + the residual b (S1, h + m + l: exact) -> C;
-//   stage 4  cv2 (1x1, 96 -> 64) over [a | b | c] (A, S1's centre, C) -> y, f32.
-// The four weight matrices (f32, one blob) stream through one three-stage LDS-DMA ring two K-steps ahead across the
-// stage boundaries (46 K-steps per tile, one 1 KiB piece per wave and step: waves 4-7 send theirs to a sink), split
-// into the three terms in registers (conv3h's AF form).  Plane buffers: 208 bytes per pixel (2 chunks x (3 planes
-// x 16 channels) + 16 bytes of padding: conflict-free 16-pixel reads); input chunk buffers 112 bytes per pixel.
-constexpr int CF32_TH = 8, CF32_TW = 16, CF32_NT = 512;
-constexpr int CF32_R1H = CF32_TH + 4, CF32_R1W = CF32_TW + 4, CF32_R1 = CF32_R1H * CF32_R1W;  // 12 x 20 = 240
-constexpr int CF32_R2H = CF32_TH + 2, CF32_R2W = CF32_TW + 2, CF32_R2 = CF32_R2H * CF32_R2W;  // 10 x 18 = 180
-constexpr int CF32_P = CF32_TH * CF32_TW;                                                      // 128
-constexpr int CF32_PS = 208, CF32_XS = 112;
-constexpr int CF32_S1 = 0, CF32_A = CF32_S1 + CF32_R1 * CF32_PS, CF32_X = CF32_A + CF32_P * CF32_PS;
-constexpr int CF32_S2 = CF32_X, CF32_C = CF32_S2 + CF32_R2 * CF32_PS;
-constexpr int CF32_XEND0 = CF32_X + 2 * 256 * CF32_XS, CF32_XEND1 = CF32_C + CF32_P * CF32_PS;
-constexpr int CF32_RING = CF32_XEND0 > CF32_XEND1 ? CF32_XEND0 : CF32_XEND1;
-constexpr int CF32_SINK = CF32_RING + 3 * 4096, CF32_LDS = CF32_SINK + 1024;
-static_assert(CF32_LDS <= 160 * 1024, "one workgroup per CU");
-// weight blob (floats, row-major [Cout][K], K ordered (ky, kx, ci)): cv1 64 x 64, m.0.cv1 32 x 288, m.0.cv2 32 x 288,
-// cv2 64 x 96; bias blob [64 | 32 | 32 | 64]
-constexpr int CF32_W1 = 0, CF32_W2 = CF32_W1 + 64 * 64, CF32_W3 = CF32_W2 + 32 * 288, CF32_W4 = CF32_W3 + 32 * 288;
-constexpr int CF32_WN = CF32_W4 + 64 * 96;  // 28672 floats
-constexpr int CF32_NK = 4 + 18 + 18 + 6;    // K-steps per tile
-
-// channels 4 g .. 4 g + 3 (g = 0..7) of a 32-channel plane pixel at p: the three planes' 8-byte pieces
+// channels 4 g .. 4 g + 3 (g = 0..7) of a 32-channel plane pixel at p (208-byte pixel rows: [chunk 2][plane 3][16
+// channels]): the three planes' 8-byte pieces
 __device__ __forceinline__ void cf32_put4(unsigned char* p, int g, const f32x4& v) {
     uint2 t[3];
     split3_bf16x4(v, t);
     unsigned char* d = p + (g >> 2) * 96 + (g & 3) * 8;
 #pragma unroll
     for (int q = 0; q < 3; ++q) *(uint2*)(d + 32 * q) = t[q];
-}
-__device__ __forceinline__ f32x4 cf32_get4(const unsigned char* p, int g) {
-    const unsigned char* d = p + (g >> 2) * 96 + (g & 3) * 8;
-    const uint2 h = *(const uint2*)d, m = *(const uint2*)(d + 32), l = *(const uint2*)(d + 64);
-    const f32x2 h0 = unpk_bf16(h.x), h1 = unpk_bf16(h.y), m0 = unpk_bf16(m.x), m1 = unpk_bf16(m.y);
-    const f32x2 l0 = unpk_bf16(l.x), l1 = unpk_bf16(l.y);
-    return (f32x4){(h0[0] + m0[0]) + l0[0], (h0[1] + m0[1]) + l0[1], (h1[0] + m1[0]) + l1[0], (h1[1] + m1[1]) + l1[1]};
-}
-
-__global__ __launch_bounds__(CF32_NT) void c2f32_kernel(const float* __restrict__ X, int ldx, int H, int W,
-                                                        const float* __restrict__ wb, const float* __restrict__ bb,
-                                                        float* __restrict__ Y, int ldy, int tiles_x, int tiles_y,
-                                                        int ntiles) {
-    extern __shared__ __align__(16) unsigned char cs[];
-    int bid = blockIdx.x;
-    {
-        const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int tx = bid % tiles_x, t2 = bid / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
-    const int oy0 = ty * CF32_TH, ox0 = tx * CF32_TW;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int r32 = lane & 31, g32 = lane >> 5;
-    constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
-
-    // ---- weight ring: global K-step g -> (layer base, K, K offset); wave w < 4 DMAs rows 16 w .. 16 w + 15 of the
-    // step's 64-row stage (lane l: row 16 w + l / 4, f32 quarter (l & 3) ^ ((row >> 2) & 3)), waves 4-7 a sink
-    const int arow = 16 * (wid & 3) + (lane >> 2), aq = (lane & 3) ^ ((arow >> 2) & 3);
-    auto dmaA = [&](int g) {
-        int base, K, ko;
-        if (g < 4) base = CF32_W1, K = 64, ko = 16 * g;
-        else if (g < 22) base = CF32_W2, K = 288, ko = 16 * (g - 4);
-        else if (g < 40) base = CF32_W3, K = 288, ko = 16 * (g - 22);
-        else base = CF32_W4, K = 96, ko = 16 * (g - 40);
-        const bool real = wid < 4 && g < CF32_NK;
-        t3_dma16(wb, CF32_WN * 4, real ? cs + CF32_RING + (g % 3) * 4096 + wid * 1024 : cs + CF32_SINK,
-                 (arow * K + 4 * aq) * 4, real ? (base + ko) * 4 : 0x7ff00000);
-    };
-    auto afrag = [&](int g, int row, bf16x8 (&ap)[3]) {  // A rows row (0..63) of step g, split
-        const unsigned char* as_ = cs + CF32_RING + (g % 3) * 4096;
-        const int sw = (row >> 2) & 3;
-        const u32x4 lo = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32) ^ sw));
-        const u32x4 hi = *(const u32x4*)(as_ + row * 64 + 16 * ((2 * g32 + 1) ^ sw));
-        split3_bf16(lo, hi, ap);
-    };
-    auto bfrag = [&](const unsigned char* p, bf16x8 (&bp)[3]) {  // p: the pixel's chunk base + 16 g32
-#pragma unroll
-        for (int q = 0; q < 3; ++q) bp[q] = *(const bf16x8*)(p + 32 * q);
-    };
-    auto in_img = [&](int yy, int xx) { return (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W; };
-
-    // ---- input chunk staging (stage 1): unit tid -> R1 pixel tid >> 1 (12 x 20 region from (oy0 - 2, ox0 - 2)),
-    // channels 8 (tid & 1) .. of the chunk
-    const int xp = tid >> 1, xg = tid & 1;
-    const int xy = oy0 - 2 + xp / CF32_R1W, xx = ox0 - 2 + xp % CF32_R1W;
-    const bool xok = xp < CF32_R1 && in_img(xy, xx);
-    const float* xsrc = xok ? X + (((int64_t)n * H + xy) * W + xx) * ldx + 8 * xg : (const float*)g_zero_page;
-    u32x4 rx[2];
-    auto loadX = [&](int c) {
-        const float* p = xok ? xsrc + 16 * c : xsrc;
-        rx[0] = *(const u32x4*)p;
-        rx[1] = *(const u32x4*)(p + 4);
-    };
-    auto storeX = [&](int b) {
-        bf16x8 t[3];
-        split3_bf16(rx[0], rx[1], t);
-        unsigned char* d = cs + CF32_X + b * 256 * CF32_XS + xp * CF32_XS + 16 * xg;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) *(bf16x8*)(d + 32 * q) = t[q];
-    };
-    auto sync_lds = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-
-    dmaA(0);
-    dmaA(1);
-    __builtin_amdgcn_sched_barrier(0);
-    loadX(0);
-    t3_waitvm<0>();
-    storeX(0);
-    sync_lds();
-
-    // ---- stage 1: cv1; wave w: R1 pixels 32 w .. (ragged past 240: read, never written), channel blocks a, b
-    {
-        f32x16 acc[2] = {(f32x16){}, (f32x16){}};
-        const int q = 32 * wid + r32;
-        for (int c = 0; c < 4; ++c) {
-            dmaA(c + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            if (c < 3) loadX(c + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            bf16x8 bp[3];
-            bfrag(cs + CF32_X + (c & 1) * 256 * CF32_XS + q * CF32_XS + 16 * g32, bp);
-#pragma unroll
-            for (int ib = 0; ib < 2; ++ib) {
-                bf16x8 ap[3];
-                afrag(c, 32 * ib + r32, ap);
-#pragma unroll
-                for (int t = 0; t < 6; ++t)
-                    acc[ib] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc[ib], 0, 0, 0);
-            }
-            t3_waitvm<0>();  // the next chunk's loads (and this step's DMA, issued before them)
-            if (c < 3) storeX((c + 1) & 1);  // the buffer step c - 1 read
-            sync_lds();
-        }
-        // epilogue: channels 32 ib + 8 j + 4 g32 + (0..3) of pixel q; b -> S1 (zero outside the image), a -> A (centre)
-        if (q < CF32_R1) {
-            const int qy = q / CF32_R1W, qx = q % CF32_R1W;
-            const bool in = in_img(oy0 - 2 + qy, ox0 - 2 + qx);
-            const bool ctr = qy >= 2 && qy < 2 + CF32_TH && qx >= 2 && qx < 2 + CF32_TW;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 b0 = *(const float4*)(bb + 8 * j + 4 * g32), b1 = *(const float4*)(bb + 32 + 8 * j + 4 * g32);
-                const f32x4 va = fz::act((f32x4){acc[0][4 * j] + b0.x, acc[0][4 * j + 1] + b0.y, acc[0][4 * j + 2] + b0.z,
-                                                  acc[0][4 * j + 3] + b0.w});
-                f32x4 vb = fz::act((f32x4){acc[1][4 * j] + b1.x, acc[1][4 * j + 1] + b1.y, acc[1][4 * j + 2] + b1.z,
-                                            acc[1][4 * j + 3] + b1.w});
-                if (!in) vb = (f32x4){0.f, 0.f, 0.f, 0.f};
-                cf32_put4(cs + CF32_S1 + q * CF32_PS, 2 * j + g32, vb);
-                if (ctr) cf32_put4(cs + CF32_A + ((qy - 2) * CF32_TW + qx - 2) * CF32_PS, 2 * j + g32, va);
-            }
-        }
-        sync_lds();
-    }
-
-    // ---- stage 2: m.0.cv1 on R2 (10 x 18 from (oy0 - 1, ox0 - 1)); waves 0-5: R2 pixels 32 w .. (ragged past 180)
-    {
-        f32x16 acc = (f32x16){};
-        const int q = 32 * wid + r32, qv = q < CF32_R2 ? q : 0;
-        const int qy = qv / CF32_R2W, qx = qv % CF32_R2W;
-        for (int kl = 0; kl < 18; ++kl) {
-            const int g = 4 + kl;
-            dmaA(g + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            if (wid < 6) {
-                const int tap = kl >> 1, ch = kl & 1;
-                bf16x8 ap[3], bp[3];
-                afrag(g, r32, ap);
-                bfrag(cs + CF32_S1 + ((qy + tap / 3) * CF32_R1W + qx + tap % 3) * CF32_PS + ch * 96 + 16 * g32, bp);
-#pragma unroll
-                for (int t = 0; t < 6; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc, 0, 0, 0);
-            }
-            t3_waitvm<1>();
-            sync_lds();
-        }
-        if (wid < 6 && q < CF32_R2) {
-            const bool in = in_img(oy0 - 1 + qy, ox0 - 1 + qx);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 b2 = *(const float4*)(bb + 64 + 8 * j + 4 * g32);
-                f32x4 v = fz::act((f32x4){acc[4 * j] + b2.x, acc[4 * j + 1] + b2.y, acc[4 * j + 2] + b2.z,
-                                           acc[4 * j + 3] + b2.w});
-                if (!in) v = (f32x4){0.f, 0.f, 0.f, 0.f};
-                cf32_put4(cs + CF32_S2 + q * CF32_PS, 2 * j + g32, v);
-            }
-        }
-        sync_lds();
-    }
-
-    // ---- stage 3: m.0.cv2 on the centre from S2, + b; waves 0-3: centre pixels 32 w ..
-    {
-        f32x16 acc = (f32x16){};
-        const int p = 32 * (wid & 3) + r32, py = p / CF32_TW, px = p % CF32_TW;
-        for (int kl = 0; kl < 18; ++kl) {
-            const int g = 22 + kl;
-            dmaA(g + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            if (wid < 4) {
-                const int tap = kl >> 1, ch = kl & 1;
-                bf16x8 ap[3], bp[3];
-                afrag(g, r32, ap);
-                bfrag(cs + CF32_S2 + ((py + tap / 3) * CF32_R2W + px + tap % 3) * CF32_PS + ch * 96 + 16 * g32, bp);
-#pragma unroll
-                for (int t = 0; t < 6; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc, 0, 0, 0);
-            }
-            t3_waitvm<1>();
-            sync_lds();
-        }
-        if (wid < 4) {
-            const unsigned char* bres = cs + CF32_S1 + ((py + 2) * CF32_R1W + px + 2) * CF32_PS;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 b3 = *(const float4*)(bb + 96 + 8 * j + 4 * g32);
-                const f32x4 v = fz::act((f32x4){acc[4 * j] + b3.x, acc[4 * j + 1] + b3.y, acc[4 * j + 2] + b3.z,
-                                                 acc[4 * j + 3] + b3.w}) + cf32_get4(bres, 2 * j + g32);
-                cf32_put4(cs + CF32_C + p * CF32_PS, 2 * j + g32, v);
-            }
-        }
-        sync_lds();
-    }
-
-    // ---- stage 4: cv2 over [a | b | c] on the centre; wave w: pixels 32 (w >> 1) .., channels 32 (w & 1) ..
-    {
-        f32x16 acc = (f32x16){};
-        const int p = 32 * (wid >> 1) + r32, ib = wid & 1, py = p / CF32_TW, px = p % CF32_TW;
-        const unsigned char* srcA = cs + CF32_A + p * CF32_PS;
-        const unsigned char* srcB = cs + CF32_S1 + ((py + 2) * CF32_R1W + px + 2) * CF32_PS;
-        const unsigned char* srcC = cs + CF32_C + p * CF32_PS;
-        for (int kl = 0; kl < 6; ++kl) {
-            const int g = 40 + kl;
-            dmaA(g + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            bf16x8 ap[3], bp[3];
-            afrag(g, 32 * ib + r32, ap);
-            bfrag((kl < 2 ? srcA : kl < 4 ? srcB : srcC) + (kl & 1) * 96 + 16 * g32, bp);
-#pragma unroll
-            for (int t = 0; t < 6; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ap[TA[t]], bp[TB[t]], acc, 0, 0, 0);
-            t3_waitvm<1>();
-            sync_lds();
-        }
-        t3_waitvm<0>();  // the zero DMAs past the last step land before the workgroup ends
-        const int oy = oy0 + py, ox = ox0 + px;
-        if (oy < H && ox < W) {
-            float* yp = Y + (((int64_t)n * H + oy) * W + ox) * ldy + 32 * ib + 4 * g32;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float4 b4 = *(const float4*)(bb + 128 + 32 * ib + 8 * j + 4 * g32);
-                *(f32x4*)(yp + 8 * j) = fz::act((f32x4){acc[4 * j] + b4.x, acc[4 * j + 1] + b4.y, acc[4 * j + 2] + b4.z,
-                                                         acc[4 * j + 3] + b4.w});
-            }
-        }
-    }
 }
 
 // ----------------------------------------------------------------------------------------- f32 32-channel 3x3
@@ -3633,28 +3345,21 @@ bool use_conv3t(const va_conv_args& a) {
            a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
 
-template <int WM, int NSTAGE, typename OutT, bool AF>
-hipError_t launch_conv3t_af(const va_conv_args& a, hipStream_t st) {
-    using Cfg = T3Cfg<WM, NSTAGE, AF>;
+template <int WM, int NSTAGE, typename OutT>
+hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3Cfg<WM, NSTAGE>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT, AF>,
+        if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT, AF>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn,
+    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn,
                        ntiles);
     return hipGetLastError();
-}
-
-// the A stage's form (VA_CONV3T, va_switch.h): the pre-split planes, or f32 split in registers (AF)
-template <int WM, int NSTAGE, typename OutT>
-hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
-    if (va_sw().conv3t == 2) return launch_conv3t_af<WM, NSTAGE, OutT, true>(a, st);
-    return launch_conv3t_af<WM, NSTAGE, OutT, false>(a, st);
 }
 
 // VA_CONV3H=0 keeps the multi-tap stride-1 layers on conv3t (A/B timing, va_switch.h)
@@ -3681,12 +3386,12 @@ bool conv3h_shape_ok(const va_conv_args& a) {
 
 bool use_conv3h(const va_conv_args& a) { return !conv3h_off() && conv3h_shape_ok(a); }
 
-template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1, bool AF = false>
-hipError_t launch_conv3h_af(const va_conv_args& a, hipStream_t st) {
-    using Cfg = T3HCfg<TNS, TPS, AF>;
+template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
+hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
+    using Cfg = T3HCfg<TNS, TPS>;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS, AF>,
+        if (hipFuncSetAttribute((const void*)conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::LDS) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -3696,17 +3401,9 @@ hipError_t launch_conv3h_af(const va_conv_args& a, hipStream_t st) {
     const int tiles_x = (a.Wo + tw - 1) / tw, tiles_y = (a.N * a.Ho + th - 1) / th;
     const int ntn = (a.Cout + Cfg::BN - 1) / Cfg::BN;
     const int ntiles = tiles_x * tiles_y * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS, AF>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a,
+    hipLaunchKernelGGL((conv3h_kernel<KH, KW, TNS, OutT, TAIL, TPS>), dim3(ntiles), dim3(T3H_NT), Cfg::LDS, st, a,
                        ntn, ntiles, lgw, tiles_x);
     return hipGetLastError();
-}
-
-// the A stage's form (VA_CONV3H, va_switch.h): the pre-split planes, or f32 split in registers (AF) -- the f32
-// weights (va_conv_args.w) are always there in f32 mode
-template <int KH, int KW, int TNS, typename OutT, bool TAIL = false, int TPS = 1>
-hipError_t launch_conv3h_v(const va_conv_args& a, hipStream_t st) {
-    if (va_sw().conv3h == 2) return launch_conv3h_af<KH, KW, TNS, OutT, TAIL, TPS, true>(a, st);
-    return launch_conv3h_af<KH, KW, TNS, OutT, TAIL, TPS, false>(a, st);
 }
 
 // the narrow f32 3x3 layers (33-64 output channels) on conv3h's 64-channel tiles: the conv3t conditions but Cout,
@@ -4222,27 +3919,6 @@ int va_seg_stem_f32(void* stream, const va_conv_args* a) {
     return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
 }
 
-int va_seg_c2f_f32(void* stream, const va_conv_args* a) {
-    if (!a || !a->x || !a->w || !a->bias || !a->y || a->dtype != VA_DTYPE_F32 || a->Cin != 64 || a->Cout != 64 ||
-        a->N <= 0 || a->H <= 0 || a->W <= 0 || a->ldx < 64 || a->ldy < 64 || a->ldx % 4 || a->ldy % 4 ||
-        ((uintptr_t)a->x & 15) || ((uintptr_t)a->y & 15) || ((uintptr_t)a->w & 15) || ((uintptr_t)a->bias & 15))
-        return VA_ERR_ARG;
-    const int tiles_x = (a->W + CF32_TW - 1) / CF32_TW, tiles_y = (a->H + CF32_TH - 1) / CF32_TH;
-    const int64_t nt = (int64_t)tiles_x * tiles_y * a->N;
-    if (nt > INT32_MAX) return VA_ERR_ARG;
-    static DevFlag attr;
-    if (!attr()) {
-        if (hipFuncSetAttribute((const void*)c2f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, CF32_LDS) !=
-            hipSuccess)
-            return VA_ERR_HIP;
-        attr() = true;
-    }
-    hipLaunchKernelGGL(c2f32_kernel, dim3((int)nt), dim3(CF32_NT), CF32_LDS, (hipStream_t)stream, (const float*)a->x,
-                       a->ldx, a->H, a->W, (const float*)a->w, a->bias, (float*)a->y, a->ldy, tiles_x, tiles_y,
-                       (int)nt);
-    return hipGetLastError() == hipSuccess ? VA_OK : VA_ERR_HIP;
-}
-
 }  // extern "C"
 
 // ---- lanes of a laned op list (va355.h VA_OP_FORK) ----
@@ -4346,9 +4022,7 @@ int va_seg_run(void* stream, const va_seg_op* ops, int32_t n) {
                          : va_seg_conv0(st, (const uint8_t*)a.x, a.N, a.H, a.W, a.w, a.bias, a.Cout, a.y, a.ldy);
                 break;
             case VA_OP_C2F:
-                rc = a.mode == 3                ? va_seg_c2fb(st, &a)
-                     : a.dtype == VA_DTYPE_F32 ? va_seg_c2f_f32(st, &a)
-                                               : va_seg_c2f(st, &a);
+                rc = a.mode == 3 ? va_seg_c2fb(st, &a) : va_seg_c2f(st, &a);
                 break;
             case VA_OP_STEM:
                 rc = a.dtype == VA_DTYPE_F32 ? va_seg_stem_f32(st, &a) : va_seg_stem(st, &a);

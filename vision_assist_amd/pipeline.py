@@ -264,12 +264,16 @@ class StreamBatches:
         if j != self.done:
             raise RuntimeError(f"batches end in begin order: expected {self.done}, got {j}")
         i = j % len(self.pipes)
-        self.s_nav.wait_event(self.ready[i])
-        with torch.cuda.stream(self.s_nav):
-            res = self.pipes[i].nav_run(stream=self.s_nav, n=n, readback=True)
-        # the next begin() on this pipeline rewrites cells / rects the grid stage just read: order it after it
-        self.s_segs[i].wait_stream(self.s_nav)
-        self.done += 1
+        try:
+            self.s_nav.wait_event(self.ready[i])
+            with torch.cuda.stream(self.s_nav):
+                res = self.pipes[i].nav_run(stream=self.s_nav, n=n, readback=True)
+        finally:
+            # a grid stage that raised loses its own batch only: the token is spent either way, so the next end()
+            # and begin() go on in order.  The next begin() on this pipeline rewrites cells / rects the
+            # grid stage just read: order it after it
+            self.s_segs[i].wait_stream(self.s_nav)
+            self.done += 1
         return res
 
 

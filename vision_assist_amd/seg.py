@@ -38,6 +38,35 @@ BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.
 NPAD = 128
 
 
+# The planner's A/B switches, read from the environment when a SegNet is built or a plan is made --
+# every default is the measured-best form; "0" turns a fusion off for a same-box comparison (tools/plan_ab.py).  The
+# library's own switches (VA_F32_SPLIT, VA_CONV3H, ...) are read in csrc/va_handle.hip.
+PLANNER_SWITCHES = {
+    "VA_CONV0": "1",        # 0: model.0 as preprocess + a conv (no fused first layer)
+    "VA_CONV0_F32M": "1",   # 0: f32 model.0 on the VALU kernel instead of the MFMA one
+    "VA_STEM": "1",         # 0: model.0 and model.1 as two launches (bf16 and f32 stems)
+    "VA_STEM_TAIL": "1",    # 0: model.2.cv1 a launch of its own instead of the f32 stem's epilogue
+    "VA_C2F": "1",          # 0: the bf16 model.2 C2f's four convs apart
+    "VA_C2FB": "1",         # 0: the batch-1 C2f blocks' layers apart
+    "VA_FOLD_PROTO": "1",   # 0: proto's upsample + cv2 unfolded
+    "VA_FUSE_UP": "1",      # 0: the FPN upsample materialised instead of read in place
+    "VA_FUSE_TAIL": "1",    # 0: no fused 1x1 tails
+    "VA_LANES": "1",        # 0: no branch-parallel lanes at small batches
+    "VA_LANES_MAX_B": "8",  # the largest batch planned with lanes
+    "VA_CONV3H": "1",       # (the library's switch, read here too: a fused f32 tail needs conv3h)
+    "VA_CONV3Q": "1",       # (likewise: the f32 32-channel tail needs conv3q)
+}
+
+
+def switch(name: str) -> str:
+    """The planner switch ``name`` (PLANNER_SWITCHES: its documented default unless the environment sets it)."""
+    return os.environ.get(name, PLANNER_SWITCHES[name])
+
+
+def switch_on(name: str) -> bool:
+    return switch(name) != "0"
+
+
 class ConvArgs(ctypes.Structure):
     _fields_ = [
         ("x", ctypes.c_void_p),
@@ -151,12 +180,9 @@ class SegOutputs:
 
 
 class SegNet:
-    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2f32: bool = False,
-                 c2fb_f32: bool = True):
-        """c2f32: run model.2 on the fused f32 C2f kernel (va_seg_c2f_f32) in f32 plans -- off by default: it measured
-        slower than the block's four launches.  c2fb_f32: the batch-1 C2f blocks of f32 plans on
-        va_seg_c2fb's f32 form where its layout keeps the intermediates as term planes (_c2fb_tile); False keeps
-        them apart (A/B)."""
+    def __init__(self, arch: Arch, folded: dict, dtype: str = "bf16", device=None, c2fb_f32: bool = True):
+        """c2fb_f32: the batch-1 C2f blocks of f32 plans on va_seg_c2fb's f32 form where its layout keeps the
+        intermediates as term planes (_c2fb_tile); False keeps them apart (A/B)."""
         _lib.require_gpu()
         self.lib = _lib.load()
         self.arch = arch
@@ -189,42 +215,42 @@ class SegNet:
         w0p = torch.zeros(w0.shape[0], 32, dtype=torch.float32)
         w0p[:, :27] = w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27)
         self.w0 = (w0p.to(self.device, self.tdtype).contiguous(), b0.float().to(self.device).contiguous())
-        self.fuse_first = w0.shape[0] % 16 == 0 and w0.shape[0] <= 64 and os.environ.get("VA_CONV0", "1") != "0"
+        self.fuse_first = w0.shape[0] % 16 == 0 and w0.shape[0] <= 64 and switch_on("VA_CONV0")
         self.w0_3 = None
         # small batches: head levels + proto on lanes beside the neck (plan() laned; VA_LANES=0 off, A/B)
-        self.lanes = os.environ.get("VA_LANES", "1") != "0"
-        self.lanes_max_b = int(os.environ.get("VA_LANES_MAX_B", "8"))
+        self.lanes = switch_on("VA_LANES")
+        self.lanes_max_b = int(switch("VA_LANES_MAX_B"))
         if dtype == "f32":  # va_seg_conv0_f32: [Cout][27], k = (ky*3 + kx)*3 + c (RGB)
             self.w0 = (w0.permute(0, 2, 3, 1).reshape(w0.shape[0], 27).float().to(self.device).contiguous(),
                        b0.float().to(self.device).contiguous())
             # va_seg_conv0_f32m: the K-padded rows as three exact bf16 terms (VA_CONV0_F32M=0: the VALU form, A/B)
-            if os.environ.get("VA_CONV0_F32M", "1") != "0":
+            if switch_on("VA_CONV0_F32M"):
                 self.w0_3 = split3_bf16(w0p).to(self.device).contiguous()
         # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
         # (bf16 wider protos -- m's 192 -- fold without the tail: conv2's plain mode-2 epilogue, then cv3 as a 1x1)
         fold_ok = arch.npr >= 128 and arch.npr % 64 == 0 and dtype in ("bf16", "f32")
-        self.proto_fold = self._fold_proto(folded) if (fold_ok and os.environ.get("VA_FOLD_PROTO", "1") != "0") \
+        self.proto_fold = self._fold_proto(folded) if (fold_ok and switch_on("VA_FOLD_PROTO")) \
             else None
         # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
         self.stem = None
-        if dtype == "bf16" and self.fuse_first and w0.shape[0] == 32 and os.environ.get("VA_STEM", "1") != "0":
+        if dtype == "bf16" and self.fuse_first and w0.shape[0] == 32 and switch_on("VA_STEM"):
             w1, b1 = folded["model.1"]
             if tuple(w1.shape) == (64, 32, 3, 3):
                 self.stem = self._pack_stem(w0p, b0, w1, b1)
         # f32: the same fusion in the f32 arithmetic (va355.h va_seg_stem_f32): model.0's three-term weights and
         # model.1's packed f32 weights; VA_STEM=0 keeps the two layers apart (A/B)
         self.stem32 = (dtype == "f32" and self.fuse_first and self.w0_3 is not None and w0.shape[0] == 32 and
-                       tuple(folded["model.1"][0].shape) == (64, 32, 3, 3) and os.environ.get("VA_STEM", "1") != "0")
+                       tuple(folded["model.1"][0].shape) == (64, 32, 3, 3) and switch_on("VA_STEM"))
         # ... with model.2.cv1 (the C2f's 1x1, 64 -> 64) in its epilogue, so model.1's map never reaches HBM either;
         # VA_STEM_TAIL=0 keeps cv1 a launch of its own (A/B).  b2 = [model.1 bias | cv1 bias]
         self.stem32_b2 = None
         pc1 = self.w.get("model.2.cv1")
-        if (self.stem32 and not c2f32 and pc1 is not None and pc1.k == 1 and pc1.cin == 64 and pc1.cout == 64 and
-                pc1.Kpad == 64 and os.environ.get("VA_STEM_TAIL", "1") != "0"):
+        if (self.stem32 and pc1 is not None and pc1.k == 1 and pc1.cin == 64 and pc1.cout == 64 and
+                pc1.Kpad == 64 and switch_on("VA_STEM_TAIL")):
             self.stem32_b2 = torch.cat([self.w["model.1"].b[:64], pc1.b[:64]]).contiguous()
         # C2f blocks the fused kernel covers (va355.h va_seg_c2f): n = 1, shortcut, 64 -> 64 (model.2 of 's')
         self.c2f_fused = {}
-        if dtype == "bf16" and os.environ.get("VA_C2F", "1") != "0":
+        if dtype == "bf16" and switch_on("VA_C2F"):
             for i, ci, co, n, shortcut in arch.c2f_plan():
                 if ci == 64 and co == 64 and n == 1 and shortcut:
                     self.c2f_fused[i] = self._pack_c2f(folded, i)
@@ -233,16 +259,10 @@ class SegNet:
         # plans take the f32 form of the same kernel for the blocks whose intermediates fit the LDS as bf16 term
         # planes (split once per value, not per read): s-seg's batch-1 forward 1.28 -> 1.21 ms, n-seg's 1.05 ->
         # 0.70.  c2fb_tile: per block index a tile side overriding _c2fb_tile's choice (tools / tests)
-        on = os.environ.get("VA_C2FB", "1") != "0" and (dtype == "bf16" or (dtype == "f32" and c2fb_f32))
+        on = switch_on("VA_C2FB") and (dtype == "bf16" or (dtype == "f32" and c2fb_f32))
         self.c2fb_max_b = C2FB_MAX_B if on else 0
         self.c2fb = {}
         self.c2fb_tile = {}
-        # f32: the same block in the f32 arithmetic (va355.h va_seg_c2f_f32), on request (c2f32)
-        self.c2f32 = {}
-        if dtype == "f32" and c2f32:
-            for i, ci, co, n, shortcut in arch.c2f_plan():
-                if ci == 64 and co == 64 and n == 1 and shortcut:
-                    self.c2f32[i] = self._pack_c2f32(folded, i)
         self._plans = {}
         # fp8: e4m3 weights with per-output-channel scales (the convs whose input channels come in 16s), and
         # the per-conv activation scales of calibrate_fp8
@@ -335,18 +355,6 @@ class SegNet:
             if B * _cdiv(h, T) * _cdiv(w, T) >= C2FB_MIN_TILES:
                 return T
         return fits[-1] if fits else 0
-
-    def _pack_c2f32(self, folded: dict, i: int):
-        """(weight blob, bias blob) of va_seg_c2f_f32: the four convs' f32 weights row-major [Cout][K] with K ordered
-        (ky, kx, ci) -- cv1 64 x 64, m.0.cv1 32 x 288, m.0.cv2 32 x 288, cv2 64 x 96 -- and their biases."""
-        parts, bias = [], []
-        for name in ("cv1", "m.0.cv1", "m.0.cv2", "cv2"):
-            w, b = folded[f"model.{i}.{name}"]
-            parts.append(w.float().permute(0, 2, 3, 1).reshape(w.shape[0], -1).reshape(-1))
-            bias.append(b.float())
-        blob = torch.cat(parts)
-        assert blob.numel() == 28672, blob.numel()
-        return blob.to(self.device).contiguous(), torch.cat(bias).to(self.device).contiguous()
 
     def _pack_fp8(self, p: Packed):
         """(e4m3 bytes [Npad][Kpad128], per-output-channel scale float [Npad]) of a packed bf16 conv: the
@@ -658,16 +666,6 @@ class SegNet:
             if pre is not None:
                 c = co // 2
                 t = pre
-            elif i in self.c2f32 and src.c == 64 and src.ld % 4 == 0 and dst.ld % 4 == 0 and up is None:
-                blob, bias = self.c2f32[i]
-                ops.append(SegOp(kind=VA_OP_C2F, a=ConvArgs(x=src.ptr, N=B, H=h, W=w, Cin=64, ldx=src.ld,
-                                                             w=blob.data_ptr(), bias=bias.data_ptr(), Cout=64,
-                                                             y=dst.ptr, ldy=dst.ld, dtype=VA_DTYPE_F32)))
-                macs = 64 * 64 + 2 * 32 * 288 + 64 * 96  # per pixel, the four convs
-                meta.append({"name": f"model.{i} (fused f32 C2f)", "kind": "conv", "M": B * h * w, "N": 64,
-                             "K": macs // 64, "k": 1, "stride": 1, "flops": 2 * B * h * w * macs,
-                             "bytes": 4 * B * h * w * 128})
-                return
             c = co // 2
             if (pre is None and B <= self.c2fb_max_b and c in (16, 32, 64, 128, 256) and n in (1, 2) and ci % 8 == 0 and
                     co % 16 == 0 and src.ld % 8 == 0 and dst.ld % 8 == 0 and (up is None or up.ld % 8 == 0) and
@@ -887,7 +885,7 @@ class SegNet:
         conv("model.9.cv2", sp, P5, h5, w5)
         # the FPN's Upsample + Concat: read in place by the consumer's 1x1 cv1 (bf16) or materialised
         ks = 64 if self.dtype == "bf16" else 32  # the conv2 K-step the upsampled prefix must align to
-        fuse_up = self.dtype != "fp8" and os.environ.get("VA_FUSE_UP", "1") != "0" and a.c5 % ks == 0 \
+        fuse_up = self.dtype != "fp8" and switch_on("VA_FUSE_UP") and a.c5 % ks == 0 \
             and a.c4 % ks == 0 and (a.c5 + a.c4) % ks == 0 and (a.c4 + a.c3) % ks == 0
         if not fuse_up:
             upsample(P5, cat11.sub(0, a.c5), h5, w5)
@@ -1032,7 +1030,7 @@ class SegNet:
         tiles (Cout 64 or 128; the fold: 128), the tail has <= 96 channels, and the launch has >= 128 tiles --
         below that conv2 would split the conv over K (batch-1 shapes), which a fused launch cannot, so the pair
         stays unfused there.  VA_FUSE_TAIL=0 / VA_CONV3H=0 turn it off."""
-        if os.environ.get("VA_FUSE_TAIL", "1") == "0" or os.environ.get("VA_CONV3H", "1") == "0":
+        if not switch_on("VA_FUSE_TAIL") or not switch_on("VA_CONV3H"):
             return False
         if p2.k != 1 or p2.cin != cout or p2.cout % 4 or p2.cout > 96 or cout not in ((128,) if fold else (64, 128)):
             return False
@@ -1047,14 +1045,14 @@ class SegNet:
         if self.dtype == "f32" and p.cin == 32 and p.cout == 32:
             # the 32-channel 3x3 (the head's cv4.l.1) on conv3q with the tail in its epilogue, where the launch has
             # four 16 x 16 tiles per CU (va_seg.hip Q3_MIN_TILES_PER_CU; M / 256 is a lower bound of its tiles)
-            if os.environ.get("VA_FUSE_TAIL", "1") == "0" or os.environ.get("VA_CONV3Q", "1") == "0":
+            if not switch_on("VA_FUSE_TAIL") or not switch_on("VA_CONV3Q"):
                 return False
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
             return (p.k == 3 and not p.deconv and p2.k == 1 and p2.cin == 32 and p2.cout <= 32 and p2.cout % 4 == 0
                     and M // 256 >= 4 * cus)
         if self.dtype == "f32":
             return p.k == 3 and not p.deconv and p.w3 is not None and self._fuse_tail_f32(p.cout, p2, M)
-        if self.dtype != "bf16" or os.environ.get("VA_FUSE_TAIL", "1") == "0":
+        if self.dtype != "bf16" or not switch_on("VA_FUSE_TAIL"):
             return False
         if p.deconv or p2.k != 1 or p2.cin != p.cout or p2.cout % 4:
             return False

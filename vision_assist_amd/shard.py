@@ -93,15 +93,33 @@ class FrameDealer:
     share a GPU).  Frames of one dealer share one size (H, W).
 
     A frame whose worker raised is handed back by get() as a RuntimeError for that frame and the stream moves on;
-    a worker process that dies makes the dealer ``broken`` (every later call raises instead of waiting)."""
+    a worker process that dies makes the dealer ``broken`` (every later call raises instead of waiting).
+
+    readers: 0 (default) copies each frame into its ring on the calling thread inside submit(); R > 0 hands the copies
+    to R reader threads (thread r fills the rings of workers w with w % R == r, in submission order), so submit()
+    returns at once and the rings fill in parallel -- one thread's copies cap the whole node's frame rate near one GPU's
+    worth.  With readers, a submitted frame must stay unmodified until its result has been returned
+    (map() over fresh frames, as a camera or a decoder yields them, is safe)."""
 
     def __init__(self, worker_factory, devices, H: int, W: int, slots: int = 4, start_timeout: float = 600.0,
-                 poll: float = 1.0):
+                 poll: float = 1.0, readers: int = 0):
+        import platform
+
         import torch.multiprocessing as tmp
         self.G = len(devices)
         if self.G < 1:
             raise ValueError("FrameDealer needs at least one worker")
+        if platform.machine() not in ("x86_64", "AMD64"):
+            # the ring's head / tail handshake is plain aligned int64 stores: correct under x86's store order only
+            raise RuntimeError(f"FrameDealer's ring handshake assumes x86 store ordering, not {platform.machine()}")
         self.H, self.W, self.slots, self.poll = H, W, slots, poll
+        need = self.G * slots * H * W * 3
+        if os.path.isdir("/dev/shm"):
+            st = os.statvfs("/dev/shm")
+            free = st.f_bavail * st.f_frsize
+            if need > free:
+                raise ValueError(f"the frame ring needs {need / 2**20:.0f} MiB of /dev/shm ({self.G} workers x {slots} "
+                                 f"slots x {H}x{W}x3), {free / 2**20:.0f} MiB are free: pass fewer slots or workers")
         self.broken: str | None = None
         ctx = tmp.get_context("spawn")
         self.ring = torch.zeros((self.G, slots, H, W, 3), dtype=torch.uint8).share_memory_()
@@ -130,6 +148,14 @@ class FrameDealer:
         self.n = 0          # frames submitted
         self.next = 0       # next frame index to hand back
         self._done = {}     # results that arrived ahead of their turn (_Failed for a frame whose worker raised)
+        self._readers = []
+        if readers > 0:
+            import queue
+            import threading
+            self._rq = [queue.SimpleQueue() for _ in range(min(readers, self.G))]
+            self._readers = [threading.Thread(target=self._reader, args=(q,), daemon=True) for q in self._rq]
+            for t in self._readers:
+                t.start()
 
     def _check_workers(self) -> None:
         for w, p in enumerate(self.procs):
@@ -158,6 +184,16 @@ class FrameDealer:
         t = torch.as_tensor(frame)
         if tuple(t.shape) != (self.H, self.W, 3) or t.dtype != torch.uint8:
             raise ValueError(f"frame must be uint8 [{self.H}, {self.W}, 3], got {tuple(t.shape)} {t.dtype}")
+        src = t.numpy() if t.device.type == "cpu" else t.cpu().numpy()
+        if self._readers:
+            self._rq[w % len(self._rq)].put((w, src))
+        else:
+            self._put(w, src)
+        self.n += 1
+        return idx
+
+    def _put(self, w: int, src: np.ndarray) -> None:
+        """Copy one frame into worker w's ring (waiting for a free slot) and publish it."""
         ctl = self._ctl[w]
         head = int(ctl[0])
         if head - int(ctl[1]) >= self.slots:  # the ring is full: wait for the worker to copy frames out
@@ -169,11 +205,21 @@ class FrameDealer:
                     self._check_workers()
                     t0 = time.monotonic()
         # numpy's copy, not torch's: torch's CPU copy of a frame wakes its OpenMP pool, whose workers then spin
-        # between frames and exhaust the box's CPU quota for every process of it (pipeline.FramePipeline._pinned)
-        np.copyto(self._ring_np[w, head % self.slots], t.numpy() if t.device.type == "cpu" else t.cpu().numpy())
+        # between frames and exhaust the box's CPU quota for every process of it (pipeline.FramePipeline._pinned);
+        # numpy releases the GIL for the copy, so reader threads copy in parallel
+        np.copyto(self._ring_np[w, head % self.slots], src)
         ctl[0] = head + 1  # publish: the worker may read the slot from now on
-        self.n += 1
-        return idx
+
+    def _reader(self, q) -> None:
+        """Reader thread: copies its workers' frames into their rings in submission order; None ends it."""
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            try:
+                self._put(*item)
+            except RuntimeError as e:  # a dead worker: the main thread's next wait sees it too (broken)
+                self.broken = self.broken or str(e)
 
     def get(self):
         """The next result in frame order (blocks until it is in); a RuntimeError for a frame whose worker raised
@@ -226,6 +272,11 @@ class FrameDealer:
 
     def close(self) -> None:
         """The workers finish the frames already dealt, then exit."""
+        for q in getattr(self, "_rq", []):
+            q.put(None)
+        for t in self._readers:
+            t.join(timeout=60)
+        self._readers = []
         self._ctl[:, 2] = 1
         for p in self.procs:
             p.join(timeout=60)
