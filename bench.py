@@ -13,13 +13,15 @@ One step = one pass of the fused hot path (vision_assist_amd.pipeline) over one 
 --batch synthetic frames per GPU (uint8 BGR, resident in HBM before the timed region;
 random-init weights of the yolov8s-seg architecture -- no checkpoints exist offline).
 Navigation runs on the network's mask when it yields one and on a planted mask otherwise
-(13 reference fixtures resampled to 640x640 + seeded procedural corridors, SURVEY.md §8d);
-with the default "natural" regime the synthetic network yields no detections, so
-post-processing has nothing to keep and A* always runs on the planted masks -- the "dense"
-extra (300 detections per frame) is the post-processing-heavy counterpart.
+(13 reference fixtures resampled to 640x640 + seeded procedural corridors); the
+default "sparse" regime gives 1-5 compact detections per frame (a trained model's frames), so
+the network's own masks reach the mask choice, contours and A* -- the "dense" / "dense_box"
+extras (300 detections per frame) are the post-processing-heavy counterparts.
 
-Multi-GPU: one process per GPU (torch.distributed.run), frames sharded, no collective on the
-data path; a gloo (CPU) process group only for the barrier + max-over-ranks timing.
+Multi-GPU: one process per GPU, frames sharded, no collective on the data path; a gloo (CPU)
+process group only for the barrier + max-over-ranks timing.  `bench.py --gpus N` starts its N
+rank processes itself (before any GPU call) when it is not already running under a launcher;
+under torch.distributed.run (the driver's form) it checks WORLD_SIZE == --gpus.
 
 Prints ONE JSON line (rank 0).
 """
@@ -68,7 +70,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16", "fp8", "w8a16"],
                    help="network arithmetic of the headline (fp8: the convs on e4m3 MFMA, BASELINE configs[4]; "
-                        "w8a16: e4m3 weights dequantized into bf16, bf16 activations and MFMA)")
+                        "w8a16: e4m3 weight bytes converted in the bf16 kernels, bf16 activations and MFMA)")
     p.add_argument("--batch", type=int, default=0, help="frames per step per GPU (0 = the dtype's default)")
     p.add_argument("--scale", default="s")
     p.add_argument("--res", type=int, default=640)
@@ -84,8 +86,8 @@ def parse():
                         "bf16 (the bf16 MFMA pipeline), "
                         "dense (300 detections per frame, the random weights' noise masks), dense_box (300 "
                         "detections per frame with solid box masks, one contour each, as a trained model's compact "
-                        "masks), c5 (YOLOv8m-seg 1280, batch 8, C5's kept form: e4m3 weights dequantized into bf16, "
-                        "bf16 activations), c5_w8a8 (the same on the e4m3 MFMA with e4m3 activations); 'none' to skip")
+                        "masks), c5 (YOLOv8m-seg 1280, batch 8, C5's kept form: e4m3 weight bytes converted to bf16 in "
+                        "the kernels, bf16 activations), c5_w8a8 (the same on the e4m3 MFMA with e4m3 activations); 'none' to skip")
     p.add_argument("--cpu-sample", type=int, default=256,
                    help="frames timed for the CPU baseline (0 = skip; 256 = ~10-20 s)")
     p.add_argument("--no-prof", action="store_true", help="skip the HIP-event timing of the isolated forwards")

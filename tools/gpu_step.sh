@@ -1,9 +1,5 @@
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_w8.py > gpurun_out/t7.log 2>&1
-rc=$?
-echo "pytest rc=$rc" >> gpurun_out/t7.log
-if [ $rc -le 1 ]; then
-  timeout -k 10 600 python -u tools/seg_layer_profile.py --scale m --res 1280 --batch 8 --dtype w8a16 --plan-ab VA_W8 --iters 20 > gpurun_out/l7.log 2>&1
-  echo "rc=$?" >> gpurun_out/l7.log
-fi
-exit $rc
+mkdir -p gpurun_out/c5
+timeout -k 10 400 python -u bench.py --scale m --res 1280 --dtype fp8 --regime dense_box --steps 20 --warmup 3 --extras none --cpu-sample 0 --no-ingest > gpurun_out/c5/w8a8_fresh.json 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --scale m --res 1280 --dtype w8a16 --regime dense_box --steps 20 --warmup 3 --extras c5_w8a8 --cpu-sample 0 --no-ingest > gpurun_out/c5/w8a16_then_w8a8.json 2>&1 || exit $?
+bash tools/gpu_prof.sh c5/prof "--scale m --res 1280 --batch 8 --dtype w8a16" --scale m --res 1280 --dtype w8a16 --regime dense_box

@@ -3464,6 +3464,10 @@ bool use_conv4(const va_conv_args& a) {
         a.ldx % 8 || ((uintptr_t)a.x & 15) || a.ldy % 8 || ((uintptr_t)a.y & 15) || a.Npad % 256 ||
         (a.res && (a.ldr % 8 || ((uintptr_t)a.res & 15))))
         return false;
+    // e4m3 weights (w8): the multi-tap layers stay on conv2, whose fragment conversion hides beside its MFMAs --
+    // m@1280's 192-channel 3x3s at 160 x 160 took 241 us on conv4 against 207-211 on conv2 (and 228-230 on the bf16
+    // conv4); the 1x1s keep conv4 (model.4.cv2 111 against 120 us; profiles/r06/c5/ab_conv4_w8.log)
+    if (a.w8 && a.kh * a.kw > 1 && mn > 1) return false;
     const int64_t tiles = (int64_t)((a.M + 255) / 256) * ((a.Cout + 255) / 256);
     return tiles >= mn;
 }
