@@ -19,8 +19,8 @@ def goldens():
     return load_goldens()
 
 
-LIB_SWITCHES = ("VA_F32_SPLIT", "VA_CONV3H", "VA_CONV3T", "VA_CONV3Q", "VA_SPLITK", "VA_CONV_PATCH", "VA_CONV4", "VA_PW",
-                "VA_CT_RUNS", "VA_CT_WGP")
+LIB_SWITCHES = ("VA_F32_SPLIT", "VA_CONV3H", "VA_CONV3T", "VA_CONV3Q", "VA_SPLITK", "VA_SPLITK_KS", "VA_CONV_PATCH",
+                "VA_CONV4", "VA_PW", "VA_CT_RUNS", "VA_CT_WGP")
 
 
 @pytest.fixture

@@ -136,6 +136,30 @@ def test_conv_split_k(dtype, cin, cout, k, stride, H, W, residual, slice_in):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("ks", ["4", "8", "13"])
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,slice_in", [
+    (256, 256, 3, 1, 20, 20, False, 0),
+    (128, 256, 3, 2, 40, 40, True, 8),
+    (512, 192, 1, 1, 17, 23, False, 0),
+    (40, 136, 3, 1, 12, 10, True, 0),
+])
+def test_split_k_reduce_form_bit_identical_to_ticket(dtype, ks, cin, cout, k, stride, H, W, residual, slice_in, switch):
+    """The reduce form (conv2_reduce_kernel, the default) adds the slabs in slice order and applies the epilogue's
+    element work as conv_epilogue does: bit-identical to the ticket combine (VA_SPLITK=ticket) at the same slice
+    count (forced, VA_SPLITK_KS), residual and ragged tiles included."""
+    ws = (torch.empty(32 << 20, dtype=torch.uint8, device="cuda"), torch.zeros(128, dtype=torch.int32, device="cuda"))
+    switch("VA_SPLITK_KS", ks)
+    switch("VA_SPLITK", "ticket")
+    t, ref = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1)
+    switch("VA_SPLITK", None)
+    r, _ = _run_single_conv(dtype, cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1)
+    assert int(ws[1].abs().sum()) == 0
+    assert torch.equal(t, r)
+    if dtype == "f32":
+        assert torch.allclose(r, ref, atol=1e-4, rtol=1e-4), (r - ref).abs().max()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_forward_batch1_split_k_matches_unsplit(dtype, monkeypatch, switch):
     """The batch-1 n-seg forward with split-K (the C2 shape) against the same forward with VA_SPLITK=0: f32 to
     f32 rounding of the reordered sums, bf16 to bf16 rounding of the stored activations."""

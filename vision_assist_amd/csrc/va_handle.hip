@@ -49,7 +49,10 @@ void read_switches(VaSwitches& s) {
     s.conv3t = !e ? 1 : e[0] == '0' ? 0 : 1;
     e = getenv("VA_CONV3Q");
     s.conv3q = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "static") == 0 ? 2 : 1;
-    s.splitk = !env_off("VA_SPLITK");
+    e = getenv("VA_SPLITK");
+    s.splitk = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "ticket") == 0 ? 2 : 1;
+    e = getenv("VA_SPLITK_KS");
+    s.splitk_ks = e ? atoi(e) : 0;
     s.patch = !env_off("VA_CONV_PATCH");
     e = getenv("VA_CONV4");
     s.conv4_min = !e ? 256 : e[0] == '0' ? -1 : strcmp(e, "all") == 0 ? 1 : 256;

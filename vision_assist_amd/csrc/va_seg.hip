@@ -828,6 +828,10 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 
     C2S(0, __builtin_amdgcn_s_memtime());
     C2S(6, __builtin_amdgcn_s_memrealtime());
+    // ksplit < 0: split K in the reduce form -- the -ksplit slices only store their slabs, conv2_reduce_kernel sums
+    // them and runs the epilogue
+    const bool kred = ksplit < 0;
+    if (kred) ksplit = -ksplit;
     int bid = blockIdx.x;
     {
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
@@ -1157,6 +1161,12 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 #pragma unroll
             for (int q = 0; q < NQ; ++q)
                 sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
+            if (kred) {
+                C2S(3, __builtin_amdgcn_s_memtime());
+                C2S(5, __builtin_amdgcn_s_memtime());
+                C2S(7, __builtin_amdgcn_s_memrealtime());
+                return;
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             int* last_s = (int*)smem;  // the stage buffers are free: the K-loop ended on a barrier
@@ -1203,6 +1213,71 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
     conv_epilogue<NT, BM, BN, TNS, OutT, decltype(orow), T>(a, acc, smem, n0, wm, wn, tid, fr, fq, orow, m0, cls);
     C2S(5, __builtin_amdgcn_s_memtime());
     C2S(7, __builtin_amdgcn_s_memrealtime());
+}
+
+// ------------------------------------------------------------------------ split-K, reduce form
+// conv2_kernel with ksplit < 0 leaves its slices' f32 partial tiles in the workspace (slab [vt][sk][q][thread]: one
+// 16-byte accumulator fragment per unit) and this kernel finishes them: a thread per (virtual tile, fragment q,
+// thread) unit sums the slices in slice order -- the ticket combine's arithmetic, so the result is bit-identical --
+// and applies conv_epilogue's element work (weight scale, bias, SiLU, residual) to its four channels of one pixel,
+// stored straight to the output.  The ticket form sums a tile's ks x 64 KiB in ONE workgroup once the last slice
+// has arrived (~0.45 us per slice at batch 1) and then runs a 2-6 us LDS epilogue on it
+// (profiles/r06/b1/phases_f32_b1.log); here every CU takes a share.  Mode 0 without a fused tail (conv2_red_ok).
+template <typename RT, typename OutT, int WM, int WN, int TNS>
+__global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int ntn, int ks, int nunits) {
+    constexpr int NT = 64 * WM * WN, NQ = TNS * 4, BM = 64 * WM, BN = 16 * TNS * WN;
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= nunits) return;
+    const int tid = u % NT, q = (u / NT) % NQ, vt = u / (NT * NQ);
+    const int wid = tid >> 6, lane = tid & 63, wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
+    const int m = (vt / ntn) * BM + wm * 64 + 16 * (q % 4) + fr;            // conv_epilogue's pixel of the unit
+    const int co = (vt % ntn) * BN + wn * 16 * TNS + 16 * (q / 4) + 4 * fq;  // and its first channel
+    if (m >= a.M || co >= a.Cout) return;
+    const f32x4* sl = (const f32x4*)a.ws + ((int64_t)vt * ks * NQ + q) * NT + tid;
+    f32x4 ac = sl[0];
+    for (int o0 = 1; o0 < ks; o0 += 8) {  // eight slabs in flight, added in slice order
+        f32x4 t[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (o0 + e < ks) t[e] = sl[(int64_t)(o0 + e) * NQ * NT];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (o0 + e < ks) ac += t[e];
+    }
+    if (sizeof(RT) == 2 && a.w8) {
+        const float4 sv = *(const float4*)(a.wscale + co);
+        ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
+    }
+    const float4 bv = *(const float4*)(a.bias + co);
+    float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
+    if (a.act) {
+        const f32x2 s01 = fz::silu2((f32x2){v[0], v[1]}), s23 = fz::silu2((f32x2){v[2], v[3]});
+        v[0] = s01[0];
+        v[1] = s01[1];
+        v[2] = s23[0];
+        v[3] = s23[1];
+    }
+    if (a.res) {
+        const RT* rp = (const RT*)a.res + (int64_t)m * a.ldr + co;
+        if constexpr (sizeof(RT) == 4) {
+            const float4 r = *(const float4*)rp;
+            v[0] += r.x, v[1] += r.y, v[2] += r.z, v[3] += r.w;
+        } else {
+            const uint2 r = *(const uint2*)rp;
+            const RT* re = (const RT*)&r;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)re[e];
+        }
+    }
+    OutT* yp = (OutT*)a.y + (int64_t)m * a.ldy + co;
+    if constexpr (sizeof(OutT) == 2) {
+        __attribute__((aligned(8))) __bf16 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+        *(uint2*)yp = *(const uint2*)o;
+    } else {
+        *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+    }
 }
 
 // ------------------------------------------------------------------------ conv3t (f32 mode, three-plane K-loop)
@@ -3348,24 +3423,34 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
 // with tiles x ks <= 256 that minimises ceil(nk / ks) ts + 1.0 + 1.5 ks, if it beats the unsplit nk ts by 15 %.
 // VA_SPLITK=0 disables it (A/B timing, va_switch.h).  Returns the slice count (1 = no split); *kper = K-steps
 // per slice (every slice non-empty).
-int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* kper) {
+int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* kper, bool red) {
     *kper = nk;
-    if (!va_sw().splitk || !a.ws || !a.wcnt || tiles >= 128 || nk < 4 || tiles > a.ncnt) return 1;
-    // cost model (us): K-steps per slice x ts + tw + tc per slice.  Swept in round 4 at batch 1 (tc 0.75 / 3, ts x1.43,
-    // tiles x ks up to 512): the f32 s-seg and bf16 n-seg forwards within 1-2 % of these constants or slower
-    // (profiles/r04/batch1/splitk_sweep.log)
-    const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f, tw = 1.0f, tc = 1.5f;
+    if (!va_sw().splitk || !a.ws || tiles >= 128 || nk < 4) return 1;
+    if (!red && (!a.wcnt || tiles > a.ncnt)) return 1;
+    // cost model (us): K-steps per slice x ts + tw + tc per slice.  Ticket form swept in round 4 at batch 1 (tc 0.75 /
+    // 3, ts x1.43, tiles x ks up to 512): the f32 s-seg and bf16 n-seg forwards within 1-2 % of these constants or
+    // slower (profiles/r04/batch1/splitk_sweep.log).  Reduce form: tw = the second launch, tc = the slabs' traffic
+    const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f;
+    const float tw = red ? 3.0f : 1.0f, tc = red ? 0.02f * tiles * (bm * bn / 16384.0f) : 1.5f;
+    const int maxks = red ? 32 : 16, maxb = red ? 512 : 256;
     int best = 1;
     float bt = nk * ts;
-    for (int ks = 2; ks <= 16 && ks <= nk / 2 && tiles * ks <= 256; ++ks) {
+    for (int ks = 2; ks <= maxks && ks <= nk / 2 && tiles * ks <= maxb; ++ks) {
         if ((int64_t)tiles * ks * bm * bn * 4 > a.ws_bytes) break;
         const float t = ((nk + ks - 1) / ks) * ts + tw + tc * ks;
-        if (t < bt) bt = t, best = ks;
+        if (va_sw().splitk_ks > 0 ? ks <= va_sw().splitk_ks : t < bt) bt = t, best = ks;
     }
-    if (best == 1 || bt > 0.85f * nk * ts) return 1;
+    if (best == 1 || (va_sw().splitk_ks <= 0 && bt > 0.85f * nk * ts)) return 1;
     const int per = (nk + best - 1) / best;
     *kper = per;
     return (nk + per - 1) / per;
+}
+
+// split K in the reduce form (conv2_reduce_kernel) where conv2 splits a launch: mode 0 without a fused tail, bf16 / f32
+// (not the fp8 conv); VA_SPLITK=ticket keeps the last-arriving-slice combine
+template <typename T>
+bool conv2_red_ok(const va_conv_args& a) {
+    return sizeof(T) != 1 && a.mode == 0 && !a.w2 && va_sw().splitk == 1;
 }
 
 template <int WM, int WN, int TNS, typename OutT, typename T = __bf16, int SPL = 0, bool W8 = false>
@@ -3377,24 +3462,31 @@ hipError_t launch_conv2(const va_conv_args& a, hipStream_t st) {
     // LDS-DMA needs every 16-byte chunk aligned: Cin, ldx multiples of VEC and a 16-byte aligned base
     const bool fk = a.Cin % KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K;
     int kper = a.Kpad / KS, ks = 1;
-    if (a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper);
-    const int nb = ntiles * ks;
-    if (a.xu) {  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
+    const bool red_ok = conv2_red_ok<T>(a);
+    if (a.mode != 1) ks = conv2_ksplit(a, ntiles, a.Kpad / KS, Cfg::BM, Cfg::BN, &kper, red_ok);
+    const bool red = ks > 1 && red_ok;
+    const int nb = ntiles * ks, kpass = red ? -ks : ks;
+    if (a.xu)  // upsampled channel prefix: the FK LDS-DMA form only (checked by va_seg_conv)
         hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, true, SPL, W8>), dim3(nb), dim3(Cfg::NT), 0,
-                           st, a, ntn, nb, ks, kper);
-        return hipGetLastError();
-    }
-    if (a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
+                           st, a, ntn, nb, kpass, kper);
+    else if (a.Cin % VEC == 0 && a.ldx % VEC == 0 && ((uintptr_t)a.x & 15) == 0 && a.Kpad % VEC == 0) {
         if (fk)
             hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, true, false, SPL, W8>), dim3(nb), dim3(Cfg::NT),
-                               0, st, a, ntn, nb, ks, kper);
+                               0, st, a, ntn, nb, kpass, kper);
         else
             hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, true, false, false, SPL, W8>), dim3(nb), dim3(Cfg::NT),
-                               0, st, a, ntn, nb, ks, kper);
+                               0, st, a, ntn, nb, kpass, kper);
     }
     else
         hipLaunchKernelGGL((conv2_kernel<T, WM, WN, TNS, OutT, false, false, false, SPL, W8>), dim3(nb), dim3(Cfg::NT), 0,
-                           st, a, ntn, nb, ks, kper);
+                           st, a, ntn, nb, kpass, kper);
+    if constexpr (sizeof(T) != 1) {
+        if (red) {
+            const int nunits = ntiles * TNS * 4 * Cfg::NT;
+            hipLaunchKernelGGL((conv2_reduce_kernel<T, OutT, WM, WN, TNS>), dim3((nunits + 255) / 256), dim3(256), 0, st,
+                               a, ntn, ks, nunits);
+        }
+    }
     return hipGetLastError();
 }
 
@@ -3511,7 +3603,7 @@ bool use_conv3t(const va_conv_args& a) {
     // (profiles/r04/batch1/small_ab.log)
     int kper;
     const int t2 = ((a.M + 127) / 128) * ((a.Cout + 127) / 128) * (a.mode == 2 ? 4 : 1);
-    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper) > 1) return false;
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 128, &kper, conv2_red_ok<float>(a)) > 1) return false;
     return (a.mode == 0 || a.mode == 2) && a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K &&
            a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }
@@ -3584,7 +3676,7 @@ bool use_conv3h_narrow(const va_conv_args& a) {
     if (!a.w3 || conv3t_off() || a.mode != 0 || a.Cout <= 32 || a.Cout > 64 || !use_conv3h(a)) return false;
     int kper;
     const int t2 = ((a.M + 127) / 128) * ((a.Cout + 63) / 64);
-    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 64, &kper) > 1) return false;
+    if (conv2_ksplit(a, t2, a.Kpad / 32, 128, 64, &kper, conv2_red_ok<float>(a)) > 1) return false;
     return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.Npad % 64 == 0 && a.ldx % 4 == 0 &&
            ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
 }

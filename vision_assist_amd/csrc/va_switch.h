@@ -11,7 +11,10 @@ struct VaSwitches {
     int conv3q;      // VA_CONV3Q=0: the 32 -> 32 stride-1 3x3 f32 layers on conv2's three-term form instead of conv3q;
                      // 2 = "static": the persistent kernels (conv3q, the f32 and bf16 stems, the bf16 C2f) on
                      // fz::tile's static schedule instead of the plan's work counter (va_fuse.h fz::wq_claim)
-    bool splitk;     // VA_SPLITK=0: no split-K for launches of few tiles
+    int splitk;      // VA_SPLITK=0: no split-K for launches of few tiles; "ticket" (2): the slices' sum and epilogue
+                     // in the last-arriving workgroup of each tile instead of conv2_reduce_kernel (the default, 1)
+    int splitk_ks;   // VA_SPLITK_KS=<n> (diagnostic sweeps only): the slice count of every split launch forced to n
+                     // (within the workspace and two workgroups per CU); 0 = the cost model
     bool patch;      // VA_CONV_PATCH=0: the narrow bf16 3x3 layers on conv_dn instead of the patch kernel
     int conv4_min;   // VA_CONV4: 0 = conv4 off (-1 here), "all" = every eligible layer (1), default 256 tiles
     bool pw;         // VA_PW=0: the bf16 128-channel 1x1 layers on conv2 instead of pw_kernel
