@@ -210,14 +210,21 @@ def test_call_matches_oracle_chain_answers():
 
     # the FrameDealer worker's batched form (shard.dropin_worker batch=k): batches of up to 8 frames (ragged: 8, 8,
     # 5, 8, 3), two in flight (batch j+1 begun before batch j's answers), answers built frame by frame in order; the
-    # frozen clock reads the frame FrameProcessor is answering
+    # frozen clock reads the stream position of the frame FrameProcessor is answering (_end_batch answers every
+    # frame of a batch once, in order, through _answer; the batch token keeps no pixels)
     from vision_assist_amd.shard import _BatchedFrameProcessor
     fl = [frames[i] for i in range(B)]
-    at = {id(f): 1_000_000.0 + 0.5 * (i + 1) for i, f in enumerate(fl)}
+    pos = {"next": 0, "cur": -1}
+    answer = fp._answer
+
+    def counted(*args, **kw):
+        pos["cur"], pos["next"] = pos["next"], pos["next"] + 1
+        return answer(*args, **kw)
+    fp._answer = counted
 
     class FrameClock:
         def __call__(self):
-            return at[id(fp.frame)]
+            return 1_000_000.0 + 0.5 * (pos["cur"] + 1)
 
     path_analyser.clock = FrameClock()
     path_analyser.previous_instructions = {}

@@ -1,17 +1,18 @@
 #!/bin/bash
-# Per-layer SQ / LDS / TA-TD / TCC counters of the f32 s-seg forward (B = 64; tools/pmc_forward.py), one rocprofv3
-# pass per counter set, each under its own time limit; then tools/pmc_summary.py maps them to layer names.
+# Per-layer SQ / LDS / TA-TD / TCC counters of the f32 s-seg forward (B = $BATCH, 64 by default; tools/pmc_forward.py),
+# one rocprofv3 pass per counter set, each under its own time limit; then tools/pmc_summary.py maps them to layer names.
 #   bash tools/pmc_conv.sh OUTDIR [extra env, e.g. VA_CONV3H=0]      (PASSES="sq lds tcc tcp fetch write" by default)
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift
 mkdir -p $O
 for kv in "$@"; do export "$kv"; done
 PASSES=${PASSES:-sq lds tcc tcp fetch write}
+BATCH=${BATCH:-64}
 run() {  # name counters...
   n=$1; shift
   case " $PASSES " in *" $n "*) ;; *) return 0;; esac
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $O/$n -o run -- \
-      python3 tools/pmc_forward.py --dtype f32 --batch 64 --out $O/plan > $O/$n.log 2>&1
+      python3 tools/pmc_forward.py --dtype f32 --batch $BATCH --out $O/plan > $O/$n.log 2>&1
   rc=$?; echo "$n rc=$rc"; return $rc
 }
 run sq SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \

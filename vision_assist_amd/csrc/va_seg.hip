@@ -1233,6 +1233,7 @@ __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int n
     const int m = (vt / ntn) * BM + wm * 64 + 16 * (q % 4) + fr;            // conv_epilogue's pixel of the unit
     const int co = (vt % ntn) * BN + wn * 16 * TNS + 16 * (q / 4) + 4 * fq;  // and its first channel
     if (m >= a.M || co >= a.Cout) return;
+    const float4 bv = *(const float4*)(a.bias + co);  // issued ahead of the slabs: one memory latency, not two
     const f32x4* sl = (const f32x4*)a.ws + ((int64_t)vt * ks * NQ + q) * NT + tid;
     f32x4 ac = sl[0];
     for (int o0 = 1; o0 < ks; o0 += 8) {  // eight slabs in flight, added in slice order
@@ -1248,7 +1249,6 @@ __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int n
         const float4 sv = *(const float4*)(a.wscale + co);
         ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
     }
-    const float4 bv = *(const float4*)(a.bias + co);
     float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
     if (a.act) {
         const f32x2 s01 = fz::silu2((f32x2){v[0], v[1]}), s23 = fz::silu2((f32x2){v[2], v[3]});
