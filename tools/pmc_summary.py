@@ -15,6 +15,7 @@ counters, plus
 import csv
 import glob
 import json
+import re
 import sys
 from collections import defaultdict
 
@@ -43,13 +44,26 @@ def main():
     rows_by_pass = []
     for c in csvs:
         disp = load([c])
-        ours = [disp[k] | {"_id": k} for k in sorted(disp) if "_kernel" in disp[k]["_name"] and ("anonymous" in disp[k]["_name"] or "_GLOBAL__N_" in disp[k]["_name"])]
+        ours0 = [disp[k] | {"_id": k} for k in sorted(disp) if "_kernel" in disp[k]["_name"] and ("anonymous" in disp[k]["_name"] or "_GLOBAL__N_" in disp[k]["_name"])]
+        # a split-K conv is two dispatches (the slices, then conv2_reduce_kernel): the reduce's counters and time are
+        # added to its conv's, one row per op
+        ours = []
+        for d in ours0:
+            if "conv2_reduce_kernel" in d["_name"] and ours:
+                prev = ours[-1]
+                for k, v in d.items():
+                    if not k.startswith("_"):
+                        prev[k] = prev.get(k, 0.0) + v
+                prev["_dur_ns"] += d["_dur_ns"]
+            else:
+                ours.append(dict(d))
         if len(ours) < n:
             raise SystemExit(f"{c}: {len(ours)} library dispatches < {n} ops")
         rows_by_pass.append(ours[-n:])  # the last forward
     out = []
     for i, op in enumerate(ops):
-        r = {"i": i, "name": op["name"], "kernel": rows_by_pass[0][i]["_name"].split("(")[0][-60:]}
+        km = re.search(r"(\w+_kernel(<[^()]*>)?)", rows_by_pass[0][i]["_name"])
+        r = {"i": i, "name": op["name"], "kernel": (km.group(1) if km else rows_by_pass[0][i]["_name"])[:80]}
         for rows in rows_by_pass:
             for k, v in rows[i].items():
                 if not k.startswith("_"):
