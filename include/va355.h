@@ -262,11 +262,6 @@ typedef struct va_conv_args {
      * streaming 1x1 (pw), which has no A stage, is skipped for these ops.  A fused tail's w2 stays bf16.  Replaces the
      * host-side dequantization into bf16 weights (round 5's w8a16 form), so HBM holds 1 byte per weight. */
     int32_t w8;
-    /* Split-K slice cap (ABI 5): 0 = the library's latency cost model (up to 32 slices per tile, conv2's reduce form);
-     * n > 0 = at most n slices.  Plans whose forwards overlap other forwards (several frames in flight on several
-     * streams: SegNet.plan with lanes off) set a small cap -- there the extra slices' prologues and slab traffic take
-     * device time from the other forwards instead of idle CUs. */
-    int32_t ksmax;
 } va_conv_args;
 
 int va_seg_conv(void* stream, const va_conv_args* a);

@@ -1184,7 +1184,7 @@ int va_abi_struct_sizes(int64_t* out, int32_t n) {
     return k < n ? k : n;
 }
 
-const char* va_version(void) { return "libva355 0.5 gfx950 abi 5 (" __DATE__ ")"; }
+const char* va_version(void) { return "libva355 0.4 gfx950 abi 4 (" __DATE__ ")"; }
 
 }  // extern "C"
 

@@ -3432,7 +3432,7 @@ int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* 
     // slower (profiles/r04/batch1/splitk_sweep.log).  Reduce form: tw = the second launch, tc = the slabs' traffic
     const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f;
     const float tw = red ? 3.0f : 1.0f, tc = red ? 0.02f * tiles * (bm * bn / 16384.0f) : 1.5f;
-    const int cap = red ? 32 : 16, maxks = a.ksmax > 0 && a.ksmax < cap ? a.ksmax : cap, maxb = red ? 512 : 256;
+    const int maxks = red ? 32 : 16, maxb = red ? 512 : 256;
     int best = 1;
     float bt = nk * ts;
     for (int ks = 2; ks <= maxks && ks <= nk / 2 && tiles * ks <= maxb; ++ks) {

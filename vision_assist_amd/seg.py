@@ -34,7 +34,6 @@ C2FB_MIN_TILES = 96  # SegNet._c2fb_tile: the fewest workgroups a tile side may 
 C2FB_CUS = 256       # SegNet._c2fb_tile_bf16: workgroups per round (one per CU)
 C2FB_FIXED = 16_000_000  # SegNet._c2fb_tile_bf16: a tile's fixed latency, in MACs
 SPLITK_WS_BYTES, SPLITK_NCNT = 32 << 20, 128  # per-plan split-K slabs / arrival counters (va_conv_args.ws)
-
 BK = 64  # K padding: the bf16 kernels step K by 64, the f32 ones by 32 (SegNet.bk)
 NPAD = 128
 
@@ -55,8 +54,6 @@ PLANNER_SWITCHES = {
     "VA_LANES": "1",        # 0: no branch-parallel lanes at small batches
     "VA_LANES_MAX_B": "8",  # the largest batch planned with lanes
     "VA_W8": "1",           # 0: w8a16 plans on the host-dequantized bf16 weights (round 5's form) instead of e4m3 bytes
-    "VA_SPLITK_OVERLAP": "8",  # split-K slice cap (va_conv_args.ksmax) of plans without lanes, whose forwards overlap
-                               # others (the C4 shape's six frames in flight); laned plans leave it to the cost model
     "VA_CONV3H": "1",       # (the library's switch, read here too: a fused f32 tail needs conv3h)
     "VA_CONV3Q": "1",       # (likewise: the f32 32-channel tail needs conv3q)
 }
@@ -94,7 +91,6 @@ class ConvArgs(ctypes.Structure):
         ("wcnt", ctypes.c_void_p),
         ("ncnt", ctypes.c_int32),
         ("w8", ctypes.c_int32),
-        ("ksmax", ctypes.c_int32),
     ]
 
 
@@ -656,8 +652,6 @@ class SegNet:
 
         def with_ws(args: ConvArgs) -> ConvArgs:
             args.ws, args.ws_bytes, args.wcnt, args.ncnt = ws.data_ptr(), ws.numel(), wcnt.data_ptr(), wcnt.numel()
-            # a plan without lanes runs beside other forwards (OverlappedPipelines, StreamBatches): fewer slices
-            args.ksmax = 0 if lanes else int(switch("VA_SPLITK_OVERLAP"))
             return args
 
         def new(h, w, c, dtype=None):
