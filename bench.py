@@ -111,6 +111,8 @@ def parse():
     p.add_argument("--dealer-batch", type=int, default=16,
                    help="frames a dealer worker runs as one device batch (up to; what waits in its ring)")
     p.add_argument("--dealer-slots", type=int, default=128, help="ring slots per dealer worker")
+    p.add_argument("--dealer-readers", type=int, default=0,
+                   help="reader threads copying frames into the dealer's rings (0: the calling thread)")
     p.add_argument("--dropin-only", action="store_true",
                    help="print only the dropin measurement's JSON (the dropin extra runs this in a child process)")
     return p.parse_args()
@@ -501,7 +503,8 @@ def dealer_rate(args, dev, frames_n: int = 1024) -> dict:
     frames = [rng.integers(0, 256, (640, 640, 3), dtype=np.uint8) for _ in range(16)]
     with FrameDealer(dropin_worker("yolov8s-seg.pt", dtype="f32", batch=args.dealer_batch, quiet=True,
                                    **regime_kwargs(args.regime, 640)),
-                     [w % ngpu for w in range(G)], 640, 640, slots=args.dealer_slots) as d:
+                     [w % ngpu for w in range(G)], 640, 640, slots=args.dealer_slots,
+                     readers=args.dealer_readers) as d:
         for _ in d.map(frames[i % 16] for i in range(32 * G)):  # warm: plans, first launches, lanes' streams
             pass
         t0 = time.perf_counter()
@@ -509,7 +512,7 @@ def dealer_rate(args, dev, frames_n: int = 1024) -> dict:
         dt = time.perf_counter() - t0
     return {"value": round(frames_n / dt, 2), "unit": "frames/s", "workers": G, "gpus": ngpu, "frames": frames_n,
             "frames_with_answer": answers, "dtype": "f32", "regime": args.regime, "worker_batch": args.dealer_batch,
-            "slots": args.dealer_slots,
+            "slots": args.dealer_slots, "readers": args.dealer_readers,
             "workload": f"one reader dealing host 640x640 frames round-robin to {args.dealer_workers_per_gpu} "
                         "FrameProcessor worker process(es) per GPU (vision_assist_amd.shard.FrameDealer: shared-memory "
                         "frame ring with shared head / tail counters), answers back in frame order; each worker runs "

@@ -1223,6 +1223,7 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 // stored straight to the output.  The ticket form sums a tile's ks x 64 KiB in ONE workgroup once the last slice
 // has arrived (~0.45 us per slice at batch 1) and then runs a 2-6 us LDS epilogue on it
 // (profiles/r06/b1/phases_f32_b1.log); here every CU takes a share.  Mode 0 without a fused tail (conv2_red_ok).
+constexpr int SK_RED_MAX = 32;  // the reduce form's slice cap (conv2_ksplit)
 template <typename RT, typename OutT, int WM, int WN, int TNS>
 __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int ntn, int ks, int nunits) {
     constexpr int NT = 64 * WM * WN, NQ = TNS * 4, BM = 64 * WM, BN = 16 * TNS * WN;
@@ -1235,16 +1236,16 @@ __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int n
     if (m >= a.M || co >= a.Cout) return;
     const float4 bv = *(const float4*)(a.bias + co);  // issued ahead of the slabs: one memory latency, not two
     const f32x4* sl = (const f32x4*)a.ws + ((int64_t)vt * ks * NQ + q) * NT + tid;
-    f32x4 ac = sl[0];
-    for (int o0 = 1; o0 < ks; o0 += 8) {  // eight slabs in flight, added in slice order
-        f32x4 t[8];
+    // every slab load issued before the first add (ks <= SK_RED_MAX: a loop of eight-load rounds waited one memory
+    // latency per round), then added in slice order
+    f32x4 t[SK_RED_MAX];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-            if (o0 + e < ks) t[e] = sl[(int64_t)(o0 + e) * NQ * NT];
+    for (int e = 0; e < SK_RED_MAX; ++e)
+        if (e < ks) t[e] = sl[(int64_t)e * NQ * NT];
+    f32x4 ac = t[0];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-            if (o0 + e < ks) ac += t[e];
-    }
+    for (int e = 1; e < SK_RED_MAX; ++e)
+        if (e < ks) ac += t[e];
     if (sizeof(RT) == 2 && a.w8) {
         const float4 sv = *(const float4*)(a.wscale + co);
         ac = ac * (f32x4){sv.x, sv.y, sv.z, sv.w};
@@ -3432,7 +3433,7 @@ int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* 
     // slower (profiles/r04/batch1/splitk_sweep.log).  Reduce form: tw = the second launch, tc = the slabs' traffic
     const float ts = a.dtype == VA_DTYPE_F32 ? 1.4f : 0.6f;
     const float tw = red ? 3.0f : 1.0f, tc = red ? 0.02f * tiles * (bm * bn / 16384.0f) : 1.5f;
-    const int maxks = red ? 32 : 16, maxb = red ? 512 : 256;
+    const int maxks = red ? SK_RED_MAX : 16, maxb = red ? 512 : 256;
     int best = 1;
     float bt = nk * ts;
     for (int ks = 2; ks <= maxks && ks <= nk / 2 && tiles * ks <= maxb; ++ks) {
