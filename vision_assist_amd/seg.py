@@ -53,49 +53,10 @@ PLANNER_SWITCHES = {
     "VA_FUSE_TAIL": "1",    # 0: no fused 1x1 tails
     "VA_LANES": "1",        # 0: no branch-parallel lanes at small batches
     "VA_LANES_MAX_B": "8",  # the largest batch planned with lanes
-    "VA_LANE_ORDER": "1",   # 0: the laned list enqueued segment by segment instead of the streams round-robin
     "VA_W8": "1",           # 0: w8a16 plans on the host-dequantized bf16 weights (round 5's form) instead of e4m3 bytes
     "VA_CONV3H": "1",       # (the library's switch, read here too: a fused f32 tail needs conv3h)
     "VA_CONV3Q": "1",       # (likewise: the f32 32-channel tail needs conv3q)
 }
-
-
-def interleave_lanes(ops_l, meta_l):
-    """The laned list in host enqueue order: the calling stream's ops (fork / join included) and each lane's
-    taken round-robin, one op each per turn, calling stream first -- instead of a whole lane segment before
-    the calling stream's next op.  Each stream's order is kept, a lane op goes out after the fork that opened
-    its segment, a fork after its lane's earlier ops, a join after all of them: the same dependencies, but
-    va_seg_run's launches no longer leave the critical path (the calling stream) waiting behind a lane's
-    dozen launches (profiles/r06/b1j/: the host's launches set the pace of the batch-1 forward's second half)."""
-    main, lq, fork_at = [], {}, {}
-    for op, mt in zip(ops_l, meta_l):
-        if op.kind in (VA_OP_FORK, VA_OP_JOIN) or op.lane == 0:
-            main.append((op, mt))
-            if op.kind == VA_OP_FORK:
-                fork_at[op.a.N] = len(main) - 1
-        else:
-            lq.setdefault(op.lane, []).append((op, mt, fork_at[op.lane]))
-    out, mi, li = [], 0, {k: 0 for k in lq}
-    total = len(main) + sum(len(v) for v in lq.values())
-    while len(out) < total:
-        moved = False
-        if mi < len(main):
-            op, mt = main[mi]
-            lane = op.a.N if op.kind in (VA_OP_FORK, VA_OP_JOIN) else 0
-            # a join waits for all of its lane's ops, a fork for the lane's ops of earlier segments
-            blocked = lane in lq and li[lane] < len(lq[lane]) and (
-                op.kind == VA_OP_JOIN or lq[lane][li[lane]][2] < mi)
-            if not blocked:
-                out.append((op, mt))
-                mi += 1
-                moved = True
-        for lane, q in lq.items():
-            if li[lane] < len(q) and q[li[lane]][2] < mi:
-                out.append(q[li[lane]][:2])
-                li[lane] += 1
-                moved = True
-        assert moved, "laned list: no op can go out"
-    return [o for o, _ in out], [m for _, m in out]
 
 
 def switch(name: str) -> str:
@@ -915,8 +876,6 @@ class SegNet:
                     take(f"H2.{br}", 0)
             for lane in (1, 2, 3) if split_h2 else (1, 2):
                 sync(VA_OP_JOIN, lane)
-            if switch_on("VA_LANE_ORDER"):
-                return interleave_lanes(out_ops, out_meta)
             return out_ops, out_meta
 
 
