@@ -54,7 +54,7 @@ def stats(path: str, out: str) -> dict:
     return res
 
 
-def agree(trace: str, bench_json: str, out: str, per_fwd: int = 55) -> dict:
+def agree(trace: str, bench_json: str, out: str, per_fwd: int = 58) -> dict:
     rows = []
     with open(trace) as f:
         for row in csv.DictReader(f):
