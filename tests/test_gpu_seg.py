@@ -159,6 +159,38 @@ def test_split_k_reduce_form_bit_identical_to_ticket(dtype, ks, cin, cout, k, st
         assert torch.allclose(r, ref, atol=1e-4, rtol=1e-4), (r - ref).abs().max()
 
 
+@pytest.mark.parametrize("cin,cout,k,stride,H,W,residual,slice_in", [
+    (256, 256, 3, 1, 20, 20, False, 0),   # 3x3 stride 1 (conv3h's shape; split, it runs on conv3t)
+    (128, 256, 3, 2, 40, 40, True, 8),    # stride 2, residual, channel slice
+    (512, 192, 1, 1, 17, 23, False, 0),   # 1x1, ragged pixel and channel tiles
+    (256, 512, 1, 1, 20, 20, True, 0),    # 1x1, four channel tiles, residual
+])
+def test_conv3t_split_k_f32(cin, cout, k, stride, H, W, residual, slice_in, switch):
+    """A batch-1 f32 layer conv2 would split over K runs on conv3t split over K (the default), its slabs in the
+    32 x 32 fragment layout summed by conv2_reduce_kernel: within the f32 bar of torch and bit-identical run to run."""
+    ws = (torch.empty(32 << 20, dtype=torch.uint8, device="cuda"), torch.zeros(128, dtype=torch.int32, device="cuda"))
+    switch("VA_CONV3T", None)
+    got, ref = _run_single_conv("f32", cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1, w3=True)
+    again, _ = _run_single_conv("f32", cin, cout, k, stride, H, W, residual, False, slice_in, ws=ws, B=1, w3=True)
+    assert torch.equal(got, again)
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
+
+
+def test_forward_batch1_conv3t_split_within_f32_bar(switch):
+    """The s-seg f32 batch-1 forward with the split layers on conv3t (default) against conv2's split-K
+    (VA_CONV3T=nosplit): every head output within the f32 rounding of reordered sums (the two forms add the same
+    exact term products in other orders)."""
+    arch, fw, net = _net("f32", "s", seed=5)
+    frames = _frames(1, seed=8)
+    switch("VA_CONV3T", "nosplit")
+    a = _gpu_heads(net, frames)
+    switch("VA_CONV3T", None)
+    b = _gpu_heads(net, frames)
+    for name, x, y in zip(("box", "cls", "coef", "proto"), a, b):
+        err = ((x - y).abs().max() / y.abs().max()).item()
+        assert err < 1e-5, f"{name}: {err}"
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_forward_batch1_split_k_matches_unsplit(dtype, monkeypatch, switch):
     """The batch-1 n-seg forward with split-K (the C2 shape) against the same forward with VA_SPLITK=0: f32 to

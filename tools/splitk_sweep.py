@@ -14,9 +14,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def apply(setting: str) -> None:
-    for k in ("VA_SPLITK", "VA_SPLITK_KS"):
+    for k in ("VA_SPLITK", "VA_SPLITK_KS", "VA_CONV3T"):
         os.environ.pop(k, None)
-    if setting == "ticket":
+    if setting.startswith("env:"):  # env:NAME=VALUE (a library switch)
+        k, v = setting[4:].split("=", 1)
+        os.environ[k] = v
+    elif setting == "ticket":
         os.environ["VA_SPLITK"] = "ticket"
     elif setting == "0":
         os.environ["VA_SPLITK"] = "0"

@@ -46,7 +46,7 @@ void read_switches(VaSwitches& s) {
     e = getenv("VA_CONV3H");
     s.conv3h = !e ? 1 : e[0] == '0' ? 0 : 1;
     e = getenv("VA_CONV3T");
-    s.conv3t = !e ? 1 : e[0] == '0' ? 0 : 1;
+    s.conv3t = !e ? 2 : e[0] == '0' ? 0 : strcmp(e, "nosplit") == 0 ? 1 : 2;
     e = getenv("VA_CONV3Q");
     s.conv3q = !e ? 1 : e[0] == '0' ? 0 : strcmp(e, "static") == 0 ? 2 : 1;
     e = getenv("VA_SPLITK");

@@ -1224,15 +1224,19 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
 // has arrived (~0.45 us per slice at batch 1) and then runs a 2-6 us LDS epilogue on it
 // (profiles/r06/b1/phases_f32_b1.log); here every CU takes a share.  Mode 0 without a fused tail (conv2_red_ok).
 constexpr int SK_RED_MAX = 32;  // the reduce form's slice cap (conv2_ksplit)
-template <typename RT, typename OutT, int WM, int WN, int TNS>
+// FRAG32: conv3t's slabs (v_mfma_f32_32x32x16 accumulators, conv_epilogue32_fill's layout: unit q = 8 ib + 4 jb + c
+// of lane l holds pixel wm 64 + 32 jb + l % 32, channels wn 16 TNS + 32 ib + 8 c + 4 (l / 32) ..)
+template <typename RT, typename OutT, int WM, int WN, int TNS, bool FRAG32 = false>
 __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int ntn, int ks, int nunits) {
     constexpr int NT = 64 * WM * WN, NQ = TNS * 4, BM = 64 * WM, BN = 16 * TNS * WN;
     const int u = blockIdx.x * 256 + threadIdx.x;
     if (u >= nunits) return;
     const int tid = u % NT, q = (u / NT) % NQ, vt = u / (NT * NQ);
     const int wid = tid >> 6, lane = tid & 63, wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
-    const int m = (vt / ntn) * BM + wm * 64 + 16 * (q % 4) + fr;            // conv_epilogue's pixel of the unit
-    const int co = (vt % ntn) * BN + wn * 16 * TNS + 16 * (q / 4) + 4 * fq;  // and its first channel
+    // conv_epilogue's (conv_epilogue32_fill's) pixel of the unit and its first channel
+    const int m = (vt / ntn) * BM + wm * 64 + (FRAG32 ? 32 * ((q >> 2) & 1) + (lane & 31) : 16 * (q % 4) + fr);
+    const int co = (vt % ntn) * BN + wn * 16 * TNS +
+                   (FRAG32 ? 32 * (q >> 3) + 8 * (q & 3) + 4 * (lane >> 5) : 16 * (q / 4) + 4 * fq);
     if (m >= a.M || co >= a.Cout) return;
     const float4 bv = *(const float4*)(a.bias + co);  // issued ahead of the slabs: one memory latency, not two
     const f32x4* sl = (const f32x4*)a.ws + ((int64_t)vt * ks * NQ + q) * NT + tid;
@@ -1313,7 +1317,7 @@ __device__ __forceinline__ void t3_waitvm() {
 // WM = 2, NSTAGE = 2: 128-pixel tiles, 4 waves, two workgroups per CU, A one K-step ahead.  B registers always
 // two K-steps ahead.
 template <int WM, int NSTAGE, typename OutT>
-__global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int ntn, int ntiles) {
+__global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int ntn, int ntiles, int ksplit, int kper) {
     using Cfg = T3Cfg<WM, NSTAGE>;
     extern __shared__ __align__(16) unsigned char smt[];
     constexpr int BM = Cfg::BM, BN = T3_BN, NT = Cfg::NT, WN = 2, TNS = 4, NA = Cfg::NA;
@@ -1322,6 +1326,12 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         const int nx = 8, q = ntiles / nx, r = ntiles % nx, xcd = bid % nx, j = bid / nx;
         bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
     }
+    // split K (ksplit > 1, mode 0, batch-1 shapes): slice sk runs K-steps [sk kper, ..) and stores its partial tile
+    // as a slab for conv2_reduce_kernel (conv2's reduce form, the 32 x 32 fragment layout); the slices of a tile are
+    // consecutive virtual blocks
+    const int sk = bid % ksplit;
+    bid /= ksplit;
+    const int vt = bid;
     const int cls = a.mode == 2 ? (bid & 3) : 0;
     if (a.mode == 2) bid >>= 2;
     const int tm = bid / ntn, tn = bid % ntn;
@@ -1333,6 +1343,9 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     const int pad_y = a.mode == 2 ? 1 - (cls >> 1) : a.pad, pad_x = a.mode == 2 ? 1 - (cls & 1) : a.pad;
     auto stA = [&](int s) { return smt + s * Cfg::STAGE; };
     auto stB = [&](int s) { return smt + s * Cfg::STAGE + BN * T3_ROW; };
+    // this slice's K-steps [kb, kb + nk) of the nk_all
+    const int nk_all = a.Kpad / T3_KS, kb = sk * kper;
+    const int nk = (nk_all - kb < kper ? nk_all - kb : kper);
 
     // ---- B staging unit of this thread: row br (pixel m0 + br), 8-channel group bg of each K-step; lanes 0-7 of
     // a wave take 8 consecutive rows of one group (conflict-free 16-byte plane stores)
@@ -1365,15 +1378,21 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         const int c = (lane & 7) ^ (row & 7) ^ ((row >> 4) & 1);
         aoff[j] = c < 6 ? ((n0 + row) * a.Kpad * 3 + 8 * c) * 2 : T3_OOR;
     }
-    auto dmaA = [&](int k, int s, bool live) {  // K-step k (channels 16 k ..) into stage s; !live: zeros
+    auto dmaA = [&](int k, int s, bool live) {  // this slice's K-step k (channels 16 (kb + k) ..) into stage s
         unsigned char* base = stA(s);
-        const int soff = live ? k * 96 : T3_OOR;
+        const int soff = live ? (kb + k) * 96 : T3_OOR;
 #pragma unroll
         for (int j = 0; j < NA; ++j)
             t3_dma16(WA, wa_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
     };
     // K-step -> (tap, channel) of the im2col row, advanced per load (uniform)
-    int ld_ky = 0, ld_kx = 0, ld_c = 0;
+    int ld_ky, ld_kx, ld_c;
+    {
+        const int tap = kb * T3_KS / a.Cin;
+        ld_c = kb * T3_KS - tap * a.Cin;
+        ld_ky = tap / a.kw;
+        ld_kx = tap - ld_ky * a.kw;
+    }
     u32x4 rb[2][2];  // B registers of two K-steps in flight
     // unconditional: out-of-range taps and the loads past the last K-step read the zero page, so the loop body
     // has no branches and the compiler's own waits on rb see one straight-line load / use pattern
@@ -1405,7 +1424,6 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
-    const int nk = a.Kpad / T3_KS;
     // prologue: A of steps 0 .. NSTAGE - 2 in their stages, B of steps 0 and 1 in registers; step 0 staged
 #pragma unroll
     for (int k = 0; k < NSTAGE - 1; ++k) dmaA(k, k, k < nk);
@@ -1468,6 +1486,17 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
     }
     if (k < nk) step(k, std::integral_constant<int, 0>{});
     t3_waitvm<0>();  // the zero-page DMAs past the last step land before the epilogue reuses the LDS
+    if (ksplit > 1) {  // the slab: unit q = 8 ib + 4 jb + c holds acc[ib][jb] items 4 c .. 4 c + 3
+        const int64_t sbase = (int64_t)vt * ksplit * 16 * NT;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const f32x16& v = acc[q >> 3][(q >> 2) & 1];
+            const int c = q & 3;
+            sk_store16(a.ws, a.ws_bytes, (int)((sbase + ((int64_t)sk * 16 + q) * NT + tid) * 16),
+                       (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]});
+        }
+        return;
+    }
     __syncthreads();
 
     auto orow = [&](int pl) -> int64_t {
@@ -3596,9 +3625,17 @@ int f32_split() { return va_sw().f32_split; }
 // VA_CONV3T=0 keeps the wide f32 layers on conv2's three-term form (A/B timing, va_switch.h)
 bool conv3t_off() { return va_sw().conv3t == 0; }
 
+// the batch-1 layers conv2 would split over K run on conv3t, split over K as well (its slices' slabs summed by
+// conv2_reduce_kernel's 32 x 32 form): the s-seg f32 batch-1 forward 885.7 -> 872.0 us, the 3x3s with K >= 1152
+// 9-12 % faster each, the rest within 2 % (profiles/r06/c3s/); VA_CONV3T=nosplit keeps them on conv2 (va_switch.h)
+bool conv3t_split_mode() { return va_sw().conv3t == 2; }
+
 // conv3t (three-plane f32 kernel): pre-split weights, Cin a multiple of its 16-channel K-step, wide tiles
 bool use_conv3t(const va_conv_args& a) {
     if (!a.w3 || conv3t_off()) return false;
+    if (conv3t_split_mode() && a.mode == 0 && conv2_red_ok<float>(a))
+        return a.Cin % T3_KS == 0 && a.K == a.kh * a.kw * a.Cin && a.Kpad == a.K && a.Kpad % 32 == 0 &&
+               a.Npad % T3_BN == 0 && a.Cout > 64 && a.ldx % 4 == 0 && ((uintptr_t)a.x & 15) == 0 && !a.xu && !a.w2;
     // a layer conv2 would split over K (batch-1 shapes) stays on conv2: on the three-plane kernels instead the batch-1
     // f32 s-seg forward took 1.77 ms (stride-1 3x3s on conv3h) / 2.08 ms (every eligible layer) against 1.29
     // (profiles/r04/batch1/small_ab.log)
@@ -3610,8 +3647,9 @@ bool use_conv3t(const va_conv_args& a) {
 }
 
 template <int WM, int NSTAGE, typename OutT>
-hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
+hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st, int ks = 1, int kper = 0) {
     using Cfg = T3Cfg<WM, NSTAGE>;
+    if (kper <= 0) kper = a.Kpad / T3_KS;
     static DevFlag attr;
     if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv3t_kernel<WM, NSTAGE, OutT>,
@@ -3621,8 +3659,14 @@ hipError_t launch_conv3t_v(const va_conv_args& a, hipStream_t st) {
     }
     const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.Cout + T3_BN - 1) / T3_BN;
     const int ntiles = ntm * ntn * (a.mode == 2 ? 4 : 1);
-    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT>), dim3(ntiles), dim3(Cfg::NT), Cfg::LDS, st, a, ntn,
-                       ntiles);
+    hipLaunchKernelGGL((conv3t_kernel<WM, NSTAGE, OutT>), dim3(ntiles * ks), dim3(Cfg::NT), Cfg::LDS, st, a, ntn,
+                       ntiles * ks, ks, kper);
+    if (ks > 1) {
+        static_assert(Cfg::NT == 256, "the reduce form's 32 x 32 layout assumes conv3t's 2 x 2 waves");
+        const int nunits = ntiles * 16 * Cfg::NT;
+        hipLaunchKernelGGL((conv2_reduce_kernel<float, OutT, 2, 2, 4, true>), dim3((nunits + 255) / 256), dim3(256), 0,
+                           st, a, ntn, ks, nunits);
+    }
     return hipGetLastError();
 }
 
@@ -3684,6 +3728,13 @@ bool use_conv3h_narrow(const va_conv_args& a) {
 
 template <typename OutT>
 hipError_t launch_conv3t(const va_conv_args& a, hipStream_t st) {
+    if (conv3t_split_mode() && a.mode == 0 && conv2_red_ok<float>(a)) {
+        // the slice count from conv2's model in 32-channel K-steps, two of conv3t's per step
+        int kper32;
+        const int tiles = ((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+        const int ks = conv2_ksplit(a, tiles, a.Kpad / 32, 128, 128, &kper32, true);
+        if (ks > 1) return launch_conv3t_v<2, 2, OutT>(a, st, ks, 2 * kper32);
+    }
     if (use_conv3h(a)) return a.mode == 2 ? launch_conv3h_v<2, 2, 4, OutT>(a, st) : launch_conv3h_v<3, 3, 4, OutT>(a, st);
     return launch_conv3t_v<2, 2, OutT>(a, st);
 }

@@ -7,7 +7,9 @@
 struct VaSwitches {
     int f32_split;   // VA_F32_SPLIT: bf16 term products per f32 product, 6 (default) or 9; 0 = the f32 MFMA
     int conv3h;      // VA_CONV3H=0: the stride-1 multi-tap f32 layers on conv3t instead of the halo-staged kernel
-    int conv3t;      // VA_CONV3T=0: the wide f32 layers on conv2's three-term form
+    int conv3t;      // VA_CONV3T=0: the wide f32 layers on conv2's three-term form; default (2): conv3t takes the
+                     // batch-1 layers conv2 would split over K too, split over K itself; "nosplit" (1): those stay on
+                     // conv2's split-K
     int conv3q;      // VA_CONV3Q=0: the 32 -> 32 stride-1 3x3 f32 layers on conv2's three-term form instead of conv3q;
                      // 2 = "static": the persistent kernels (conv3q, the f32 and bf16 stems, the bf16 C2f) on
                      // fz::tile's static schedule instead of the plan's work counter (va_fuse.h fz::wq_claim)
