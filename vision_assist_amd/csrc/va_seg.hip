@@ -3448,11 +3448,12 @@ hipError_t launch_conv(const va_conv_args& a, hipStream_t st) {
 // Split-K policy (va_conv_args.ws): a launch of fewer than 128 tiles leaves most of the 256 CUs idle while each
 // tile walks its whole K loop, one LDS-DMA round trip + barrier per K-step -- the batch-1 forward's cost.  Cost
 // model per tile (us, measured at batch 1, profiles/r03/splitk/): ts per K-step (f32 three-term 1.4, bf16 0.6);
-// splitting into ks slices costs a slab write + ticket (1.0) and ~1.5 per slice of the combine (one workgroup reads
-// ks x 64 KiB).  Pick the ks <= 16
-// with tiles x ks <= 256 that minimises ceil(nk / ks) ts + 1.0 + 1.5 ks, if it beats the unsplit nk ts by 15 %.
-// VA_SPLITK=0 disables it (A/B timing, va_switch.h).  Returns the slice count (1 = no split); *kper = K-steps
-// per slice (every slice non-empty).
+// splitting into ks slices costs, in the ticket form (red = false), a slab write + ticket (1.0) and ~1.5 per slice of
+// the combine (one workgroup reads ks x 64 KiB): ks <= 16, tiles x ks <= 256; in the reduce form (red, the default:
+// conv2_reduce_kernel) the second launch (3.0) and the slabs' traffic (0.02 per 128 x 128 tile-slice): ks <= 32,
+// tiles x ks <= 512.  Pick the ks minimising ceil(nk / ks) ts + tw + tc ks, if it beats the unsplit nk ts by 15 %
+// (VA_SPLITK_KS forces a count for sweeps).  VA_SPLITK=0 disables it (A/B timing, va_switch.h).  Returns the slice
+// count (1 = no split); *kper = K-steps per slice (every slice non-empty).
 int conv2_ksplit(const va_conv_args& a, int tiles, int nk, int bm, int bn, int* kper, bool red) {
     *kper = nk;
     if (!va_sw().splitk || !a.ws || tiles >= 128 || nk < 4) return 1;
