@@ -16,5 +16,5 @@ for r in $(seq 1 "$ROUNDS"); do
 done
 i=0; for e in "$@"; do i=$((i + 1)); echo "alt$i = $e"; done
 for f in "$OUT"/*.json; do
-  echo "$f $(python -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);c=d['extras']['bf16'];print(c['value'],c['roofline']['frac'])")"
+  echo "$f $(python -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);c=d['extras']['bf16'];print(c['value'],c.get('ms_per_step'))")"
 done
