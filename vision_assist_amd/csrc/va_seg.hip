@@ -1158,15 +1158,18 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             // epilogue (a second slab in flight under the adds would cost 64 VGPRs: past 256, one wave per SIMD)
             constexpr int NQ = TNS * 4;
             const int64_t sbase = (int64_t)vt * ksplit * NQ * NT;
+            if (kred) {  // plain stores: the reduce kernel reads them after the launch boundary, from this XCD's L2
 #pragma unroll
-            for (int q = 0; q < NQ; ++q)
-                sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
-            if (kred) {
+                for (int q = 0; q < NQ; ++q)
+                    ((f32x4*)a.ws)[sbase + ((int64_t)sk * NQ + q) * NT + tid] = acc[q / 4][q % 4];
                 C2S(3, __builtin_amdgcn_s_memtime());
                 C2S(5, __builtin_amdgcn_s_memtime());
                 C2S(7, __builtin_amdgcn_s_memrealtime());
                 return;
             }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             int* last_s = (int*)smem;  // the stage buffers are free: the K-loop ended on a barrier
@@ -1229,7 +1232,14 @@ constexpr int SK_RED_MAX = 32;  // the reduce form's slice cap (conv2_ksplit)
 template <typename RT, typename OutT, int WM, int WN, int TNS, bool FRAG32 = false>
 __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int ntn, int ks, int nunits) {
     constexpr int NT = 64 * WM * WN, NQ = TNS * 4, BM = 64 * WM, BN = 16 * TNS * WN;
-    const int u = blockIdx.x * 256 + threadIdx.x;
+    // the GEMM's XCD-aware order: consecutive blocks on one XCD, so a tile's reducers run on the XCD whose L2 holds
+    // its slices' slabs
+    int bid = blockIdx.x;
+    {
+        const int nb = gridDim.x, nx = 8, q = nb / nx, r = nb % nx, xcd = bid % nx, j = bid / nx;
+        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+    }
+    const int u = bid * 256 + threadIdx.x;
     if (u >= nunits) return;
     const int tid = u % NT, q = (u / NT) % NQ, vt = u / (NT * NQ);
     const int wid = tid >> 6, lane = tid & 63, wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
@@ -1492,8 +1502,8 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         for (int q = 0; q < 16; ++q) {
             const f32x16& v = acc[q >> 3][(q >> 2) & 1];
             const int c = q & 3;
-            sk_store16(a.ws, a.ws_bytes, (int)((sbase + ((int64_t)sk * 16 + q) * NT + tid) * 16),
-                       (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]});
+            ((f32x4*)a.ws)[sbase + ((int64_t)sk * 16 + q) * NT + tid] = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2],
+                                                                               v[4 * c + 3]};
         }
         return;
     }
