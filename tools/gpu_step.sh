@@ -1,9 +1,5 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/xr
-L=$PWD/vision_assist_amd
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_seg.py -k "split_k or conv3t_split" > gpurun_out/xr/tests.log 2>&1 || exit $?
-for r in 1 2 3; do
-  timeout -k 10 200 python -u tools/splitk_sweep.py --settings default --rounds 4 > gpurun_out/xr/new_$r.log 2>&1 || exit $?
-  VA355_LIB=$L/libva355_prev.so timeout -k 10 200 python -u tools/splitk_sweep.py --settings default --rounds 4 > gpurun_out/xr/prev_$r.log 2>&1 || exit $?
-done
-grep -h '^{' gpurun_out/xr/new_*.log gpurun_out/xr/prev_*.log > gpurun_out/xr/summary.txt
+mkdir -p gpurun_out/w3t
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/w3t/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > gpurun_out/w3t/fetch.log 2>&1 || exit $?
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/w3t/write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > gpurun_out/w3t/write.log 2>&1 || exit $?
+PASSES="fetch write" BATCH=256 timeout -k 10 400 bash tools/pmc_conv.sh w3t/b256 > gpurun_out/w3t/b256.log 2>&1 || exit $?

@@ -1158,18 +1158,15 @@ __global__ __launch_bounds__(64 * WM* WN) void conv2_kernel(va_conv_args a, int 
             // epilogue (a second slab in flight under the adds would cost 64 VGPRs: past 256, one wave per SIMD)
             constexpr int NQ = TNS * 4;
             const int64_t sbase = (int64_t)vt * ksplit * NQ * NT;
-            if (kred) {  // plain stores: the reduce kernel reads them after the launch boundary, from this XCD's L2
 #pragma unroll
-                for (int q = 0; q < NQ; ++q)
-                    ((f32x4*)a.ws)[sbase + ((int64_t)sk * NQ + q) * NT + tid] = acc[q / 4][q % 4];
+            for (int q = 0; q < NQ; ++q)
+                sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
+            if (kred) {
                 C2S(3, __builtin_amdgcn_s_memtime());
                 C2S(5, __builtin_amdgcn_s_memtime());
                 C2S(7, __builtin_amdgcn_s_memrealtime());
                 return;
             }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-                sk_store16(a.ws, a.ws_bytes, (int)(((sbase + ((int64_t)sk * NQ + q) * NT) + tid) * 16), acc[q / 4][q % 4]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             int* last_s = (int*)smem;  // the stage buffers are free: the K-loop ended on a barrier
@@ -1232,14 +1229,7 @@ constexpr int SK_RED_MAX = 32;  // the reduce form's slice cap (conv2_ksplit)
 template <typename RT, typename OutT, int WM, int WN, int TNS, bool FRAG32 = false>
 __global__ __launch_bounds__(256) void conv2_reduce_kernel(va_conv_args a, int ntn, int ks, int nunits) {
     constexpr int NT = 64 * WM * WN, NQ = TNS * 4, BM = 64 * WM, BN = 16 * TNS * WN;
-    // the GEMM's XCD-aware order: consecutive blocks on one XCD, so a tile's reducers run on the XCD whose L2 holds
-    // its slices' slabs
-    int bid = blockIdx.x;
-    {
-        const int nb = gridDim.x, nx = 8, q = nb / nx, r = nb % nx, xcd = bid % nx, j = bid / nx;
-        bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
-    }
-    const int u = bid * 256 + threadIdx.x;
+    const int u = blockIdx.x * 256 + threadIdx.x;
     if (u >= nunits) return;
     const int tid = u % NT, q = (u / NT) % NQ, vt = u / (NT * NQ);
     const int wid = tid >> 6, lane = tid & 63, wm = wid / WN, wn = wid % WN, fr = lane & 15, fq = lane >> 4;
@@ -1395,11 +1385,12 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         for (int j = 0; j < NA; ++j)
             t3_dma16(WA, wa_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
     };
-    // K-step -> (tap, channel) of the im2col row, advanced per load (uniform)
+    // K-step -> (16-channel chunk, tap) of the im2col row, chunk-major as the w3 runs (seg.py w3_rows: a chunk's taps
+    // in a row, so its input footprint stays in L2 across them), advanced per load (uniform)
     int ld_ky, ld_kx, ld_c;
     {
-        const int tap = kb * T3_KS / a.Cin;
-        ld_c = kb * T3_KS - tap * a.Cin;
+        const int taps = a.kh * a.kw, ch = kb / taps, tap = kb - ch * taps;
+        ld_c = ch * T3_KS;
         ld_ky = tap / a.kw;
         ld_kx = tap - ld_ky * a.kw;
     }
@@ -1412,12 +1403,11 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
         rb[slot][0] = *(const u32x4*)p;
         rb[slot][1] = *(const u32x4*)(p + 4);
-        ld_c += T3_KS;
-        if (ld_c == a.Cin) {
-            ld_c = 0;
-            if (++ld_kx == a.kw) {
-                ld_kx = 0;
-                ++ld_ky;
+        if (++ld_kx == a.kw) {
+            ld_kx = 0;
+            if (++ld_ky == a.kh) {
+                ld_ky = 0;
+                ld_c += T3_KS;
             }
         }
     };
@@ -1502,8 +1492,8 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         for (int q = 0; q < 16; ++q) {
             const f32x16& v = acc[q >> 3][(q >> 2) & 1];
             const int c = q & 3;
-            ((f32x4*)a.ws)[sbase + ((int64_t)sk * 16 + q) * NT + tid] = (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2],
-                                                                               v[4 * c + 3]};
+            sk_store16(a.ws, a.ws_bytes, (int)((sbase + ((int64_t)sk * 16 + q) * NT + tid) * 16),
+                       (f32x4){v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]});
         }
         return;
     }
@@ -1624,7 +1614,7 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
         const int row = o / T3H_ROW, c = ((o - row * T3H_ROW) >> 4) ^ ((row >> 3) & 1);
         aoff[j] = ((n0 + row) * a.Kpad * 3 + 8 * c) * 2;
     }
-    // stage s <- the weights of taps TPS t .. of chunk c (kl_h = tap * nch + chunk, or -1: zeros); a piece's tap
+    // stage s <- the weights of taps TPS t .. of chunk c (kl_h = chunk * T + tap, or -1: zeros); a piece's tap
     // block is wave-uniform, so the per-tap source offset is a scalar select
     auto dmaA = [&](int kl0, int kl1, int s) {
         unsigned char* base = stA(s);
@@ -1638,8 +1628,8 @@ __global__ __launch_bounds__(T3H_NT) void conv3h_kernel(va_conv_args a, int ntn,
             t3_dma16(WA, wa_bytes, real ? base + P * 1024 : smh + Cfg::SINK, aoff[j], real ? soff : OOR);
         }
     };
-    // the kl of tap slot h of step t of chunk c (-1 past the taps or the chunks)
-    auto klof = [&](int c, int t, int h) { return (c < nch && TPS * t + h < T) ? (TPS * t + h) * nch + c : -1; };
+    // the w3 run of tap slot h of step t of chunk c (chunk-major, seg.py w3_rows; -1 past the taps or the chunks)
+    auto klof = [&](int c, int t, int h) { return (c < nch && TPS * t + h < T) ? c * T + TPS * t + h : -1; };
 
     // ---- halo units: u = tid + 256 j -> halo pixel u >> 1 (row hy, column hx), channels 8 (u & 1) .. of a chunk
     const void* zpage = (const void*)g_zero_page;

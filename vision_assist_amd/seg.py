@@ -155,7 +155,7 @@ def w8_order(q: torch.Tensor, inverse: bool = False) -> torch.Tensor:
 def split3_bf16(w: torch.Tensor) -> torch.Tensor:
     """f32 [..., K] (K % 8 == 0) -> bf16 [..., K / 8, 3, 8]: per 8-element group the round-to-nearest bf16 h of each
     value, then m = bf16(x - h), then l = bf16(x - h - m) -- x == h + m + l exactly (both subtractions are exact in
-    f32, l has at most 8 significant bits; tests/test_split_cpu.py), the layout conv3t_kernel stages."""
+    f32, l has at most 8 significant bits; tests/test_split_cpu.py), the planes conv3t_kernel / conv3h_kernel stage (w3_rows orders their K)."""
     w = w.float()
     h = w.to(torch.bfloat16)
     r = w - h.float()
@@ -163,6 +163,17 @@ def split3_bf16(w: torch.Tensor) -> torch.Tensor:
     lo = (r - m.float()).to(torch.bfloat16)
     g = w.shape[:-1] + (w.shape[-1] // 8, 8)
     return torch.stack([h.reshape(g), m.reshape(g), lo.reshape(g)], -2).contiguous()
+
+
+def w3_rows(w: torch.Tensor, taps: int, cin: int) -> torch.Tensor:
+    """The pre-split planes' K order (va_conv_args.w3): f32 rows [..., K = taps x cin] (K = tap cin + c, the im2col
+    order) re-ordered chunk-major -- 16-channel chunk, then tap, then channel (K' = (c // 16) taps 16 + 16 tap + c % 16)
+    -- and split (split3_bf16): a K-step's 96-byte run is (chunk, tap), so conv3t walks all taps of a chunk in a row
+    (the chunk's input footprint stays in L2 across its taps; tap-major, a stride-2 layer re-read its input from HBM)
+    and conv3h's per-chunk tap loop reads consecutive runs."""
+    lead = w.shape[:-1]
+    w = w.float().reshape(*lead, taps, cin // 16, 16).transpose(-3, -2).reshape(*lead, taps * cin)
+    return split3_bf16(w)
 
 
 class Slice:
@@ -541,7 +552,7 @@ class SegNet:
         p = Packed(wm.to(self.device, self.tdtype).contiguous(),
                    bt.float().reshape(-1).to(self.device).contiguous(), ci, o, 2, K, Kpad, Npad)
         if self.store == "f32" and ci % 16 == 0 and K == Kpad:
-            p.w3 = split3_bf16(p.w)
+            p.w3 = w3_rows(p.w, 4, ci)
         return p
 
     def _fold_rows(self, folded: dict, wfull: torch.Tensor | None = None) -> torch.Tensor:
@@ -615,7 +626,7 @@ class SegNet:
         p = Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
                    Kpad, Npad)
         if self.store == "f32" and cin_p % 16 == 0 and K == Kpad:
-            p.w3 = split3_bf16(p.w)
+            p.w3 = w3_rows(p.w, kh * kw, cin_p)
         return p
 
     # ------------------------------------------------------------------ planning
