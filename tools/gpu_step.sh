@@ -1,5 +1,5 @@
 export TMPDIR=/tmp
-mkdir -p gpurun_out/w3t
-timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/w3t/fetch -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > gpurun_out/w3t/fetch.log 2>&1 || exit $?
-timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/w3t/write -o run -- python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-prof --no-ingest --extras none > gpurun_out/w3t/write.log 2>&1 || exit $?
-PASSES="fetch write" BATCH=256 timeout -k 10 400 bash tools/pmc_conv.sh w3t/b256 > gpurun_out/w3t/b256.log 2>&1 || exit $?
+mkdir -p gpurun_out/r6f5
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6f5/smoke.log 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py > gpurun_out/r6f5/bench.json 2> gpurun_out/r6f5/bench.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r6f5/prof -o run -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --extras none > gpurun_out/r6f5/rocprof_stats.log 2>&1 || exit $?
