@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the C4 extra (bench.py --extras c4; headline steps cut to 3): interleaved runs of the default and of
-# each environment setting given.   tools/ab_c4.sh <tag> <rounds> "VAR=V [VAR=V..]" ...
+# each setting given -- environment assignments, optionally followed by ':: <extra bench.py arguments>'.
+#   tools/ab_c4.sh <tag> <rounds> "VAR=V [VAR=V..]" "GPU_MAX_HW_QUEUES=8 :: --c4-seg-streams 4" ...
 set -e -o pipefail
 TAG=$1; ROUNDS=$2; shift 2
 OUT=gpurun_out/$TAG
@@ -11,7 +12,9 @@ for r in $(seq 1 "$ROUNDS"); do
   i=0
   for e in "$@"; do
     i=$((i + 1))
-    env $e timeout -k 10 200 $B > "$OUT/alt${i}_$r.json" 2> "$OUT/alt${i}_$r.err"
+    ev=${e%%::*}; ar=""
+    [[ "$e" == *::* ]] && ar=${e#*::}
+    env $ev timeout -k 10 200 $B $ar > "$OUT/alt${i}_$r.json" 2> "$OUT/alt${i}_$r.err"
   done
 done
 i=0; for e in "$@"; do i=$((i + 1)); echo "alt$i = $e"; done
