@@ -234,10 +234,11 @@ typedef struct va_conv_args {
     float rscale;
     /* VA_DTYPE_F32 only: the weights pre-split into their three exact bf16 terms h, m, l (x = h + m + l, each the
      * round-to-nearest bf16 of what remains), [Npad][Kpad / 8][3][8] -- per 8-channel K group the 8 h, then the
-     * 8 m, then the 8 l -- with K ordered chunk-major: 16-channel chunk, then tap, then channel (K' = (c / 16) taps 16
-     * + 16 tap + c % 16; the 96-byte run of a (chunk, tap) is one K-step; seg.py w3_rows).  When set (and Cin % 16 ==
-     * 0, Npad % 128 == 0, K == Kpad, mode 0 or 2) the conv runs on the three-plane kernels (va_seg.hip conv3t_kernel /
-     * conv3h_kernel); NULL keeps conv2's in-loop split. */
+     * 8 m, then the 8 l -- with K ordered group-major: G-channel group, then tap, then channel (K' = (c / G) taps G +
+     * G tap + c % G; G = 32 when stride == 2, kh kw > 1 and Cin % 32 == 0, else 16; a K-step is one 96-byte run of 16
+     * channels; seg.py w3_rows / w3_group).  When set (and Cin % 16 == 0, Npad % 128 == 0, K == Kpad, mode 0 or 2) the
+     * conv runs on the three-plane kernels (va_seg.hip conv3t_kernel / conv3h_kernel); NULL keeps conv2's in-loop
+     * split. */
     const void* w3;
     /* Optional split-K workspace (any dtype; conv2's LDS-DMA form, mode 0 / 2): when ws != NULL and the layer has
      * too few output tiles to fill the chip (a batch-1 forward's 40 x 40 and 20 x 20 layers), the dispatcher may

@@ -43,7 +43,7 @@ def _run_single_conv(dtype, cin, cout, k, stride, H, W, residual=False, deconv=F
     net.device = torch.device("cuda")
     from vision_assist_amd import _lib
     net.lib = _lib.load()
-    p = net._pack(w, b, deconv=deconv)
+    p = net._pack(w, b, deconv=deconv, stride=stride)
     ld_in = cin + slice_in + 8
     xin = torch.zeros(B, H, W, ld_in, dtype=net.tdtype, device="cuda")
     xin[..., slice_in:slice_in + cin] = x.permute(0, 2, 3, 1).to(net.tdtype).cuda()

@@ -1385,12 +1385,16 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         for (int j = 0; j < NA; ++j)
             t3_dma16(WA, wa_bytes, base + (wid + 2 * WM * j) * 1024, aoff[j], soff);
     };
-    // K-step -> (16-channel chunk, tap) of the im2col row, chunk-major as the w3 runs (seg.py w3_rows: a chunk's taps
-    // in a row, so its input footprint stays in L2 across them), advanced per load (uniform)
-    int ld_ky, ld_kx, ld_c;
+    // K-step -> (channel group, tap, 16-channel half) of the im2col row, group-major as the w3 runs (seg.py w3_rows: a
+    // group's taps in a row, so its input footprint stays in L2 across them; gh = 2 sixteen-channel K-steps per (group,
+    // tap) on the stride-2 3x3s -- seg.py w3_group's rule -- so both 64-byte halves of a pixel's 128-byte line are read
+    // in consecutive K-steps), advanced per load (uniform)
+    const int gh = a.stride == 2 && a.kh * a.kw > 1 && a.Cin % 32 == 0 ? 2 : 1;
+    int ld_ky, ld_kx, ld_c, ld_h;
     {
-        const int taps = a.kh * a.kw, ch = kb / taps, tap = kb - ch * taps;
-        ld_c = ch * T3_KS;
+        const int per = a.kh * a.kw * gh, grp = kb / per, r = kb - grp * per, tap = r / gh;
+        ld_h = r - tap * gh;
+        ld_c = (grp * gh + ld_h) * T3_KS;
         ld_ky = tap / a.kw;
         ld_kx = tap - ld_ky * a.kw;
     }
@@ -1403,11 +1407,17 @@ __global__ __launch_bounds__(128 * WM) void conv3t_kernel(va_conv_args a, int nt
         const float* p = ok ? X + (b_base + (int64_t)hi * a.W + wi) * a.ldx + ld_c + 8 * bg : (const float*)zpage;
         rb[slot][0] = *(const u32x4*)p;
         rb[slot][1] = *(const u32x4*)(p + 4);
-        if (++ld_kx == a.kw) {
-            ld_kx = 0;
-            if (++ld_ky == a.kh) {
-                ld_ky = 0;
-                ld_c += T3_KS;
+        if (++ld_h < gh) {
+            ld_c += T3_KS;
+        } else {
+            ld_h = 0;
+            ld_c -= (gh - 1) * T3_KS;
+            if (++ld_kx == a.kw) {
+                ld_kx = 0;
+                if (++ld_ky == a.kh) {
+                    ld_ky = 0;
+                    ld_c += gh * T3_KS;
+                }
             }
         }
     };

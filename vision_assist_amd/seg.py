@@ -165,14 +165,21 @@ def split3_bf16(w: torch.Tensor) -> torch.Tensor:
     return torch.stack([h.reshape(g), m.reshape(g), lo.reshape(g)], -2).contiguous()
 
 
-def w3_rows(w: torch.Tensor, taps: int, cin: int) -> torch.Tensor:
+def w3_group(stride: int, taps: int, cin: int) -> int:
+    """Input channels per K group of a layer's w3 planes (w3_rows): 32 for the stride-2 multi-tap convs with Cin % 32
+    == 0 (conv3t then reads both 64-byte halves of an input pixel's 128-byte line in consecutive K-steps), else 16.
+    va_seg.hip conv3t_kernel applies the same rule to the layer's va_conv_args."""
+    return 32 if stride == 2 and taps > 1 and cin % 32 == 0 else 16
+
+
+def w3_rows(w: torch.Tensor, taps: int, cin: int, g: int = 16) -> torch.Tensor:
     """The pre-split planes' K order (va_conv_args.w3): f32 rows [..., K = taps x cin] (K = tap cin + c, the im2col
-    order) re-ordered chunk-major -- 16-channel chunk, then tap, then channel (K' = (c // 16) taps 16 + 16 tap + c % 16)
-    -- and split (split3_bf16): a K-step's 96-byte run is (chunk, tap), so conv3t walks all taps of a chunk in a row
-    (the chunk's input footprint stays in L2 across its taps; tap-major, a stride-2 layer re-read its input from HBM)
-    and conv3h's per-chunk tap loop reads consecutive runs."""
+    order) re-ordered group-major -- g-channel group, then tap, then channel (K' = (c // g) taps g + g tap + c % g; g =
+    w3_group: 16, or 32 on the stride-2 3x3s) -- and split (split3_bf16): a K-step's 96-byte run is 16 channels of one
+    (group, tap), so conv3t walks all taps of a group in a row (the group's input footprint stays in L2 across its taps;
+    tap-major, a stride-2 layer re-read its input from HBM) and conv3h's per-chunk tap loop reads consecutive runs."""
     lead = w.shape[:-1]
-    w = w.float().reshape(*lead, taps, cin // 16, 16).transpose(-3, -2).reshape(*lead, taps * cin)
+    w = w.float().reshape(*lead, taps, cin // g, g).transpose(-3, -2).reshape(*lead, taps * cin)
     return split3_bf16(w)
 
 
@@ -235,7 +242,7 @@ class SegNet:
         self.w8w = {}  # w8a16: prefix -> (e4m3 bytes [Npad][Kpad], per-row scale float [Npad])
         for prefix, kind, ci, co, k in arch.conv_specs():
             w, b = folded[prefix]
-            self.w[prefix] = self._pack(w, b, deconv=(kind == "deconv"))
+            self.w[prefix] = self._pack(w, b, deconv=(kind == "deconv"), stride=arch.stride_of(prefix))
             if self.form == "w8a16":
                 self.w8w[prefix] = self._pack_e4m3(self._rows(folded_f[prefix][0], deconv=(kind == "deconv")))
         # the three head branches' first 3x3 convs share their input: one GEMM per level
@@ -607,7 +614,7 @@ class SegNet:
         wm[:cout, :K] = wp.reshape(cout, K)
         return wm
 
-    def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False) -> Packed:
+    def _pack(self, w: torch.Tensor, b: torch.Tensor, deconv: bool = False, stride: int = 1) -> Packed:
         if deconv:  # ConvTranspose2d weight [Cin, Cout, 2, 2] -> 1x1 GEMM rows q*Cout + co, q = dy*2 + dx
             cin, cout = w.shape[0], w.shape[1]
             wg = w.permute(2, 3, 1, 0).reshape(4 * cout, cin)  # [dy, dx, co, ci]
@@ -626,7 +633,7 @@ class SegNet:
         p = Packed(wm.to(self.device, self.tdtype).contiguous(), bm.to(self.device).contiguous(), cin_p, cout, kh, K,
                    Kpad, Npad)
         if self.store == "f32" and cin_p % 16 == 0 and K == Kpad:
-            p.w3 = w3_rows(p.w, kh * kw, cin_p)
+            p.w3 = w3_rows(p.w, kh * kw, cin_p, w3_group(stride, kh * kw, cin_p))
         return p
 
     # ------------------------------------------------------------------ planning

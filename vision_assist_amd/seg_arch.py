@@ -114,6 +114,12 @@ class Arch:
             (21, self.c4 + self.c5, self.c5, self.rep(3), False),
         ]
 
+    STRIDE2 = ("model.0", "model.1", "model.3", "model.5", "model.7", "model.16", "model.19")
+
+    def stride_of(self, prefix: str) -> int:
+        """The stride of a conv_specs module: the backbone's downsampling Convs and the neck's two (yolov8-seg.yaml)."""
+        return 2 if prefix in self.STRIDE2 else 1
+
     def conv_specs(self):
         """Every parameterised module in state-dict order:
         (prefix, kind, c_in, c_out, k) with kind in {'conv' (Conv+BN+SiLU), 'conv2d' (plain, bias), 'deconv'}."""
