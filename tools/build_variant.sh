@@ -6,7 +6,7 @@ set -e
 SEG=$1; NAME=$2; shift 2; EXTRA="$*"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CSRC=$ROOT/vision_assist_amd/csrc
-FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I$CSRC -I$ROOT/include"
+FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I$CSRC -I$ROOT/include -mllvm -amdgpu-atomic-optimizer-strategy=None"
 OBJS="va_nav.o va_c2f.o va_c2fb.o va_stem.o va_pw.o va_post.o va_contour.o va_fp8.o va_handle.o"
 make -s -C "$CSRC" $OBJS
 SRC=$CSRC/.variant_$NAME.hip  # next to the real source: relative includes resolve

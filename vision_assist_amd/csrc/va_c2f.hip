@@ -120,7 +120,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
     const float* b3 = b1 + 96;                              // m.0.cv2 [32]
     const float* b4 = b1 + 128;                             // cv2 [64]
 
-    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 before the stage-2 barrier of tile j - 1
+    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 in tile j - 2 as its stage 2 starts, published after that stage
     volatile int* slot = (volatile int*)(cf_smem + C::LDS);
     int t, nx;  // this tile, the next
     if (g.wq) {
@@ -267,6 +267,8 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
         mark(k, 1);
         const int tn = nx;
         if (tn >= 0) load_tile(tn);  // lands during stages 2-4
+        int cl = 0;  // the tile after next: claimed here, published after stage 2 (va_fuse.h wq_claim_raw)
+        if (g.wq && tid == 0) cl = fz::wq_claim_raw(g.wq);
         __syncthreads();
         mark(k, 2);
 
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(C::NW * 64, C::WPC) void c2f_kernel(const __bf16* _
         else
             stage2(std::integral_constant<int, NG2 - 1>{});
         mark(k, 3);
-        if (g.wq && tid == 0) slot[(k + 1) & 1] = fz::wq_claim(g.wq, g.ntiles);
+        if (g.wq && tid == 0) slot[(k + 1) & 1] = cl < g.ntiles ? cl : -1;
         __syncthreads();
         mark(k, 4);
         nx = g.wq ? __builtin_amdgcn_readfirstlane(slot[(k + 1) & 1]) : fz::tile(g.ntiles, k + 1);

@@ -88,6 +88,13 @@ __device__ __forceinline__ int wq_claim(int* cnt, int ntiles) {
     const int v = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v < ntiles ? v : -1;
 }
+// the counter's raw value, for a claim issued well ahead of its use (conv3q, the f32 stem): the range check
+// (v < ntiles) is made where the claim is published, so the returning atomic's wait lands there too -- with the
+// compiler's atomic optimizer off for the file (Makefile), which would otherwise broadcast the result through a
+// readfirstlane and wait for it at once
+__device__ __forceinline__ int wq_claim_raw(int* cnt) {
+    return __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void wq_release(int* cnt) {
     if (__hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
         __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

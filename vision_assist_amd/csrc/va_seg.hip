@@ -2896,8 +2896,8 @@ constexpr int S32_TP = 400, S32_T = S32_LDS, S32_W1 = S32_T + 64 * S32_TP, S32_L
 static_assert(S32_LDS_T <= 160 * 1024, "LDS with the tail");
 
 // DYN: the work-queue schedule (wq_claim; the tiles' frame patches are loaded two tiles ahead, so the claims run two
-// ahead too: tile j's index sits in LDS slot j % 3, written by thread 0 after the partial-sum barrier of the tile two
-// before it and read at the start of the tile before it)
+// ahead too: tile j's index sits in LDS slot j % 3, claimed by thread 0 at the start of the tile three before it,
+// written before that tile's partial-sum barrier and read at the start of the tile before j)
 template <bool TAIL, bool DYN>
 __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __restrict__ frames, int N, int H, int W,
                                                            const __bf16* __restrict__ w03, const float* __restrict__ b0,
@@ -2996,6 +2996,10 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         const int tn = nx;
         const int tn2 = DYN ? __builtin_amdgcn_readfirstlane(slot[(k + 1) % 3]) : fz::tile(ntiles, k + 1);
         const u32x4 pf2 = load_patch(tn2);  // two tiles ahead
+        int cl = 0;  // DYN: the tile three ahead, claimed here and published after the K-loop (the returning atomic's
+        if constexpr (DYN) {  // ~1 us lands during model.0 / model.1 instead of stalling wave 0 before a barrier)
+            if (tid == 0) cl = fz::wq_claim_raw(wq);
+        }
 
         // ---- model.0 on the 9 x 33 region: group g = 16 region pixels (the last group ragged); region pixel q <->
         // model.0 (2 oy0 - 1 + q / 33, 2 ox0 - 1 + q % 33); its window starts at patch row 2 (q / 33), byte 6 (q % 33) + 7
@@ -3051,10 +3055,10 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         f32x16 a2 = acc0 + acc1;
         f32x16* part = (f32x16*)(s32 + S32_PART + (wid & 3) * 4096) + lane;
         if (kh) *part = a2;
-        __syncthreads();
         if constexpr (DYN) {
-            if (tid == 0) slot[(k + 2) % 3] = fz::wq_claim(wq, ntiles);  // read after this tile's last barrier
+            if (tid == 0) slot[(k + 2) % 3] = cl < ntiles ? cl : -1;  // read at iteration k + 1 (last read at k - 2)
         }
+        __syncthreads();
         // ---- epilogue: lane (r32, g32) holds channels 32 wn + 8 j + 4 g32 + (0..3) of its pixel, j = 0..3
         const int oy = oy0 + py, ox = ox0 + px;
         if constexpr (TAIL) {
@@ -3168,12 +3172,15 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const float* __restrict__ x = (const float*)a.x;
     const int H = a.H, W = a.W, ldx = a.ldx;
-    // DYN: the claimed tiles, published by thread 0 in two alternating slots (iteration k writes slot k & 1, whose
-    // last readers read it before the barrier that ended iteration k - 1)
+    // DYN: the claimed tiles, published by thread 0 in two alternating slots, one tile ahead of their use: iteration
+    // k reads slot k & 1 (claimed during iteration k - 1's K-loop, or in the prologue) and writes slot (k + 1) & 1
     volatile int* slot = (volatile int*)(q3 + Q3_LDS);
     int t;
     if constexpr (DYN) {
-        if (tid == 0) slot[0] = fz::wq_claim(a.wcnt, ntiles);
+        if (tid == 0) {
+            slot[0] = fz::wq_claim(a.wcnt, ntiles);
+            slot[1] = fz::wq_claim(a.wcnt, ntiles);
+        }
         __syncthreads();
         t = __builtin_amdgcn_readfirstlane(slot[0]);
     } else {
@@ -3232,12 +3239,14 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             const int c = tid + Q3_NT * i;
             if (c < Q3_NCH) cf32_put4(q3 + (c >> 3) * Q3_PS, c & 7, __builtin_bit_cast(f32x4, hv[i]));
         }
-        int tn;
+        int tn, cl = 0;
         if constexpr (DYN) {
-            if (tid == 0) slot[k & 1] = fz::wq_claim(a.wcnt, ntiles);
-            __syncthreads();  // planes complete; the next tile published
+            __syncthreads();  // planes complete; slot k & 1 holds the next tile (claimed an iteration earlier)
             tn = __builtin_amdgcn_readfirstlane(slot[k & 1]);
             load_halo(tn, hv);  // the next tile's halo, in flight during this tile's K-loop
+            // the tile after next: the returning atomic (~1 us at the memory side) lands during the K-loop and is
+            // published after it, instead of stalling thread 0's wave -- and the barrier -- right here
+            if (tid == 0) cl = fz::wq_claim_raw(a.wcnt);
         } else {
             tn = fz::tile(ntiles, k);
             load_halo(tn, hv);
@@ -3267,6 +3276,10 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
         if (kh) {
             part[0] = acc[0];
             part[64] = acc[1];
+        }
+        if constexpr (DYN) {
+            // read at iteration k + 1 after its first barrier; last read at iteration k - 1, before this one's
+            if (tid == 0) slot[(k + 1) & 1] = cl < ntiles ? cl : -1;
         }
         __syncthreads();  // partial sums complete; every wave is done with this tile's planes
         if (!kh) {

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
     const float* b0 = (const float*)(st_smem + ST_BIAS);  // model.0 [32]
     const float* b1 = b0 + 32;                              // model.1 [64]
 
-    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 before the last barrier of tile j - 2
+    // work queue: tile j's index in LDS slot j & 1, claimed by thread 0 at the start of tile j - 2 and published
+    // before its last barrier
     volatile int* slot = (volatile int*)(st_smem + ST_LDS);
     int t, nx;  // this tile, the next
     if (g.wq) {
@@ -156,6 +157,8 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
         const int n = t / g.tpf, rr = t % g.tpf, oy1 = (rr / g.tx) * ST_T, ox1 = (rr % g.tx) * ST_T;
         const int tn = nx;
         if (tn >= 0) load_span(tn);  // lands during this tile; converted into P16 after model.1
+        int cl = 0;  // the tile after next: claimed here, published before the last barrier (va_fuse.h wq_claim_raw)
+        if (g.wq && tid == 0) cl = fz::wq_claim_raw(g.wq);
 
         // ---- model.0 on the 33 x 33 region (M0 row mr <-> model.0 row 2 oy1 - 1 + mr, column j likewise)
         {
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(ST_NW * 64, 1) void stem_kernel(const uint8_t* __re
         }
         mark(k, 3);
         if (tn >= 0) store_span();
-        if (g.wq && tid == 0) slot[(k + 1) & 1] = fz::wq_claim(g.wq, g.ntiles);
+        if (g.wq && tid == 0) slot[(k + 1) & 1] = cl < g.ntiles ? cl : -1;
         __syncthreads();
         mark(k, 4);
         nx = g.wq ? __builtin_amdgcn_readfirstlane(slot[(k + 1) & 1]) : fz::tile(g.ntiles, k + 1);
