@@ -3165,6 +3165,11 @@ constexpr int Q3_PART = Q3_HP * Q3_PS, Q3_LDS = Q3_PART + 4 * 2 * 64 * 64;  // p
 // activations, no exchange between lanes
 constexpr int Q3_W2 = Q3_LDS + 16, Q3_LDS_T = Q3_W2 + 32 * 2 * 3 * 32;
 static_assert(Q3_LDS_T <= 160 * 1024, "one workgroup per CU");
+// RES (no tail, a.res set: model.2's second bottleneck conv): the tile's residual, 256 pixels x 32 channels f32
+// (pixel p at 128 p), DMA'd into LDS as the K-loop starts and read by the epilogue -- its HBM latency used to sit
+// between the partial-sum barrier and the stores of every tile (model.2.m.0.cv2 982 us against m.0.cv1's 764)
+constexpr int Q3_RES = Q3_LDS + 16, Q3_LDS_R = Q3_RES + 256 * 128;
+static_assert(Q3_LDS_R <= 160 * 1024, "one workgroup per CU");
 
 template <bool DYN, bool TAIL = false>
 __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int tiles_x, int tiles_y, int ntiles) {
@@ -3232,6 +3237,20 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
         }
     }
     constexpr int TA[6] = {0, 0, 1, 0, 1, 2}, TB[6] = {0, 1, 0, 2, 1, 0};
+    const bool pre_res = !TAIL && a.res != nullptr;  // uniform
+    // the residual of tile (ty, tx) of image n into RES: DMA i = wid + 8 u (1 KiB, pixels 8 i ..), lane l -> pixel
+    // 8 i + (l >> 3), channels 4 (l & 7) ..; pixels outside the image read zeros (never stored)
+    auto dma_res = [&](int n, int ty, int tx) {
+        const int rb = H * W * a.ldr * 4;
+        const float* rn = (const float*)a.res + (int64_t)n * H * W * a.ldr;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = wid + 8 * u, p = 8 * i + (lane >> 3), c = lane & 7;
+            const int iy = ty * Q3_T + (p >> 4), ix = tx * Q3_T + (p & 15);
+            const int vo = iy < H && ix < W ? ((iy * W + ix) * a.ldr + 4 * c) * 4 : 0x7ff00000;
+            t3_dma16(rn, rb, q3 + Q3_RES + 1024 * i, vo, 0);
+        }
+    };
     for (int k = 1; t >= 0; ++k) {
         const int tx = t % tiles_x, t2 = t / tiles_x, ty = t2 % tiles_y, n = t2 / tiles_y;
 #pragma unroll
@@ -3252,6 +3271,8 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             load_halo(tn, hv);
             __syncthreads();  // planes complete
         }
+        // (RES was last read by the previous tile's epilogue, before the barrier above)
+        if (pre_res) dma_res(n, ty, tx);
 
         f32x16 acc[2] = {(f32x16){}, (f32x16){}};
 #pragma unroll
@@ -3281,7 +3302,8 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
             // read at iteration k + 1 after its first barrier; last read at iteration k - 1, before this one's
             if (tid == 0) slot[(k + 1) & 1] = cl < ntiles ? cl : -1;
         }
-        __syncthreads();  // partial sums complete; every wave is done with this tile's planes
+        if (pre_res) t3_waitvm<0>();  // this wave's residual DMAs landed (the halo loads before them long since)
+        __syncthreads();  // partial sums complete; every wave is done with this tile's planes; RES complete
         if (!kh) {
             // lane (r32, g32) holds channels 8 j + 4 g32 + (0..3), j = 0..3, of its block's pixel r32
 #pragma unroll
@@ -3329,7 +3351,9 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
                         const float4 bv = *(const float4*)(a.bias + 8 * j + 4 * g32);
                         f32x4 v = {s[4 * j] + bv.x, s[4 * j + 1] + bv.y, s[4 * j + 2] + bv.z, s[4 * j + 3] + bv.w};
                         if (a.act) v = fz::act(v);
-                        if (a.res) v = v + *(const f32x4*)((const float*)a.res + pix * a.ldr + 4 * g32 + 8 * j);
+                        if (pre_res)
+                            v = v + *(const f32x4*)(q3 + Q3_RES + 128 * ((4 * pb + 2 * b + (r32 >> 4)) * Q3_T + (r32 & 15)) +
+                                                    16 * (2 * j + g32));
                         *(f32x4*)(yp + 8 * j) = v;
                     }
                 }
@@ -3806,7 +3830,8 @@ bool conv3q_shape_ok(const va_conv_args& a) {
     return a.mode == 0 && a.kh == 3 && a.kw == 3 && a.stride == 1 && a.pad == 1 && a.H == a.Ho && a.W == a.Wo &&
            a.Cin == 32 && a.Cout == 32 && a.K == 288 && a.Kpad == 288 && !a.xu && a.ldx % 4 == 0 && a.ldy % 4 == 0 &&
            ((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.y & 15) == 0 && ((uintptr_t)a.w & 15) == 0 &&
-           ((uintptr_t)a.bias & 15) == 0 && (!a.res || (a.ldr % 4 == 0 && ((uintptr_t)a.res & 15) == 0));
+           ((uintptr_t)a.bias & 15) == 0 &&
+           (!a.res || (a.ldr % 4 == 0 && ((uintptr_t)a.res & 15) == 0 && (int64_t)a.H * a.W * a.ldr * 4 < (1ll << 31)));
 }
 bool use_conv3q(const va_conv_args& a) {
     if (!va_sw().conv3q || a.w2 || !conv3q_shape_ok(a)) return false;
@@ -3824,9 +3849,9 @@ hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     static DevFlag attr;
     if (!attr()) {
         if (hipFuncSetAttribute((const void*)conv3q_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Q3_LDS + 16) != hipSuccess ||
+                                Q3_LDS_R) != hipSuccess ||
             hipFuncSetAttribute((const void*)conv3q_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                Q3_LDS + 16) != hipSuccess ||
+                                Q3_LDS_R) != hipSuccess ||
             hipFuncSetAttribute((const void*)conv3q_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 Q3_LDS_T) != hipSuccess ||
             hipFuncSetAttribute((const void*)conv3q_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3844,7 +3869,8 @@ hipError_t launch_conv3q(const va_conv_args& a, hipStream_t st) {
     if (a.w2)
         dyn ? go(conv3q_kernel<true, true>, Q3_LDS_T) : go(conv3q_kernel<false, true>, Q3_LDS_T);
     else
-        dyn ? go(conv3q_kernel<true, false>, Q3_LDS + 16) : go(conv3q_kernel<false, false>, Q3_LDS + 16);
+        dyn ? go(conv3q_kernel<true, false>, a.res ? Q3_LDS_R : Q3_LDS + 16)
+            : go(conv3q_kernel<false, false>, a.res ? Q3_LDS_R : Q3_LDS + 16);
     return hipGetLastError();
 }
 
