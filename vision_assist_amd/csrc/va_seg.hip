@@ -3150,9 +3150,9 @@ __device__ __forceinline__ void cf32_put4(unsigned char* p, int g, const f32x4& 
 // the K-loop.  Persistent: one 512-thread workgroup per CU walks the tiles (fz::tile, XCD-contiguous runs), the next
 // tile's halo in flight in registers during this one's MFMAs.  Wave w computes output rows 4 (w & 3) .. + 3 of the
 // tile (two 32-pixel blocks) x 32 channels over K-steps 9 (w >> 2) .. + 8 (tap x 16-channel chunk), the six term
-// products per K-step and block on v_mfma_f32_32x32x16_bf16 (the two blocks are the two accumulator chains); waves
-// 4-7 hand their partial sums to waves 0-3 through LDS, which add bias, SiLU and the residual (Bottleneck's
-// shortcut) and write f32.
+// products per K-step and block on v_mfma_f32_32x32x16_bf16 (the two blocks are the two accumulator chains); the two
+// waves of a row pair swap partial sums through LDS, each finishing one block: bias, SiLU and the residual
+// (Bottleneck's shortcut), f32 stores.
 constexpr int Q3_T = 16, Q3_HW = Q3_T + 2, Q3_HP = Q3_HW * Q3_HW;  // 16 x 16 tile, 18 x 18 = 324-pixel halo
 constexpr int Q3_NT = 512, Q3_PS = 208;
 constexpr int Q3_NCH = Q3_HP * 8;                    // 16-byte input chunks (4 channels) per halo: 2592
@@ -3292,23 +3292,21 @@ __global__ __launch_bounds__(Q3_NT, 1) void conv3q_kernel(va_conv_args a, int ti
                 for (int b = 0; b < 2; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(apr[i][TA[u]], bp[b][TB[u]], acc[b], 0, 0, 0);
         }
-        // K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 bytes per lane and block)
+        // K halves: wave (pb, kh) hands its partner (pb, 1 - kh) the partial sums of block 1 - kh and finishes block kh
+        // (lane-ordered, 64 bytes per lane): the epilogue on all eight waves, one block each (s = the K half-0 sum +
+        // the half-1 sum either way: the same f32 addition as one wave finishing both blocks)
         f32x16* part = (f32x16*)(q3 + Q3_PART + pb * 8192) + lane;
-        if (kh) {
-            part[0] = acc[0];
-            part[64] = acc[1];
-        }
+        part[64 * (1 - kh)] = kh ? acc[0] : acc[1];
         if constexpr (DYN) {
             // read at iteration k + 1 after its first barrier; last read at iteration k - 1, before this one's
             if (tid == 0) slot[(k + 1) & 1] = cl < ntiles ? cl : -1;
         }
         if (pre_res) t3_waitvm<0>();  // this wave's residual DMAs landed (the halo loads before them long since)
         __syncthreads();  // partial sums complete; every wave is done with this tile's planes; RES complete
-        if (!kh) {
+        {
             // lane (r32, g32) holds channels 8 j + 4 g32 + (0..3), j = 0..3, of its block's pixel r32
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const f32x16 s = acc[b] + part[64 * b];
+            for (int b = kh, be = kh + 1; b < be; ++b) {  // block kh (a loop for the continue below)
+                const f32x16 s = (kh ? acc[1] : acc[0]) + part[64 * b];
                 const int oy = ty * Q3_T + 4 * pb + 2 * b + (r32 >> 4), ox = tx * Q3_T + (r32 & 15);
                 const bool inside = oy < H && ox < W;
                 // (the tail's MFMAs take every lane's operands -- its A rows from lanes of pixels outside the map
