@@ -3051,10 +3051,23 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(apr[i][TA[u + 1]], bp[TB[u + 1]], acc1, 0, 0, 0);
             }
         }
-        // ---- K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 B per lane)
+        // ---- K halves: waves 4-7 hand their partial sums to waves 0-3 (lane-ordered, 64 B per lane); TAIL: the two
+        // waves of a K pair swap halves instead -- wave kh finishes channel groups j = 2 kh, 2 kh + 1 (16 B each)
         f32x16 a2 = acc0 + acc1;
         f32x16* part = (f32x16*)(s32 + S32_PART + (wid & 3) * 4096) + lane;
-        if (kh) *part = a2;
+        auto quad = [&](int j) { return (f32x4){a2[4 * j], a2[4 * j + 1], a2[4 * j + 2], a2[4 * j + 3]}; };
+        if constexpr (TAIL) {
+            f32x4* ph = (f32x4*)part;  // the partner's groups (kh is wave-uniform: a scalar branch, constant indices)
+            if (kh) {
+                ph[0] = quad(0);
+                ph[1] = quad(1);
+            } else {
+                ph[2] = quad(2);
+                ph[3] = quad(3);
+            }
+        } else {
+            if (kh) *part = a2;
+        }
         if constexpr (DYN) {
             if (tid == 0) slot[(k + 2) % 3] = cl < ntiles ? cl : -1;  // read at iteration k + 1 (last read at k - 2)
         }
@@ -3064,19 +3077,31 @@ __global__ __launch_bounds__(S32_NT, 1) void stem32_kernel(const uint8_t* __rest
         if constexpr (TAIL) {
             // model.1's activations -> the T planes (every pixel of the tile: an outside one is finite and unstored);
             // channel c = 32 wn + 8 j + 4 g32 + e sits in chunk c / 16, at byte 2 (c % 16) of each plane's 32 bytes
-            if (!kh) {
-                a2 = a2 + *part;
+            {
+                // the K half-0 sum + the half-1 sum, as before (wave kh holds half kh of its own groups)
+                const f32x4* ph = (const f32x4*)part;
                 unsigned char* tp = s32 + S32_T + (32 * wm + r32) * S32_TP + 8 * g32;
+                auto finish = [&](auto KHc) {
+                    constexpr int KH = decltype(KHc)::value;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint2 tt3[3];
-                    split3_bf16x4(fz::act((f32x4){a2[4 * j] + bo[j].x, a2[4 * j + 1] + bo[j].y,
-                                                  a2[4 * j + 2] + bo[j].z, a2[4 * j + 3] + bo[j].w}),
-                                  tt3);
-                    unsigned char* d = tp + (2 * wn + (j >> 1)) * 96 + 16 * (j & 1);
+                    for (int u = 0; u < 2; ++u) {
+                        constexpr int J0 = 2 * KH;
+                        const int j = J0 + u;
+                        const f32x4 mine = quad(j), oth = ph[j];
+                        const f32x4 sm = KH ? oth + mine : mine + oth;
+                        uint2 tt3[3];
+                        split3_bf16x4(fz::act((f32x4){sm[0] + bo[j].x, sm[1] + bo[j].y, sm[2] + bo[j].z,
+                                                      sm[3] + bo[j].w}),
+                                      tt3);
+                        unsigned char* d = tp + (2 * wn + KH) * 96 + 16 * u;
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) *(uint2*)(d + 32 * p) = tt3[p];
-                }
+                        for (int p = 0; p < 3; ++p) *(uint2*)(d + 32 * p) = tt3[p];
+                    }
+                };
+                if (kh)
+                    finish(std::integral_constant<int, 1>{});
+                else
+                    finish(std::integral_constant<int, 0>{});
             }
             __syncthreads();  // T complete; M0 and the partial sums free for the next tile; its patch stored
             if (!kh) {
